@@ -1,0 +1,191 @@
+"""In-tree default plugins the reference profile keeps enabled.
+
+The reference's profile only *adds* GPU at score/postBind (reference
+deploy/scheduler.yaml:16-23), so upstream defaults (queue sort, node filters,
+resource fit, default binder) stay on.  These are the subset that matters for GPU pods.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Optional, Tuple
+
+from ..api import constants as C
+from ..api import objects as O
+from .interface import (BindPlugin, CycleState, FilterPlugin, NodeScore, PreFilterPlugin, QueueSortPlugin,
+                        ScoreExtensions, ScorePlugin, Status)
+from .runtime import Registry
+
+Obj = Dict[str, Any]
+
+
+class PrioritySort(QueueSortPlugin):
+    NAME = "PrioritySort"
+
+    def __init__(self, args=None, handle=None):
+        pass
+
+    def less(self, a, b) -> bool:
+        pa, pb = O.priority(a.pod), O.priority(b.pod)
+        if pa != pb:
+            return pa > pb
+        return a.timestamp < b.timestamp
+
+
+class NodeUnschedulable(FilterPlugin):
+    NAME = "NodeUnschedulable"
+
+    def __init__(self, args=None, handle=None):
+        pass
+
+    def filter(self, state, pod, node_info):
+        node = node_info.node
+        if O.node_unschedulable(node):
+            t = {"key": "node.kubernetes.io/unschedulable", "effect": "NoSchedule"}
+            if not O.tolerates(pod, t):
+                return Status.unschedulable("node(s) were unschedulable", self.NAME, True)
+        if not O.node_ready(node):
+            return Status.unschedulable("node(s) were not ready", self.NAME, True)
+        return None
+
+
+class NodeName(FilterPlugin):
+    NAME = "NodeName"
+
+    def __init__(self, args=None, handle=None):
+        pass
+
+    def filter(self, state, pod, node_info):
+        want = pod.get("spec", {}).get("nodeName")
+        if want and want != node_info.name:
+            return Status.unschedulable("node(s) didn't match the requested node name", self.NAME, True)
+        return None
+
+
+class TaintToleration(FilterPlugin):
+    NAME = "TaintToleration"
+
+    def __init__(self, args=None, handle=None):
+        pass
+
+    def filter(self, state, pod, node_info):
+        for t in O.node_taints(node_info.node):
+            if t.get("effect") not in ("NoSchedule", "NoExecute"):
+                continue
+            if not O.tolerates(pod, t):
+                return Status.unschedulable(f"node(s) had untolerated taint {{{t.get('key')}: {t.get('value', '')}}}",
+                                            self.NAME, True)
+        return None
+
+
+class NodeAffinity(FilterPlugin):
+    NAME = "NodeAffinity"
+
+    def __init__(self, args=None, handle=None):
+        pass
+
+    def filter(self, state, pod, node_info):
+        sel = pod.get("spec", {}).get("nodeSelector") or {}
+        lab = O.labels(node_info.node)
+        for k, v in sel.items():
+            if lab.get(k) != v:
+                return Status.unschedulable("node(s) didn't match Pod's node affinity/selector", self.NAME, True)
+        aff = (pod.get("spec", {}).get("affinity") or {}).get("nodeAffinity") or {}
+        req = aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
+        terms = req.get("nodeSelectorTerms") or []
+        if terms:
+            from ..kube.patch import match_label_selector
+            ok = any(match_label_selector(lab, {"matchExpressions": t.get("matchExpressions") or []})
+                     for t in terms)
+            if not ok:
+                return Status.unschedulable("node(s) didn't match Pod's node affinity/selector", self.NAME, True)
+        return None
+
+
+_FIT_KEY = "NodeResourcesFit/req"
+
+
+class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
+    NAME = "NodeResourcesFit"
+
+    def __init__(self, args=None, handle=None):
+        self.ignored = set((args or {}).get("ignoredResources", []))
+
+    def pre_filter(self, state, pod):
+        state.write(_FIT_KEY, O.pod_requests(pod))
+        return None
+
+    def filter(self, state, pod, node_info):
+        req = state.read(_FIT_KEY)
+        if req is None:
+            req = O.pod_requests(pod)
+        if node_info.free(C.RESOURCE_PODS) < 1 and C.RESOURCE_PODS in node_info.allocatable:
+            return Status.unschedulable("Too many pods", self.NAME)
+        for r, v in req.items():
+            if v <= 0 or r in self.ignored:
+                continue
+            if r not in node_info.allocatable and r.startswith(("amd.com/", "nvidia.com/")):
+                return Status.unschedulable(f"Insufficient {r}", self.NAME)
+            if r in node_info.allocatable and node_info.free(r) < v - 1e-9:
+                return Status.unschedulable(f"Insufficient {r}", self.NAME)
+        return None
+
+
+class _ResourceScore(ScorePlugin):
+    RES = (C.RESOURCE_CPU, C.RESOURCE_MEMORY)
+
+    def __init__(self, args=None, handle=None):
+        self.handle = handle
+
+    def _fractions(self, pod, node_name):
+        ni = self.handle.snapshot().get(node_name)
+        req = O.pod_requests(pod)
+        fr = []
+        for r in self.RES:
+            alloc = ni.allocatable.get(r, 0.0) if ni else 0.0
+            if alloc <= 0:
+                continue
+            fr.append(min(1.0, (ni.requested.get(r, 0.0) + req.get(r, 0.0)) / alloc))
+        return fr
+
+
+class NodeResourcesLeastAllocated(_ResourceScore):
+    NAME = "NodeResourcesLeastAllocated"
+
+    def score(self, state, pod, node_name):
+        fr = self._fractions(pod, node_name)
+        if not fr:
+            return 0, None
+        return int(sum((1 - f) * C.MAX_NODE_SCORE for f in fr) / len(fr)), None
+
+
+class NodeResourcesBalancedAllocation(_ResourceScore):
+    NAME = "NodeResourcesBalancedAllocation"
+
+    def score(self, state, pod, node_name):
+        fr = self._fractions(pod, node_name)
+        if len(fr) < 2:
+            return C.MAX_NODE_SCORE, None
+        mean = sum(fr) / len(fr)
+        var = sum((f - mean) ** 2 for f in fr) / len(fr)
+        return int((1 - var ** 0.5) * C.MAX_NODE_SCORE), None
+
+
+class DefaultBinder(BindPlugin):
+    NAME = "DefaultBinder"
+
+    def __init__(self, args=None, handle=None):
+        self.handle = handle
+
+    def bind(self, state, pod, node_name):
+        try:
+            self.handle.client.bind(O.namespace(pod), O.name(pod), node_name, O.uid(pod))
+        except Exception as e:
+            return Status.error(f"binding rejected: {e}", self.NAME)
+        return None
+
+
+def default_registry() -> Registry:
+    r = Registry()
+    for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
+                NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder):
+        r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
+    return r

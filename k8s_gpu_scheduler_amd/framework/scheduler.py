@@ -1,0 +1,348 @@
+"""The scheduler: informers -> queue -> scheduling cycle -> binding cycle.
+
+Upstream kube-scheduler's scheduleOne, which the reference inherits unchanged
+("kube-scheduler scheduleOne → Filter → RunScorePlugins → NormalizeScore
+→ selectHost → Reserve/Permit → PreBind → Bind → PostBind"), re-implemented for the
+standalone `gpu-scheduler`:
+
+* pods with `spec.schedulerName` in our profiles are queued (reference pods opt in via
+  `schedulerName: gpu-scheduler`, deploy/busybox/busybox.yaml:17);
+* the scheduling cycle takes a cache snapshot, filters, scores, picks the host with the
+  reservoir-sampled max (upstream selectHost), assumes the pod and runs Reserve/Permit;
+* the binding cycle (PreBind, Bind, PostBind) runs async on a worker pool or inline
+  (`bind_async=False`, used by the bench and tests); failures Unreserve + forget + requeue.
+"""
+from __future__ import annotations
+
+import logging
+import random
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from ..api import objects as O
+from ..kube.client import KubeClient
+from ..kube.informer import SharedInformerFactory
+from .cache import SchedulerCache, Snapshot
+from .config import SchedulerConfig
+from .interface import Code, CycleState, Status
+from .queue import QueuedPodInfo, SchedulingQueue
+from .runtime import Framework, Registry
+
+log = logging.getLogger(__name__)
+Obj = Dict[str, Any]
+
+
+@dataclass
+class ScheduleResult:
+    pod_key: str
+    node: str = ""
+    status: Status = field(default_factory=Status.success)
+    scores: Dict[str, int] = field(default_factory=dict)
+    evaluated: int = 0
+    feasible: int = 0
+    latency_s: float = 0.0
+    bound: bool = False
+
+
+class Handle:
+    """What plugins can reach (framework.Handle in upstream)."""
+
+    def __init__(self, scheduler: "Scheduler"):
+        self._s = scheduler
+
+    @property
+    def client(self) -> KubeClient:
+        return self._s.client
+
+    @property
+    def informer_factory(self) -> SharedInformerFactory:
+        return self._s.informers
+
+    @property
+    def cache(self) -> SchedulerCache:
+        return self._s.cache
+
+    def snapshot(self) -> Snapshot:
+        return self._s.current_snapshot()
+
+    def event(self, obj: Obj, reason: str, message: str, type_: str = "Normal") -> None:
+        if self._s.record_events:
+            self.client.create_event(obj, reason, message, type_)
+
+    @property
+    def extras(self) -> Dict[str, Any]:
+        return self._s.extras
+
+
+class Scheduler:
+    def __init__(self, client: KubeClient, config: SchedulerConfig, registry: Registry,
+                 bind_async: bool = True, bind_workers: int = 16, record_events: bool = True,
+                 seed: Optional[int] = None, extras: Optional[Dict[str, Any]] = None,
+                 informers: Optional[SharedInformerFactory] = None):
+        self.client = client
+        self.config = config
+        self.cache = SchedulerCache()
+        self.informers = informers or SharedInformerFactory(client)
+        self.extras: Dict[str, Any] = dict(extras or {})
+        self.record_events = record_events
+        self.handle = Handle(self)
+        self.frameworks: Dict[str, Framework] = {}
+        self._snapshot: Optional[Snapshot] = None
+        for prof in config.profiles:
+            self.frameworks[prof.scheduler_name] = Framework(prof, registry, self.handle, config.parallelism)
+        first = next(iter(self.frameworks.values()))
+        self.queue = SchedulingQueue(self._queue_less(first), config.pod_initial_backoff_s,
+                                     config.pod_max_backoff_s)
+        self.bind_async = bind_async
+        self._bind_pool = ThreadPoolExecutor(bind_workers, thread_name_prefix="bind") if bind_async else None
+        self._rng = random.Random(seed)
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._results_lock = threading.Lock()
+        self.results: List[ScheduleResult] = []
+        self.keep_results = True
+        self.on_result: Optional[Callable[[ScheduleResult], None]] = None
+        self.stats = {"scheduled": 0, "unschedulable": 0, "errors": 0, "bind_failures": 0}
+        self._pending_binds = 0
+        self._bind_cv = threading.Condition()
+        self._started = False
+
+    @staticmethod
+    def _queue_less(fw: Framework):
+        less = fw.queue_sort_less()
+        return less
+
+    # ---------------------------------------------------------------- event wiring
+    def _responsible(self, pod: Obj) -> bool:
+        return O.scheduler_name(pod) in self.frameworks
+
+    def _on_pod_add(self, pod: Obj) -> None:
+        if O.node_name_of(pod):
+            self.cache.add_pod(pod)
+        elif self._responsible(pod) and not O.is_terminal(pod):
+            self.queue.add(pod)
+
+    def _on_pod_update(self, old: Obj, new: Obj) -> None:
+        if O.node_name_of(new):
+            if O.is_terminal(new):
+                self.cache.remove_pod(new)
+                self.queue.move_all_to_active_or_backoff("PodTerminated")
+            else:
+                self.cache.update_pod(new)
+        elif self._responsible(new) and not O.is_terminal(new):
+            if O.resource_version(old) != O.resource_version(new):
+                self.queue.update(new)
+
+    def _on_pod_delete(self, pod: Obj) -> None:
+        if O.node_name_of(pod):
+            self.cache.remove_pod(pod)
+            self.queue.move_all_to_active_or_backoff("AssignedPodDelete")
+        else:
+            self.queue.delete(pod)
+
+    def _on_node_add(self, node: Obj) -> None:
+        self.cache.add_node(node)
+        self.queue.move_all_to_active_or_backoff("NodeAdd")
+
+    def _on_node_update(self, old: Obj, new: Obj) -> None:
+        self.cache.update_node(new)
+        self.queue.move_all_to_active_or_backoff("NodeUpdate")
+
+    def _on_node_delete(self, node: Obj) -> None:
+        self.cache.remove_node(node)
+
+    def start_informers(self) -> None:
+        if self._started:
+            return
+        self._started = True
+        pods, nodes = self.informers.pods(), self.informers.nodes()
+        self.informers.config_maps()
+        nodes.add_event_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
+        pods.add_event_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
+        self.informers.start()
+        self.informers.wait_for_cache_sync()
+
+    # ---------------------------------------------------------------- cycle
+    def current_snapshot(self) -> Snapshot:
+        if self._snapshot is None:
+            self._snapshot = self.cache.snapshot()
+        return self._snapshot
+
+    def _select_host(self, scores: List[Any]) -> str:
+        best, cnt, sel = None, 0, ""
+        for ns in scores:
+            if best is None or ns.score > best:
+                best, cnt, sel = ns.score, 1, ns.name
+            elif ns.score == best:
+                cnt += 1
+                if self._rng.randrange(cnt) == 0:
+                    sel = ns.name
+        return sel
+
+    def schedule_one(self, pi: QueuedPodInfo) -> ScheduleResult:
+        t0 = time.perf_counter()
+        pod = pi.pod
+        fw = self.frameworks.get(O.scheduler_name(pod))
+        res = ScheduleResult(O.key(pod))
+        if fw is None:
+            res.status = Status.error("no profile for scheduler " + O.scheduler_name(pod))
+            return res
+        self._snapshot = self.cache.snapshot()
+        state = CycleState()
+        nodes = self._snapshot.list()
+        res.evaluated = len(nodes)
+        st = fw.run_pre_filter(state, pod)
+        if not st.ok:
+            return self._fail(pi, fw, state, res, st, t0)
+        feasible, failed = fw.find_feasible(state, pod, nodes)
+        res.feasible = len(feasible)
+        if not feasible:
+            _, pst = fw.run_post_filter(state, pod, failed)
+            reasons = sorted({m for s in failed.values() for m in s.reasons})
+            msg = f"0/{len(nodes)} nodes are available: " + ", ".join(reasons) if nodes else "no nodes available"
+            return self._fail(pi, fw, state, res, Status.unschedulable(msg), t0)
+        if len(feasible) == 1 and not fw.points["score"]:
+            host = feasible[0].name
+        else:
+            st = fw.run_pre_score(state, pod, feasible)
+            if not st.ok:
+                return self._fail(pi, fw, state, res, st, t0)
+            scores, st = fw.run_score(state, pod, feasible)
+            if not st.ok:
+                return self._fail(pi, fw, state, res, st, t0)
+            res.scores = {s.name: s.score for s in scores}
+            host = self._select_host(scores)
+        # assume + reserve
+        self.cache.assume_pod(pod, host)
+        st = fw.run_reserve(state, pod, host)
+        if not st.ok:
+            fw.run_unreserve(state, pod, host)
+            self.cache.forget_pod(pod)
+            return self._fail(pi, fw, state, res, st, t0)
+        st, wait = fw.run_permit(state, pod, host)
+        if not st.ok and st.code != Code.WAIT:
+            fw.run_unreserve(state, pod, host)
+            self.cache.forget_pod(pod)
+            return self._fail(pi, fw, state, res, st, t0)
+        res.node = host
+        self._snapshot = None
+        if self._bind_pool is not None:
+            with self._bind_cv:
+                self._pending_binds += 1
+            self._bind_pool.submit(self._binding_cycle, fw, state, pi, host, res, t0)
+        else:
+            self._binding_cycle(fw, state, pi, host, res, t0)
+        return res
+
+    def _binding_cycle(self, fw: Framework, state: CycleState, pi: QueuedPodInfo, host: str,
+                       res: ScheduleResult, t0: float) -> None:
+        pod = pi.pod
+        try:
+            st = fw.run_pre_bind(state, pod, host)
+            if st.ok:
+                st = fw.run_bind(state, pod, host)
+            if not st.ok:
+                fw.run_unreserve(state, pod, host)
+                self.cache.forget_pod(pod)
+                self.stats["bind_failures"] += 1
+                res.status = st
+                self.handle.event(pod, "FailedScheduling", f"Binding rejected: {st.message()}", "Warning")
+                self.queue.add_unschedulable(pi)
+            else:
+                self.cache.finish_binding(pod)
+                self.queue.done(pod)
+                res.bound = True
+                self.stats["scheduled"] += 1
+                self.handle.event(pod, "Scheduled", f"Successfully assigned {O.key(pod)} to {host}")
+                fw.run_post_bind(state, pod, host)
+        except Exception as e:  # keep the loop alive
+            log.exception("binding cycle failed")
+            fw.run_unreserve(state, pod, host)
+            self.cache.forget_pod(pod)
+            res.status = Status.error(str(e))
+            self.stats["errors"] += 1
+            self.queue.add_unschedulable(pi)
+        finally:
+            res.latency_s = time.perf_counter() - t0
+            self._record(res)
+            if self._bind_pool is not None:
+                with self._bind_cv:
+                    self._pending_binds -= 1
+                    self._bind_cv.notify_all()
+
+    def _fail(self, pi: QueuedPodInfo, fw: Framework, state: CycleState, res: ScheduleResult,
+              st: Status, t0: float) -> ScheduleResult:
+        res.status = st
+        res.latency_s = time.perf_counter() - t0
+        if st.code == Code.ERROR:
+            self.stats["errors"] += 1
+            log.warning("scheduling %s failed: %s", res.pod_key, st.message())
+        else:
+            self.stats["unschedulable"] += 1
+        self.handle.event(pi.pod, "FailedScheduling", st.message(), "Warning")
+        self.queue.add_unschedulable(pi)
+        self._snapshot = None
+        self._record(res)
+        return res
+
+    def _record(self, res: ScheduleResult) -> None:
+        if self.keep_results:
+            with self._results_lock:
+                self.results.append(res)
+        if self.on_result:
+            self.on_result(res)
+
+    # ---------------------------------------------------------------- loops
+    def schedule_pending(self, max_pods: Optional[int] = None, timeout_s: float = 0.0) -> List[ScheduleResult]:
+        """Drain the active queue synchronously (tests / bench)."""
+        out = []
+        while max_pods is None or len(out) < max_pods:
+            pi = self.queue.pop(timeout_s)
+            if pi is None:
+                break
+            out.append(self.schedule_one(pi))
+        return out
+
+    def wait_for_binds(self, timeout_s: float = 30.0) -> bool:
+        deadline = time.monotonic() + timeout_s
+        with self._bind_cv:
+            while self._pending_binds > 0:
+                rem = deadline - time.monotonic()
+                if rem <= 0:
+                    return False
+                self._bind_cv.wait(rem)
+        return True
+
+    def run(self) -> None:
+        self.start_informers()
+        last_cleanup = time.monotonic()
+        while not self._stop.is_set():
+            pi = self.queue.pop(0.2)
+            if time.monotonic() - last_cleanup > 1.0:
+                self.cache.cleanup_expired()
+                last_cleanup = time.monotonic()
+            if pi is None:
+                continue
+            try:
+                self.schedule_one(pi)
+            except Exception:
+                log.exception("schedule_one crashed")
+                self.queue.add_unschedulable(pi)
+
+    def start(self) -> None:
+        self._thread = threading.Thread(target=self.run, name="scheduler", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.queue.close()
+        if self._thread:
+            self._thread.join(timeout=5)
+        if self._bind_pool:
+            self._bind_pool.shutdown(wait=True)
+        for fw in self.frameworks.values():
+            fw.close()
+        self.informers.stop()

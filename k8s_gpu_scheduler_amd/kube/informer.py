@@ -1,0 +1,280 @@
+"""List+watch informers, indexers and listers.
+
+Equivalent of the client-go SharedInformerFactory the reference builds lazily inside
+Score (reference gpu_plugins.go:785-795, resync 3 s) and in the profiler/redisCtl
+(10 min; pkg/profiler/cmd/client/client.go:51-56).  Differences (fixes SURVEY §2.9 #8):
+the factory is built once at scheduler start, is owned by one object (no package
+globals mutated from parallel Score), and handles watch expiry (410 Gone) by relisting.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+from ..api import objects as O
+from .client import FakeCluster, Gone, KubeClient, WatchEvent
+from .patch import match_field_selector, match_label_selector
+
+log = logging.getLogger(__name__)
+Obj = Dict[str, Any]
+Handler = Callable[..., None]
+
+
+class Indexer:
+    """Thread-safe object store keyed by namespace/name with secondary indexes."""
+
+    def __init__(self) -> None:
+        self._lock = threading.RLock()
+        self._items: Dict[str, Obj] = {}
+        self._index_funcs: Dict[str, Callable[[Obj], List[str]]] = {}
+        self._indices: Dict[str, Dict[str, set]] = {}
+
+    def add_index(self, idx_name: str, fn: Callable[[Obj], List[str]]) -> None:
+        with self._lock:
+            self._index_funcs[idx_name] = fn
+            self._indices[idx_name] = {}
+            for k, o in self._items.items():
+                for v in fn(o):
+                    self._indices[idx_name].setdefault(v, set()).add(k)
+
+    def _unindex(self, k: str, o: Obj) -> None:
+        for n, fn in self._index_funcs.items():
+            for v in fn(o):
+                s = self._indices[n].get(v)
+                if s:
+                    s.discard(k)
+
+    def _index(self, k: str, o: Obj) -> None:
+        for n, fn in self._index_funcs.items():
+            for v in fn(o):
+                self._indices[n].setdefault(v, set()).add(k)
+
+    def upsert(self, obj: Obj) -> Optional[Obj]:
+        k = O.key(obj)
+        with self._lock:
+            old = self._items.get(k)
+            if old is not None:
+                self._unindex(k, old)
+            self._items[k] = obj
+            self._index(k, obj)
+            return old
+
+    def delete(self, obj: Obj) -> Optional[Obj]:
+        k = O.key(obj)
+        with self._lock:
+            old = self._items.pop(k, None)
+            if old is not None:
+                self._unindex(k, old)
+            return old
+
+    def replace(self, objs: List[Obj]) -> None:
+        with self._lock:
+            self._items = {}
+            for n in self._indices:
+                self._indices[n] = {}
+            for o in objs:
+                self.upsert(o)
+
+    def get_by_key(self, k: str) -> Optional[Obj]:
+        with self._lock:
+            return self._items.get(k)
+
+    def by_index(self, idx_name: str, value: str) -> List[Obj]:
+        with self._lock:
+            return [self._items[k] for k in self._indices.get(idx_name, {}).get(value, ()) if k in self._items]
+
+    def list(self) -> List[Obj]:
+        with self._lock:
+            return list(self._items.values())
+
+    def keys(self) -> List[str]:
+        with self._lock:
+            return list(self._items.keys())
+
+    def __len__(self) -> int:
+        return len(self._items)
+
+
+class Lister:
+    def __init__(self, indexer: Indexer, namespaced: bool):
+        self.indexer = indexer
+        self.namespaced = namespaced
+
+    def list(self, namespace: Optional[str] = None, label_selector: Any = None,
+             field_selector: Optional[str] = None) -> List[Obj]:
+        if namespace and self.namespaced:
+            objs = self.indexer.by_index("namespace", namespace)
+        else:
+            objs = self.indexer.list()
+        return [o for o in objs if match_label_selector(O.labels(o), label_selector)
+                and match_field_selector(o, field_selector)]
+
+    def get(self, name: str, namespace: Optional[str] = None) -> Optional[Obj]:
+        k = f"{namespace or 'default'}/{name}" if self.namespaced else name
+        return self.indexer.get_by_key(k)
+
+
+class Informer:
+    def __init__(self, client: KubeClient, resource: str, resync_s: float = 0.0,
+                 namespace: Optional[str] = None):
+        from .client import NAMESPACED
+        self.client = client
+        self.resource = resource
+        self.namespace = namespace
+        self.resync_s = resync_s
+        self.indexer = Indexer()
+        namespaced = NAMESPACED[resource]
+        if namespaced:
+            self.indexer.add_index("namespace", lambda o: [O.namespace(o)])
+        if resource == "pods":
+            self.indexer.add_index("nodeName", lambda o: [O.node_name_of(o)] if O.node_name_of(o) else [])
+        self.lister = Lister(self.indexer, namespaced)
+        self._handlers: List[Dict[str, Optional[Handler]]] = []
+        self._synced = threading.Event()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._cancel: Optional[Callable[[], None]] = None
+        self._rv = ""
+
+    def add_event_handler(self, on_add: Optional[Handler] = None, on_update: Optional[Handler] = None,
+                          on_delete: Optional[Handler] = None) -> None:
+        self._handlers.append({"add": on_add, "update": on_update, "delete": on_delete})
+        if self._synced.is_set():
+            for o in self.indexer.list():
+                if on_add:
+                    on_add(o)
+
+    def _dispatch(self, ev: WatchEvent) -> None:
+        typ, obj = ev.get("type"), ev.get("object")
+        if typ == "BOOKMARK":
+            self._rv = O.resource_version(obj)
+            return
+        if typ == "ERROR" or obj is None:
+            return
+        if self.namespace and O.namespace(obj) != self.namespace:
+            return
+        self._rv = O.resource_version(obj) or self._rv
+        if typ == "DELETED":
+            old = self.indexer.delete(obj)
+            for h in self._handlers:
+                if h["delete"]:
+                    h["delete"](old or obj)
+        else:
+            old = self.indexer.upsert(obj)
+            for h in self._handlers:
+                if old is None and h["add"]:
+                    h["add"](obj)
+                elif old is not None and h["update"]:
+                    h["update"](old, obj)
+
+    def _list(self) -> None:
+        items, rv = self.client.list(self.resource, self.namespace)
+        prev = {O.key(o): o for o in self.indexer.list()}
+        self.indexer.replace(items)
+        self._rv = rv
+        new_keys = set()
+        for o in items:
+            k = O.key(o)
+            new_keys.add(k)
+            for h in self._handlers:
+                if k in prev:
+                    if h["update"]:
+                        h["update"](prev[k], o)
+                elif h["add"]:
+                    h["add"](o)
+        for k, o in prev.items():
+            if k not in new_keys:
+                for h in self._handlers:
+                    if h["delete"]:
+                        h["delete"](o)
+
+    def start(self) -> None:
+        if isinstance(self.client, FakeCluster) and self.client.sync_watch:
+            # Subscribe first so nothing created between list and subscribe is lost.
+            self._cancel = self.client.subscribe(self.resource, self._dispatch)
+            self._list()
+            self._synced.set()
+            return
+        self._thread = threading.Thread(target=self._run, name=f"informer-{self.resource}", daemon=True)
+        self._thread.start()
+
+    def _run(self) -> None:
+        backoff = 0.05
+        last_resync = time.monotonic()
+        while not self._stop.is_set():
+            try:
+                if not self._synced.is_set() or not self._rv:
+                    self._list()
+                    self._synced.set()
+                for ev in self.client.watch(self.resource, self.namespace, self._rv, timeout_s=1.0):
+                    self._dispatch(ev)
+                    if self._stop.is_set():
+                        return
+                if self.resync_s and time.monotonic() - last_resync > self.resync_s:
+                    last_resync = time.monotonic()
+                    for o in self.indexer.list():
+                        for h in self._handlers:
+                            if h["update"]:
+                                h["update"](o, o)
+                backoff = 0.05
+            except Gone:
+                log.info("watch on %s expired (410); relisting", self.resource)
+                self._rv = ""
+            except Exception as e:  # network/apiserver errors: back off and relist
+                log.warning("informer %s error: %s", self.resource, e)
+                self._stop.wait(backoff)
+                backoff = min(backoff * 2, 5.0)
+                self._rv = ""
+
+    def wait_for_cache_sync(self, timeout_s: float = 30.0) -> bool:
+        return self._synced.wait(timeout_s)
+
+    def has_synced(self) -> bool:
+        return self._synced.is_set()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._cancel:
+            self._cancel()
+
+
+class SharedInformerFactory:
+    """One informer per resource, shared by every consumer."""
+
+    def __init__(self, client: KubeClient, resync_s: float = 0.0, namespace: Optional[str] = None):
+        self.client = client
+        self.resync_s = resync_s
+        self.namespace = namespace
+        self._informers: Dict[str, Informer] = {}
+        self._lock = threading.Lock()
+
+    def informer(self, resource: str) -> Informer:
+        with self._lock:
+            inf = self._informers.get(resource)
+            if inf is None:
+                inf = Informer(self.client, resource, self.resync_s, self.namespace)
+                self._informers[resource] = inf
+            return inf
+
+    def pods(self) -> Informer:
+        return self.informer("pods")
+
+    def nodes(self) -> Informer:
+        return self.informer("nodes")
+
+    def config_maps(self) -> Informer:
+        return self.informer("configmaps")
+
+    def start(self) -> None:
+        for inf in list(self._informers.values()):
+            if not inf._synced.is_set() and inf._thread is None and inf._cancel is None:
+                inf.start()
+
+    def wait_for_cache_sync(self, timeout_s: float = 30.0) -> bool:
+        return all(inf.wait_for_cache_sync(timeout_s) for inf in list(self._informers.values()))
+
+    def stop(self) -> None:
+        for inf in self._informers.values():
+            inf.stop()

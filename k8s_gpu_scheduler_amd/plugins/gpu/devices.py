@@ -1,0 +1,245 @@
+"""Device inventory and the per-device reservation ledger.
+
+The reference knows a node's devices only as a JSON list of UUIDs in Redis
+(reference pkg/profiler/cmd/client/client.go:70-76) and assumes one physical GPU per node
+(`<nUUIDs>P_<model>`).  An MI355X node has 8 GPUs, each optionally
+split into SPX/DPX/QPX/CPX compute partitions, so the inventory here is a list of
+`Device`s (physical index, partition index, CUs, HBM, NUMA), and the ledger accounts
+fractional use at **XCD granularity**: a GPU (or partition) is 8/P XCD "units" of 32 CUs
+each, a fractional pod gets a contiguous, naturally aligned run of units (buddy style),
+and its CU mask covers exactly those XCDs -- each co-located pod then owns its XCDs'
+private L2s instead of sharing them (MI355X has one 4 MiB L2 per XCD).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import threading
+from dataclasses import dataclass, field
+from typing import Any, Dict, Iterable, List, Optional, Tuple
+
+from ...api import constants as C
+from ...api import objects as O
+
+Obj = Dict[str, Any]
+CUS_PER_XCD = C.MI355X_CUS // C.MI355X_XCDS     # 32
+
+
+def synth_uuid(node: str, gpu: int, part: int = -1) -> str:
+    h = hashlib.md5(f"{node}/{gpu}/{part}".encode()).hexdigest()
+    u = f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:32]}"
+    return f"GPU-{u}" if part < 0 else f"GPU-{u}"
+
+
+@dataclass
+class Device:
+    uuid: str
+    node: str
+    gpu: int                    # physical GPU index on the node (0..7)
+    partition: int = 0          # partition index inside the GPU
+    partitions: int = 1         # partitions per GPU (SPX=1 .. CPX=8)
+    cus: int = C.MI355X_CUS
+    hbm_gib: float = float(C.MI355X_HBM_GIB)
+    numa: int = 0
+    model: str = C.MI355X
+    units: int = 0              # XCD units (32 CUs each)
+    first_xcd: int = 0          # first XCD of the GPU owned by this device
+
+    def __post_init__(self) -> None:
+        if not self.units:
+            self.units = max(1, self.cus // CUS_PER_XCD)
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"uuid": self.uuid, "gpu": self.gpu, "partition": self.partition, "partitions": self.partitions,
+                "cus": self.cus, "hbm_gib": self.hbm_gib, "numa": self.numa, "model": self.model,
+                "first_xcd": self.first_xcd}
+
+    @classmethod
+    def from_json(cls, node: str, d: Dict[str, Any]) -> "Device":
+        return cls(uuid=d["uuid"], node=node, gpu=int(d.get("gpu", 0)), partition=int(d.get("partition", 0)),
+                   partitions=int(d.get("partitions", 1)), cus=int(d.get("cus", C.MI355X_CUS)),
+                   hbm_gib=float(d.get("hbm_gib", C.MI355X_HBM_GIB)), numa=int(d.get("numa", 0)),
+                   model=d.get("model", C.MI355X), first_xcd=int(d.get("first_xcd", 0)))
+
+
+def devices_for_node(node: Obj, uuids: Optional[List[str]] = None,
+                     descriptors: Optional[List[Dict[str, Any]]] = None) -> List[Device]:
+    """Inventory of a node: from the agent's descriptors if published, else from the
+    node labels (GPU count + compute partition), with Redis UUIDs (reference schema)
+    assigned in order when given."""
+    nm = O.name(node)
+    if descriptors:
+        return [Device.from_json(nm, d) for d in descriptors]
+    gpus = O.node_gpu_count(node)
+    parts = O.node_partitions_per_gpu(node)
+    model = O.node_gpu_model(node) or C.MI355X
+    mem_parts = C.MEMORY_PARTITIONS.get(O.labels(node).get(C.LABEL_MEMORY_PARTITION, "NPS1"), 1)
+    out: List[Device] = []
+    i = 0
+    for g in range(gpus):
+        for p in range(parts):
+            u = uuids[i] if uuids and i < len(uuids) else synth_uuid(nm, g, p if parts > 1 else -1)
+            # NPS1: all partitions share the GPU's HBM; account an equal split so the
+            # ledger never over-commits it.
+            hbm = C.MI355X_HBM_GIB / max(parts, mem_parts)
+            out.append(Device(u, nm, g, p, parts, C.MI355X_CUS // parts, hbm,
+                              numa=0 if g < max(gpus // 2, 1) else 1, model=model,
+                              first_xcd=p * (C.MI355X_XCDS // parts)))
+            i += 1
+    if uuids and len(uuids) > len(out) and not gpus:
+        # Unlabelled node with UUIDs (reference-style): one device per UUID.
+        out = [Device(u, nm, k, 0, 1) for k, u in enumerate(uuids)]
+    return out
+
+
+def xcd_cu_mask(first_xcd: int, n_xcd: int, cus: int = C.MI355X_CUS, xcds: int = C.MI355X_XCDS) -> List[int]:
+    """CU mask (list of 32-bit words, bit i = logical CU i) selecting all CUs of XCDs
+    [first_xcd, first_xcd+n_xcd).  Logical CU ids are distributed round-robin over the
+    XCDs (CU i lives on XCD i % 8) -- the layout `ops.cumask.probe_xcd_map` verifies on
+    the device."""
+    bits = [0] * ((cus + 31) // 32)
+    for cu in range(cus):
+        if first_xcd <= cu % xcds < first_xcd + n_xcd:
+            bits[cu // 32] |= 1 << (cu % 32)
+    return bits
+
+
+def mask_to_hex(words: List[int]) -> str:
+    """HSA_CU_MASK style: 0x<hex> with word 0 least significant."""
+    v = 0
+    for i, w in enumerate(words):
+        v |= (w & 0xFFFFFFFF) << (32 * i)
+    return hex(v)
+
+
+@dataclass
+class PodUse:
+    key: str
+    name: str
+    slo: float
+    cu: int
+    hbm_gib: float
+    units: Tuple[int, int]       # (first unit, count) inside the device
+    whole: bool = False
+
+
+@dataclass
+class DeviceState:
+    device: Device
+    used_units: List[bool] = field(default_factory=list)
+    hbm_used: float = 0.0
+    pods: Dict[str, PodUse] = field(default_factory=dict)
+
+    def __post_init__(self) -> None:
+        if not self.used_units:
+            self.used_units = [False] * self.device.units
+
+    @property
+    def free_units(self) -> int:
+        return self.used_units.count(False)
+
+    @property
+    def hbm_free(self) -> float:
+        return self.device.hbm_gib - self.hbm_used
+
+    def find_units(self, n: int) -> Optional[int]:
+        """Best-fit aligned run of n free units (alignment = next pow2 >= n)."""
+        if n > len(self.used_units):
+            return None
+        align = 1
+        while align < n:
+            align *= 2
+        best, best_free_around = None, None
+        for s in range(0, len(self.used_units) - n + 1, align):
+            if not any(self.used_units[s:s + n]):
+                # prefer placements inside the most-used aligned block (less fragmentation)
+                blk = max(align * 2, 2)
+                b0 = (s // blk) * blk
+                free_in_blk = self.used_units[b0:b0 + blk].count(False)
+                if best is None or free_in_blk < best_free_around:
+                    best, best_free_around = s, free_in_blk
+        return best
+
+
+class DeviceLedger:
+    """Per-node device reservations, updated by Reserve/Unreserve and informer events.
+    Thread-safe; Score reads a consistent view under the lock."""
+
+    def __init__(self) -> None:
+        self._lock = threading.RLock()
+        self.nodes: Dict[str, Dict[str, DeviceState]] = {}
+        self.pod_index: Dict[str, Tuple[str, List[str]]] = {}     # pod key -> (node, uuids)
+        self.generation = 0
+
+    def set_devices(self, node: str, devices: Iterable[Device]) -> None:
+        with self._lock:
+            old = self.nodes.get(node, {})
+            new: Dict[str, DeviceState] = {}
+            for d in devices:
+                st = old.get(d.uuid)
+                if st is not None and st.device.units == d.units:
+                    st.device = d
+                    new[d.uuid] = st
+                else:
+                    new[d.uuid] = DeviceState(d)
+            self.nodes[node] = new
+            self.generation += 1
+
+    def devices(self, node: str) -> List[DeviceState]:
+        with self._lock:
+            return list(self.nodes.get(node, {}).values())
+
+    def has_node(self, node: str) -> bool:
+        return node in self.nodes
+
+    def reserve(self, node: str, pod_key: str, pod_name: str, slo: float,
+                allocs: List[Tuple[str, int, int, float, bool]]) -> bool:
+        """allocs: (uuid, first_unit, n_units, hbm_gib, whole).  All-or-nothing."""
+        with self._lock:
+            if pod_key in self.pod_index:
+                self.release(pod_key)
+            states = self.nodes.get(node, {})
+            for uuid, u0, n, hbm, whole in allocs:
+                st = states.get(uuid)
+                if st is None or any(st.used_units[u0:u0 + n]) or u0 + n > len(st.used_units):
+                    return False
+                if hbm > st.hbm_free + 1e-6:
+                    return False
+            for uuid, u0, n, hbm, whole in allocs:
+                st = states[uuid]
+                for u in range(u0, u0 + n):
+                    st.used_units[u] = True
+                st.hbm_used += hbm
+                st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole)
+            self.pod_index[pod_key] = (node, [a[0] for a in allocs])
+            self.generation += 1
+            return True
+
+    def release(self, pod_key: str) -> bool:
+        with self._lock:
+            ent = self.pod_index.pop(pod_key, None)
+            if ent is None:
+                return False
+            node, uuids = ent
+            for uuid in uuids:
+                st = self.nodes.get(node, {}).get(uuid)
+                if st is None:
+                    continue
+                use = st.pods.pop(pod_key, None)
+                if use is None:
+                    continue
+                u0, n = use.units
+                for u in range(u0, u0 + n):
+                    st.used_units[u] = False
+                st.hbm_used = max(0.0, st.hbm_used - use.hbm_gib)
+            self.generation += 1
+            return True
+
+    def placement(self, pod_key: str) -> Optional[Tuple[str, List[str]]]:
+        with self._lock:
+            return self.pod_index.get(pod_key)
+
+    def snapshot_json(self) -> str:
+        with self._lock:
+            return json.dumps({n: {u: {"free_units": s.free_units, "hbm_used": s.hbm_used, "pods": list(s.pods)}
+                                   for u, s in devs.items()} for n, devs in self.nodes.items()})

@@ -1,0 +1,465 @@
+"""The "GPU" scheduler plugin for MI355X nodes.
+
+Reference: `type GPU` implementing Score + NormalizeScore + PostBind
+(reference pkg/plugins/gpu_plugin/gpu_plugins.go:39-44,779-926).  Two modes:
+
+* ``mode: parity`` -- reproduces the reference behaviour exactly (`parity.ParityLogic`):
+  node model from the node name, UUIDs from Redis, residents' SLOs from their
+  ConfigMaps' CUDA_VISIBLE_DEVICES, one recommender RPC per lookup, shuffled UUIDs,
+  ConfigMap writes inside Score, A30 MIG reconfigure, random-UUID PostBind with MPS env.
+  Used to pass the SURVEY §2.7.4 parity vectors.
+
+* ``mode: fixed`` (default) -- the MI355X design, fixing SURVEY §2.9 #1-#10:
+  PreFilter parses the GPU request (whole GPUs / partitions, or fractional CUs + HBM);
+  Filter checks per-device capacity in the ledger (XCD-granular CU units + HBM) and, for
+  multi-GPU pods, an xGMI clique (`topology.select_gpu_set`); PreScore fetches the
+  incoming pod's predictions once; Score evaluates every candidate device with the
+  reference's SLO/interference objective (`scoring.device_score`, native C++ batch
+  core) blended with XCD-packing and live telemetry terms -- no I/O, no side effects;
+  NormalizeScore is the reference's min-max; Reserve/Unreserve commit the device choice
+  to the ledger; PreBind writes the device env (ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES,
+  HSA_CU_MASK, HBM cap; reference CUDA_* keys with `compatEnv`) into the pod's envFrom
+  ConfigMaps and annotations *before* bind, so the container starts with it (§2.9 #7).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import threading
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from ...api import constants as C
+from ...api import objects as O
+from ...framework.interface import (CycleState, FilterPlugin, NodeScore, PostBindPlugin, PreBindPlugin,
+                                    PreFilterPlugin, PreScorePlugin, ReservePlugin, ScoreExtensions, ScorePlugin,
+                                    Status, min_max_normalize)
+from ...kube.resources import Resources
+from ...recommender.client import CachedPredictions, PredictionProvider, RecommenderClient, RpcPredictions
+from ...telemetry.cache import TelemetryCache
+from .devices import CUS_PER_XCD, Device, DeviceLedger, DeviceState, devices_for_node, mask_to_hex, xcd_cu_mask
+from .scoring import Resident, score_devices
+from .topology import Topology, select_gpu_set
+
+log = logging.getLogger(__name__)
+Obj = Dict[str, Any]
+
+_REQ = "GPU/request"
+_PRED = "GPU/predictions"
+_CHOICE = "GPU/choice"
+
+
+@dataclass
+class GpuRequest:
+    whole: int = 0          # whole devices (GPUs or partitions)
+    units: int = 0          # XCD units for a fractional pod
+    cu: int = 0
+    hbm_gib: float = 0.0
+    slo: float = 0.0
+    gpu_pod: bool = False
+
+
+@dataclass
+class Choice:
+    node: str
+    allocs: List[Tuple[str, int, int, float, bool]] = field(default_factory=list)  # uuid,u0,n,hbm,whole
+    score: float = 0.0
+    devices: List[Device] = field(default_factory=list)
+
+
+@dataclass
+class GPUArgs:
+    mode: str = "fixed"
+    w_slo: float = 1.0
+    w_pack: float = 1.0
+    w_telemetry: float = 0.5
+    pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated)
+    model: str = C.MI355X
+    default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
+    compat_env: bool = True
+    predictions: str = "cache"        # cache | rpc | none
+    recommender: str = ""
+    redis: str = ""
+    redis_password: str = C.REDIS_PASSWORD
+    prometheus: str = ""
+    parity_master: str = ""
+    parity_reconfigure: bool = True
+    reconfigure_timeout_s: float = 60.0
+    parity_shuffle: bool = True
+    seed: Optional[int] = None
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "GPUArgs":
+        a = cls()
+        alias = {"weightSLO": "w_slo", "weightPack": "w_pack", "weightTelemetry": "w_telemetry",
+                 "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
+                 "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
+                 "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle"}
+        for k, v in (d or {}).items():
+            k = alias.get(k, k)
+            if hasattr(a, k):
+                setattr(a, k, v)
+        return a
+
+
+class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, ScoreExtensions, ReservePlugin,
+                PreBindPlugin, PostBindPlugin):
+    NAME = C.PLUGIN_NAME
+
+    def __init__(self, args: Optional[Dict[str, Any]] = None, handle: Any = None,
+                 predictions: Optional[PredictionProvider] = None, redis: Any = None,
+                 telemetry: Optional[TelemetryCache] = None, ledger: Optional[DeviceLedger] = None):
+        self.args = GPUArgs.from_dict(args or {})
+        self.handle = handle
+        extras = getattr(handle, "extras", {}) if handle is not None else {}
+        self.telemetry = telemetry or extras.get("telemetry") or TelemetryCache()
+        self.ledger = ledger or extras.get("ledger") or DeviceLedger()
+        self.redis = redis if redis is not None else extras.get("redis")
+        self.predictions = predictions or extras.get("predictions")
+        self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
+        self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
+        self._lock = threading.RLock()
+        self._client: Optional[RecommenderClient] = None
+        self.SCORE_DOES_IO = self.args.mode == "parity"
+        if self.predictions is None and self.args.recommender and self.args.predictions != "none":
+            self._client = RecommenderClient(self.args.recommender)
+            self.predictions = (RpcPredictions(self._client) if self.args.predictions == "rpc"
+                                else CachedPredictions(self._client))
+        if self.redis is None and self.args.redis:
+            from ...store.resp import Redis
+            self.redis = Redis.connect(self.args.redis, self.args.redis_password)
+        self.parity = None
+        if self.args.mode == "parity":
+            from .parity import ParityLogic
+            self.parity = ParityLogic(self)
+        if handle is not None:
+            self._wire_informers()
+
+    # ------------------------------------------------------------------ wiring
+    def _wire_informers(self) -> None:
+        try:
+            inf = self.handle.informer_factory
+        except AttributeError:
+            return
+        inf.nodes().add_event_handler(self._on_node, lambda o, n: self._on_node(n), None)
+        inf.pods().add_event_handler(self._on_pod, lambda o, n: self._on_pod(n), self._on_pod_delete)
+
+    def _on_node(self, node: Obj) -> None:
+        name = O.name(node)
+        uuids, descs = None, None
+        if self.redis is not None:
+            try:
+                from ...store import schema
+                uuids = schema.read_uuids(self.redis, name)
+                descs = schema.read_devices(self.redis, name)
+                topo = self.redis.get_or(schema.topology_key(name))
+                if topo:
+                    self.topologies[name] = Topology.from_json(json.loads(topo))
+            except Exception as e:
+                log.debug("redis inventory for %s unavailable: %s", name, e)
+        devs = devices_for_node(node, uuids, descs)
+        self.ledger.set_devices(name, devs)
+        if name not in self.topologies:
+            n_gpu = max((d.gpu for d in devs), default=-1) + 1
+            if n_gpu:
+                self.topologies[name] = Topology.fully_connected(n_gpu)
+
+    def _on_pod(self, pod: Obj) -> None:
+        """Rebuild reservations of assigned pods from their annotations (scheduler restart
+        recovery) and release finished ones."""
+        if O.is_terminal(pod):
+            self.ledger.release(O.key(pod))
+            return
+        node = O.node_name_of(pod)
+        ann = O.annotations(pod).get(C.ANNOT_DEVICES)
+        if not node or not ann or self.ledger.placement(O.key(pod)) is not None:
+            return
+        try:
+            allocs = json.loads(O.annotations(pod).get(C.ANNOT_DEVICE_INDICES, "[]"))
+            allocs = [tuple(a) for a in allocs]
+        except json.JSONDecodeError:
+            return
+        if allocs:
+            self.ledger.reserve(node, O.key(pod), O.name(pod), O.pod_slo(pod), allocs)
+
+    def _on_pod_delete(self, pod: Obj) -> None:
+        self.ledger.release(O.key(pod))
+
+    # ------------------------------------------------------------------ request
+    def parse_request(self, pod: Obj) -> GpuRequest:
+        g, cu, mem = O.gpu_request(pod)
+        slo = O.pod_slo(pod)
+        r = GpuRequest(slo=slo, hbm_gib=mem)
+        if cu > 0:
+            r.cu = min(cu, C.MI355X_CUS)
+            r.units = max(1, math.ceil(r.cu / CUS_PER_XCD))
+            r.gpu_pod = True
+        elif g > 0:
+            r.whole = g
+            r.gpu_pod = True
+        elif mem > 0 or slo > 0:
+            r.cu = self.args.default_cu
+            r.units = max(1, math.ceil(r.cu / CUS_PER_XCD))
+            r.gpu_pod = True
+        # round fractional units up to a power of two (aligned XCD groups)
+        if r.units:
+            p = 1
+            while p < r.units:
+                p *= 2
+            r.units = min(p, C.MI355X_XCDS)
+            r.cu = r.units * CUS_PER_XCD
+        return r
+
+    # ------------------------------------------------------------------ extension points
+    def pre_filter(self, state: CycleState, pod: Obj) -> Optional[Status]:
+        if self.parity is not None:
+            return None
+        req = self.parse_request(pod)
+        state.write(_REQ, req)
+        if not req.gpu_pod:
+            return Status.skip()
+        return None
+
+    def filter(self, state: CycleState, pod: Obj, node_info: Any) -> Optional[Status]:
+        if self.parity is not None:
+            return None
+        req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
+        node = node_info.node
+        if any(t.get("key") == C.TAINT_PARTITIONING for t in O.node_taints(node)):
+            return Status.unschedulable("node is being re-partitioned", self.NAME)
+        if not self.ledger.has_node(node_info.name):
+            self._on_node(node)
+        choice = self._best_choice(state, pod, req, node_info.name, scoring=False)
+        if choice is None:
+            return Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME)
+        return None
+
+    def pre_score(self, state: CycleState, pod: Obj, nodes: List[Any]) -> Optional[Status]:
+        if self.parity is not None:
+            return None
+        req: GpuRequest = state.read(_REQ)
+        if req is None or not req.gpu_pod:
+            return Status.skip()
+        state.write(_PRED, self._pod_predictions(O.name(pod)))
+        state.write(_CHOICE, {})
+        return None
+
+    def score(self, state: CycleState, pod: Obj, node_name: str) -> Tuple[int, Optional[Status]]:
+        if self.parity is not None:
+            try:
+                return self.parity.logic(node_name, pod), None
+            except Exception as e:
+                return 0, Status.error(f"Error in Logic() in Score(): {e}", self.NAME)
+        req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
+        choice = self._best_choice(state, pod, req, node_name, scoring=True)
+        if choice is None:
+            return 0, None
+        choices = state.read(_CHOICE)
+        if choices is None:
+            choices = {}
+            state.write(_CHOICE, choices)
+        choices[node_name] = choice
+        return max(C.MIN_NODE_SCORE, min(C.MAX_NODE_SCORE, int(choice.score))), None
+
+    def score_extensions(self) -> ScoreExtensions:
+        return self
+
+    def normalize_score(self, state: CycleState, pod: Obj, scores: List[NodeScore]) -> Optional[Status]:
+        min_max_normalize(scores)
+        return None
+
+    def reserve(self, state: CycleState, pod: Obj, node_name: str) -> Optional[Status]:
+        if self.parity is not None:
+            return None
+        req: GpuRequest = state.read(_REQ)
+        if req is None or not req.gpu_pod:
+            return None
+        choice = (state.read(_CHOICE) or {}).get(node_name)
+        if choice is None:
+            choice = self._best_choice(state, pod, req, node_name, scoring=True)
+        if choice is None or not self.ledger.reserve(node_name, O.key(pod), O.name(pod), req.slo, choice.allocs):
+            return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
+        state.write(_CHOICE + "/reserved", choice)
+        return None
+
+    def unreserve(self, state: CycleState, pod: Obj, node_name: str) -> None:
+        if self.parity is not None:
+            return
+        self.ledger.release(O.key(pod))
+
+    def pre_bind(self, state: CycleState, pod: Obj, node_name: str) -> Optional[Status]:
+        if self.parity is not None:
+            return None
+        choice: Optional[Choice] = state.read(_CHOICE + "/reserved")
+        if choice is None:
+            return None
+        env = self.device_env(choice)
+        ann = {C.ANNOT_DEVICES: ",".join(a[0] for a in choice.allocs),
+               C.ANNOT_DEVICE_INDICES: json.dumps([list(a) for a in choice.allocs]),
+               C.ANNOT_CU_MASK: env.get(C.ENV_CU_MASK, "")}
+        res = Resources(self.handle.client, O.namespace(pod))
+        try:
+            res.annotate_pod(O.name(pod), ann)
+            res.append_to_existing_config_maps_in_pod(O.name(pod), env, True, pod=pod)
+        except Exception as e:
+            return Status.error(f"PreBind: writing device assignment failed: {e}", self.NAME)
+        state.write("GPU/env", env)
+        return None
+
+    def post_bind(self, state: CycleState, pod: Obj, node_name: str) -> None:
+        if self.parity is not None:
+            self.parity.post_bind(pod, node_name)
+
+    def close(self) -> None:
+        if self._client is not None:
+            self._client.close()
+
+    # ------------------------------------------------------------------ env
+    def device_env(self, choice: Choice) -> Dict[str, str]:
+        devs = {d.uuid: d for d in choice.devices}
+        uuids = [a[0] for a in choice.allocs]
+        idx = [str(devs[u].gpu) if u in devs else "" for u in uuids]
+        env = {C.ENV_ROCR_VISIBLE: ",".join(uuids), C.ENV_HIP_VISIBLE: ",".join(i for i in idx if i)}
+        frac = [a for a in choice.allocs if not a[4]]
+        if frac:
+            u, u0, n, hbm, _ = frac[0]
+            d = devs.get(u)
+            first = (d.first_xcd if d else 0) + u0
+            env[C.ENV_CU_MASK] = f"{idx[0] or 0}:{mask_to_hex(xcd_cu_mask(first, n))}"
+            env[C.ENV_HBM_LIMIT] = f"{hbm:g}"
+        if self.args.compat_env:
+            env[C.ENV_CUDA_VISIBLE] = env[C.ENV_ROCR_VISIBLE]
+            if frac:
+                n = frac[0][2]
+                env[C.ENV_MPS_THREADS] = str(int(100 * n / C.MI355X_XCDS))
+                env[C.ENV_MPS_MEM] = f"0={int(frac[0][3] * 1024)}MB" if frac[0][3] else ""
+            else:
+                env[C.ENV_MPS_THREADS] = ""
+                env[C.ENV_MPS_MEM] = ""
+        return env
+
+    # ------------------------------------------------------------------ predictions
+    def _pod_predictions(self, name: str) -> Tuple[Dict[str, float], Dict[str, float]]:
+        if self.predictions is None:
+            return {}, {}
+        with self._lock:
+            hit = self._resident_memo.get(name)
+        if hit is not None:
+            return hit
+        try:
+            conf = self.predictions.configurations(name)
+            intf = self.predictions.interference(f"{name}_{self.args.model}")
+        except Exception as e:  # recommender down -> degrade to packing/telemetry
+            log.debug("predictions for %s unavailable: %s", name, e)
+            return {}, {}
+        with self._lock:
+            if len(self._resident_memo) > 65536:
+                self._resident_memo.clear()
+            self._resident_memo[name] = (conf, intf)
+        return conf, intf
+
+    # ------------------------------------------------------------------ device choice
+    def _col(self, units: int, dev_units: int) -> str:
+        p = max(1, dev_units // max(units, 1))
+        return f"{p}P_{self.args.model}"
+
+    def _residents(self, st: DeviceState) -> List[Resident]:
+        out = []
+        for use in st.pods.values():
+            conf, intf = self._pod_predictions(use.name)
+            col = self._col(use.units[1], st.device.units)
+            out.append(Resident(use.name, use.slo, conf, intf, col))
+        return out
+
+    def _best_choice(self, state: CycleState, pod: Obj, req: GpuRequest, node: str,
+                     scoring: bool) -> Optional[Choice]:
+        states = self.ledger.devices(node)
+        if not states:
+            return None
+        if req.whole:
+            return self._whole_choice(req, node, states)
+        cands: List[Tuple[DeviceState, int]] = []
+        for st in states:
+            if st.hbm_free + 1e-6 < req.hbm_gib:
+                continue
+            u0 = st.find_units(req.units)
+            if u0 is None:
+                continue
+            cands.append((st, u0))
+        if not cands:
+            return None
+        if not scoring:
+            st, u0 = cands[0]
+            return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], 0.0, [st.device])
+        a = self.args
+        name = O.name(pod)
+        conf, intf = state.read(_PRED) or self._pod_predictions(name)
+        slo_scores: List[Optional[float]] = [None] * len(cands)
+        if a.w_slo and req.slo > 0 and conf:
+            residents = [self._residents(st) for st, _ in cands]
+            preds, cols = [], []
+            for st, _ in cands:
+                col = self._col(req.units, st.device.units)
+                cols.append(col)
+                preds.append(conf.get(col, -1.0))
+            # one batch per distinct (column) -- typically all candidates share it
+            for col in set(cols):
+                ids = [i for i, c in enumerate(cols) if c == col]
+                vals = score_devices([residents[i] for i in ids], name, req.slo,
+                                     preds[ids[0]] if preds[ids[0]] is not None else -1.0, intf, col)
+                for i, v in zip(ids, vals):
+                    slo_scores[i] = v
+        best: Optional[Choice] = None
+        for i, (st, u0) in enumerate(cands):
+            parts: List[Tuple[float, float]] = []
+            if slo_scores[i] is not None:
+                parts.append((a.w_slo, slo_scores[i]))
+            if a.w_pack:
+                gpu_units = [s for s in states if s.device.gpu == st.device.gpu]
+                tot = sum(s.device.units for s in gpu_units)
+                used = sum(s.device.units - s.free_units for s in gpu_units) + req.units
+                frac = used / max(tot, 1)
+                pk = 100.0 * frac if a.pack == "binpack" else 100.0 * (1.0 - frac)
+                parts.append((a.w_pack, pk))
+            if a.w_telemetry:
+                smp = self.telemetry.get(node, st.device.uuid)
+                if smp is not None:
+                    hbm_ok = 1.0 if smp.vram_total_mb - smp.vram_used_mb >= req.hbm_gib * 1024 else 0.0
+                    parts.append((a.w_telemetry, 100.0 * (1.0 - min(1.0, smp.gfx_activity)) * hbm_ok))
+            wsum = sum(w for w, _ in parts)
+            sc = sum(w * v for w, v in parts) / wsum if wsum > 0 else 0.0
+            if best is None or sc > best.score:
+                best = Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], sc, [st.device])
+        return best
+
+    def _whole_choice(self, req: GpuRequest, node: str, states: List[DeviceState]) -> Optional[Choice]:
+        free = [st for st in states if not st.pods and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)]
+        if len(free) < req.whole:
+            return None
+        per = req.hbm_gib / max(req.whole, 1)
+        parts = states[0].device.partitions
+        if req.whole == 1 or parts > 1:
+            # single device (or partitions): least-fragmenting = GPU with most used devices
+            used_per_gpu: Dict[int, int] = {}
+            for st in states:
+                if st.pods:
+                    used_per_gpu[st.device.gpu] = used_per_gpu.get(st.device.gpu, 0) + 1
+            free.sort(key=lambda s: (-used_per_gpu.get(s.device.gpu, 0), s.device.gpu, s.device.partition))
+            pick = free[:req.whole]
+            sc = 100.0 * (1.0 if req.whole == 1 else 0.8)
+            return Choice(node, [(s.device.uuid, 0, s.device.units, per, True) for s in pick], sc,
+                          [s.device for s in pick])
+        topo = self.topologies.get(node) or Topology.fully_connected(max(s.device.gpu for s in states) + 1)
+        by_gpu = {st.device.gpu: st for st in free}
+        sel = select_gpu_set(topo, list(by_gpu), req.whole)
+        if sel is None:
+            return None
+        gpus, quality = sel
+        pick = [by_gpu[g] for g in gpus]
+        return Choice(node, [(s.device.uuid, 0, s.device.units, per, True) for s in pick], 100.0 * quality,
+                      [s.device for s in pick])
+
+
+def register(registry: Any) -> None:
+    registry.register(C.PLUGIN_NAME, lambda args, handle: GPUPlugin(args, handle))

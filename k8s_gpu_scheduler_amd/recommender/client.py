@@ -1,0 +1,158 @@
+"""Recommender clients and the scheduler-side prediction providers.
+
+* `RecommenderClient` -- the Go wrappers `ImputeConfigurations(url, index)` /
+  `ImputeInterference(url, index)` (reference pkg/recommender/go_client/pkg/client_call.go:11-37)
+  but with one persistent channel and a deadline (the reference dials per call,
+  SURVEY §2.9 #9).
+* `PredictionProvider` -- what the GPU plugin consumes: `configurations(name)` /
+  `interference(name)` -> {column: value}.
+  - `RpcPredictions`: one RPC per lookup (parity mode; same call pattern as the
+    reference's Score).
+  - `CachedPredictions`: the whole completed matrices are pulled once per model version
+    (ExportTable) or computed in-process from a `TrainedTable`; a lookup is then a dict
+    hit + the reference's substring row match, memoised per request string.  Score does
+    zero I/O (SURVEY §6.3 "the bar the MI355X build beats").
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+import grpc
+
+from . import proto as P
+from .tables import TrainedTable, find_index_for_request
+
+
+class RecommenderClient:
+    def __init__(self, addr: str, timeout_s: float = 1.0, new_channel_per_call: bool = False):
+        self.addr, self.timeout_s = addr, timeout_s
+        self.new_channel_per_call = new_channel_per_call
+        self._ch: Optional[grpc.Channel] = None
+        self._lock = threading.Lock()
+
+    def _channel(self) -> grpc.Channel:
+        with self._lock:
+            if self._ch is None:
+                self._ch = grpc.insecure_channel(self.addr)
+            return self._ch
+
+    def _call(self, method: str, req: Any) -> Any:
+        if self.new_channel_per_call:
+            with grpc.insecure_channel(self.addr) as ch:
+                return P.stub_method(ch, method)(req, timeout=self.timeout_s)
+        return P.stub_method(self._channel(), method)(req, timeout=self.timeout_s)
+
+    def impute_configurations(self, index: str) -> Any:
+        return self._call(f"/{P.SERVICE}/ImputeConfigurations", P.Request(index=index))
+
+    def impute_interference(self, index: str) -> Any:
+        return self._call(f"/{P.SERVICE}/ImputeInterference", P.Request(index=index))
+
+    def export_table(self, table: str) -> Any:
+        return self._call(f"/{P.EXT_SERVICE}/ExportTable", P.TableRequest(table=table))
+
+    def recommend_resources(self, pod: str, cu: int, hbm_gib: float, slo: float) -> Any:
+        return self._call(f"/{P.EXT_SERVICE}/RecommendResources",
+                          P.ResizeRequest(pod=pod, requested_cu=cu, requested_hbm_gib=hbm_gib, slo=slo))
+
+    def version(self) -> Any:
+        return self._call(f"/{P.EXT_SERVICE}/Version", P.Empty())
+
+    def close(self) -> None:
+        with self._lock:
+            if self._ch is not None:
+                self._ch.close()
+                self._ch = None
+
+
+def reply_to_map(reply: Any) -> Dict[str, float]:
+    """zip(columns, result) like reference gpu_plugins.go:322-325 (an unknown index reply
+    has result=[0] and no columns -> empty map)."""
+    return {c: float(v) for c, v in zip(reply.columns, reply.result)}
+
+
+class PredictionProvider:
+    def configurations(self, name: str) -> Dict[str, float]:
+        raise NotImplementedError
+
+    def interference(self, name: str) -> Dict[str, float]:
+        raise NotImplementedError
+
+
+class RpcPredictions(PredictionProvider):
+    def __init__(self, client: RecommenderClient):
+        self.client = client
+        self.calls = 0
+
+    def configurations(self, name: str) -> Dict[str, float]:
+        self.calls += 1
+        return reply_to_map(self.client.impute_configurations(name))
+
+    def interference(self, name: str) -> Dict[str, float]:
+        self.calls += 1
+        return reply_to_map(self.client.impute_interference(name))
+
+
+class _Tab:
+    def __init__(self, index: List[str], columns: List[str], rows: List[List[float]], version: str):
+        self.index, self.columns, self.version = index, columns, version
+        self.by_label = {lab: dict(zip(columns, vals)) for lab, vals in zip(index, rows)}
+        self.memo: Dict[str, Dict[str, float]] = {}
+
+    def lookup(self, request: str) -> Dict[str, float]:
+        hit = self.memo.get(request)
+        if hit is not None:
+            return hit
+        lab = find_index_for_request(request.replace("-", "_"), self.index)
+        out = self.by_label.get(lab, {}) if lab else {}
+        self.memo[request] = out
+        return out
+
+
+class CachedPredictions(PredictionProvider):
+    """In-process, zero-I/O predictions.  Source: a RecommenderClient (ExportTable,
+    refreshed when `refresh()` sees a new version) or local TrainedTables."""
+
+    def __init__(self, client: Optional[RecommenderClient] = None,
+                 conf: Optional[TrainedTable] = None, intf: Optional[TrainedTable] = None,
+                 refresh_s: float = 30.0):
+        self.client = client
+        self.refresh_s = refresh_s
+        self._last = 0.0
+        self._conf: Optional[_Tab] = None
+        self._intf: Optional[_Tab] = None
+        if conf is not None:
+            self._conf = _Tab(conf.table.index, conf.table.columns, conf.completed().tolist(), conf.version)
+        if intf is not None:
+            self._intf = _Tab(intf.table.index, intf.table.columns, intf.completed().tolist(), intf.version)
+        if client is not None:
+            self.refresh(force=True)
+
+    def refresh(self, force: bool = False) -> None:
+        if self.client is None:
+            return
+        now = time.monotonic()
+        if not force and now - self._last < self.refresh_s:
+            return
+        self._last = now
+        for name in ("configurations", "interference"):
+            t = self.client.export_table(name)
+            cur = self._conf if name == "configurations" else self._intf
+            if cur is not None and cur.version == t.version:
+                continue
+            tab = _Tab([r.index for r in t.rows], list(t.columns), [list(r.values) for r in t.rows], t.version)
+            if name == "configurations":
+                self._conf = tab
+            else:
+                self._intf = tab
+
+    def configurations(self, name: str) -> Dict[str, float]:
+        return self._conf.lookup(name) if self._conf else {}
+
+    def interference(self, name: str) -> Dict[str, float]:
+        return self._intf.lookup(name) if self._intf else {}
+
+    def tables(self) -> "tuple[Optional[_Tab], Optional[_Tab]]":
+        return self._conf, self._intf

@@ -1,0 +1,181 @@
+"""Recommender gRPC server.
+
+Behaviour of the reference server (reference pkg/recommender/recom_server.py):
+* env CONFIGURATIONS_DATA_PATH / INTERFERENCE_DATA_PATH / PORT (50051) / JOB_DELAY (30)
+  (:30-52);
+* fit one imputer per matrix at start (:215-235), retrain in the background when the
+  file's md5 changes (:74-134), swap the new model in (:141-148);
+* RPC: `-`→`_`, first row label that is a substring, impute that row, reply
+  (values, column names); unknown index or no model -> result=[0], columns=[]
+  (:150-170).
+
+Fixes: existence is checked before hashing, the swap is under a lock
+(§5.2 race), the retrain loop survives exceptions, the thread pool size is configurable.
+Extensions (separate `gpusched.recommender.Extended` service): ExportTable (completed
+matrices for the scheduler's in-process cache), RecommendResources (resize from
+Redis history), Version.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+from concurrent import futures
+from typing import Any, Callable, Dict, Optional
+
+import grpc
+
+from ..api import constants as C
+from . import proto as P
+from .resize import recommend
+from .tables import Table, TrainedTable, file_version
+
+log = logging.getLogger(__name__)
+
+DEFAULT_CONF = "configurations_train.ods"
+DEFAULT_INTF = "interference_train.ods"
+
+
+class ModelSlot:
+    """One matrix + model with md5-driven hot reload and a locked swap."""
+
+    def __init__(self, name: str, path: str, kind: str = "iterative", **model_kw: Any):
+        self.name, self.path, self.kind, self.model_kw = name, path, kind, model_kw
+        self._lock = threading.Lock()
+        self.current: Optional[TrainedTable] = None
+        self.version: Optional[str] = None
+
+    def load_if_changed(self) -> bool:
+        v = file_version(self.path)
+        if v is None:
+            log.info("%s: train data not found at %s", self.name, self.path)
+            return False
+        if v == self.version:
+            return False
+        trained = TrainedTable.fit(Table.read_tsv(self.path), self.kind, v, **self.model_kw)
+        with self._lock:
+            self.current, self.version = trained, v
+        log.info("%s: trained version %s (%d x %d)", self.name, v[:8], len(trained.table.index),
+                 len(trained.table.columns))
+        return True
+
+    def set_table(self, table: Table, version: str = "mem") -> None:
+        trained = TrainedTable.fit(table, self.kind, version, **self.model_kw)
+        with self._lock:
+            self.current, self.version = trained, version
+
+    def get(self) -> Optional[TrainedTable]:
+        with self._lock:
+            return self.current
+
+
+class RecommenderService:
+    def __init__(self, configurations_path: str = "", interference_path: str = "",
+                 kind: str = "iterative", job_delay_s: float = C.RECOMMENDER_JOB_DELAY_S,
+                 history_source: Optional[Callable[[str], Any]] = None, model: str = "MI355X"):
+        self.conf = ModelSlot("configurations", configurations_path, kind)
+        self.intf = ModelSlot("interference", interference_path, kind)
+        self.job_delay_s = job_delay_s
+        self.history_source = history_source
+        self.model = model
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.calls = 0
+
+    @classmethod
+    def from_env(cls, **kw: Any) -> "RecommenderService":
+        return cls(os.getenv("CONFIGURATIONS_DATA_PATH", DEFAULT_CONF),
+                   os.getenv("INTERFERENCE_DATA_PATH", DEFAULT_INTF),
+                   job_delay_s=float(os.getenv("JOB_DELAY", C.RECOMMENDER_JOB_DELAY_S)), **kw)
+
+    # ------------------------------------------------------------------ training loop
+    def train(self) -> None:
+        for slot in (self.conf, self.intf):
+            try:
+                slot.load_if_changed()
+            except Exception as e:
+                log.warning("%s: training failed: %s", slot.name, e)
+
+    def start_retrain_loop(self) -> None:
+        def loop() -> None:
+            while not self._stop.wait(self.job_delay_s):
+                self.train()
+        self._thread = threading.Thread(target=loop, daemon=True, name="recommender-retrain")
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    # ------------------------------------------------------------------ RPC logic
+    @staticmethod
+    def _impute(slot: ModelSlot, index: str) -> Any:
+        self_reply = P.Reply()
+        t = slot.get()
+        if t is None:
+            self_reply.result.append(0)
+            return self_reply
+        res = t.lookup(index)
+        if not res:
+            self_reply.result.append(0)
+            return self_reply
+        return P.set_protobuf_reply(list(res.values()), list(res.keys()), self_reply)
+
+    def ImputeConfigurations(self, request: Any, context: Any) -> Any:
+        self.calls += 1
+        return self._impute(self.conf, request.index)
+
+    def ImputeInterference(self, request: Any, context: Any) -> Any:
+        self.calls += 1
+        return self._impute(self.intf, request.index)
+
+    def ExportTable(self, request: Any, context: Any) -> Any:
+        slot = self.conf if request.table in ("", "configurations") else self.intf
+        out = P.Table()
+        t = slot.get()
+        if t is None:
+            return out
+        full = t.completed()
+        out.columns.extend(t.table.columns)
+        out.version = t.version or ""
+        for lab, vals in zip(t.table.index, full):
+            r = out.rows.add()
+            r.index = lab
+            r.values.extend(float(v) for v in vals)
+        return out
+
+    def RecommendResources(self, request: Any, context: Any) -> Any:
+        hist = self.history_source(request.pod) if self.history_source else []
+        t = self.conf.get()
+        conf = t.lookup(request.pod) if t is not None else None
+        adv = recommend(hist or [], request.requested_cu or 256, request.requested_hbm_gib or 0.0,
+                        request.slo, conf, self.model)
+        return P.ResizeReply(recommended_cu=adv.cu, recommended_hbm_gib=adv.hbm_gib, samples=adv.samples,
+                             reason=adv.reason)
+
+    def Version(self, request: Any, context: Any) -> Any:
+        return P.VersionReply(configurations=self.conf.version or "", interference=self.intf.version or "",
+                              model=self.conf.kind)
+
+    # ------------------------------------------------------------------ server
+    def make_server(self, port: int = C.RECOMMENDER_PORT, workers: int = C.RECOMMENDER_WORKERS,
+                    host: str = "[::]") -> "tuple[grpc.Server, int]":
+        server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers))
+        server.add_generic_rpc_handlers((
+            P.generic_handler(P.SERVICE, {"ImputeConfigurations": self.ImputeConfigurations,
+                                          "ImputeInterference": self.ImputeInterference}),
+            P.generic_handler(P.EXT_SERVICE, {"ExportTable": self.ExportTable,
+                                              "RecommendResources": self.RecommendResources,
+                                              "Version": self.Version}),
+        ))
+        bound = server.add_insecure_port(f"{host}:{port}")
+        server.start()
+        return server, bound
+
+
+def serve(port: int = C.RECOMMENDER_PORT, workers: int = C.RECOMMENDER_WORKERS) -> None:
+    svc = RecommenderService.from_env()
+    svc.train()
+    svc.start_retrain_loop()
+    server, bound = svc.make_server(port, workers)
+    log.info("recommender listening on %d", bound)
+    server.wait_for_termination()
