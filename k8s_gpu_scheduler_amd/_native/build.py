@@ -1,0 +1,95 @@
+"""Build the native extension modules in-tree (gfx950 only).
+
+  _core  native/core/*.cpp   host C++ (g++)            scoring core
+  _smi   native/smi/*.cpp    host C++ + libamd_smi     telemetry / topology / partitions
+  _hip   native/hip/*        hipcc --offload-arch=gfx950  device query, CU-masked streams,
+                                                        MFMA/HBM load kernels, xGMI probes
+
+`python -m k8s_gpu_scheduler_amd._native.build [--force] [--asan]` (also called by
+`__graft_entry__.build()`).  Outputs land next to this file so they travel with the repo
+snapshot to the GPU box.  `--asan` builds the host-only modules with
+-fsanitize=address,undefined (host sanitizers only; GPU ASan is not used).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+NATIVE = os.path.join(REPO, "native")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes() -> List[str]:
+    import pybind11
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _targets(asan: bool = False) -> List[Tuple[str, List[str], List[str]]]:
+    inc = _py_includes()
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"] if asan else []
+    core_src = sorted(glob.glob(os.path.join(NATIVE, "core", "*.cpp")))
+    smi_src = sorted(glob.glob(os.path.join(NATIVE, "smi", "*.cpp")))
+    hip_src = sorted(glob.glob(os.path.join(NATIVE, "hip", "*.hip")) + glob.glob(os.path.join(NATIVE, "hip", "*.cpp")))
+    out = [
+        ("_core", core_src, ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", *san, *inc, *core_src]),
+        ("_smi", smi_src, ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *san, *inc, f"-I{ROCM}/include",
+                           *smi_src, f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib", "-pthread"]),
+        ("_hip", hip_src, [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17",
+                           "-shared", "-fPIC", *inc, *hip_src, f"-Wl,-rpath,{ROCM}/lib"]),
+    ]
+    return out
+
+
+def _stale(out: str, srcs: List[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    deps = srcs + glob.glob(os.path.join(NATIVE, "**", "*.h"), recursive=True)
+    mt = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > mt for s in deps)
+
+
+def build(force: bool = False, asan: bool = False, only: Tuple[str, ...] = (), verbose: bool = False) -> List[str]:
+    built = []
+    jobs = []
+    for name, srcs, cmd in _targets(asan):
+        if only and name not in only:
+            continue
+        out = os.path.join(HERE, name + ("_asan" if asan else "") + EXT)
+        if not force and not _stale(out, srcs):
+            continue
+        jobs.append((name, out, cmd + ["-o", out + ".tmp"]))
+
+    def run(job):
+        name, out, cmd = job
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        if p.returncode != 0:
+            raise RuntimeError(f"building {name} failed:\n{p.stderr[-4000:]}")
+        os.replace(out + ".tmp", out)
+        return out
+
+    with ThreadPoolExecutor(max(1, len(jobs))) as ex:
+        built = list(ex.map(run, jobs))
+    return built
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asan", action="store_true")
+    ap.add_argument("--only", nargs="*", default=[])
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    for p in build(a.force, a.asan, tuple(a.only), a.verbose):
+        print("built", p)

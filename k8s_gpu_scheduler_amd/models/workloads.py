@@ -1,0 +1,147 @@
+"""Synthetic pod workloads (the "model families" the scheduler places).
+
+The reference characterises 18 MLPerf-style inference workloads -- {onnx, tensorflow} x
+{mobilenet, resnet50, ssd_mobilenet} x batch {1024, 2048, 4096} -- only through their
+measured throughput per GPU share (reference
+pkg/recommender/recommender/configurations_train.ods) and pairwise interference
+(interference_train.ods).  There are no model binaries to run here, so each workload is
+re-created as a kernel mix with the same *character* on MI355X, built from the native
+load kernels (ops.loadgen):
+
+  resnet50       compute-bound: a chain of bf16 MFMA GEMMs (+bias+ReLU fused)
+  mobilenet      memory-bound: HBM triad passes (depthwise-like) + one small GEMM
+  ssd_mobilenet  mixed: GEMMs and HBM streaming in similar proportion
+
+The batch suffix scales the GEMM M dimension and the streamed bytes; the framework prefix
+selects a different layer shape (onnx: 2048-wide, tensorflow: 1536/2560-wide).  One
+*iteration* ("query batch") runs the op list once; a pod's throughput is iterations/s,
+its SLO a minimum iterations/s -- the same semantics as the reference's SLO env
+(SURVEY.md §2.7.1).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Tuple
+
+
+@dataclass(frozen=True)
+class Op:
+    kind: str              # "gemm" | "triad"
+    M: int = 0
+    N: int = 0
+    K: int = 0
+    relu: bool = True
+    n_floats: int = 0      # triad
+
+    @property
+    def flops(self) -> float:
+        return 2.0 * self.M * self.N * self.K if self.kind == "gemm" else 2.0 * self.n_floats
+
+    @property
+    def bytes(self) -> float:
+        if self.kind == "gemm":
+            return 2.0 * (self.M * self.K + self.N * self.K + self.M * self.N)
+        return 12.0 * self.n_floats
+
+
+@dataclass(frozen=True)
+class Workload:
+    name: str
+    family: str                  # resnet50 | mobilenet | ssd_mobilenet
+    framework: str               # onnx | tensorflow
+    batch: int
+    ops: Tuple[Op, ...]
+    hbm_gib: float               # declared footprint (request)
+
+    @property
+    def flops(self) -> float:
+        return sum(o.flops for o in self.ops)
+
+    @property
+    def bytes(self) -> float:
+        return sum(o.bytes for o in self.ops)
+
+    @property
+    def intensity(self) -> float:
+        return self.flops / max(self.bytes, 1.0)
+
+
+def _mk(framework: str, family: str, batch: int) -> Workload:
+    wide = 2048 if framework == "onnx" else 2560
+    narrow = 1024 if framework == "onnx" else 1536
+    m = batch                                         # 1024 / 2048 / 4096
+    if family == "resnet50":
+        ops = (Op("gemm", m, wide, wide), Op("gemm", m, wide, wide), Op("gemm", m, wide, wide))
+        hbm = 8.0
+    elif family == "mobilenet":
+        ops = (Op("triad", n_floats=m * 16384), Op("triad", n_floats=m * 16384),
+               Op("gemm", m, narrow, narrow))
+        hbm = 4.0
+    else:  # ssd_mobilenet
+        ops = (Op("gemm", m, wide, narrow), Op("triad", n_floats=m * 16384), Op("gemm", m, narrow, wide))
+        hbm = 6.0
+    return Workload(f"{framework}_{family}_{batch}", family, framework, batch, ops, hbm * (batch / 1024) ** 0.5)
+
+
+FRAMEWORKS = ("onnx", "tensorflow")
+FAMILIES = ("mobilenet", "resnet50", "ssd_mobilenet")
+BATCHES = (1024, 2048, 4096)
+
+CATALOG: Dict[str, Workload] = {}
+for _fw in FRAMEWORKS:
+    for _fa in FAMILIES:
+        for _b in BATCHES:
+            _w = _mk(_fw, _fa, _b)
+            CATALOG[_w.name] = _w
+NAMES: List[str] = sorted(CATALOG)
+INDEX: Dict[str, int] = {n: i for i, n in enumerate(NAMES)}
+
+
+def workload_for_pod(pod_name: str) -> Workload:
+    """Same matching rule as the recommender: first catalog name that is a substring of
+    the pod name with '-' -> '_' (reference recom_server.py:67-71)."""
+    nm = pod_name.replace("-", "_")
+    for n in sorted(CATALOG, key=len, reverse=True):
+        if n in nm:
+            return CATALOG[n]
+    raise KeyError(pod_name)
+
+
+# ---------------------------------------------------------------- analytic predictions
+def roofline_seconds(w: Workload, share: float, peak_tflops: float = 1100.0, hbm_tbps: float = 5.5,
+                     share_bw_exp: float = 0.6) -> float:
+    """Per-iteration time on a `share` of the GPU's XCDs.  Compute scales linearly with
+    the share; a CU subset can still pull a super-linear fraction of HBM bandwidth
+    (share**share_bw_exp).  Defaults are measured MI355X rates of the native kernels
+    (gemm ~1.1 PF on a whole chip, triad ~5.5 TB/s); `profile_workloads` replaces this
+    with measurements."""
+    t = 0.0
+    for o in w.ops:
+        if o.kind == "gemm":
+            t += max(o.flops / (peak_tflops * 1e12 * share), o.bytes / (hbm_tbps * 1e12 * share ** share_bw_exp))
+        else:
+            t += o.bytes / (hbm_tbps * 1e12 * share ** share_bw_exp)
+    return t
+
+
+def analytic_tables(model: str = "MI355X", parts=(1, 2, 4, 8)) -> Tuple[List[str], List[str], List[List[float]],
+                                                                         List[str], List[List[float]]]:
+    """(conf_index, conf_cols, conf_values, intf_cols, intf_values) -- configuration
+    throughput (iterations/s) per partition share and pairwise interference (throughput
+    lost when co-located on the same GPU: HBM contention between memory-heavy kernels),
+    in the reference's matrix layout."""
+    idx = list(NAMES)
+    cols = [f"{p}P_{model}" for p in parts]
+    conf = [[1.0 / roofline_seconds(CATALOG[n], 1.0 / p) for p in parts] for n in idx]
+    intf_vals = []
+    for n in idx:
+        a = CATALOG[n]
+        base = 1.0 / roofline_seconds(a, 0.25)
+        mem_a = min(1.0, 1.0 / max(a.intensity / 100.0, 1e-3))
+        row = []
+        for m in idx:
+            b = CATALOG[m]
+            mem_b = min(1.0, 1.0 / max(b.intensity / 100.0, 1e-3))
+            row.append(base * 0.25 * mem_a * mem_b)
+        intf_vals.append(row)
+    return idx, cols, conf, list(idx), intf_vals

@@ -1,0 +1,72 @@
+"""Torch-facing wrappers for the HIP load kernels (native/hip/loadgen.hip).
+
+`gemm(a, bt)` computes act(a @ bt.T + bias) in bf16 on MFMA; `triad(a, b, c, s)` streams
+HBM.  Shapes are validated on the host before launch (the kernels have no bounds checks
+by design).  On a GPU box the native module is mandatory: there is no PyTorch fallback
+path here (tests compare against torch fp32 references instead).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _native
+
+BM, BN, BK = 128, 128, 64
+
+
+def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def check_gemm_shapes(M: int, N: int, K: int) -> None:
+    if M <= 0 or N <= 0 or K <= 0 or M % BM or N % BN or K % BK:
+        raise ValueError(f"gemm shape ({M},{N},{K}) must be positive multiples of ({BM},{BN},{BK})")
+
+
+def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+         relu: bool = False, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """out[M,N] = act(a[M,K] @ bt[N,K]^T + bias[N]) -- bf16 in/out, fp32 accumulate."""
+    if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
+        raise TypeError("gemm expects bf16 operands")
+    if not (a.is_cuda and bt.is_cuda):
+        raise ValueError("gemm expects device tensors")
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"gemm shape mismatch {tuple(a.shape)} x {tuple(bt.shape)}^T")
+    if a.stride(1) != 1 or bt.stride(1) != 1:
+        raise ValueError("gemm expects row-major (K-contiguous) operands")
+    M, K = a.shape
+    N = bt.shape[0]
+    check_gemm_shapes(M, N, K)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise ValueError("bad output tensor")
+    bptr = 0
+    if bias is not None:
+        if bias.dtype != torch.float32 or bias.numel() != N or not bias.is_contiguous():
+            raise ValueError("bias must be a contiguous fp32 vector of length N")
+        bptr = bias.data_ptr()
+    _native.hip().gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
+                               bt.stride(0), out.stride(0), relu, _stream_ptr(stream))
+    return out
+
+
+def triad(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, s: float = 1.5, blocks: int = 0,
+          stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """a = b + s*c (fp32, contiguous, numel % 4 == 0)."""
+    for t in (a, b, c):
+        if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("triad expects contiguous fp32 device tensors")
+    n = a.numel()
+    if b.numel() != n or c.numel() != n or n % 4:
+        raise ValueError("triad: sizes must match and be a multiple of 4")
+    _native.hip().stream_triad(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), n, int(blocks),
+                               _stream_ptr(stream))
+    return a
+
+
+def gemm_flops(M: int, N: int, K: int) -> float:
+    return 2.0 * M * N * K

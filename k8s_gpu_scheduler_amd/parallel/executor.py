@@ -1,0 +1,174 @@
+"""Per-GPU pod executor ("kubelet + container runtime" of the bench and e2e tests).
+
+One process per GPU.  The executor receives the scheduler's placements for its device
+(pod id, workload, CU-slice unit range, iterations), runs each pod's kernel mix on a HIP
+stream whose CU mask is exactly the pod's CU slices (ops.cumask.MaskedStream), and measures
+per-pod device time with HIP events.  Epochs are ordered on the device by an event
+barrier (every stream of epoch t+1 waits for every stream of epoch t), so the scheduler's
+capacity model (units free when the previous epoch's pods finish) holds without host
+synchronisation: the host can schedule epoch t+1 while the GPU executes epoch t.
+
+Working buffers are allocated once per (workload, slot) and reused -- a warm container.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..models.workloads import CATALOG, NAMES, Op, Workload
+from ..ops import loadgen
+from ..plugins.gpu.devices import cu_slice_mask
+
+
+@dataclass
+class PodRun:
+    pod_id: int
+    workload: str
+    first_unit: int
+    n_units: int
+    iters: int
+    slo: float = 0.0
+    start: Optional[torch.cuda.Event] = None
+    end: Optional[torch.cuda.Event] = None
+    ms: float = 0.0
+
+    @property
+    def throughput(self) -> float:
+        return self.iters / (self.ms / 1e3) if self.ms > 0 else 0.0
+
+
+class _Buffers:
+    def __init__(self, w: Workload, device: torch.device):
+        self.ops: List[Tuple[Op, tuple]] = []
+        g = torch.Generator(device="cpu").manual_seed(hash(w.name) & 0xFFFF)
+        for o in w.ops:
+            if o.kind == "gemm":
+                a = ((torch.rand(o.M, o.K, generator=g) * 2 - 1).to(torch.bfloat16)).to(device)
+                bt = ((torch.rand(o.N, o.K, generator=g) * 2 - 1).to(torch.bfloat16) * 0.05).to(device)
+                bias = torch.zeros(o.N, dtype=torch.float32, device=device)
+                c = torch.empty(o.M, o.N, dtype=torch.bfloat16, device=device)
+                self.ops.append((o, (a, bt, bias, c)))
+            else:
+                x = torch.ones(o.n_floats, dtype=torch.float32, device=device)
+                y = torch.ones(o.n_floats, dtype=torch.float32, device=device)
+                z = torch.ones(o.n_floats, dtype=torch.float32, device=device)
+                self.ops.append((o, (x, y, z)))
+
+
+class DeviceExecutor:
+    def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
+        self.device = device
+        self.dev = torch.device("cuda", device)
+        self.use_cu_masks = use_cu_masks
+        self.units = units_per_gpu
+        self._streams: Dict[Tuple[int, int], object] = {}
+        self._bufs: Dict[Tuple[str, int, int], _Buffers] = {}
+        self._last_events: List[torch.cuda.Event] = []
+        self.epoch_runs: List[List[PodRun]] = []
+        self.flops_done = 0.0
+        self.bytes_done = 0.0
+
+    def stream_for(self, first_unit: int, n_units: int):
+        key = (first_unit, n_units)
+        st = self._streams.get(key)
+        if st is None:
+            if self.use_cu_masks:
+                from ..ops.cumask import MaskedStream
+                st = MaskedStream(cu_slice_mask(first_unit, n_units), self.device)
+            else:
+                st = _PlainStream(self.device)
+            self._streams[key] = st
+        return st
+
+    def buffers(self, w: Workload, first_unit: int, n_units: int) -> _Buffers:
+        k = (w.name, first_unit, n_units)
+        b = self._bufs.get(k)
+        if b is None:
+            b = _Buffers(w, self.dev)
+            self._bufs[k] = b
+        return b
+
+    def warm(self, placements: List[PodRun]) -> None:
+        """Pre-create streams/buffers (outside any timed region)."""
+        for p in placements:
+            self.stream_for(p.first_unit, p.n_units)
+            self.buffers(CATALOG[p.workload], p.first_unit, p.n_units)
+        torch.cuda.synchronize(self.device)
+
+    def launch_epoch(self, runs: List[PodRun]) -> None:
+        """Enqueue one epoch's pods; returns immediately (async)."""
+        barrier = self._last_events
+        new_events: List[torch.cuda.Event] = []
+        by_stream: Dict[Tuple[int, int], List[PodRun]] = {}
+        for r in runs:
+            by_stream.setdefault((r.first_unit, r.n_units), []).append(r)
+        for (u0, n), lst in by_stream.items():
+            st = self.stream_for(u0, n).stream
+            for ev in barrier:
+                st.wait_event(ev)
+            for r in lst:
+                w = CATALOG[r.workload]
+                bufs = self.buffers(w, u0, n)
+                r.start = torch.cuda.Event(enable_timing=True)
+                r.end = torch.cuda.Event(enable_timing=True)
+                r.start.record(st)
+                for _ in range(r.iters):
+                    for o, t in bufs.ops:
+                        if o.kind == "gemm":
+                            a, bt, bias, c = t
+                            loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st)
+                        else:
+                            x, y, z = t
+                            loadgen.triad(x, y, z, 1.0001, stream=st)
+                r.end.record(st)
+                self.flops_done += w.flops * r.iters
+                self.bytes_done += w.bytes * r.iters
+            done = torch.cuda.Event()
+            done.record(st)
+            new_events.append(done)
+        if new_events:
+            self._last_events = new_events
+        self.epoch_runs.append(runs)
+
+    def join_current(self) -> None:
+        """Make the default stream wait for all enqueued work (no host sync)."""
+        cur = torch.cuda.current_stream(self.device)
+        for ev in self._last_events:
+            cur.wait_event(ev)
+
+    def collect(self, runs: List[PodRun]) -> Dict[str, float]:
+        """After a sync: per-pod times + busy accounting for one epoch."""
+        busy_unit_ms = 0.0
+        t_first, t_last = None, None
+        slo_ok = 0
+        for r in runs:
+            r.ms = r.start.elapsed_time(r.end)
+            busy_unit_ms += r.ms * r.n_units
+            if r.slo <= 0 or r.throughput >= r.slo:
+                slo_ok += 1
+        if runs:
+            starts = [r.start for r in runs]
+            ends = [r.end for r in runs]
+            t0 = starts[0]
+            t_first = min(t0.elapsed_time(s) for s in starts)
+            t_last = max(t0.elapsed_time(e) for e in ends)
+        span = (t_last - t_first) if runs else 0.0
+        return {"pods": float(len(runs)), "busy_unit_ms": busy_unit_ms, "span_ms": span,
+                "slo_ok": float(slo_ok)}
+
+    def close(self) -> None:
+        torch.cuda.synchronize(self.device)
+        for s in self._streams.values():
+            s.close()
+        self._streams.clear()
+
+
+class _PlainStream:
+    def __init__(self, device: int):
+        self.stream = torch.cuda.Stream(device=device)
+
+    def close(self) -> None:
+        pass

@@ -5,10 +5,13 @@ The reference knows a node's devices only as a JSON list of UUIDs in Redis
 (`<nUUIDs>P_<model>`).  An MI355X node has 8 GPUs, each optionally
 split into SPX/DPX/QPX/CPX compute partitions, so the inventory here is a list of
 `Device`s (physical index, partition index, CUs, HBM, NUMA), and the ledger accounts
-fractional use at **XCD granularity**: a GPU (or partition) is 8/P XCD "units" of 32 CUs
-each, a fractional pod gets a contiguous, naturally aligned run of units (buddy style),
-and its CU mask covers exactly those XCDs -- each co-located pod then owns its XCDs'
-private L2s instead of sharing them (MI355X has one 4 MiB L2 per XCD).
+fractional use in **CU-slice units**: a GPU is 8 units of 32 CUs, where unit u is
+word u of the 256-bit HIP CU mask.  Measured on MI355X (tools/diag_gpu.py,
+profiles/diag_r01.json): in SPX mode mask bit i selects CU i//8 of XCC i%8, and a mask
+that leaves any XCC without CUs is ignored by the driver, so a unit is 4 CUs on *every*
+XCD (XCD isolation needs a real compute partition, DPX/QPX/CPX, which the agent applies
+through amd-smi).  A fractional pod gets a contiguous, naturally aligned run of units
+(buddy style) and its CU mask is exactly those words.
 """
 from __future__ import annotations
 
@@ -43,7 +46,7 @@ class Device:
     numa: int = 0
     model: str = C.MI355X
     units: int = 0              # XCD units (32 CUs each)
-    first_xcd: int = 0          # first XCD of the GPU owned by this device
+    first_xcd: int = 0          # first CU-slice unit of the GPU owned by this device
 
     def __post_init__(self) -> None:
         if not self.units:
@@ -84,7 +87,7 @@ def devices_for_node(node: Obj, uuids: Optional[List[str]] = None,
             hbm = C.MI355X_HBM_GIB / max(parts, mem_parts)
             out.append(Device(u, nm, g, p, parts, C.MI355X_CUS // parts, hbm,
                               numa=0 if g < max(gpus // 2, 1) else 1, model=model,
-                              first_xcd=p * (C.MI355X_XCDS // parts)))
+                              first_xcd=0))   # a partition is its own HIP device: units restart at 0
             i += 1
     if uuids and len(uuids) > len(out) and not gpus:
         # Unlabelled node with UUIDs (reference-style): one device per UUID.
@@ -92,16 +95,19 @@ def devices_for_node(node: Obj, uuids: Optional[List[str]] = None,
     return out
 
 
-def xcd_cu_mask(first_xcd: int, n_xcd: int, cus: int = C.MI355X_CUS, xcds: int = C.MI355X_XCDS) -> List[int]:
-    """CU mask (list of 32-bit words, bit i = logical CU i) selecting all CUs of XCDs
-    [first_xcd, first_xcd+n_xcd).  Logical CU ids are distributed round-robin over the
-    XCDs (CU i lives on XCD i % 8) -- the layout `ops.cumask.probe_xcd_map` verifies on
-    the device."""
-    bits = [0] * ((cus + 31) // 32)
-    for cu in range(cus):
-        if first_xcd <= cu % xcds < first_xcd + n_xcd:
-            bits[cu // 32] |= 1 << (cu % 32)
-    return bits
+def cu_slice_mask(first_unit: int, n_units: int, cus: int = C.MI355X_CUS) -> List[int]:
+    """CU mask (list of 32-bit words, bit i = logical CU i) for units [first_unit,
+    first_unit+n_units): word u is all ones.  Each word covers CUs 4u..4u+3 of every one
+    of the 8 XCCs (bit i -> XCC i % 8, CU i // 8 inside it; verified by
+    ops.cumask.probe_xcd_map)."""
+    words = [0] * ((cus + 31) // 32)
+    for u in range(first_unit, min(first_unit + n_units, len(words))):
+        words[u] = 0xFFFFFFFF
+    return words
+
+
+# backwards-compatible name used by earlier tools
+xcd_cu_mask = cu_slice_mask
 
 
 def mask_to_hex(words: List[int]) -> str:

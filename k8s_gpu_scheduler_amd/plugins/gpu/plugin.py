@@ -11,11 +11,11 @@ Reference: `type GPU` implementing Score + NormalizeScore + PostBind
 
 * ``mode: fixed`` (default) -- the MI355X design, fixing SURVEY §2.9 #1-#10:
   PreFilter parses the GPU request (whole GPUs / partitions, or fractional CUs + HBM);
-  Filter checks per-device capacity in the ledger (XCD-granular CU units + HBM) and, for
+  Filter checks per-device capacity in the ledger (32-CU mask-word units + HBM) and, for
   multi-GPU pods, an xGMI clique (`topology.select_gpu_set`); PreScore fetches the
   incoming pod's predictions once; Score evaluates every candidate device with the
   reference's SLO/interference objective (`scoring.device_score`, native C++ batch
-  core) blended with XCD-packing and live telemetry terms -- no I/O, no side effects;
+  core) blended with unit-packing and live telemetry terms -- no I/O, no side effects;
   NormalizeScore is the reference's min-max; Reserve/Unreserve commit the device choice
   to the ledger; PreBind writes the device env (ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES,
   HSA_CU_MASK, HBM cap; reference CUDA_* keys with `compatEnv`) into the pod's envFrom
@@ -38,7 +38,7 @@ from ...framework.interface import (CycleState, FilterPlugin, NodeScore, PostBin
 from ...kube.resources import Resources
 from ...recommender.client import CachedPredictions, PredictionProvider, RecommenderClient, RpcPredictions
 from ...telemetry.cache import TelemetryCache
-from .devices import CUS_PER_XCD, Device, DeviceLedger, DeviceState, devices_for_node, mask_to_hex, xcd_cu_mask
+from .devices import CUS_PER_XCD, Device, DeviceLedger, DeviceState, devices_for_node, mask_to_hex, cu_slice_mask
 from .scoring import Resident, score_devices
 from .topology import Topology, select_gpu_set
 
@@ -326,7 +326,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             u, u0, n, hbm, _ = frac[0]
             d = devs.get(u)
             first = (d.first_xcd if d else 0) + u0
-            env[C.ENV_CU_MASK] = f"{idx[0] or 0}:{mask_to_hex(xcd_cu_mask(first, n))}"
+            env[C.ENV_CU_MASK] = f"{idx[0] or 0}:{mask_to_hex(cu_slice_mask(first, n))}"
             env[C.ENV_HBM_LIMIT] = f"{hbm:g}"
         if self.args.compat_env:
             env[C.ENV_CUDA_VISIBLE] = env[C.ENV_ROCR_VISIBLE]

@@ -24,6 +24,8 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 f32 = np.float32
+# below this many residents the Python loop beats packing arrays for the C++ core
+NATIVE_MIN_RESIDENTS = 8
 
 
 def f32_interference(values: Iterable[float]) -> np.float32:
@@ -187,10 +189,10 @@ def score_devices(residents_per_device: List[Sequence[Resident]], incoming_name:
                   incoming_pred: float, incoming_intf: Dict[str, float], default_col: str) -> List[float]:
     """Batch form; uses the native core when available (identical results)."""
     try:
-        from ..._native import core as _core
+        from ..._native import score_core as _core
     except Exception:
         _core = None
-    if _core is not None and _core.available():
+    if _core is not None and _core.available() and sum(len(r) for r in residents_per_device) >= NATIVE_MIN_RESIDENTS:
         return _core.score_devices(residents_per_device, incoming_name, incoming_slo, incoming_pred,
                                    incoming_intf, default_col)
     return [device_score(r, incoming_name, incoming_slo, incoming_pred, incoming_intf, default_col)

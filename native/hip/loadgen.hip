@@ -1,0 +1,197 @@
+// Load-generator kernels: the GPU work a scheduled pod performs on its XCDs.
+//
+// The reference has no GPU code; its pods are external MLPerf-style
+// inference containers whose throughput the recommender matrices describe
+// (pkg/recommender/recommender/configurations_train.ods).  The MI355X build needs real,
+// controllable load on the chip to measure "achieved node GPU-util %" (BASELINE.json), so
+// each synthetic workload is a mix of:
+//
+//  * gemm_bf16_nt -- C[M,N] = act(A[M,K] . Bt[N,K]^T (+bias)), bf16 in / f32 accumulate /
+//    bf16 out, on MFMA (v_mfma_f32_16x16x32_bf16).  128x128x64 block tile, 4 waves (2x2),
+//    64x64 per wave = 4x4 MFMA tiles; both operands staged global->LDS with 16-byte
+//    global_load_lds (no VGPR round trip) into a double-buffered, XOR-swizzled LDS image
+//    (bank-conflict-free ds_read_b128 fragment reads); stage of tile t+1 is issued before
+//    the MFMAs of tile t; XCD-aware bijective block remap + grouped tile order for L2 reuse.
+//    Epilogue fuses bias + ReLU and packs to bf16.
+//  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
+#include <cstdint>
+
+#include "api.h"
+#include "common.h"
+
+namespace gs {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int THREADS = 256;
+constexpr int TILE_BYTES = BM * BK * 2;                 // 16 KiB per operand tile
+constexpr int LDS_BYTES = 2 /*bufs*/ * 2 /*A,B*/ * TILE_BYTES;   // 64 KiB
+constexpr int GROUP_M = 8;
+
+typedef const void __attribute__((address_space(1)))* gptr_t;
+typedef void __attribute__((address_space(3)))* lptr_t;
+
+// Issue the glds for one 128x64 bf16 tile (rows [r0, r0+128), k [k0, k0+64)) of a
+// row-major matrix with leading dimension ld (elements).  Logical 16-byte chunk kc of row
+// r lands at physical chunk kc ^ ((r >> 1) & 7) of that row's 128-byte LDS line; the LDS
+// image itself is lane-linear (glds requirement), so the swizzle is applied on the
+// per-lane SOURCE address (rule: linear dest + permuted source + same permutation on read).
+__device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld, int r0, int k0,
+                                           char* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < TILE_BYTES / 16 / THREADS; ++i) {     // 4 rounds
+    const int chunk = i * THREADS + wave * 64 + lane;
+    const int r = chunk >> 3;
+    const int p = chunk & 7;
+    const int kc = p ^ ((r >> 1) & 7);
+    const __bf16* src = g + (size_t)(r0 + r) * ld + k0 + kc * 8;
+    char* dst = lds_tile + (i * THREADS + wave * 64) * 16;  // wave-uniform base
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const char* lds_tile, int row, int kchunk) {
+  const int phys = kchunk ^ ((row >> 1) & 7);
+  return *reinterpret_cast<const bf16x8*>(lds_tile + row * (BK * 2) + phys * 16);
+}
+
+template <bool RELU, bool BIAS>
+__global__ void __launch_bounds__(THREADS, 2)
+gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
+                    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  // ---- XCD-aware bijective remap, then grouped (GROUP_M) tile order ----------------
+  const int nwg = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b % kXcds;
+  const int q = nwg / kXcds, rem = nwg % kXcds;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (wgid % per_group) % gsize;
+  const int tn = (wgid % per_group) / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto tileA = [&](int buf) { return smem + buf * 2 * TILE_BYTES; };
+  auto tileB = [&](int buf) { return smem + buf * 2 * TILE_BYTES + TILE_BYTES; };
+
+  const int nt = K / BK;
+  stage_tile(A, lda, m0, 0, tileA(0), wave, lane);
+  stage_tile(Bt, ldb, n0, 0, tileB(0), wave, lane);
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int fk = lane >> 4;
+  int buf = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) {
+      stage_tile(A, lda, m0, (t + 1) * BK, tileA(buf ^ 1), wave, lane);
+      stage_tile(Bt, ldb, n0, (t + 1) * BK, tileB(buf ^ 1), wave, lane);
+    }
+    const char* a_t = tileA(buf);
+    const char* b_t = tileB(buf);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = lds_frag(a_t, wm * 64 + i * 16 + frow, kk * 4 + fk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = lds_frag(b_t, wn * 64 + j * 16 + frow, kk * 4 + fk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();   // tile t+1 landed (vmcnt(0) before the barrier) and tile t fully read
+    buf ^= 1;
+  }
+
+  // ---- epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r -------------------
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn * 64 + j * 16 + frow;
+      const float bv = BIAS ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + fk * 4 + r;
+        float v = acc[i][j][r] + bv;
+        if (RELU) v = v > 0.f ? v : 0.f;
+        C[(size_t)row * ldc + col] = (__bf16)v;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) stream_triad_kernel(float4* __restrict__ a, const float4* __restrict__ b,
+                                                           const float4* __restrict__ c, float s, size_t n4) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n4; i += stride) {
+    float4 x = b[i], y = c[i];
+    a[i] = make_float4(x.x + s * y.x, x.y + s * y.y, x.z + s * y.z, x.w + s * y.w);
+  }
+}
+
+static void check_align(const void* p, const char* what) {
+  if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
+}
+
+void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
+                  int ldc, bool relu, uintptr_t stream) {
+  // Host-side shape checks: the kernel has no bounds checks by design.
+  if (M <= 0 || N <= 0 || K <= 0) throw std::runtime_error("gemm: empty shape");
+  if (M % BM || N % BN || K % BK) throw std::runtime_error("gemm: M,N must be multiples of 128 and K of 64");
+  if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8) throw std::runtime_error("gemm: bad leading dims");
+  check_align(reinterpret_cast<void*>(a), "A");
+  check_align(reinterpret_cast<void*>(bt), "Bt");
+  const dim3 grid((M / BM) * (N / BN)), block(THREADS);
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  auto A = reinterpret_cast<const __bf16*>(a);
+  auto B = reinterpret_cast<const __bf16*>(bt);
+  auto Cp = reinterpret_cast<__bf16*>(c);
+  auto bp = reinterpret_cast<const float*>(bias);
+  if (relu && bias)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (bias)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  HIP_CHECK(hipGetLastError());
+}
+
+void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream) {
+  if (n_floats % 4) throw std::runtime_error("triad: n must be a multiple of 4");
+  check_align(reinterpret_cast<void*>(a), "a");
+  check_align(reinterpret_cast<void*>(b), "b");
+  check_align(reinterpret_cast<void*>(c), "c");
+  if (blocks <= 0) blocks = 2048;
+  hipLaunchKernelGGL(stream_triad_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<float4*>(a), reinterpret_cast<const float4*>(b),
+                     reinterpret_cast<const float4*>(c), s, n_floats / 4);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace gs
