@@ -88,8 +88,20 @@ def resource_version(obj: Obj) -> str:
     return obj.get("metadata", {}).get("resourceVersion", "")
 
 
-def deepcopy(obj: Obj) -> Obj:
+def deepcopy(obj: Any) -> Any:
+    """Deep copy of a JSON-shaped object (dict/list/scalars) -- ~5x faster than
+    copy.deepcopy, which matters on the apiserver/informer hot path."""
+    t = type(obj)
+    if t is dict:
+        return {k: (v if type(v) in _SCALARS else deepcopy(v)) for k, v in obj.items()}
+    if t is list:
+        return [v if type(v) in _SCALARS else deepcopy(v) for v in obj]
+    if t in _SCALARS:
+        return obj
     return copy.deepcopy(obj)
+
+
+_SCALARS = (str, int, float, bool, type(None))
 
 
 # --------------------------------------------------------------------------- constructors

@@ -158,17 +158,21 @@ class FakeCluster(KubeClient):
         O.meta(obj)["resourceVersion"] = str(rv)
 
     def _emit(self, resource: str, typ: str, obj: Obj) -> None:
-        ev = WatchEvent(type=typ, object=O.deepcopy(obj))
+        # One immutable snapshot is shared by the history, every inline subscriber and
+        # every watch queue: like client-go's shared informer cache, consumers must treat
+        # watched objects as read-only (the store itself keeps its own copy).
+        snap = O.deepcopy(obj)
+        ev = WatchEvent(type=typ, object=snap)
         h = self._history[resource]
         h.append((int(O.resource_version(obj) or self._cur_rv), ev))
         if len(h) > self._history_len:
             del h[: len(h) - self._history_len]
         for cb in list(self._subs[resource]):
-            cb(WatchEvent(type=typ, object=O.deepcopy(obj)))
+            cb(ev)
         ns_obj = O.namespace(obj) if NAMESPACED[resource] else None
         for ns, q in list(self._queues[resource]):
             if ns is None or ns == ns_obj:
-                q.put(WatchEvent(type=typ, object=O.deepcopy(obj)))
+                q.put(ev)
 
     @property
     def resource_version(self) -> str:

@@ -6,7 +6,7 @@ and the REST client both need a faithful implementation of the same wire semanti
 """
 from __future__ import annotations
 
-import copy
+from ..api.objects import deepcopy as _dc
 import re
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -43,28 +43,28 @@ def _walk(doc: Any, toks: List[str]) -> Any:
 
 def _add(doc: Any, toks: List[str], value: Any, replace: bool = False) -> Any:
     if not toks:
-        return copy.deepcopy(value)
+        return _dc(value)
     parent = _walk(doc, toks[:-1])
     last = toks[-1]
     if isinstance(parent, list):
         if last == "-":
             if replace:
                 raise PatchError("replace with '-' index")
-            parent.append(copy.deepcopy(value))
+            parent.append(_dc(value))
         else:
             i = int(last)
             if replace:
                 if i >= len(parent):
                     raise PatchError("replace index out of range")
-                parent[i] = copy.deepcopy(value)
+                parent[i] = _dc(value)
             else:
                 if i > len(parent):
                     raise PatchError("add index out of range")
-                parent.insert(i, copy.deepcopy(value))
+                parent.insert(i, _dc(value))
     elif isinstance(parent, dict):
         if replace and last not in parent:
             raise PatchError(f"replace: key {last!r} missing")
-        parent[last] = copy.deepcopy(value)
+        parent[last] = _dc(value)
     else:
         raise PatchError("parent is not a container")
     return doc
@@ -86,7 +86,7 @@ def _remove(doc: Any, toks: List[str]) -> Tuple[Any, Any]:
 
 def apply_json_patch(doc: Any, ops: List[Dict[str, Any]]) -> Any:
     """Apply an RFC 6902 patch; returns a new document (input untouched)."""
-    out = copy.deepcopy(doc)
+    out = _dc(doc)
     for op in ops:
         kind = op.get("op")
         toks = _split_pointer(op.get("path", ""))
@@ -100,7 +100,7 @@ def apply_json_patch(doc: Any, ops: List[Dict[str, Any]]) -> Any:
             except PatchError:
                 parent = _walk(out, toks[:-1]) if toks else None
                 if isinstance(parent, dict):
-                    parent[toks[-1]] = copy.deepcopy(op.get("value"))
+                    parent[toks[-1]] = _dc(op.get("value"))
                 else:
                     raise
         elif kind == "remove":
@@ -122,15 +122,15 @@ def apply_json_patch(doc: Any, ops: List[Dict[str, Any]]) -> Any:
 def apply_merge_patch(doc: Any, patch: Any) -> Any:
     """RFC 7386: null deletes, dicts merge recursively, everything else replaces."""
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
-    out = copy.deepcopy(doc) if isinstance(doc, dict) else {}
+        return _dc(patch)
+    out = _dc(doc) if isinstance(doc, dict) else {}
     for k, v in patch.items():
         if v is None:
             out.pop(k, None)
         elif isinstance(v, dict):
             out[k] = apply_merge_patch(out.get(k, {}), v)
         else:
-            out[k] = copy.deepcopy(v)
+            out[k] = _dc(v)
     return out
 
 

@@ -26,6 +26,7 @@ from __future__ import annotations
 import json
 import logging
 import math
+import random
 import threading
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -74,7 +75,7 @@ class GPUArgs:
     w_slo: float = 1.0
     w_pack: float = 1.0
     w_telemetry: float = 0.5
-    pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated)
+    pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
     compat_env: bool = True
@@ -120,6 +121,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
         self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
         self._lock = threading.RLock()
+        self._rng = random.Random(self.args.seed)
         self._client: Optional[RecommenderClient] = None
         self.SCORE_DOES_IO = self.args.mode == "parity"
         if self.predictions is None and self.args.recommender and self.args.predictions != "none":
@@ -411,6 +413,9 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                 for i, v in zip(ids, vals):
                     slo_scores[i] = v
         best: Optional[Choice] = None
+        if a.pack == "random":
+            st, u0 = cands[self._rng.randrange(len(cands))]
+            return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], 50.0, [st.device])
         for i, (st, u0) in enumerate(cands):
             parts: List[Tuple[float, float]] = []
             if slo_scores[i] is not None:
