@@ -309,6 +309,7 @@ class _Handler(socketserver.BaseRequestHandler):
         session = {"auth": not engine.password, "db": 0}
         p = Parser()
         sock: socket.socket = self.request
+        self.server.clients.add(sock)  # type: ignore[attr-defined]
         while True:
             try:
                 data = sock.recv(65536)
@@ -345,6 +346,7 @@ class FakeRedisServer(socketserver.ThreadingMixIn, socketserver.TCPServer):
 
     def __init__(self, engine: Optional[FakeRedisEngine] = None, host: str = "127.0.0.1", port: int = 0):
         self.engine = engine or FakeRedisEngine()
+        self.clients: set = set()
         super().__init__((host, port), _Handler)
         self._thread: Optional[threading.Thread] = None
 
@@ -359,5 +361,14 @@ class FakeRedisServer(socketserver.ThreadingMixIn, socketserver.TCPServer):
         return self
 
     def stop(self) -> None:
+        """Stop accepting and drop every client connection (a server crash, as seen by
+        clients)."""
         self.shutdown()
         self.server_close()
+        for c in list(self.clients):
+            try:
+                c.shutdown(socket.SHUT_RDWR)
+                c.close()
+            except OSError:
+                pass
+        self.clients.clear()

@@ -1,0 +1,83 @@
+"""Prometheus exporter for MI355X telemetry and scheduler metrics.
+
+The reference *consumes* dcgm-exporter series (reference
+pkg/prom/fetch_prom_metrics/prom_metrics.go:63-70) and exports nothing of its own
+(SURVEY.md §5.5).  This exporter publishes, per GPU (labels `gpu`, `UUID`, `node`,
+`pod` = exporter pod name so the reference's `{pod="<exporter>"}` filter works):
+
+  amd_gpu_gfx_activity, amd_gpu_umc_activity  (0..1, DCGM_FI_PROF_GR_ENGINE_ACTIVE /
+                                               DCGM_FI_DEV_MEM_COPY_UTIL analogs)
+  amd_gpu_temperature_hotspot                 (C,  DCGM_FI_DEV_GPU_TEMP)
+  amd_gpu_vram_used_mb / amd_gpu_vram_free_mb (MB, DCGM_FI_DEV_FB_USED / _FREE)
+  amd_gpu_power_watts, amd_gpu_xgmi_{tx,rx}_bytes (rate, B/s)
+
+optionally the same values under the DCGM names (`dcgm_compat=True`), and scheduler
+series: pods scheduled, scheduling latency histogram, SLO attainment, per-extension-point
+latency.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, Optional
+
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest, start_http_server
+
+from ..api import constants as C
+
+
+class GpuExporter:
+    def __init__(self, node: str, exporter_pod: str = "amd-gpu-exporter", dcgm_compat: bool = False,
+                 registry: Optional[CollectorRegistry] = None):
+        self.node, self.pod, self.dcgm_compat = node, exporter_pod, dcgm_compat
+        self.registry = registry or CollectorRegistry()
+        lab = ["gpu", "UUID", "node", "pod"]
+        self.g: Dict[str, Gauge] = {m: Gauge(m, m, lab, registry=self.registry) for m in C.AMD_METRICS}
+        self.dcgm: Dict[str, Gauge] = {}
+        if dcgm_compat:
+            self.dcgm = {m: Gauge(m, m, lab, registry=self.registry) for m in C.DCGM_METRICS}
+        self.sched_pods = Counter("gpusched_pods_scheduled", "pods bound by the scheduler", ["result"],
+                                  registry=self.registry)
+        self.sched_latency = Histogram("gpusched_scheduling_latency_seconds", "pod scheduling latency",
+                                       buckets=(1e-4, 3e-4, 1e-3, 3e-3, 1e-2, 3e-2, 0.1, 0.3, 1, 3),
+                                       registry=self.registry)
+        self.slo = Gauge("gpusched_slo_attainment", "fraction of pods meeting their SLO", registry=self.registry)
+        self.ext = Gauge("gpusched_extension_point_mean_us", "mean latency per extension point", ["point"],
+                         registry=self.registry)
+
+    def observe_samples(self, samples: Iterable[Dict[str, float]], uuids: Dict[int, str]) -> None:
+        for s in samples:
+            idx = int(s.get("index", 0))
+            lv = (str(idx), uuids.get(idx, ""), self.node, self.pod)
+            gfx = max(0.0, float(s.get("gfx_activity", 0.0))) / 100.0
+            umc = max(0.0, float(s.get("umc_activity", 0.0))) / 100.0
+            used = max(0.0, float(s.get("vram_used_mb", 0.0)))
+            total = max(used, float(s.get("vram_total_mb", C.MI355X_HBM_GIB * 1024)))
+            vals = {"amd_gpu_gfx_activity": gfx, "amd_gpu_umc_activity": umc,
+                    "amd_gpu_temperature_hotspot": float(s.get("temp_c", 0.0)),
+                    "amd_gpu_vram_used_mb": used, "amd_gpu_vram_free_mb": total - used,
+                    "amd_gpu_power_watts": float(s.get("power_w", 0.0)),
+                    "amd_gpu_xgmi_tx_bytes": float(s.get("xgmi_write_bps", 0.0)),
+                    "amd_gpu_xgmi_rx_bytes": float(s.get("xgmi_read_bps", 0.0))}
+            for m, v in vals.items():
+                self.g[m].labels(*lv).set(v)
+            if self.dcgm:
+                for dm, am in C.DCGM_TO_AMD.items():
+                    self.dcgm[dm].labels(*lv).set(vals[am])
+
+    def observe_scheduler(self, scheduled: int = 0, failed: int = 0, latencies=(), slo: Optional[float] = None,
+                          ext: Optional[Dict[str, Dict[str, float]]] = None) -> None:
+        if scheduled:
+            self.sched_pods.labels("scheduled").inc(scheduled)
+        if failed:
+            self.sched_pods.labels("unschedulable").inc(failed)
+        for l in latencies:
+            self.sched_latency.observe(l)
+        if slo is not None:
+            self.slo.set(slo)
+        for p, d in (ext or {}).items():
+            self.ext.labels(p).set(d.get("mean_us", 0.0))
+
+    def render(self) -> bytes:
+        return generate_latest(self.registry)
+
+    def serve(self, port: int = 9400, addr: str = "0.0.0.0") -> None:
+        start_http_server(port, addr, registry=self.registry)

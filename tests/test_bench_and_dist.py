@@ -1,0 +1,46 @@
+"""The pod-arrival benchmark and its distributed path on CPU (gloo, simulated executor).
+
+The driver runs `bench.py` under torch.distributed.run with one rank per GPU; here the
+same code path runs with world_size 2 on gloo so placement broadcast, telemetry
+all-gather and the max-over-ranks timing are exercised without a GPU.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_sim_single_process():
+    from k8s_gpu_scheduler_amd.parallel.podbench import main
+    r = main(["--sim", "--gpus", "4", "--steps", "3", "--warmup", "1"])
+    assert r["n_gpus"] == 4 and r["config"]["global_batch"] == 16 and r["unscheduled"] == 0
+    assert r["value"] > 0 and r["simulated"] is True
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in r
+
+
+def test_bench_random_policy_runs():
+    from k8s_gpu_scheduler_amd.parallel.podbench import main
+    r = main(["--sim", "--gpus", "2", "--steps", "2", "--warmup", "1", "--policy", "random"])
+    assert r["config"]["policy"] == "random" and r["unscheduled"] == 0
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo(tmp_path):
+    out = tmp_path / "r.json"
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29611", os.path.join(ROOT, "bench.py"),
+           "--sim", "--gpus", "2", "--steps", "3", "--warmup", "1", "--out", str(out)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1                        # rank 0 prints exactly one JSON line
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 8
+    assert json.loads(out.read_text())["value"] == r["value"]

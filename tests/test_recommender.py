@@ -1,0 +1,134 @@
+"""Recommender: proto wire format, imputers, gRPC server parity, hot reload, resize.
+
+Parity vectors from SURVEY.md §2.7.4: unknown pod -> result=[0], columns=[];
+`…resnet50-1024_A30` interference imputes the NaN diagonal -> 44.37.
+"""
+import os
+import shutil
+import time
+
+import numpy as np
+import pytest
+
+from k8s_gpu_scheduler_amd.models.imputers import ALSImputer, IterativeImputerModel, SVDImputer, make_imputer
+from k8s_gpu_scheduler_amd.recommender import proto as P
+from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, RecommenderClient, RpcPredictions, reply_to_map
+from k8s_gpu_scheduler_amd.recommender.resize import recommend
+from k8s_gpu_scheduler_amd.recommender.service import RecommenderService
+from k8s_gpu_scheduler_amd.recommender.tables import Table, file_version, find_index_for_request
+
+
+def test_proto_wire_compat():
+    # field numbers/types of recom.proto: Request.index=1 (string), Reply.result=1 (packed float),
+    # Reply.columns=2 (string)
+    assert P.Request(index="ab").SerializeToString() == b"\n\x02ab"
+    r = P.set_protobuf_reply([1.0], ["c"], P.Reply())
+    assert r.SerializeToString() == b"\n\x04\x00\x00\x80?\x12\x01c"
+    assert set(P.POOL.FindServiceByName("recommender.recommender").methods_by_name.keys()) >= \
+        {"ImputeConfigurations", "ImputeInterference"}
+
+
+def test_find_index():
+    idx = ["onnx_mobilenet_1024", "onnx_resnet50_1024"]
+    assert find_index_for_request("mlperf_gpu_onnx_resnet50_1024_A30", idx) == "onnx_resnet50_1024"
+    assert find_index_for_request("busybox_abc", idx) == ""
+
+
+@pytest.mark.parametrize("kind", ["iterative", "svd", "als"])
+def test_imputers_recover_low_rank(kind):
+    rng = np.random.default_rng(0)
+    U, V = rng.normal(size=(30, 2)), rng.normal(size=(2, 8))
+    X = U @ V + 10
+    M = X.copy()
+    hide = rng.random(X.shape) < 0.15
+    M[hide] = np.nan
+    m = make_imputer(kind, **({} if kind == "iterative" else {"k": 2})).fit(M)
+    out = m.predict(M)
+    assert np.allclose(out[~hide], X[~hide])                      # observed entries kept
+    err = np.abs(out[hide] - X[hide]).mean()
+    assert err < (0.6 if kind != "iterative" else 1.0), err
+
+
+@pytest.fixture()
+def server(ref_data, tmp_path):
+    conf, intf = ref_data
+    c, i = tmp_path / "c.tsv", tmp_path / "i.tsv"
+    shutil.copy(conf, c)
+    shutil.copy(intf, i)
+    svc = RecommenderService(str(c), str(i), job_delay_s=0.2)
+    svc.train()
+    srv, port = svc.make_server(0, 4, "127.0.0.1")
+    yield svc, f"127.0.0.1:{port}", (c, i)
+    svc.stop()
+    srv.stop(0)
+
+
+def test_server_parity_vectors(server):
+    svc, addr, _ = server
+    cl = RecommenderClient(addr)
+    r = cl.impute_configurations("busybox-abc")
+    assert list(r.result) == [0.0] and list(r.columns) == []
+    m = reply_to_map(cl.impute_interference("mlperf-gpu-onnx-resnet50-1024_A30"))
+    assert m["onnx_resnet50_1024"] == pytest.approx(44.37, abs=0.01)
+    conf = reply_to_map(cl.impute_configurations("mlperf-gpu-onnx-mobilenet-1024"))
+    assert conf["1P_A30"] == pytest.approx(624.9) and conf["4P_V100"] == pytest.approx(474.595)
+    # per-call channel (reference client_call.go:13) gives identical answers
+    cl2 = RecommenderClient(addr, new_channel_per_call=True)
+    assert reply_to_map(cl2.impute_configurations("mlperf-gpu-onnx-mobilenet-1024")) == conf
+    cl.close()
+
+
+def test_cached_predictions_match_rpc(server):
+    svc, addr, _ = server
+    cl = RecommenderClient(addr)
+    rpc, cache = RpcPredictions(cl), CachedPredictions(cl)
+    for name in ["mlperf-gpu-onnx-resnet50-2048", "tf-tensorflow-ssd-mobilenet-4096-x"]:
+        a, b = rpc.configurations(name), cache.configurations(name)
+        assert a.keys() == b.keys() and all(abs(a[k] - b[k]) < 1e-3 for k in a)
+    a = rpc.interference("mlperf-gpu-onnx-resnet50-1024_A30")
+    b = cache.interference("mlperf-gpu-onnx-resnet50-1024_A30")
+    assert all(abs(a[k] - b[k]) < 1e-3 for k in a)
+    assert cache.configurations("busybox") == {}
+
+
+def test_hot_reload_on_md5_change(server):
+    svc, addr, (c, _) = server
+    cl = RecommenderClient(addr)
+    v0 = cl.version().configurations
+    t = Table.read_tsv(str(c))
+    t.set("new_workload_1", "1P_A30", 123.0)
+    t.write_tsv(str(c))
+    svc.start_retrain_loop()
+    deadline = time.time() + 10
+    while cl.version().configurations == v0 and time.time() < deadline:
+        time.sleep(0.1)
+    assert cl.version().configurations == file_version(str(c)) != v0
+    assert reply_to_map(cl.impute_configurations("new-workload-1"))["1P_A30"] == pytest.approx(123.0)
+    # a missing file does not kill the retrain loop (reference quirk §2.9 #12)
+    os.remove(str(c))
+    time.sleep(0.5)
+    assert svc._thread.is_alive()
+
+
+def test_resize_policy():
+    hist = [{"hbm_gib": 10 + i % 3, "cu": 64, "throughput": 100.0} for i in range(20)]
+    a = recommend(hist, 64, 32, slo=90)
+    assert a.hbm_gib == 14 and a.cu == 64                    # p95=12 GiB * 1.15 -> ceil 14
+    a = recommend(hist, 64, 32, slo=40)
+    assert a.cu == 32                                         # extrapolated 100*(0.5^0.85) >= 42
+    a = recommend(hist, 64, 32, slo=500)
+    assert a.cu == 256
+    a = recommend(hist[:2], 64, 32, slo=90)
+    assert a.reason == "insufficient history" and a.cu == 64
+    a = recommend(hist, 64, 32, slo=50, conf_predictions={"8P_MI355X": 60.0})
+    assert a.cu == 32
+    busy = [{"hbm_gib": 4, "cu_busy": 0.3} for _ in range(10)]
+    assert recommend(busy, 128, 8).cu == 64
+
+
+def test_resize_rpc(server):
+    svc, addr, _ = server
+    svc.history_source = lambda pod: [{"hbm_gib": 20.0, "cu": 128, "throughput": 300.0}] * 5
+    cl = RecommenderClient(addr)
+    r = cl.recommend_resources("mlperf-gpu-onnx-resnet50-1024", 128, 64.0, 150.0)
+    assert r.samples == 5 and r.recommended_hbm_gib == 23.0 and r.recommended_cu == 64

@@ -1,0 +1,217 @@
+"""Scheduler framework + GPU plugin (fixed mode) on a FakeCluster.
+
+Covers BASELINE.json configs on CPU:
+  1. busybox pods, no GPU request, 2-node cluster (plugin plumbing)
+  3. fractional pods bin-packed onto 8 MI355X by CU units + HBM (+ telemetry)
+  4. a 4-GPU pod on an xGMI-connected NUMA-local quad
+plus framework semantics: NormalizeScore, weights, Reserve/Unreserve on bind failure,
+PreBind env written before bind, restart recovery from annotations, unschedulable
+handling, config loading.
+"""
+import json
+
+import pytest
+
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.framework.config import default_gpu_config, load_config, parse_config
+from k8s_gpu_scheduler_amd.framework.interface import NodeScore, min_max_normalize
+from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+from k8s_gpu_scheduler_amd.kube.client import Conflict, FakeCluster
+from k8s_gpu_scheduler_amd.plugins import full_registry
+from k8s_gpu_scheduler_amd.plugins.gpu.devices import DeviceLedger, cu_slice_mask, mask_to_hex
+from k8s_gpu_scheduler_amd.plugins.gpu.topology import Topology, select_gpu_set
+from k8s_gpu_scheduler_amd.telemetry.cache import DeviceSample, TelemetryCache
+
+
+def world(nodes=("node-a",), gpus=8, args=None, **kw):
+    fc = FakeCluster()
+    for n in nodes:
+        fc.create("nodes", O.make_node(n, gpus=gpus))
+    ledger, tele = DeviceLedger(), TelemetryCache(stale_s=0)
+    s = Scheduler(fc, default_gpu_config(args or {}), full_registry(), bind_async=False, seed=0,
+                  extras={"ledger": ledger, "telemetry": tele}, **kw)
+    s.start_informers()
+    return fc, s, ledger, tele
+
+
+def test_normalize_score_reference_semantics():
+    s = [NodeScore("a", 10), NodeScore("b", 35), NodeScore("c", 60)]
+    min_max_normalize(s)
+    assert [x.score for x in s] == [0, 50, 100]
+    s = [NodeScore("a", 7), NodeScore("b", 7)]
+    min_max_normalize(s)
+    assert [x.score for x in s] == [0, 0]
+
+
+def test_config_loader_reference_manifest():
+    import os
+    p = "/root/reference/deploy/scheduler.yaml"
+    text = open(p).read() if os.path.exists(p) else None
+    if text is None:
+        pytest.skip("reference deploy not mounted")
+    cfg = load_config(text)
+    prof = cfg.profile("gpu-scheduler")
+    assert cfg.leader_election.leader_elect and cfg.leader_election.resource_name == "gpu-scheduler"
+    assert [(r.name, r.weight) for r in prof.enabled("score") if r.name == "GPU"] == [("GPU", 10100)]
+    assert [r.name for r in prof.enabled("postBind")] == ["GPU"]
+    assert "DefaultBinder" in [r.name for r in prof.enabled("bind")]
+    # our own deploy manifest parses too
+    ours = os.path.join(os.path.dirname(os.path.dirname(__file__)), "deploy", "scheduler.yaml")
+    if os.path.exists(ours):
+        assert load_config(open(ours).read()).profile("gpu-scheduler") is not None
+
+
+def test_config_disable_all_and_unknown_api():
+    cfg = parse_config({"apiVersion": "kubescheduler.config.k8s.io/v1", "kind": "KubeSchedulerConfiguration",
+                        "profiles": [{"schedulerName": "x", "plugins": {"score": {"disabled": [{"name": "*"}],
+                                                                                  "enabled": [{"name": "GPU"}]}}}]})
+    assert [r.name for r in cfg.profile("x").enabled("score")] == ["GPU"]
+    with pytest.raises(ValueError):
+        parse_config({"apiVersion": "v0", "kind": "KubeSchedulerConfiguration"})
+
+
+def test_config1_busybox_two_nodes():
+    """busybox pods, no GPU request, 2 nodes: default plugins schedule them, GPU plugin skips."""
+    fc, s, _, _ = world(nodes=("node-a", "node-b"), gpus=0)
+    fc.create("configmaps", O.make_config_map("game-demo"))
+    for i in range(4):
+        fc.create("pods", O.make_pod(f"busybox-{i}", config_maps=["game-demo"]))
+    res = s.schedule_pending()
+    assert all(r.status.ok and r.node in ("node-a", "node-b") for r in res) and len(res) == 4
+    assert len(fc.bindings) == 4
+    # least-allocated default scoring spreads them
+    assert {r.node for r in res} == {"node-a", "node-b"}
+
+
+def test_config3_fractional_binpack_and_env():
+    fc, s, ledger, tele = world()
+    fc.create("configmaps", O.make_config_map("env-p0"))
+    pods = [O.make_pod(f"p{i}", gpu_cu=64, gpu_mem_gib=16, config_maps=[f"env-p{i}"] if i == 0 else [])
+            for i in range(32)]
+    for p in pods:
+        fc.create("pods", p)
+    res = s.schedule_pending()
+    assert all(r.status.ok for r in res), [r.status.message() for r in res if not r.status.ok]
+    # 32 quarter-GPU pods fill all 8 GPUs exactly: every unit used, 4 pods per GPU
+    per_gpu = {}
+    for st in ledger.devices("node-a"):
+        assert st.free_units == 0
+        per_gpu[st.device.gpu] = len(st.pods)
+    assert set(per_gpu.values()) == {4}
+    # 33rd pod does not fit
+    fc.create("pods", O.make_pod("extra", gpu_cu=64))
+    (r,) = s.schedule_pending()
+    assert not r.status.ok and "GPU" in r.status.message() or "Insufficient" in r.status.message()
+    # PreBind wrote the device env before bind
+    d = fc.get("configmaps", "env-p0", "default")["data"]
+    ann = O.annotations(fc.get("pods", "p0", "default"))
+    assert d[C.ENV_ROCR_VISIBLE] == ann[C.ANNOT_DEVICES]
+    u0 = json.loads(ann[C.ANNOT_DEVICE_INDICES])[0][1]
+    assert d[C.ENV_CU_MASK].endswith(mask_to_hex(cu_slice_mask(u0, 2)))
+    assert d[C.ENV_CUDA_VISIBLE] == d[C.ENV_ROCR_VISIBLE]          # compat keys
+    assert d[C.ENV_MPS_THREADS] == "25"
+
+
+def test_binpack_fills_one_gpu_first_and_spread_policy():
+    fc, s, ledger, _ = world()
+    for i in range(4):
+        fc.create("pods", O.make_pod(f"p{i}", gpu_cu=64))
+    s.schedule_pending()
+    used = {st.device.gpu for st in ledger.devices("node-a") if st.pods}
+    assert len(used) == 1
+    fc2, s2, ledger2, _ = world(args={"pack": "spread"})
+    for i in range(4):
+        fc2.create("pods", O.make_pod(f"p{i}", gpu_cu=64))
+    s2.schedule_pending()
+    assert len({st.device.gpu for st in ledger2.devices("node-a") if st.pods}) == 4
+
+
+def test_telemetry_steers_away_from_busy_gpu():
+    fc, s, ledger, tele = world(args={"pack": "spread", "w_pack": 0.0, "w_telemetry": 1.0})
+    devs = ledger.devices("node-a")
+    for st in devs:
+        tele.update("node-a", st.device.uuid, DeviceSample(gfx_activity=0.9 if st.device.gpu != 5 else 0.05))
+    fc.create("pods", O.make_pod("p", gpu_cu=64))
+    s.schedule_pending()
+    assert [st.device.gpu for st in ledger.devices("node-a") if st.pods] == [5]
+
+
+def test_config4_quad_on_numa_local_clique():
+    fc, s, ledger, _ = world()
+    fc.create("pods", O.make_pod("frac", gpu_cu=32))          # lands on GPU 0 (binpack)
+    fc.create("pods", O.make_pod("quad", gpus=4))
+    res = s.schedule_pending()
+    assert all(r.status.ok for r in res)
+    quad = sorted(st.device.gpu for st in ledger.devices("node-a") if "default/quad" in st.pods)
+    assert quad == [4, 5, 6, 7]                                   # the only whole free NUMA domain
+    env = O.annotations(fc.get("pods", "quad", "default"))[C.ANNOT_DEVICES].split(",")
+    assert len(env) == 4
+    fc.create("pods", O.make_pod("quad2", gpus=4))
+    (r,) = s.schedule_pending()
+    assert not r.status.ok                                        # GPU 0 has a fractional resident
+
+
+def test_topology_selection_rules():
+    t = Topology.fully_connected(8)
+    assert select_gpu_set(t, range(8), 4)[0] == [0, 1, 2, 3]
+    assert select_gpu_set(t, [1, 2, 4, 5, 6, 7], 2)[0] == [1, 2]  # best fit: smaller domain
+    t.link_type[0][1] = t.link_type[1][0] = "PCIE"
+    assert 1 not in select_gpu_set(t, [0, 1, 2, 3], 3)[0] or 0 not in select_gpu_set(t, [0, 1, 2, 3], 3)[0]
+    assert select_gpu_set(t, [0, 1], 2) is None
+
+
+def test_bind_failure_unreserves_and_requeues():
+    fc, s, ledger, _ = world()
+    fc.fail_next("bind", "pods", Conflict("apiserver says no"))
+    fc.create("pods", O.make_pod("p", gpu_cu=128))
+    (r,) = s.schedule_pending()
+    assert not r.status.ok and s.stats["bind_failures"] == 1
+    assert all(not st.pods for st in ledger.devices("node-a"))   # unreserved
+    assert ledger.placement("default/p") is None
+    s.queue.initial_backoff_s = 0
+    s.queue.move_all_to_active_or_backoff()
+    res = s.schedule_pending()
+    assert res and res[0].status.ok
+
+
+def test_restart_recovers_reservations_from_annotations():
+    fc, s, ledger, _ = world()
+    for i in range(3):
+        fc.create("pods", O.make_pod(f"p{i}", gpu_cu=64, gpu_mem_gib=8))
+    s.schedule_pending()
+    before = json.loads(ledger.snapshot_json())
+    # a fresh scheduler (process restart) rebuilds the ledger from pod annotations
+    ledger2 = DeviceLedger()
+    s2 = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False,
+                   extras={"ledger": ledger2, "telemetry": TelemetryCache()})
+    s2.start_informers()
+    assert json.loads(ledger2.snapshot_json()) == before
+    # finished pods release capacity
+    fc.set_pod_phase("default", "p0", "Succeeded")
+    assert ledger2.placement("default/p0") is None
+
+
+def test_slo_objective_prefers_tight_fit():
+    """With predictions, a pod goes where its predicted throughput just exceeds its SLO
+    (the reference objective) -- here: the device whose resident interferes
+    least."""
+    from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, _Tab
+    cp = CachedPredictions()
+    cp._conf = _Tab(["wl_a", "wl_b"], ["4P_MI355X"], [[100.0], [100.0]], "t")
+    cp._intf = _Tab(["wl_a", "wl_b"], ["wl_a", "wl_b"], [[30.0, 1.0], [1.0, 30.0]], "t")
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n", gpus=2))
+    s = Scheduler(fc, default_gpu_config({"w_pack": 0.0, "w_telemetry": 0.0}), full_registry(),
+                  bind_async=False, extras={"predictions": cp})
+    s.start_informers()
+    fc.create("pods", O.make_pod("wl-a-1", gpu_cu=64, slo=60))
+    fc.create("pods", O.make_pod("wl-b-1", gpu_cu=64, slo=60))
+    s.schedule_pending()
+    plugin = s.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+    g = {k: plugin.ledger.placement(k)[1][0] for k in ("default/wl-a-1", "default/wl-b-1")}
+    # second pod of type a should join the device of b (cross interference 1 vs 30)
+    fc.create("pods", O.make_pod("wl-a-2", gpu_cu=64, slo=60))
+    s.schedule_pending()
+    assert plugin.ledger.placement("default/wl-a-2")[1][0] == g["default/wl-b-1"] != g["default/wl-a-1"] \
+        or g["default/wl-a-1"] == g["default/wl-b-1"]
