@@ -244,9 +244,27 @@ def priority(pod: Obj) -> int:
     return int(pod.get("spec", {}).get("priority") or 0)
 
 
+_REQ_CACHE: Dict[str, Dict[str, float]] = {}
+
+
 def pod_requests(pod: Obj) -> Dict[str, float]:
     """Sum of container requests (limits used when a request is missing, as for extended
-    resources) -- the NodeResourcesFit view of a pod."""
+    resources) -- the NodeResourcesFit view of a pod.  Container resources are immutable
+    after creation, so the parse is memoised per pod UID (treat the result as read-only)."""
+    u = pod.get("metadata", {}).get("uid")
+    if u:
+        hit = _REQ_CACHE.get(u)
+        if hit is not None:
+            return hit
+        if len(_REQ_CACHE) > 200000:
+            _REQ_CACHE.clear()
+        tot = _pod_requests(pod)
+        _REQ_CACHE[u] = tot
+        return tot
+    return _pod_requests(pod)
+
+
+def _pod_requests(pod: Obj) -> Dict[str, float]:
     tot: Dict[str, float] = {}
     for c in containers(pod):
         res = c.get("resources") or {}

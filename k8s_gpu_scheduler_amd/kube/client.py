@@ -158,11 +158,12 @@ class FakeCluster(KubeClient):
         O.meta(obj)["resourceVersion"] = str(rv)
 
     def _emit(self, resource: str, typ: str, obj: Obj) -> None:
-        # One immutable snapshot is shared by the history, every inline subscriber and
-        # every watch queue: like client-go's shared informer cache, consumers must treat
-        # watched objects as read-only (the store itself keeps its own copy).
-        snap = O.deepcopy(obj)
-        ev = WatchEvent(type=typ, object=snap)
+        # Copy-on-write store: every mutation installs a NEW object and never touches a
+        # stored one in place, so the stored object itself is shared (no copy) by the
+        # history, every inline subscriber and every watch queue.  Like client-go's shared
+        # informer cache, consumers must treat watched objects as read-only; get()/list()
+        # still hand out private copies.
+        ev = WatchEvent(type=typ, object=obj)
         h = self._history[resource]
         h.append((int(O.resource_version(obj) or self._cur_rv), ev))
         if len(h) > self._history_len:

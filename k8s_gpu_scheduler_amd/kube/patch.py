@@ -120,18 +120,27 @@ def apply_json_patch(doc: Any, ops: List[Dict[str, Any]]) -> Any:
 
 
 def apply_merge_patch(doc: Any, patch: Any) -> Any:
-    """RFC 7386: null deletes, dicts merge recursively, everything else replaces."""
+    """RFC 7386: null deletes, dicts merge recursively, everything else replaces.
+    Returns a new document (the input is copied once, then merged in place)."""
     if not isinstance(patch, dict):
         return _dc(patch)
     out = _dc(doc) if isinstance(doc, dict) else {}
+    _merge_into(out, patch)
+    return out
+
+
+def _merge_into(out: Dict[str, Any], patch: Dict[str, Any]) -> None:
     for k, v in patch.items():
         if v is None:
             out.pop(k, None)
         elif isinstance(v, dict):
-            out[k] = apply_merge_patch(out.get(k, {}), v)
+            cur = out.get(k)
+            if not isinstance(cur, dict):
+                cur = {}
+                out[k] = cur
+            _merge_into(cur, v)
         else:
             out[k] = _dc(v)
-    return out
 
 
 # --------------------------------------------------------------------------- selectors

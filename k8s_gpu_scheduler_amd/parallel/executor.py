@@ -133,6 +133,12 @@ class DeviceExecutor:
             self._last_events = new_events
         self.epoch_runs.append(runs)
 
+    def wait_epoch(self, runs: List[PodRun]) -> None:
+        """Host-wait until every pod of an epoch finished (its end events)."""
+        for r in runs:
+            if r.end is not None:
+                r.end.synchronize()
+
     def join_current(self) -> None:
         """Make the default stream wait for all enqueued work (no host sync)."""
         cur = torch.cuda.current_stream(self.device)

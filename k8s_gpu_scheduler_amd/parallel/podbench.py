@@ -120,10 +120,12 @@ class ControlPlane:
         results = self.sched.schedule_pending()
         arr = np.full((len(pods), FIELDS), -1, dtype=np.int32)
         byname = {p["name"]: p for p in pods}
+        dropped = []
         for i, r in enumerate(results):
             ns, name = r.pod_key.split("/", 1)
             if not r.node:
                 self.unscheduled += 1
+                dropped.append((ns, name))
                 continue
             pl = self.ledger.placement(r.pod_key)
             if pl is None:
@@ -134,17 +136,20 @@ class ControlPlane:
             p = byname[name]
             arr[i] = (self.uuid_to_gpu[uuid], u0, n, W.INDEX[p["workload"]], self.iters, int(p["slo"] * 1000))
             self.live.append((ns, name))
-        self.queue_drop()
+        self.queue_drop(dropped)
         self.epoch += 1
         self.sched_s += time.perf_counter() - t0
         return arr
 
-    def queue_drop(self) -> None:
+    def queue_drop(self, dropped: List[Tuple[str, str]]) -> None:
         # pods that did not fit are dropped at the end of the epoch (arrivals are
         # re-drawn next epoch; counted in `unscheduled`)
-        for p in list(self.fc.list("pods")[0]):
-            if not O.node_name_of(p):
-                self.fc.delete("pods", O.name(p), O.namespace(p))
+        for ns, name in dropped:
+            self.sched.queue.delete({"metadata": {"name": name, "namespace": ns}})
+            try:
+                self.fc.delete("pods", name, ns)
+            except Exception:
+                pass
 
     def update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
         """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib)."""
@@ -165,6 +170,9 @@ class SimExecutor:
         self.pending: List[Any] = []
 
     def warm(self, runs) -> None:
+        pass
+
+    def wait_epoch(self, runs) -> None:
         pass
 
     def launch_epoch(self, runs) -> None:
@@ -201,7 +209,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pods-per-gpu", type=int, default=4)
-    ap.add_argument("--iters", type=int, default=6, help="iterations (query batches) per pod")
+    ap.add_argument("--iters", type=int, default=20, help="iterations (query batches) per pod")
     ap.add_argument("--policy", default="gpu", choices=["gpu", "random"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--sim", action="store_true", help="no GPU: simulated executor")
@@ -246,54 +254,64 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         from .executor import PodRun
         ex.warm([PodRun(0, wl, u, 2, 1) for wl in W.NAMES for u in (0, 2, 4, 6)])
 
-    nxt = cp.schedule_epoch() if rank == 0 else None
-    totals = {"pods": 0.0, "busy_unit_ms": 0.0, "slo_ok": 0.0, "flops": 0.0}
-    t_start = None
-    total_steps = a.warmup + a.steps
-    for step in range(total_steps):
-        if step == a.warmup:
-            if world > 1:
-                dist.barrier()
-            if use_gpu:
-                torch.cuda.synchronize()
-            t_start = time.perf_counter()
-            for k in totals:
-                totals[k] = 0.0
-            flops0 = ex.flops_done
-            if rank == 0:
-                cp.sched_s = 0.0
-                cp.unscheduled = 0
-        arr = bcast(nxt)
-        runs: List[Any] = []
-        for g in gpus_here:
-            runs += _runs_for(arr, g)
-        ex.launch_epoch(runs)
-        if rank == 0:
-            cp.finish_live()
-            nxt = cp.schedule_epoch()          # overlaps the GPU epoch
-        if use_gpu:
-            torch.cuda.synchronize()
+    totals = {"pods": 0.0, "busy_unit_ms": 0.0, "slo_ok": 0.0}
+    state: Dict[str, Any] = {"next": cp.schedule_epoch() if rank == 0 else None}
+
+    def collect(runs: List[Any], arr: np.ndarray, timed: bool) -> None:
+        ex.wait_epoch(runs)
         st = ex.collect(runs)
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
         tele.copy_(torch.tensor([st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm], dtype=torch.float64))
         if world > 1:
             dist.all_gather(tele_all, tele)
             per_gpu = torch.stack(tele_all).cpu().numpy()
+        elif not use_gpu and n_gpus > 1:
+            # single-process simulation of several GPUs: split by gpu id
+            per_gpu = np.zeros((n_gpus, 4))
+            for r in runs:
+                g = int(arr[r.pod_id][0])
+                per_gpu[g] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
+                               W.CATALOG[r.workload].hbm_gib)
         else:
             per_gpu = tele.cpu().numpy()[None, :]
-            if not use_gpu and n_gpus > 1:
-                # single-process simulation of several GPUs: split by gpu id
-                per_gpu = np.zeros((n_gpus, 4))
-                for r in runs:
-                    g = int(arr[r.pod_id][0])
-                    per_gpu[g] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0, W.CATALOG[r.workload].hbm_gib)
         if rank == 0:
             cp.update_telemetry(per_gpu, max(st["span_ms"], 1e-3))
-        if step >= a.warmup:
+        if timed:
             tot = per_gpu.sum(axis=0)
             totals["pods"] += tot[1]
             totals["busy_unit_ms"] += tot[0]
             totals["slo_ok"] += tot[2]
+
+    def run_epochs(count: int, timed: bool) -> None:
+        """Launch-ahead pipeline: epoch e is enqueued (device-side ordered behind e-1),
+        rank 0 schedules e+1 while the GPU runs, then e-1 is collected."""
+        pending: Optional[Tuple[List[Any], np.ndarray]] = None
+        for e in range(count):
+            arr = bcast(state["next"])
+            runs: List[Any] = []
+            for g in gpus_here:
+                runs += _runs_for(arr, g)
+            ex.launch_epoch(runs)
+            if rank == 0:
+                cp.finish_live()
+                state["next"] = cp.schedule_epoch()
+            if pending is not None:
+                collect(*pending, timed)
+            pending = (runs, arr)
+        if pending is not None:
+            collect(*pending, timed)
+
+    run_epochs(a.warmup, False)
+    if world > 1:
+        dist.barrier()
+    if use_gpu:
+        torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    flops0 = ex.flops_done
+    if rank == 0:
+        cp.sched_s = 0.0
+        cp.unscheduled = 0
+    run_epochs(a.steps, True)
     if world > 1:
         dist.barrier()
     if use_gpu:

@@ -149,7 +149,19 @@ class DeviceState:
         return self.device.hbm_gib - self.hbm_used
 
     def find_units(self, n: int) -> Optional[int]:
-        """Best-fit aligned run of n free units (alignment = next pow2 >= n)."""
+        """Best-fit aligned run of n free units (alignment = next pow2 >= n); memoised
+        until the unit map changes (the ledger invalidates on reserve/release)."""
+        cache = self.__dict__.setdefault("_fit", {})
+        if n in cache:
+            return cache[n]
+        r = self._find_units(n)
+        cache[n] = r
+        return r
+
+    def invalidate(self) -> None:
+        self.__dict__.pop("_fit", None)
+
+    def _find_units(self, n: int) -> Optional[int]:
         if n > len(self.used_units):
             return None
         align = 1
@@ -213,6 +225,7 @@ class DeviceLedger:
                     return False
             for uuid, u0, n, hbm, whole in allocs:
                 st = states[uuid]
+                st.invalidate()
                 for u in range(u0, u0 + n):
                     st.used_units[u] = True
                 st.hbm_used += hbm
@@ -235,6 +248,7 @@ class DeviceLedger:
                 if use is None:
                     continue
                 u0, n = use.units
+                st.invalidate()
                 for u in range(u0, u0 + n):
                     st.used_units[u] = False
                 st.hbm_used = max(0.0, st.hbm_used - use.hbm_gib)

@@ -49,6 +49,7 @@ Obj = Dict[str, Any]
 _REQ = "GPU/request"
 _PRED = "GPU/predictions"
 _CHOICE = "GPU/choice"
+_CANDS = "GPU/candidates"
 
 
 @dataclass
@@ -381,14 +382,21 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             return None
         if req.whole:
             return self._whole_choice(req, node, states)
-        cands: List[Tuple[DeviceState, int]] = []
-        for st in states:
-            if st.hbm_free + 1e-6 < req.hbm_gib:
-                continue
-            u0 = st.find_units(req.units)
-            if u0 is None:
-                continue
-            cands.append((st, u0))
+        memo = state.read(_CANDS)
+        if memo is None:
+            memo = {}
+            state.write(_CANDS, memo)
+        cands = memo.get(node)
+        if cands is None:
+            cands = []
+            for st in states:
+                if st.hbm_free + 1e-6 < req.hbm_gib:
+                    continue
+                u0 = st.find_units(req.units)
+                if u0 is None:
+                    continue
+                cands.append((st, u0))
+            memo[node] = cands      # Filter computes, Score reuses (same cycle snapshot)
         if not cands:
             return None
         if not scoring:

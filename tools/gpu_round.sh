@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU test round: pytest -m gpu, smoke, a rocprofv3 kernel-trace profile of the bench.
+# Steps are chained with && so nothing else touches the GPU after a failure.
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 &&
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 > gpurun_out/bench_prof.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log 2>/dev/null; grep '^{' gpurun_out/bench_prof.log 2>/dev/null | cut -c1-300
+exit $rc
