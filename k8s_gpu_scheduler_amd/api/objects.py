@@ -141,7 +141,8 @@ def make_pod(pod_name: str, *, ns: str = "default", scheduler: str = C.SCHEDULER
              env: Optional[Dict[str, str]] = None, annotations_: Optional[Dict[str, str]] = None,
              labels_: Optional[Dict[str, str]] = None, image: str = "busybox:latest",
              node_name: Optional[str] = None, phase: str = "Pending", priority: int = 0,
-             tolerations: Optional[List[Obj]] = None, node_selector: Optional[Dict[str, str]] = None) -> Obj:
+             tolerations: Optional[List[Obj]] = None, node_selector: Optional[Dict[str, str]] = None,
+             gpu_limits: bool = True) -> Obj:
     """Build a Pod in the shape the reference's e2e fixtures use
     (reference deploy/busybox/busybox.yaml:15-28: schedulerName, envFrom configMapRef, env SLO)."""
     envs = []
@@ -159,7 +160,7 @@ def make_pod(pod_name: str, *, ns: str = "default", scheduler: str = C.SCHEDULER
     container = {"name": "main", "image": image, "env": envs,
                  "envFrom": [{"configMapRef": {"name": cm}} for cm in config_maps],
                  "resources": {"requests": req, "limits": {k: v for k, v in req.items()
-                                                           if k.startswith("amd.com/")}}}
+                                                           if k.startswith("amd.com/") and gpu_limits}}}
     spec = {"schedulerName": scheduler, "containers": [container], "priority": priority}
     if node_name:
         spec["nodeName"] = node_name
@@ -284,6 +285,17 @@ def gpu_request(pod: Obj) -> Tuple[int, int, float]:
     r = pod_requests(pod)
     return (int(r.get(C.RESOURCE_GPU, 0)), int(r.get(C.RESOURCE_GPU_CU, 0)),
             float(r.get(C.RESOURCE_GPU_MEM, 0.0)))
+
+
+def gpu_qos(pod: Obj) -> str:
+    """"Guaranteed" when the fractional CU request is also its limit (hard CU mask),
+    "Burstable" when only requested (accounted share, may use idle CUs) -- the
+    Kubernetes QoS rule applied to amd.com/gpu-cu."""
+    for c in containers(pod):
+        res = c.get("resources") or {}
+        if C.RESOURCE_GPU_CU in (res.get("requests") or {}) and C.RESOURCE_GPU_CU not in (res.get("limits") or {}):
+            return "Burstable"
+    return "Guaranteed"
 
 
 def wants_gpu(pod: Obj) -> bool:

@@ -1,0 +1,290 @@
+"""`gpu-sched` command line: every binary of the reference as one entry point.
+
+  gpu-sched scheduler   --config scheduler-config.yaml [--kubeconfig K] [--v 3]
+                        (reference: gpu-sched --config=/config/scheduler-config.yaml --v=3,
+                         deploy/scheduler.yaml:63-66; leader election from the config)
+  gpu-sched extender    --config ... --port 8888   (kube-scheduler extender front-end)
+  gpu-sched recommender --port 50051               (reference recom_server.py; env
+                         CONFIGURATIONS_DATA_PATH / INTERFERENCE_DATA_PATH / PORT / JOB_DELAY)
+  gpu-sched agent       --node $NODE_NAME          (reference profiler DaemonSet)
+  gpu-sched redisctl    -l/--list -f/--flush -c/--config   (reference redisCtl.go:22-26)
+  gpu-sched devquery                               (reference gpu_profiling.cpp, all devices)
+  gpu-sched profile     (measure the MI355X configuration/interference tables)
+  gpu-sched bench       (pod-arrival benchmark; same as bench.py)
+  gpu-sched fake-cluster --port 6443               (HTTP fake apiserver for local runs)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import signal
+import socket
+import sys
+import threading
+import time
+from typing import List, Optional
+
+from ..api import constants as C
+
+
+def _client(kubeconfig: str = "", fake_url: str = ""):
+    from ..kube.rest import RestClient, RestConfig
+    if fake_url:
+        return RestClient(RestConfig(fake_url))
+    return RestClient.auto(kubeconfig)
+
+
+def _endpoints(args, client):
+    from ..utils.discovery import Endpoints
+    ep = Endpoints.from_env()
+    if getattr(args, "redis", ""):
+        ep.redis = args.redis
+    if getattr(args, "recommender", ""):
+        ep.recommender = args.recommender
+    if not (ep.redis and ep.recommender) and not getattr(args, "no_discovery", False):
+        try:
+            ep.discover(client)
+        except Exception as e:
+            logging.warning("service discovery failed: %s", e)
+    return ep
+
+
+def _build_scheduler(args, client):
+    from ..framework.config import default_gpu_config, load_config
+    from ..framework.scheduler import Scheduler
+    from ..plugins import full_registry
+    cfg = load_config(args.config) if args.config else default_gpu_config({})
+    ep = _endpoints(args, client)
+    for prof in cfg.profiles:
+        gargs = prof.plugin_config.setdefault(C.PLUGIN_NAME, {})
+        if ep.redis and not gargs.get("redis"):
+            gargs["redis"] = ep.redis
+            gargs.setdefault("redis_password", ep.redis_password)
+        if ep.recommender and not gargs.get("recommender"):
+            gargs["recommender"] = ep.recommender
+    return cfg, Scheduler(client, cfg, full_registry())
+
+
+def cmd_scheduler(args) -> int:
+    from ..kube.leader import LeaderElector
+    client = _client(args.kubeconfig, args.fake_apiserver)
+    cfg, sched = _build_scheduler(args, client)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *a: stop.set())
+    if cfg.leader_election.leader_elect:
+        le = cfg.leader_election
+        ident = f"{socket.gethostname()}_{os.getpid()}"
+        elector = LeaderElector(client, le.resource_name, le.resource_namespace, ident, le.lease_duration_s,
+                                le.renew_deadline_s, le.retry_period_s, on_started_leading=sched.start,
+                                on_stopped_leading=stop.set)
+        elector.start()
+    else:
+        sched.start()
+    try:
+        while not stop.is_set():
+            stop.wait(1.0)
+    except KeyboardInterrupt:
+        pass
+    sched.stop()
+    return 0
+
+
+def cmd_extender(args) -> int:
+    from ..framework.extender import Extender, ExtenderServer
+    client = _client(args.kubeconfig, args.fake_apiserver)
+    _, sched = _build_scheduler(args, client)
+    sched.start_informers()
+    srv = ExtenderServer(Extender(sched), "0.0.0.0", args.port).start()
+    logging.info("extender listening on %s", srv.url)
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        srv.stop()
+    return 0
+
+
+def cmd_recommender(args) -> int:
+    from ..recommender.service import RecommenderService
+    svc = RecommenderService.from_env(kind=args.model)
+    if args.redis:
+        from ..store import schema
+        from ..store.resp import Redis
+        r = Redis.connect(args.redis, args.redis_password)
+        svc.history_source = lambda pod: schema.read_history(r, pod)
+    svc.train()
+    svc.start_retrain_loop()
+    port = int(os.getenv("PORT", args.port))
+    server, bound = svc.make_server(port, args.workers)
+    logging.info("recommender serving on :%d", bound)
+    server.wait_for_termination()
+    return 0
+
+
+def cmd_agent(args) -> int:
+    from ..agent.agent import NodeAgent
+    from ..agent.devices import best_source, synthetic_node
+    from ..store.resp import Redis
+    from ..telemetry.exporter import GpuExporter
+    node = args.node or os.getenv("NODE_NAME") or socket.gethostname()
+    client = None
+    try:
+        client = _client(args.kubeconfig, args.fake_apiserver)
+    except Exception as e:
+        logging.warning("no apiserver access (%s); partition reconcile disabled", e)
+    ep = _endpoints(args, client) if client is not None else None
+    addr = args.redis or (ep.redis if ep else "")
+    if not addr:
+        logging.error("Redis not found")
+        return 1
+    redis = Redis.connect(addr, args.redis_password)
+    src = synthetic_node(args.synthetic, node=node) if args.synthetic else best_source()
+    exp = GpuExporter(node, os.getenv("POD_NAME", "amd-gpu-exporter"), dcgm_compat=args.dcgm_compat)
+    if args.metrics_port:
+        exp.serve(args.metrics_port)
+    agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp)
+    if args.once:
+        agent.step()
+        return 0
+    agent.run()
+    return 0
+
+
+def cmd_redisctl(args) -> int:
+    """List every key/value and/or flush (reference redisCtl.go:21-80)."""
+    from ..store.resp import Redis
+    addr = args.redis
+    if not addr:
+        client = _client(args.config)
+        ep = _endpoints(args, client)
+        addr = ep.redis
+    if not addr:
+        print("Redis not found", file=sys.stderr)
+        return 1
+    r = Redis.connect(addr, args.redis_password)
+    if args.list:
+        for k in r.get_keys():
+            try:
+                print(f"{k}: {r.get(k)}")
+            except Exception:
+                print(f"{k}: <{r.backend.execute('TYPE', k) if hasattr(r.backend, 'execute') else 'non-string'}>")
+    if args.flush:
+        r.flush()
+    return 0
+
+
+def cmd_devquery(args) -> int:
+    from .. import _native
+    h = _native.hip(required=False)
+    out = {"hip": h.query_all() if h is not None else [], "smi": None}
+    s = _native.smi()
+    if s is not None:
+        x = s.Smi()
+        if x.init():
+            out["smi"] = {"devices": x.devices(), "topology": x.topology(), "samples": x.sample()}
+            x.shutdown()
+        else:
+            out["smi"] = {"error": x.error()}
+    print(json.dumps(out, indent=1, default=str))
+    return 0
+
+
+def cmd_profile(args) -> int:
+    from ..models.profile import main as prof_main
+    return prof_main(args.rest)
+
+
+def cmd_bench(args) -> int:
+    from ..parallel.podbench import main as bench_main
+    bench_main(args.rest)
+    return 0
+
+
+def cmd_fake_cluster(args) -> int:
+    from ..api import objects as O
+    from ..kube.fake_apiserver import FakeApiServer
+    srv = FakeApiServer(port=args.port).start()
+    for i in range(args.nodes):
+        srv.cluster.create("nodes", O.make_node(f"mi355x-node-{i}", gpus=args.gpus))
+    print(srv.url, flush=True)
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        srv.stop()
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="gpu-sched", description="MI355X-native Kubernetes GPU scheduler")
+    p.add_argument("--v", type=int, default=2, help="log verbosity (klog style)")
+    sub = p.add_subparsers(dest="cmd", required=True)
+
+    def common(sp):
+        sp.add_argument("--kubeconfig", default="")
+        sp.add_argument("--fake-apiserver", default="", help="URL of a fake apiserver")
+        sp.add_argument("--redis", default="")
+        sp.add_argument("--redis-password", default=C.REDIS_PASSWORD)
+        sp.add_argument("--recommender", default="")
+        sp.add_argument("--no-discovery", action="store_true")
+
+    s = sub.add_parser("scheduler")
+    common(s)
+    s.add_argument("--config", default="")
+    s.set_defaults(fn=cmd_scheduler)
+    s = sub.add_parser("extender")
+    common(s)
+    s.add_argument("--config", default="")
+    s.add_argument("--port", type=int, default=8888)
+    s.set_defaults(fn=cmd_extender)
+    s = sub.add_parser("recommender")
+    s.add_argument("--port", type=int, default=C.RECOMMENDER_PORT)
+    s.add_argument("--workers", type=int, default=C.RECOMMENDER_WORKERS)
+    s.add_argument("--model", default="iterative", choices=["iterative", "svd", "als"])
+    s.add_argument("--redis", default="")
+    s.add_argument("--redis-password", default=C.REDIS_PASSWORD)
+    s.set_defaults(fn=cmd_recommender)
+    s = sub.add_parser("agent")
+    common(s)
+    s.add_argument("--node", default="")
+    s.add_argument("--poll", type=float, default=C.PROFILER_POLL_S)
+    s.add_argument("--metrics-port", type=int, default=9400)
+    s.add_argument("--dcgm-compat", action="store_true")
+    s.add_argument("--synthetic", type=int, default=0, help="fake N GPUs (no hardware)")
+    s.add_argument("--once", action="store_true")
+    s.set_defaults(fn=cmd_agent)
+    s = sub.add_parser("redisctl")
+    s.add_argument("-l", "--list", action="store_true", help="List redis' data")
+    s.add_argument("-f", "--flush", action="store_true", help="Flush redis database")
+    s.add_argument("-c", "--config", default=os.path.expanduser("~/.kube/config"), help="Kubernetes config path")
+    s.add_argument("--redis", default="")
+    s.add_argument("--redis-password", default=C.REDIS_PASSWORD)
+    s.add_argument("--no-discovery", action="store_true")
+    s.set_defaults(fn=cmd_redisctl)
+    s = sub.add_parser("devquery")
+    s.set_defaults(fn=cmd_devquery)
+    s = sub.add_parser("profile")
+    s.add_argument("rest", nargs=argparse.REMAINDER)
+    s.set_defaults(fn=cmd_profile)
+    s = sub.add_parser("bench")
+    s.add_argument("rest", nargs=argparse.REMAINDER)
+    s.set_defaults(fn=cmd_bench)
+    s = sub.add_parser("fake-cluster")
+    s.add_argument("--port", type=int, default=6443)
+    s.add_argument("--nodes", type=int, default=1)
+    s.add_argument("--gpus", type=int, default=8)
+    s.set_defaults(fn=cmd_fake_cluster)
+    return p
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = build_parser().parse_args(argv)
+    logging.basicConfig(level=logging.DEBUG if args.v >= 4 else logging.INFO if args.v >= 2 else logging.WARNING,
+                        format="%(asctime)s %(levelname).1s %(name)s] %(message)s")
+    return int(args.fn(args) or 0)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

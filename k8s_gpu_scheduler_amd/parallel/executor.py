@@ -3,9 +3,9 @@
 One process per GPU.  The executor receives the scheduler's placements for its device
 (pod id, workload, CU-slice unit range, iterations), runs each pod's kernel mix on a HIP
 stream whose CU mask is exactly the pod's CU slices (ops.cumask.MaskedStream), and measures
-per-pod device time with HIP events.  Epochs are ordered on the device by an event
-barrier (every stream of epoch t+1 waits for every stream of epoch t), so the scheduler's
-capacity model (units free when the previous epoch's pods finish) holds without host
+per-pod device time with HIP events.  Pods are ordered on the device per CU-slice unit
+(a pod waits for the previous occupant of each of its units), so the scheduler's
+capacity model (a unit is free when its previous pod finishes) holds without host
 synchronisation: the host can schedule epoch t+1 while the GPU executes epoch t.
 
 Working buffers are allocated once per (workload, slot) and reused -- a warm container.
@@ -31,6 +31,7 @@ class PodRun:
     n_units: int
     iters: int
     slo: float = 0.0
+    masked: bool = True          # Guaranteed QoS: hard CU mask; Burstable: accounted share only
     start: Optional[torch.cuda.Event] = None
     end: Optional[torch.cuda.Event] = None
     ms: float = 0.0
@@ -67,15 +68,16 @@ class DeviceExecutor:
         self._streams: Dict[Tuple[int, int], object] = {}
         self._bufs: Dict[Tuple[str, int, int], _Buffers] = {}
         self._last_events: List[torch.cuda.Event] = []
+        self._unit_last: Dict[int, Tuple[Tuple[int, int], torch.cuda.Event]] = {}
         self.epoch_runs: List[List[PodRun]] = []
         self.flops_done = 0.0
         self.bytes_done = 0.0
 
-    def stream_for(self, first_unit: int, n_units: int):
-        key = (first_unit, n_units)
+    def stream_for(self, first_unit: int, n_units: int, masked: bool = True):
+        key = (first_unit, n_units, masked)
         st = self._streams.get(key)
         if st is None:
-            if self.use_cu_masks:
+            if self.use_cu_masks and masked:
                 from ..ops.cumask import MaskedStream
                 st = MaskedStream(cu_slice_mask(first_unit, n_units), self.device)
             else:
@@ -94,43 +96,47 @@ class DeviceExecutor:
     def warm(self, placements: List[PodRun]) -> None:
         """Pre-create streams/buffers (outside any timed region)."""
         for p in placements:
-            self.stream_for(p.first_unit, p.n_units)
+            self.stream_for(p.first_unit, p.n_units, p.masked)
             self.buffers(CATALOG[p.workload], p.first_unit, p.n_units)
         torch.cuda.synchronize(self.device)
 
     def launch_epoch(self, runs: List[PodRun]) -> None:
-        """Enqueue one epoch's pods; returns immediately (async)."""
-        barrier = self._last_events
-        new_events: List[torch.cuda.Event] = []
-        by_stream: Dict[Tuple[int, int], List[PodRun]] = {}
+        """Enqueue one epoch's pods; returns immediately (async).
+
+        Ordering is per CU-slice unit, not per epoch: a pod waits (device-side) only for
+        the last pod that occupied any of ITS units on another stream; pods reusing the
+        same unit range share a stream and are ordered by it.  So a slot whose pod
+        finished early starts its next pod at once instead of idling until the slowest
+        pod of the epoch completes (work-conserving), while two pods never overlap on the
+        same CUs -- exactly the ledger's capacity model."""
         for r in runs:
-            by_stream.setdefault((r.first_unit, r.n_units), []).append(r)
-        for (u0, n), lst in by_stream.items():
-            st = self.stream_for(u0, n).stream
-            for ev in barrier:
-                st.wait_event(ev)
-            for r in lst:
-                w = CATALOG[r.workload]
-                bufs = self.buffers(w, u0, n)
-                r.start = torch.cuda.Event(enable_timing=True)
-                r.end = torch.cuda.Event(enable_timing=True)
-                r.start.record(st)
-                for _ in range(r.iters):
-                    for o, t in bufs.ops:
-                        if o.kind == "gemm":
-                            a, bt, bias, c = t
-                            loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st)
-                        else:
-                            x, y, z = t
-                            loadgen.triad(x, y, z, 1.0001, stream=st)
-                r.end.record(st)
-                self.flops_done += w.flops * r.iters
-                self.bytes_done += w.bytes * r.iters
-            done = torch.cuda.Event()
-            done.record(st)
-            new_events.append(done)
-        if new_events:
-            self._last_events = new_events
+            key = (r.first_unit, r.n_units, r.masked)
+            st = self.stream_for(*key).stream
+            waited = set()
+            for u in range(r.first_unit, r.first_unit + r.n_units):
+                last = self._unit_last.get(u)
+                if last is not None and last[0] != key and id(last[1]) not in waited:
+                    st.wait_event(last[1])
+                    waited.add(id(last[1]))
+            w = CATALOG[r.workload]
+            bufs = self.buffers(w, r.first_unit, r.n_units)
+            r.start = torch.cuda.Event(enable_timing=True)
+            r.end = torch.cuda.Event(enable_timing=True)
+            r.start.record(st)
+            for _ in range(r.iters):
+                for o, t in bufs.ops:
+                    if o.kind == "gemm":
+                        a, bt, bias, c = t
+                        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st)
+                    else:
+                        x, y, z = t
+                        loadgen.triad(x, y, z, 1.0001, stream=st)
+            r.end.record(st)
+            for u in range(r.first_unit, r.first_unit + r.n_units):
+                self._unit_last[u] = (key, r.end)
+            self.flops_done += w.flops * r.iters
+            self.bytes_done += w.bytes * r.iters
+        self._last_events = [ev for _, ev in {id(e): (k, e) for k, e in self._unit_last.values()}.values()]
         self.epoch_runs.append(runs)
 
     def wait_epoch(self, runs: List[PodRun]) -> None:

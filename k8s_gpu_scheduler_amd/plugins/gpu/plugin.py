@@ -60,6 +60,7 @@ class GpuRequest:
     hbm_gib: float = 0.0
     slo: float = 0.0
     gpu_pod: bool = False
+    burstable: bool = False
 
 
 @dataclass
@@ -68,6 +69,7 @@ class Choice:
     allocs: List[Tuple[str, int, int, float, bool]] = field(default_factory=list)  # uuid,u0,n,hbm,whole
     score: float = 0.0
     devices: List[Device] = field(default_factory=list)
+    burstable: bool = False
 
 
 @dataclass
@@ -193,7 +195,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
     def parse_request(self, pod: Obj) -> GpuRequest:
         g, cu, mem = O.gpu_request(pod)
         slo = O.pod_slo(pod)
-        r = GpuRequest(slo=slo, hbm_gib=mem)
+        r = GpuRequest(slo=slo, hbm_gib=mem, burstable=O.gpu_qos(pod) == "Burstable")
         if cu > 0:
             r.cu = min(cu, C.MI355X_CUS)
             r.units = max(1, math.ceil(r.cu / CUS_PER_XCD))
@@ -281,6 +283,8 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         choice = (state.read(_CHOICE) or {}).get(node_name)
         if choice is None:
             choice = self._best_choice(state, pod, req, node_name, scoring=True)
+        if choice is not None:
+            choice.burstable = req.burstable
         if choice is None or not self.ledger.reserve(node_name, O.key(pod), O.name(pod), req.slo, choice.allocs):
             return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
         state.write(_CHOICE + "/reserved", choice)
@@ -325,7 +329,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         idx = [str(devs[u].gpu) if u in devs else "" for u in uuids]
         env = {C.ENV_ROCR_VISIBLE: ",".join(uuids), C.ENV_HIP_VISIBLE: ",".join(i for i in idx if i)}
         frac = [a for a in choice.allocs if not a[4]]
-        if frac:
+        if frac and not choice.burstable:
             u, u0, n, hbm, _ = frac[0]
             d = devs.get(u)
             first = (d.first_xcd if d else 0) + u0

@@ -1,0 +1,167 @@
+"""Node agent (profiler) + REST client against the HTTP fake apiserver.
+
+Agent parity: publishes `<node>` -> JSON UUID list only when it changes (reference
+pkg/profiler/profile_gpu.sh:3-13), MIG/partition filtering, stdin protocol
+(reference pkg/profiler/test.sh); new: device descriptors/topology keys, async partition
+reconcile with taint/untaint, per-pod usage history.
+"""
+import json
+import time
+
+import pytest
+
+from k8s_gpu_scheduler_amd.agent.agent import NodeAgent, pod_of_pid, publish_from_stdin
+from k8s_gpu_scheduler_amd.agent.devices import StaticSource, parse_smi_list, synthetic_node
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+from k8s_gpu_scheduler_amd.kube.client import FakeCluster, NotFound
+from k8s_gpu_scheduler_amd.kube.fake_apiserver import FakeApiServer
+from k8s_gpu_scheduler_amd.kube.informer import SharedInformerFactory
+from k8s_gpu_scheduler_amd.kube.rest import RestClient, RestConfig
+from k8s_gpu_scheduler_amd.plugins import full_registry
+from k8s_gpu_scheduler_amd.store import schema
+from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+from k8s_gpu_scheduler_amd.store.resp import Redis
+
+
+def rds():
+    return Redis(FakeRedisBackend(FakeRedisEngine()))
+
+
+def test_parse_smi_listing():
+    txt = ("GPU 0: NVIDIA A30 (UUID: GPU-ac0112df-7098-6c59-5c4f-a57fa666f808)\n"
+           "  MIG 2g.12gb Device 0: (UUID: MIG-7a700938-2114-5d88-a93c-167c2a498910)\n")
+    assert parse_smi_list(txt) == ["GPU-ac0112df-7098-6c59-5c4f-a57fa666f808",
+                                   "MIG-7a700938-2114-5d88-a93c-167c2a498910"]
+
+
+def test_stdin_protocol_reference_fixture():
+    r = rds()
+    lines = ["1", "2", "3", "['GPU-ac0112df-7098-6c59-5c4f-a57fa666f808', 'MIG-7a700938-2114-5d88-a93c-167c2a498910',"
+                            " 'MIG-c8956631-ac65-59d3-9065-c8764799febf']"]
+    publish_from_stdin(lines, r)
+    assert json.loads(r.get("1")) == ["MIG-7a700938-2114-5d88-a93c-167c2a498910",
+                                      "MIG-c8956631-ac65-59d3-9065-c8764799febf"]
+
+
+def test_agent_publishes_on_change_only():
+    r = rds()
+    src = synthetic_node(8, node="n1")
+    ag = NodeAgent("n1", r, src)
+    assert ag.publish() and not ag.publish()
+    assert len(schema.read_uuids(r, "n1")) == 8
+    assert len(schema.read_devices(r, "n1")) == 8
+    assert json.loads(r.get(schema.topology_key("n1")))["n"] == 8
+    src.desc = src.desc[:7]                        # a GPU disappeared (reset / UUID change)
+    assert ag.publish() and len(schema.read_uuids(r, "n1")) == 7
+
+
+def test_agent_partition_reconcile_end_to_end():
+    """Label asks for CPX -> agent taints, applies, republishes 64 partition UUIDs,
+    untaints; the scheduler then sees 64 devices of 32 CUs."""
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=8))
+    r = rds()
+    src = synthetic_node(8, node="n1")
+    ag = NodeAgent("n1", r, src, client=fc)
+    ag.publish()
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "CPX"}}}, "merge")
+    assert ag.reconcile_partitions()
+    assert len(src.partition_calls) == 8 and ag.current_partition() == "CPX"
+    assert len(schema.read_uuids(r, "n1")) == 64
+    assert not O.node_taints(fc.get("nodes", "n1"))
+    assert json.loads(r.get(schema.partition_key("n1")))["state"] == "applied"
+    assert not ag.reconcile_partitions()           # idempotent
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, extras={"redis": r})
+    s.start_informers()
+    plugin = s.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+    devs = plugin.ledger.devices("n1")
+    assert len(devs) == 64 and all(d.device.cus == 32 for d in devs)
+    fc.create("pods", O.make_pod("p", gpus=1))
+    (res,) = s.schedule_pending()
+    assert res.status.ok
+
+
+def test_tainted_node_is_filtered():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=8, taints=[{"key": C.TAINT_PARTITIONING, "value": "CPX",
+                                                         "effect": "NoSchedule"}]))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False)
+    s.start_informers()
+    fc.create("pods", O.make_pod("p", gpu_cu=64))
+    (res,) = s.schedule_pending()
+    assert not res.status.ok
+
+
+def test_history_and_cgroup_attribution(tmp_path):
+    proc = tmp_path / "proc" / "4242"
+    proc.mkdir(parents=True)
+    (proc / "cgroup").write_text("0::/kubepods.slice/kubepods-burstable-pod1234abcd_5678_90ab_cdef_1234567890ab.slice/x\n")
+    assert pod_of_pid(4242, str(tmp_path / "proc")) == "1234abcd-5678-90ab-cdef-1234567890ab"
+
+    class Src(StaticSource):
+        def processes(self, index):
+            return [{"pid": 4242, "vram_bytes": 8 * 2**30, "cu_occupancy": 64}] if index == 0 else []
+    r = rds()
+    src = Src(synthetic_node(2).devices())
+    ag = NodeAgent("n1", r, src, pod_resolver=lambda pid: pod_of_pid(pid, str(tmp_path / "proc")))
+    n = ag.record_history({"1234abcd-5678-90ab-cdef-1234567890ab": "default/wl-pod"})
+    assert n == 1
+    h = schema.read_history(r, "default/wl-pod")
+    assert h[0]["hbm_gib"] == 8 and h[0]["cu_busy"] == 0.25
+
+
+@pytest.fixture()
+def api():
+    srv = FakeApiServer(token="t0k").start()
+    yield srv
+    srv.stop()
+
+
+def test_rest_client_crud_patch_bind_watch(api, tmp_path):
+    kc = api.kubeconfig(str(tmp_path / "kubeconfig"))
+    cl = RestClient(RestConfig.from_kubeconfig(kc))
+    cl.create("nodes", O.make_node("n1"))
+    cl.create("pods", O.make_pod("p1"), "default")
+    cl.create("configmaps", O.make_config_map("cm", {"a": "1"}), "default")
+    items, rv = cl.list("pods", "default")
+    assert [O.name(p) for p in items] == ["p1"] and rv
+    cl.patch("pods", "p1", [{"op": "add", "path": "/metadata/labels/x", "value": "y"}], "json", "default")
+    cl.patch("configmaps", "cm", {"data": {"b": "2"}}, "merge", "default")
+    assert cl.get("configmaps", "cm", "default")["data"] == {"a": "1", "b": "2"}
+    assert cl.list("pods", "default", label_selector="x=y")[0]
+    cl.bind("default", "p1", "n1")
+    assert O.node_name_of(cl.get("pods", "p1", "default")) == "n1"
+    assert cl.list("pods", None, field_selector="spec.nodeName=n1")[0]
+    with pytest.raises(NotFound):
+        cl.get("pods", "nope", "default")
+    evs = []
+    for ev in cl.watch("configmaps", "default", rv, timeout_s=1):
+        evs.append(ev["type"])
+        if len(evs) >= 1:
+            break
+    assert evs == ["MODIFIED"]
+    cl.delete("pods", "p1", "default", 0)
+    with pytest.raises(Exception):
+        RestClient(RestConfig(api.url, token="wrong")).list("pods", "default")
+
+
+def test_scheduler_over_rest_with_threaded_informers(api, tmp_path):
+    cl = RestClient(RestConfig(api.url, token="t0k"))
+    api.cluster.create("nodes", O.make_node("n1", gpus=8))
+    inf = SharedInformerFactory(cl)
+    s = Scheduler(cl, default_gpu_config({}), full_registry(), bind_async=True, informers=inf)
+    s.start()
+    try:
+        for i in range(6):
+            cl.create("pods", O.make_pod(f"p{i}", gpu_cu=64), "default")
+        deadline = time.time() + 20
+        while time.time() < deadline and len(api.cluster.bindings) < 6:
+            time.sleep(0.05)
+        assert len(api.cluster.bindings) == 6
+        ann = O.annotations(api.cluster.get("pods", "p0", "default"))
+        assert ann[C.ANNOT_DEVICES].startswith("GPU-")
+    finally:
+        s.stop()

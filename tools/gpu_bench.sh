@@ -5,8 +5,8 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 240 python bench.py --steps 20 --warmup 3 --out gpurun_out/b_default.json > gpurun_out/b_default.log 2>&1 &&
-timeout -k 10 240 python bench.py --steps 20 --warmup 3 --no-cu-mask --out gpurun_out/b_nomask.json > gpurun_out/b_nomask.log 2>&1 &&
+timeout -k 10 240 python bench.py --steps 20 --warmup 3 --qos guaranteed --out gpurun_out/b_guaranteed.json > gpurun_out/b_guaranteed.log 2>&1 &&
 timeout -k 10 240 python bench.py --steps 20 --warmup 3 --policy random --out gpurun_out/b_random.json > gpurun_out/b_random.log 2>&1
 rc=$?
-for f in gpurun_out/b_*.log; do echo "== $f"; grep '^{' $f | cut -c1-400; tail -2 $f | grep -v '^{'; done
+for f in gpurun_out/b_*.json; do echo "== $f"; python -c "import json,sys; d=json.load(open('$f')); print({k:d.get(k) for k in ['value','ms_per_step','gpu_util_pct','cu_share_occupancy_pct','mfma_util_pct','achieved_tflops','slo_attainment_pct','host_ms_per_step_rank0']})"; done
 exit $rc
