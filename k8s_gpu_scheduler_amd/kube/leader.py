@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import datetime as dt
 import logging
+import math
 import threading
 import time
 from typing import Callable, Optional
@@ -52,7 +53,7 @@ class LeaderElector:
 
     def try_acquire_or_renew(self) -> bool:
         now = _now()
-        spec = {"holderIdentity": self.identity, "leaseDurationSeconds": int(self.lease_duration_s),
+        spec = {"holderIdentity": self.identity, "leaseDurationSeconds": max(1, int(math.ceil(self.lease_duration_s))),
                 "renewTime": _fmt(now)}
         try:
             lease = self.client.get("leases", self.name, self.ns)

@@ -24,6 +24,7 @@ std::vector<uint32_t> probe_xcd(uintptr_t stream, int n);
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
                   int ldc, bool relu, uintptr_t stream);
 void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream);
+void set_triad_variant(int v);
 std::vector<int> peer_access_matrix();
 double peer_copy_gbps(int src, int dst, size_t bytes, int iters);
 }  // namespace gs

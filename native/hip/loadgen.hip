@@ -153,6 +153,54 @@ __global__ void __launch_bounds__(256) stream_triad_kernel(float4* __restrict__ 
   }
 }
 
+// Unrolled variant: each thread moves U float4 per trip with all loads issued before
+// any store (U outstanding 16-B loads per stream per lane), block-contiguous so every
+// load instruction is one coalesced 1 KiB wave access; NT selects non-temporal
+// (streaming) loads/stores so the one-touch stream does not evict L2/MALL lines.
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) stream_triad_u(float4* __restrict__ a_, const float4* __restrict__ b_,
+                                                      const float4* __restrict__ c_, float s, size_t n4) {
+  auto a = reinterpret_cast<f32x4*>(a_);
+  auto b = reinterpret_cast<const f32x4*>(b_);
+  auto c = reinterpret_cast<const f32x4*>(c_);
+  const size_t tile = (size_t)blockDim.x * U;
+  const size_t step = (size_t)gridDim.x * tile;
+  for (size_t base = (size_t)blockIdx.x * tile + threadIdx.x; base < n4; base += step) {
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const size_t i = base + (size_t)k * blockDim.x;
+      if (i < n4) {
+        if (NT) {
+          x[k] = __builtin_nontemporal_load(b + i);
+          y[k] = __builtin_nontemporal_load(c + i);
+        } else {
+          x[k] = b[i];
+          y[k] = c[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const size_t i = base + (size_t)k * blockDim.x;
+      if (i < n4) {
+        const f32x4 r = x[k] + s * y[k];
+        if (NT)
+          __builtin_nontemporal_store(r, a + i);
+        else
+          a[i] = r;
+      }
+    }
+  }
+}
+
+static int g_triad_variant = 3;
+
+void set_triad_variant(int v) {
+  if (v < 0 || v > 5) throw std::runtime_error("triad variant must be 0..5");
+  g_triad_variant = v;
+}
+
 static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
@@ -188,9 +236,19 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
   check_align(reinterpret_cast<void*>(b), "b");
   check_align(reinterpret_cast<void*>(c), "c");
   if (blocks <= 0) blocks = 2048;
-  hipLaunchKernelGGL(stream_triad_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<float4*>(a), reinterpret_cast<const float4*>(b),
-                     reinterpret_cast<const float4*>(c), s, n_floats / 4);
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  auto A = reinterpret_cast<float4*>(a);
+  auto B = reinterpret_cast<const float4*>(b);
+  auto Cc = reinterpret_cast<const float4*>(c);
+  const size_t n4 = n_floats / 4;
+  switch (g_triad_variant) {
+    case 0: hipLaunchKernelGGL(stream_triad_kernel, dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 1: hipLaunchKernelGGL((stream_triad_u<2, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 2: hipLaunchKernelGGL((stream_triad_u<4, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 3: hipLaunchKernelGGL((stream_triad_u<4, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 4: hipLaunchKernelGGL((stream_triad_u<8, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    default: hipLaunchKernelGGL((stream_triad_u<2, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+  }
   HIP_CHECK(hipGetLastError());
 }
 
