@@ -13,7 +13,7 @@ import torch
 
 from .. import _native
 
-BM, BN, BK = 128, 128, 64
+BM, BN, BK = 64, 64, 64          # minimum granularity; the tile (128x128 / 64x128 / 64x64) is picked per shape
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> int:

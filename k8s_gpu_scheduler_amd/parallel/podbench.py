@@ -55,12 +55,31 @@ NODE = "mi355x-node-0"
 FIELDS = 7    # gpu, first_unit, n_units, workload_id, iters, slo_milli, masked
 
 
+DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
+
+
 def analytic_predictions() -> CachedPredictions:
     idx, cols, conf, icols, intf = W.analytic_tables()
     cp = CachedPredictions()
     cp._conf = _Tab(idx, cols, conf, "analytic")
     cp._intf = _Tab(idx, icols, intf, "analytic")
     return cp
+
+
+def measured_predictions(data_dir: str = DATA_DIR) -> Optional[CachedPredictions]:
+    """Predictions from the MI355X tables measured by models.profile (completed by the
+    recommender's imputer when sparse); None if they have not been produced yet."""
+    cpath = os.path.join(data_dir, "configurations_mi355x.tsv")
+    ipath = os.path.join(data_dir, "interference_mi355x.tsv")
+    if not (os.path.isfile(cpath) and os.path.isfile(ipath)):
+        return None
+    from ..recommender.tables import Table, TrainedTable
+    conf, intf = Table.read_tsv(cpath), Table.read_tsv(ipath)
+    if set(conf.index) != set(W.NAMES):
+        return None
+    kind = "iterative" if np.isnan(intf.values).any() or np.isnan(conf.values).any() else "svd"
+    return CachedPredictions(conf=TrainedTable.fit(conf, kind, "measured"),
+                             intf=TrainedTable.fit(intf, kind, "measured"))
 
 
 class ControlPlane:
@@ -77,7 +96,7 @@ class ControlPlane:
         self.fc.create("nodes", O.make_node(NODE, gpus=n_gpus))
         self.telemetry = TelemetryCache(stale_s=0)
         self.ledger = DeviceLedger()
-        self.predictions = predictions or analytic_predictions()
+        self.predictions = predictions or measured_predictions() or analytic_predictions()
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "pack": "binpack", "compat_env": False}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})

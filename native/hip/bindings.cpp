@@ -53,6 +53,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("stream_triad", &gs::stream_triad, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("s"),
         py::arg("n_floats"), py::arg("blocks"), py::arg("stream"), py::call_guard<py::gil_scoped_release>());
   m.def("set_triad_variant", &gs::set_triad_variant, py::arg("variant"));
+  m.def("set_gemm_tile", &gs::set_gemm_tile, py::arg("tile"));
+  m.def("pick_gemm_tile", &gs::pick_gemm_tile, py::arg("M"), py::arg("N"));
   m.def("peer_access_matrix", &gs::peer_access_matrix);
   m.def("peer_copy_gbps", &gs::peer_copy_gbps, py::arg("src"), py::arg("dst"), py::arg("bytes"),
         py::arg("iters") = 10, py::call_guard<py::gil_scoped_release>());

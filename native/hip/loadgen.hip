@@ -24,24 +24,25 @@ namespace gs {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BK = 64;
 constexpr int THREADS = 256;
-constexpr int TILE_BYTES = BM * BK * 2;                 // 16 KiB per operand tile
-constexpr int LDS_BYTES = 2 /*bufs*/ * 2 /*A,B*/ * TILE_BYTES;   // 64 KiB
 constexpr int GROUP_M = 8;
 
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
-// Issue the glds for one 128x64 bf16 tile (rows [r0, r0+128), k [k0, k0+64)) of a
+// Issue the glds for one ROWSx64 bf16 tile (rows [r0, r0+ROWS), k [k0, k0+64)) of a
 // row-major matrix with leading dimension ld (elements).  Logical 16-byte chunk kc of row
 // r lands at physical chunk kc ^ ((r >> 1) & 7) of that row's 128-byte LDS line; the LDS
 // image itself is lane-linear (glds requirement), so the swizzle is applied on the
 // per-lane SOURCE address (rule: linear dest + permuted source + same permutation on read).
+// With two 128-B rows per 256-B bank row, lanes 0-15 of a ds_read_b128 (rows r..r+15,
+// same logical chunk) then hit 16 distinct 16-B slots: conflict-free.
+template <int ROWS>
 __device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld, int r0, int k0,
                                            char* lds_tile, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < TILE_BYTES / 16 / THREADS; ++i) {     // 4 rounds
+  for (int i = 0; i < ROWS * BK * 2 / 16 / THREADS; ++i) {
     const int chunk = i * THREADS + wave * 64 + lane;
     const int r = chunk >> 3;
     const int p = chunk & 7;
@@ -57,11 +58,16 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds_tile, int row, int kc
   return *reinterpret_cast<const bf16x8*>(lds_tile + row * (BK * 2) + phys * 16);
 }
 
-template <bool RELU, bool BIAS>
+// Block tile BM x BN (64 or 128 each), 4 waves as 2x2, each wave (BM/2) x (BN/2) =
+// MI x NJ MFMA 16x16 tiles.  Small tiles exist so that the small-M GEMMs of the workload
+// catalog still launch >= 256 workgroups (one per CU) instead of idling half the chip.
+template <int BM, int BN, bool RELU, bool BIAS>
 __global__ void __launch_bounds__(THREADS, 2)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int MI = BM / 32, NJ = BN / 32;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
 
   // ---- XCD-aware bijective remap, then grouped (GROUP_M) tile order ----------------
   const int nwg = gridDim.x;
@@ -82,42 +88,42 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   const int lane = threadIdx.x & (kWave - 1);
   const int wm = wave >> 1, wn = wave & 1;
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto tileA = [&](int buf) { return smem + buf * 2 * TILE_BYTES; };
-  auto tileB = [&](int buf) { return smem + buf * 2 * TILE_BYTES + TILE_BYTES; };
+  auto tileA = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES); };
+  auto tileB = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES) + A_BYTES; };
 
   const int nt = K / BK;
-  stage_tile(A, lda, m0, 0, tileA(0), wave, lane);
-  stage_tile(Bt, ldb, n0, 0, tileB(0), wave, lane);
+  stage_tile<BM>(A, lda, m0, 0, tileA(0), wave, lane);
+  stage_tile<BN>(Bt, ldb, n0, 0, tileB(0), wave, lane);
   __syncthreads();
 
   const int frow = lane & 15;
   const int fk = lane >> 4;
   int buf = 0;
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) {
-      stage_tile(A, lda, m0, (t + 1) * BK, tileA(buf ^ 1), wave, lane);
-      stage_tile(Bt, ldb, n0, (t + 1) * BK, tileB(buf ^ 1), wave, lane);
+    if (t + 1 < nt) {   // issue tile t+1 before the MFMAs of tile t
+      stage_tile<BM>(A, lda, m0, (t + 1) * BK, tileA(buf ^ 1), wave, lane);
+      stage_tile<BN>(Bt, ldb, n0, (t + 1) * BK, tileB(buf ^ 1), wave, lane);
     }
     const char* a_t = tileA(buf);
     const char* b_t = tileB(buf);
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[4], bf[4];
+      bf16x8 af[MI], bf[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = lds_frag(a_t, wm * 64 + i * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < MI; ++i) af[i] = lds_frag(a_t, wm * (BM / 2) + i * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = lds_frag(b_t, wn * 64 + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < NJ; ++j) bf[j] = lds_frag(b_t, wn * (BN / 2) + j * 16 + frow, kk * 4 + fk);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -125,16 +131,16 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
     buf ^= 1;
   }
 
-  // ---- epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r -------------------
+  // ---- epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r; fused bias + ReLU --
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn * 64 + j * 16 + frow;
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + wn * (BN / 2) + j * 16 + frow;
       const float bv = BIAS ? bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + fk * 4 + r;
+        const int row = m0 + wm * (BM / 2) + i * 16 + fk * 4 + r;
         float v = acc[i][j][r] + bv;
         if (RELU) v = v > 0.f ? v : 0.f;
         C[(size_t)row * ldc + col] = (__bf16)v;
@@ -194,10 +200,13 @@ __global__ void __launch_bounds__(256) stream_triad_u(float4* __restrict__ a_, c
   }
 }
 
-static int g_triad_variant = 3;
+// 6 = auto: working set (3 arrays) <= 96 MiB -> cached 2x-unrolled loads (the stream
+// stays in the 256 MiB Infinity Cache across iterations: 7.1 TB/s measured), larger ->
+// non-temporal 4x (6.5 TB/s vs 6.1 for torch.add) -- profiles/r01_kernel_bench.json.
+static int g_triad_variant = 6;
 
 void set_triad_variant(int v) {
-  if (v < 0 || v > 5) throw std::runtime_error("triad variant must be 0..5");
+  if (v < 0 || v > 6) throw std::runtime_error("triad variant must be 0..6");
   g_triad_variant = v;
 }
 
@@ -205,28 +214,57 @@ static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
 
+template <int BM, int BN>
+static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
+                        int ldb, int ldc, bool relu, hipStream_t s) {
+  const dim3 grid((M / BM) * (N / BN)), block(THREADS);
+  if (relu && bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+}
+
+static int g_gemm_tile = 0;   // 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 64x64
+
+void set_gemm_tile(int t) {
+  if (t < 0 || t > 3) throw std::runtime_error("gemm tile must be 0..3");
+  g_gemm_tile = t;
+}
+
+int pick_gemm_tile(int M, int N) {
+  if (g_gemm_tile) return g_gemm_tile;
+  // largest tile that still gives >= 256 workgroups (one per CU); else the smallest
+  if ((M / 128) * (N / 128) >= kCus) return 1;
+  if ((M / 64) * (N / 128) >= kCus && N % 128 == 0) return 2;
+  return 3;
+}
+
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
                   int ldc, bool relu, uintptr_t stream) {
   // Host-side shape checks: the kernel has no bounds checks by design.
   if (M <= 0 || N <= 0 || K <= 0) throw std::runtime_error("gemm: empty shape");
-  if (M % BM || N % BN || K % BK) throw std::runtime_error("gemm: M,N must be multiples of 128 and K of 64");
+  if (M % 64 || N % 64 || K % BK) throw std::runtime_error("gemm: M,N must be multiples of 64 and K of 64");
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8) throw std::runtime_error("gemm: bad leading dims");
   check_align(reinterpret_cast<void*>(a), "A");
   check_align(reinterpret_cast<void*>(bt), "Bt");
-  const dim3 grid((M / BM) * (N / BN)), block(THREADS);
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto A = reinterpret_cast<const __bf16*>(a);
   auto B = reinterpret_cast<const __bf16*>(bt);
   auto Cp = reinterpret_cast<__bf16*>(c);
   auto bp = reinterpret_cast<const float*>(bias);
-  if (relu && bias)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
-  else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
-  else if (bias)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  int t = pick_gemm_tile(M, N);
+  if (t == 1 && (M % 128 || N % 128)) t = 3;
+  if (t == 2 && N % 128) t = 3;
+  if (t == 1)
+    launch_gemm<128, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
+  else if (t == 2)
+    launch_gemm<64, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    launch_gemm<64, 64>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -235,13 +273,15 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
   check_align(reinterpret_cast<void*>(a), "a");
   check_align(reinterpret_cast<void*>(b), "b");
   check_align(reinterpret_cast<void*>(c), "c");
-  if (blocks <= 0) blocks = 2048;
+  if (blocks <= 0) blocks = 8192;
   auto st = reinterpret_cast<hipStream_t>(stream);
   auto A = reinterpret_cast<float4*>(a);
   auto B = reinterpret_cast<const float4*>(b);
   auto Cc = reinterpret_cast<const float4*>(c);
   const size_t n4 = n_floats / 4;
-  switch (g_triad_variant) {
+  int variant = g_triad_variant;
+  if (variant == 6) variant = (n_floats * 12 <= (size_t)96 << 20) ? 1 : 3;
+  switch (variant) {
     case 0: hipLaunchKernelGGL(stream_triad_kernel, dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 1: hipLaunchKernelGGL((stream_triad_u<2, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 2: hipLaunchKernelGGL((stream_triad_u<4, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;

@@ -38,6 +38,24 @@ def test_gemm_matches_fp32_reference(M, N, K, relu, bias):
     assert err <= 0.01 * ref.abs().max().item() + 1e-2, err
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3])
+def test_gemm_every_tile_variant(tile):
+    from k8s_gpu_scheduler_amd import _native
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    h = _native.hip()
+    h.set_gemm_tile(tile)
+    try:
+        for (M, N, K) in [(256, 256, 128), (384, 640, 320), (1024, 1536, 1536)]:
+            a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            bt = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+            b = torch.randn(N, device="cuda")
+            out = loadgen.gemm(a, bt, bias=b, relu=True)
+            ref = torch.relu(a.float() @ bt.float().T + b)
+            assert (out.float() - ref).abs().max().item() <= 0.01 * ref.abs().max().item() + 1e-2
+    finally:
+        h.set_gemm_tile(0)
+
+
 def test_gemm_layout_identity_asymmetric():
     """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
     from k8s_gpu_scheduler_amd.ops import loadgen
@@ -53,6 +71,9 @@ def test_gemm_rejects_bad_shapes():
     a = torch.zeros(100, 64, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(ValueError):
         loadgen.gemm(a, torch.zeros(128, 64, device="cuda", dtype=torch.bfloat16))
+    with pytest.raises(ValueError):
+        loadgen.gemm(torch.zeros(128, 96, device="cuda", dtype=torch.bfloat16),
+                     torch.zeros(128, 96, device="cuda", dtype=torch.bfloat16))
 
 
 def test_triad_matches_reference():

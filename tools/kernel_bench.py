@@ -45,17 +45,24 @@ def main():
                 loadgen.triad(x, y, z, 1.5)
                 torch.cuda.synchronize()
                 assert torch.allclose(x, ref), v
-        h.set_triad_variant(3)
+        h.set_triad_variant(6)
     shapes = sorted({(o.M, o.N, o.K) for w in W.CATALOG.values() for o in w.ops if o.kind == "gemm"})
     for (M, N, K) in shapes:
         a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         bt = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         bias = torch.zeros(N, device="cuda")
+        tiles = {}
+        for tile in (1, 2, 3):
+            h.set_gemm_tile(tile)
+            tiles[tile] = 2 * M * N * K / t_ms(lambda: loadgen.gemm(a, bt, out=c, bias=bias, relu=True)) / 1e9
+        h.set_gemm_tile(0)
         ours = t_ms(lambda: loadgen.gemm(a, bt, out=c, bias=bias, relu=True))
         th = t_ms(lambda: torch.relu(torch.addmm(bias.to(torch.bfloat16), a, bt.T)))
-        out["gemm"].append({"shape": [M, N, K], "ours_us": ours * 1e3, "torch_us": th * 1e3,
-                            "ours_tflops": 2 * M * N * K / ours / 1e9, "torch_tflops": 2 * M * N * K / th / 1e9})
+        out["gemm"].append({"shape": [M, N, K], "auto_tile": h.pick_gemm_tile(M, N), "ours_us": ours * 1e3,
+                            "torch_us": th * 1e3, "ours_tflops": 2 * M * N * K / ours / 1e9,
+                            "torch_tflops": 2 * M * N * K / th / 1e9,
+                            "tile_tflops": {str(k): round(v, 1) for k, v in tiles.items()}})
     os.makedirs("gpurun_out", exist_ok=True)
     json.dump(out, open("gpurun_out/kernel_bench.json", "w"), indent=1)
     best = {}
