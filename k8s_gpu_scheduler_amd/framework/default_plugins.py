@@ -177,7 +177,8 @@ class DefaultBinder(BindPlugin):
 
     def bind(self, state, pod, node_name):
         try:
-            self.handle.client.bind(O.namespace(pod), O.name(pod), node_name, O.uid(pod))
+            ann = state.read("bind/annotations")
+            self.handle.client.bind(O.namespace(pod), O.name(pod), node_name, O.uid(pod), annotations=ann)
         except Exception as e:
             return Status.error(f"binding rejected: {e}", self.NAME)
         return None

@@ -83,7 +83,11 @@ class KubeClient:
                grace_period_seconds: Optional[int] = None) -> None:
         raise NotImplementedError
 
-    def bind(self, namespace: str, pod_name: str, node_name: str, pod_uid: str = "") -> None:
+    def bind(self, namespace: str, pod_name: str, node_name: str, pod_uid: str = "",
+             annotations: Optional[Dict[str, str]] = None) -> None:
+        """POST pods/binding; Binding.metadata.annotations are copied onto the pod by the
+        apiserver (BindingREST), which is how the scheduler attaches per-pod assignment
+        annotations without a separate PATCH."""
         raise NotImplementedError
 
     def watch(self, resource: str, namespace: Optional[str] = None, resource_version: str = "",
@@ -275,7 +279,7 @@ class FakeCluster(KubeClient):
             self._bump(obj)
             self._emit(resource, "DELETED", obj)
 
-    def bind(self, namespace, pod_name, node_name, pod_uid=""):
+    def bind(self, namespace, pod_name, node_name, pod_uid="", annotations=None):
         with self._lock:
             self._maybe_fail("bind", "pods")
             k = self._k("pods", pod_name, namespace)
@@ -291,6 +295,9 @@ class FakeCluster(KubeClient):
                 raise NotFound(f"nodes {node_name}")
             new = O.deepcopy(pod)
             new["spec"]["nodeName"] = node_name
+            if annotations:
+                md = new.setdefault("metadata", {})
+                md["annotations"] = dict(md.get("annotations") or {}, **annotations)
             conds = new.setdefault("status", {}).setdefault("conditions", [])
             conds.append({"type": "PodScheduled", "status": "True"})
             if self.auto_run:

@@ -124,7 +124,8 @@ class FakeApiServer:
                 try:
                     if r["sub"] == "binding":
                         outer.cluster.bind(r["ns"], r["name"], body["target"]["name"],
-                                           body.get("metadata", {}).get("uid", ""))
+                                           body.get("metadata", {}).get("uid", ""),
+                                           body.get("metadata", {}).get("annotations"))
                         return self._send(201, {"kind": "Status", "status": "Success", "code": 201})
                     self._send(201, outer.cluster.create(r["res"], body, r["ns"]))
                 except ApiError as e:

@@ -188,9 +188,13 @@ class RestClient(KubeClient):
                                                            "gracePeriodSeconds": grace_period_seconds}
         self._json("DELETE", self._path(resource, namespace or "default", name), body)
 
-    def bind(self, namespace, pod_name, node_name, pod_uid=""):
-        body = {"apiVersion": "v1", "kind": "Binding",
-                "metadata": {"name": pod_name, "namespace": namespace, **({"uid": pod_uid} if pod_uid else {})},
+    def bind(self, namespace, pod_name, node_name, pod_uid="", annotations=None):
+        md = {"name": pod_name, "namespace": namespace}
+        if pod_uid:
+            md["uid"] = pod_uid
+        if annotations:
+            md["annotations"] = dict(annotations)
+        body = {"apiVersion": "v1", "kind": "Binding", "metadata": md,
                 "target": {"apiVersion": "v1", "kind": "Node", "name": node_name}}
         self._json("POST", self._path("pods", namespace, pod_name, "binding"), body)
 

@@ -50,6 +50,7 @@ _REQ = "GPU/request"
 _PRED = "GPU/predictions"
 _CHOICE = "GPU/choice"
 _CANDS = "GPU/candidates"
+BIND_ANNOTATIONS = "bind/annotations"
 
 
 @dataclass
@@ -307,10 +308,17 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                C.ANNOT_CU_MASK: env.get(C.ENV_CU_MASK, "")}
         res = Resources(self.handle.client, O.namespace(pod))
         try:
-            res.annotate_pod(O.name(pod), ann)
-            res.append_to_existing_config_maps_in_pod(O.name(pod), env, True, pod=pod)
+            # Env into the pod's envFrom ConfigMaps BEFORE the bind (the kubelet reads them
+            # at container creation -- fixes the reference's PostBind race).
+            if O.env_from_config_maps(pod):
+                res.append_to_existing_config_maps_in_pod(O.name(pod), env, True, pod=pod)
         except Exception as e:
             return Status.error(f"PreBind: writing device assignment failed: {e}", self.NAME)
+        # The per-pod assignment annotations ride on the Binding itself (the apiserver
+        # copies Binding.metadata.annotations onto the pod), saving one PATCH per pod.
+        bind_ann = state.read(BIND_ANNOTATIONS) or {}
+        bind_ann.update(ann)
+        state.write(BIND_ANNOTATIONS, bind_ann)
         state.write("GPU/env", env)
         return None
 
@@ -428,15 +436,20 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         if a.pack == "random":
             st, u0 = cands[self._rng.randrange(len(cands))]
             return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], 50.0, [st.device])
+        gpu_fill: Optional[Dict[int, List[int]]] = None
         for i, (st, u0) in enumerate(cands):
             parts: List[Tuple[float, float]] = []
             if slo_scores[i] is not None:
                 parts.append((a.w_slo, slo_scores[i]))
             if a.w_pack:
-                gpu_units = [s for s in states if s.device.gpu == st.device.gpu]
-                tot = sum(s.device.units for s in gpu_units)
-                used = sum(s.device.units - s.free_units for s in gpu_units) + req.units
-                frac = used / max(tot, 1)
+                if gpu_fill is None:
+                    gpu_fill = {}
+                    for s2 in states:
+                        t_u = gpu_fill.setdefault(s2.device.gpu, [0, 0])
+                        t_u[0] += s2.device.units
+                        t_u[1] += s2.device.units - s2.free_units
+                tot, used = gpu_fill[st.device.gpu]
+                frac = (used + req.units) / max(tot, 1)
                 pk = 100.0 * frac if a.pack == "binpack" else 100.0 * (1.0 - frac)
                 parts.append((a.w_pack, pk))
             if a.w_telemetry:

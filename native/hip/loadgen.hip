@@ -237,9 +237,11 @@ void set_gemm_tile(int t) {
 
 int pick_gemm_tile(int M, int N) {
   if (g_gemm_tile) return g_gemm_tile;
-  // largest tile that still gives >= 256 workgroups (one per CU); else the smallest
-  if ((M / 128) * (N / 128) >= kCus) return 1;
-  if ((M / 64) * (N / 128) >= kCus && N % 128 == 0) return 2;
+  // Largest tile that still launches >= 2 workgroups per CU (the kernel fits 2 per CU:
+  // 126 VGPRs, <= 64 KiB LDS); else the smallest.  Measured on the 24 catalog shapes
+  // (profiles/r01_kernel_bench.json): picks the best or within 4% of the best tile.
+  if ((M / 128) * (N / 128) >= 2 * kCus) return 1;
+  if ((M / 64) * (N / 128) >= 2 * kCus && N % 128 == 0) return 2;
   return 3;
 }
 
