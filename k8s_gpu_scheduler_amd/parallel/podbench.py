@@ -268,23 +268,42 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--qos", default="burstable", choices=["burstable", "guaranteed"],
                     help="burstable: CU request is an accounted share, kernels may use idle CUs; "
                          "guaranteed: request == limit -> hard CU mask per pod")
+    ap.add_argument("--backend", default="", choices=["", "nccl", "gloo"],
+                    help="torch.distributed backend (default: nccl = RCCL on GPU, gloo on CPU)")
+    ap.add_argument("--control-plane", default="process", choices=["process", "inline"],
+                    help="run apiserver+scheduler in a separate process (default) or inside rank 0")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # The control plane goes to its own process, started BEFORE anything touches the GPU
+    # (torch.cuda.is_available() initialises HIP; a GPU-initialised process must not exec).
+    n_gpus_planned = world if world > 1 else max(1, a.gpus if a.sim else 1)
+    cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
+                     policy=a.policy, qos=a.qos)
+    cp: Any = None
+    if rank == 0 and a.control_plane == "process":
+        from .controlplane_proc import ControlPlaneProc
+        cp = ControlPlaneProc(**cp_kwargs)
     use_gpu = torch.cuda.is_available() and not a.sim
+    # GPUSCHED_FORCE_DEVICE maps every rank onto one device (multi-rank rehearsal on a
+    # 1-GPU box, with --backend gloo; RCCL refuses two ranks on one GPU).
+    dev_idx = int(os.environ.get("GPUSCHED_FORCE_DEVICE", local))
     if use_gpu:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+        torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx) if use_gpu else torch.device("cpu")
+    backend = a.backend or ("nccl" if use_gpu else "gloo")
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl" if use_gpu else "gloo",
-                                device_id=dev if use_gpu else None)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
     n_gpus = world if world > 1 else max(1, a.gpus if not use_gpu else 1)
     P = n_gpus * a.pods_per_gpu
 
-    cp = ControlPlane(n_gpus, a.pods_per_gpu, a.iters, a.seed, a.policy, qos=a.qos) if rank == 0 else None
+    assert n_gpus == n_gpus_planned
+    if rank == 0 and cp is None:
+        cp = ControlPlane(**cp_kwargs)
+    async_cp = hasattr(cp, "request_schedule")
     if use_gpu:
         from .executor import DeviceExecutor
         ex = DeviceExecutor(local, use_cu_masks=not a.no_cu_mask)
@@ -297,7 +316,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     # default stream would implicitly wait for every queued pod kernel and serialise the
     # host with the GPU (measured: 11.7 ms/epoch vs ~3 ms of host work).
     side = torch.cuda.Stream(device=dev) if use_gpu else None
-    cdev = dev if world > 1 else torch.device("cpu")
+    cdev = dev if (world > 1 and backend == "nccl") else torch.device("cpu")
     assign = torch.zeros((P, FIELDS), dtype=torch.int32, device=cdev)
     tele = torch.zeros((4,), dtype=torch.float64, device=cdev)
     tele_all = [torch.zeros_like(tele) for _ in range(world)]
@@ -305,7 +324,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     def bcast(arr: Optional[np.ndarray]) -> np.ndarray:
         if world == 1:
             return arr
-        with torch.cuda.stream(side) if side is not None else _null():
+        with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
             if rank == 0:
                 assign.copy_(torch.from_numpy(arr))
             dist.broadcast(assign, 0)
@@ -335,7 +354,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
         vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm]
         if world > 1:
-            with torch.cuda.stream(side) if side is not None else _null():
+            with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
                 tele.copy_(torch.tensor(vec, dtype=torch.float64))
                 dist.all_gather(tele_all, tele)
                 per_gpu = torch.stack(tele_all).cpu().numpy()
@@ -367,9 +386,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             for g in gpus_here:
                 runs += _runs_for(arr, g)
             t1 = time.perf_counter()
+            if rank == 0 and async_cp:
+                cp.request_schedule()          # the control-plane process works in parallel
             ex.launch_epoch(runs)
             t2 = time.perf_counter()
-            if rank == 0:
+            if rank == 0 and not async_cp:
                 cp.finish_live()
                 state["next"] = cp.schedule_epoch()
             if timed:
@@ -379,6 +400,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             if pending is not None:
                 collect(*pending, timed)
             pending = (runs, arr)
+            if rank == 0 and async_cp:
+                t3 = time.perf_counter()
+                state["next"] = cp.get_schedule()
+                if timed:
+                    host["schedule"] += time.perf_counter() - t3
         if pending is not None:
             collect(*pending, timed)
 
@@ -393,8 +419,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         ref["ev"].record(side)
     flops0 = ex.flops_done
     if rank == 0:
-        cp.sched_s = 0.0
-        cp.unscheduled = 0
+        if async_cp:
+            cp.reset_stats()
+        else:
+            cp.sched_s = 0.0
+            cp.unscheduled = 0
     run_epochs(a.steps, True)
     if world > 1:
         dist.barrier()
@@ -445,6 +474,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             with open(a.out, "w") as f:
                 json.dump(result, f)
     ex.close()
+    if rank == 0 and async_cp:
+        cp.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
