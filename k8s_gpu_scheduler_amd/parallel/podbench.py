@@ -5,18 +5,18 @@ Headline metric (BASELINE.json): "pods scheduled/sec + achieved node GPU-util %,
 8xMI355X by live HBM/CU-util (Score path)".
 
 Per step (an *epoch*):
-  * rank 0 owns the control plane: FakeCluster apiserver, the scheduler with the GPU
-    plugin (fixed mode: SLO/interference objective on the recommender's MI355X tables +
-    unit packing + live telemetry), and the pod-arrival process (Poisson-sampled workload
-    mix, pods_per_gpu x N quarter-GPU pods per epoch, SLOs drawn around the predicted
-    quarter-GPU throughput);
-  * placements go to every rank with one RCCL broadcast (int32 [P, 6] on the device);
-  * each rank runs its GPU's pods on CU-masked streams (parallel.executor) -- real MFMA
-    GEMM / HBM traffic from the native kernels;
-  * rank 0 schedules epoch t+1 while the GPUs execute epoch t (the device-side event
-    barrier keeps epochs ordered), then every rank syncs, and per-GPU telemetry (busy
-    CU-time, pod throughputs, SLO hits) is all-gathered over RCCL into the scheduler's
-    TelemetryCache for the next Score.
+  * rank 0 owns the control plane -- in a separate process (parallel.controlplane_proc):
+    FakeCluster apiserver, the scheduler with the GPU plugin (fixed mode: SLO/interference
+    objective on the MI355X tables measured by models.profile + unit packing + live
+    telemetry), and the pod-arrival process (Zipf-weighted workload mix, pods_per_gpu x N
+    quarter-GPU pods per epoch, SLOs drawn around the predicted quarter-GPU throughput);
+  * placements go to every rank with one RCCL broadcast (int32 [P, 7] on the device);
+  * each rank runs its GPU's pods on per-slot streams (parallel.executor) -- real MFMA
+    GEMM / HBM traffic from the native kernels; pods are ordered on the device per CU-slice
+    unit, so epoch t+1 is enqueued behind epoch t without a host sync;
+  * the control plane schedules epoch t+1 while the GPUs execute epoch t; epoch t-1's
+    per-GPU telemetry (busy CU-time, pod throughputs, SLO hits) is all-gathered over RCCL
+    into the scheduler's TelemetryCache for the next Score.
 The reported value is the whole-job rate of pods scheduled AND run to completion;
 `gpu_util_pct` is the fraction of wall time each GPU had at least one pod kernel running
 (union of HIP-event intervals; the engine-active notion amd-smi's gfx_activity and
@@ -306,7 +306,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     async_cp = hasattr(cp, "request_schedule")
     if use_gpu:
         from .executor import DeviceExecutor
-        ex = DeviceExecutor(local, use_cu_masks=not a.no_cu_mask)
+        ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
     else:
         ex = SimExecutor()
     gpus_here = [rank] if world > 1 else list(range(n_gpus))

@@ -137,6 +137,32 @@ def test_executor_epoch_and_bench_smoke():
     assert r["value"] > 0 and not r["simulated"] and r["unscheduled"] == 0
 
 
+def test_rccl_probe_single_rank(tmp_path, monkeypatch):
+    """RCCL path of the placement probe (world size 1 on the 1-GPU box)."""
+    import json
+    from k8s_gpu_scheduler_amd.parallel import rccl_probe
+    for k in ("WORLD_SIZE", "RANK", "MASTER_ADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29587")
+    out = tmp_path / "p.json"
+    assert rccl_probe.main(["--sizes", "1M,8M", "--iters", "3", "--out", str(out)]) == 0
+    res = json.loads(out.read_text())["results"]
+    assert {r["op"] for r in res} == {"all_reduce", "all_gather", "reduce_scatter"}
+    assert all(r["time_us"] > 0 for r in res)
+
+
+def test_als_imputer_on_gpu():
+    import numpy as np
+    from k8s_gpu_scheduler_amd.models.imputers import ALSImputer
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(200, 2)) @ rng.normal(size=(2, 16)) + 5
+    M = X.copy()
+    hide = rng.random(X.shape) < 0.2
+    M[hide] = np.nan
+    out = ALSImputer(k=2, device="cuda").fit(M).predict(M)
+    assert np.abs(out[hide] - X[hide]).mean() < 0.5
+
+
 def test_peer_matrix_and_smi():
     from k8s_gpu_scheduler_amd import _native
     m = _native.hip().peer_access_matrix()
