@@ -62,6 +62,7 @@ class GpuRequest:
     slo: float = 0.0
     gpu_pod: bool = False
     burstable: bool = False
+    implicit: bool = False  # SLO env only, no amd.com/* request: GPU preferred, not required
 
 
 @dataclass
@@ -208,6 +209,10 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             r.cu = self.args.default_cu
             r.units = max(1, math.ceil(r.cu / CUS_PER_XCD))
             r.gpu_pod = True
+            # the reference scores every SLO-labelled pod but never filters one out
+            # (busybox on a CPU-only cluster still schedules): only an explicit
+            # amd.com/* request makes the GPU a hard requirement
+            r.implicit = mem <= 0
         # round fractional units up to a power of two (aligned XCD groups)
         if r.units:
             p = 1
@@ -237,7 +242,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         if not self.ledger.has_node(node_info.name):
             self._on_node(node)
         choice = self._best_choice(state, pod, req, node_info.name, scoring=False)
-        if choice is None:
+        if choice is None and not req.implicit:
             return Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME)
         return None
 
@@ -286,6 +291,8 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             choice = self._best_choice(state, pod, req, node_name, scoring=True)
         if choice is not None:
             choice.burstable = req.burstable
+        elif req.implicit:
+            return None                 # no free GPU share: runs without one
         if choice is None or not self.ledger.reserve(node_name, O.key(pod), O.name(pod), req.slo, choice.allocs):
             return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
         state.write(_CHOICE + "/reserved", choice)

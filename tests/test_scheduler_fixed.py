@@ -84,6 +84,23 @@ def test_config1_busybox_two_nodes():
     assert {r.node for r in res} == {"node-a", "node-b"}
 
 
+def test_slo_only_pod_prefers_gpu_but_does_not_require_one():
+    """The reference's busybox fixture carries an SLO env and no GPU request: it must still
+    schedule on a CPU-only cluster, and gets a default GPU share where one exists."""
+    fc, s, ledger, _ = world(nodes=("node-a", "node-b"), gpus=0)
+    fc.create("pods", O.make_pod("busybox-slo", slo=10))
+    (r,) = s.schedule_pending()
+    assert r.status.ok and ledger.placement("default/busybox-slo") is None
+    fc2, s2, ledger2, _ = world()
+    fc2.create("pods", O.make_pod("busybox-slo", slo=10))
+    (r2,) = s2.schedule_pending()
+    assert r2.status.ok and ledger2.placement("default/busybox-slo") is not None
+    # an explicit amd.com/gpu-cu request stays a hard requirement
+    fc.create("pods", O.make_pod("needs-gpu", gpu_cu=32))
+    (r3,) = s.schedule_pending()
+    assert not r3.status.ok
+
+
 def test_config3_fractional_binpack_and_env():
     fc, s, ledger, tele = world()
     fc.create("configmaps", O.make_config_map("env-p0"))
