@@ -141,8 +141,8 @@ class SchedulerCache:
             k = O.key(pod)
             if k in self._pod_node:
                 self._unplace(pod)
-            p = O.deepcopy(pod)
-            p.setdefault("spec", {})["nodeName"] = node_name
+            p = dict(pod)        # path copy: watched objects are read-only (COW store)
+            p["spec"] = dict(pod.get("spec") or {}, nodeName=node_name)
             self._place(p, node_name)
             self._assumed[k] = 0.0
 

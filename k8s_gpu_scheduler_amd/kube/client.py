@@ -206,10 +206,13 @@ class FakeCluster(KubeClient):
                 raise NotFound(f"{resource} {namespace}/{name}")
             return O.deepcopy(obj)
 
-    def create(self, resource, obj, namespace=None):
+    def create(self, resource, obj, namespace=None, owned=False):
+        """owned=True: the caller hands the object over (never touches it again) and does
+        not need the stored copy back -- skips both defensive copies (bulk arrivals)."""
         with self._lock:
             self._maybe_fail("create", resource)
-            obj = O.deepcopy(obj)
+            if not owned:
+                obj = O.deepcopy(obj)
             md = O.meta(obj)
             if NAMESPACED[resource]:
                 md["namespace"] = namespace or md.get("namespace") or "default"
@@ -227,7 +230,7 @@ class FakeCluster(KubeClient):
             self._bump(obj)
             self._store[resource][k] = obj
             self._emit(resource, "ADDED", obj)
-            return O.deepcopy(obj)
+            return None if owned else O.deepcopy(obj)
 
     def update(self, resource, obj, namespace=None):
         with self._lock:
@@ -293,15 +296,17 @@ class FakeCluster(KubeClient):
             node = self._store["nodes"].get(node_name)
             if node is None:
                 raise NotFound(f"nodes {node_name}")
-            new = O.deepcopy(pod)
-            new["spec"]["nodeName"] = node_name
+            # path copy: stored objects are never mutated in place (copy-on-write store,
+            # see _emit), so only the sub-objects the binding changes are copied
+            new = dict(pod)
+            new["spec"] = dict(pod.get("spec") or {}, nodeName=node_name)
+            md = new["metadata"] = dict(pod.get("metadata") or {})
             if annotations:
-                md = new.setdefault("metadata", {})
                 md["annotations"] = dict(md.get("annotations") or {}, **annotations)
-            conds = new.setdefault("status", {}).setdefault("conditions", [])
-            conds.append({"type": "PodScheduled", "status": "True"})
+            st = new["status"] = dict(pod.get("status") or {})
+            st["conditions"] = list(st.get("conditions") or []) + [{"type": "PodScheduled", "status": "True"}]
             if self.auto_run:
-                new["status"]["phase"] = "Running"
+                st["phase"] = "Running"
             self._bump(new)
             self._store["pods"][k] = new
             self.bindings.append((namespace, pod_name, node_name))

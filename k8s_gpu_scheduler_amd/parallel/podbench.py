@@ -142,7 +142,7 @@ class ControlPlane:
             w = W.CATALOG[p["workload"]]
             pod = O.make_pod(p["name"], gpu_cu=self.cu_per_pod, gpu_mem_gib=round(w.hbm_gib, 1),
                              slo=round(p["slo"], 3), gpu_limits=self.qos == "guaranteed")
-            self.fc.create("pods", pod)
+            self.fc.create("pods", pod, owned=True)
         results = self.sched.schedule_pending()
         arr = np.full((len(pods), FIELDS), -1, dtype=np.int32)
         byname = {p["name"]: p for p in pods}

@@ -160,6 +160,7 @@ class DeviceState:
 
     def invalidate(self) -> None:
         self.__dict__.pop("_fit", None)
+        self.__dict__.pop("_slo", None)     # plugin's resident summary (scoring.DeviceSummary)
 
     def _find_units(self, n: int) -> Optional[int]:
         if n > len(self.used_units):

@@ -14,8 +14,9 @@ Reference: `type GPU` implementing Score + NormalizeScore + PostBind
   Filter checks per-device capacity in the ledger (32-CU mask-word units + HBM) and, for
   multi-GPU pods, an xGMI clique (`topology.select_gpu_set`); PreScore fetches the
   incoming pod's predictions once; Score evaluates every candidate device with the
-  reference's SLO/interference objective (`scoring.device_score`, native C++ batch
-  core) blended with unit-packing and live telemetry terms -- no I/O, no side effects;
+  reference's SLO/interference objective (the `scoring.device_score` terms, evaluated
+  incrementally from a cached per-device resident summary, `scoring.fast_device_score`)
+  blended with unit-packing and live telemetry terms -- no I/O, no side effects;
   NormalizeScore is the reference's min-max; Reserve/Unreserve commit the device choice
   to the ledger; PreBind writes the device env (ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES,
   HSA_CU_MASK, HBM cap; reference CUDA_* keys with `compatEnv`) into the pod's envFrom
@@ -40,7 +41,7 @@ from ...kube.resources import Resources
 from ...recommender.client import CachedPredictions, PredictionProvider, RecommenderClient, RpcPredictions
 from ...telemetry.cache import TelemetryCache
 from .devices import CUS_PER_XCD, Device, DeviceLedger, DeviceState, devices_for_node, mask_to_hex, cu_slice_mask
-from .scoring import Resident, score_devices
+from .scoring import DeviceSummary, Resident, build_device_summary, fast_device_score, workload_column
 from .topology import Topology, select_gpu_set
 
 log = logging.getLogger(__name__)
@@ -125,6 +126,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         self.predictions = predictions or extras.get("predictions")
         self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
         self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
+        self._col_memo: Dict[str, Optional[str]] = {}
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)
         self._client: Optional[RecommenderClient] = None
@@ -386,6 +388,22 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         p = max(1, dev_units // max(units, 1))
         return f"{p}P_{self.args.model}"
 
+    def _workload_col(self, name: str, intf: Dict[str, float]) -> Optional[str]:
+        hit = self._col_memo.get(name, False)
+        if hit is False:
+            hit = workload_column(name, intf) if intf else None
+            if len(self._col_memo) > 65536:
+                self._col_memo.clear()
+            self._col_memo[name] = hit
+        return hit
+
+    def _device_summary(self, st: DeviceState) -> DeviceSummary:
+        res = []
+        for use in st.pods.values():
+            conf, intf = self._pod_predictions(use.name)
+            res.append((use.name, use.slo, conf.get(self._col(use.units[1], st.device.units)), intf))
+        return build_device_summary(res)
+
     def _residents(self, st: DeviceState) -> List[Resident]:
         out = []
         for use in st.pods.values():
@@ -426,19 +444,13 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         conf, intf = state.read(_PRED) or self._pod_predictions(name)
         slo_scores: List[Optional[float]] = [None] * len(cands)
         if a.w_slo and req.slo > 0 and conf:
-            residents = [self._residents(st) for st, _ in cands]
-            preds, cols = [], []
-            for st, _ in cands:
-                col = self._col(req.units, st.device.units)
-                cols.append(col)
-                preds.append(conf.get(col, -1.0))
-            # one batch per distinct (column) -- typically all candidates share it
-            for col in set(cols):
-                ids = [i for i, c in enumerate(cols) if c == col]
-                vals = score_devices([residents[i] for i in ids], name, req.slo,
-                                     preds[ids[0]] if preds[ids[0]] is not None else -1.0, intf, col)
-                for i, v in zip(ids, vals):
-                    slo_scores[i] = v
+            x_col = self._workload_col(name, intf)
+            for i, (st, _) in enumerate(cands):
+                summ = st.__dict__.get("_slo")
+                if summ is None:
+                    summ = st.__dict__["_slo"] = self._device_summary(st)
+                slo_scores[i] = fast_device_score(summ, name, x_col, req.slo,
+                                                  conf.get(self._col(req.units, st.device.units), -1.0), intf)
         best: Optional[Choice] = None
         if a.pack == "random":
             st, u0 = cands[self._rng.randrange(len(cands))]

@@ -185,6 +185,85 @@ def mps_env(value: str) -> Tuple[str, str]:
     return "", ""
 
 
+def workload_column(name: str, row: Dict[str, float]) -> Optional[str]:
+    """The interference column a pod name resolves to (first column that is a substring of
+    the name with '-'→'_', as match_column), or None."""
+    nm = name.replace("-", "_")
+    for col in row:
+        if col in nm:
+            return col
+    return None
+
+
+@dataclass
+class DeviceSummary:
+    """Fixed-mode per-device resident summary, rebuilt only when the device's residents
+    change (the ledger invalidates it on Reserve/Unreserve).  Each resident term keeps
+    its SLO, its predicted throughput and the interference it already receives from the
+    OTHER residents, so scoring an incoming pod is O(residents) dict lookups instead of
+    the reference's O(residents^2) substring scans per candidate (gpu_plugins.go:589-612)."""
+    terms: List[Tuple[str, float, float, float, Dict[str, float]]]   # name, slo, pred, base intf, intf row
+    cols: List[Tuple[str, str]]                                       # (name, interference column)
+
+
+def build_device_summary(residents: Sequence[Tuple[str, float, Optional[float], Dict[str, float]]]) -> DeviceSummary:
+    """residents: (name, slo, pred in its own column or None, its interference row)."""
+    cols = []
+    for name, _, _, row in residents:
+        c = workload_column(name, row) if row else None
+        if c is not None:
+            cols.append((name, c))
+    terms = []
+    for name, slo, pred, row in residents:
+        if slo == 0 or pred is None:
+            continue
+        base = 0.0
+        for other, c in cols:
+            if other != name:
+                base += row.get(c, 0.0)
+        terms.append((name, float(slo), float(pred), base, row))
+    return DeviceSummary(terms, cols)
+
+
+def fast_device_score(s: DeviceSummary, x_name: str, x_col: Optional[str], x_slo: float, x_pred: float,
+                      x_intf: Dict[str, float]) -> float:
+    """The device_score objective (same terms and aggregation) in float64 from a
+    DeviceSummary -- fixed mode only; parity mode keeps the float32 Go numerics."""
+    neg_sum = pos_sum = 0.0
+    n_neg = n_pos = 0
+    for name, slo, pred, base, row in s.terms:
+        i = base
+        if x_col is not None and name != x_name:
+            i += row.get(x_col, 0.0)
+        d = (slo - (pred - i)) / slo
+        if d > 0:
+            neg_sum += 1.0 / (1.0 + (abs(d) + 1.0) ** 2)
+            n_neg += 1
+        else:
+            pos_sum += 1.0 / (1.0 + abs(d))
+            n_pos += 1
+    if x_pred != -1 and x_slo > 0:
+        i = 0.0
+        for other, c in s.cols:
+            if other != x_name:
+                i += x_intf.get(c, 0.0)
+        d = (x_slo - (x_pred - i)) / x_slo
+        if d > 0:
+            neg_sum += 1.0 / (1.0 + (abs(d) + 1.0) ** 2)
+            n_neg += 1
+        else:
+            pos_sum += 1.0 / (1.0 + abs(d))
+            n_pos += 1
+    if n_pos and n_neg:
+        k = n_neg / (n_neg + n_pos)
+        return 100.0 * ((1 - k) * pos_sum / n_pos) + 100.0 * (k * neg_sum / n_neg)
+    if n_neg:
+        return 100.0 * neg_sum / n_neg
+    if n_pos:
+        return 100.0 * pos_sum / n_pos
+    return 0.0
+
+
 def score_devices(residents_per_device: List[Sequence[Resident]], incoming_name: str, incoming_slo: float,
                   incoming_pred: float, incoming_intf: Dict[str, float], default_col: str) -> List[float]:
     """Batch form; uses the native core when available (identical results)."""
