@@ -27,8 +27,10 @@ def check_gemm_shapes(M: int, N: int, K: int) -> None:
 
 
 def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
-         relu: bool = False, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
-    """out[M,N] = act(a[M,K] @ bt[N,K]^T + bias[N]) -- bf16 in/out, fp32 accumulate."""
+         relu: bool = False, stream: Optional[torch.cuda.Stream] = None, cu_budget: int = 0) -> torch.Tensor:
+    """out[M,N] = act(a[M,K] @ bt[N,K]^T + bias[N]) -- bf16 in/out, fp32 accumulate.
+    cu_budget: CUs this GEMM can expect to own (the pod's share when pods co-run; 0 = the
+    whole chip) -- steers the tile choice (native pick_gemm_tile)."""
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
         raise TypeError("gemm expects bf16 operands")
     if not (a.is_cuda and bt.is_cuda):
@@ -50,7 +52,7 @@ def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, 
             raise ValueError("bias must be a contiguous fp32 vector of length N")
         bptr = bias.data_ptr()
     _native.hip().gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
-                               bt.stride(0), out.stride(0), relu, _stream_ptr(stream))
+                               bt.stride(0), out.stride(0), relu, _stream_ptr(stream), cu_budget)
     return out
 
 

@@ -20,7 +20,7 @@ import torch
 
 from ..models.workloads import CATALOG, NAMES, Op, Workload
 from ..ops import loadgen
-from ..plugins.gpu.devices import cu_slice_mask
+from ..plugins.gpu.devices import CUS_PER_XCD as CUS_PER_UNIT, cu_slice_mask
 
 
 @dataclass
@@ -60,6 +60,12 @@ class _Buffers:
 
 
 class DeviceExecutor:
+    # co-run launch policy (tools/pod_mix.py measures these on the catalog mix):
+    #   gemm_share   -- tell the GEMM tile picker the pod's CU share instead of the chip
+    #   triad_blocks -- workgroups per stream-kernel launch (0 = the kernel's default)
+    gemm_share = True
+    triad_blocks = 0
+
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
         self.device = device
         self.dev = torch.device("cuda", device)
@@ -120,6 +126,7 @@ class DeviceExecutor:
                     waited.add(id(last[1]))
             w = CATALOG[r.workload]
             bufs = self.buffers(w, r.first_unit, r.n_units)
+            budget = r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
             r.start = torch.cuda.Event(enable_timing=True)
             r.end = torch.cuda.Event(enable_timing=True)
             r.start.record(st)
@@ -127,10 +134,10 @@ class DeviceExecutor:
                 for o, t in bufs.ops:
                     if o.kind == "gemm":
                         a, bt, bias, c = t
-                        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st)
+                        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
                     else:
                         x, y, z = t
-                        loadgen.triad(x, y, z, 1.0001, stream=st)
+                        loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
             r.end.record(st)
             for u in range(r.first_unit, r.first_unit + r.n_units):
                 self._unit_last[u] = (key, r.end)

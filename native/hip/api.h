@@ -22,11 +22,11 @@ void destroy_stream(uintptr_t s);
 std::vector<uint32_t> get_stream_mask(uintptr_t s);
 std::vector<uint32_t> probe_xcd(uintptr_t stream, int n);
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
-                  int ldc, bool relu, uintptr_t stream);
+                  int ldc, bool relu, uintptr_t stream, int cu_budget);
 void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream);
 void set_triad_variant(int v);
 void set_gemm_tile(int t);
-int pick_gemm_tile(int M, int N);
+int pick_gemm_tile(int M, int N, int cu_budget);
 std::vector<int> peer_access_matrix();
 double peer_copy_gbps(int src, int dst, size_t bytes, int iters);
 }  // namespace gs

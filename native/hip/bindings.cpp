@@ -49,12 +49,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("probe_xcd", &gs::probe_xcd, py::arg("stream"), py::arg("n"));
   m.def("gemm_bf16_nt", &gs::gemm_bf16_nt, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("bias"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("relu"),
-        py::arg("stream"), py::call_guard<py::gil_scoped_release>());
+        py::arg("stream"), py::arg("cu_budget") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("stream_triad", &gs::stream_triad, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("s"),
         py::arg("n_floats"), py::arg("blocks"), py::arg("stream"), py::call_guard<py::gil_scoped_release>());
   m.def("set_triad_variant", &gs::set_triad_variant, py::arg("variant"));
   m.def("set_gemm_tile", &gs::set_gemm_tile, py::arg("tile"));
-  m.def("pick_gemm_tile", &gs::pick_gemm_tile, py::arg("M"), py::arg("N"));
+  m.def("pick_gemm_tile", &gs::pick_gemm_tile, py::arg("M"), py::arg("N"), py::arg("cu_budget") = 0);
   m.def("peer_access_matrix", &gs::peer_access_matrix);
   m.def("peer_copy_gbps", &gs::peer_copy_gbps, py::arg("src"), py::arg("dst"), py::arg("bytes"),
         py::arg("iters") = 10, py::call_guard<py::gil_scoped_release>());

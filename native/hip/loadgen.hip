@@ -7,12 +7,12 @@
 // each synthetic workload is a mix of:
 //
 //  * gemm_bf16_nt -- C[M,N] = act(A[M,K] . Bt[N,K]^T (+bias)), bf16 in / f32 accumulate /
-//    bf16 out, on MFMA (v_mfma_f32_16x16x32_bf16).  128x128x64 block tile, 4 waves (2x2),
-//    64x64 per wave = 4x4 MFMA tiles; both operands staged global->LDS with 16-byte
+//    bf16 out, on MFMA (v_mfma_f32_16x16x32_bf16).  Block tiles 64x64 .. 256x256 (4 or 8
+//    waves; 64x64 or 128x64 per wave) picked per shape; both operands staged global->LDS with 16-byte
 //    global_load_lds (no VGPR round trip) into a double-buffered, XOR-swizzled LDS image
 //    (bank-conflict-free ds_read_b128 fragment reads); stage of tile t+1 is issued before
 //    the MFMAs of tile t; XCD-aware bijective block remap + grouped tile order for L2 reuse.
-//    Epilogue fuses bias + ReLU and packs to bf16.
+//    Epilogue fuses bias + ReLU and stores packed bf16x4.
 //  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
 #include <cstdint>
 
@@ -23,9 +23,9 @@ namespace gs {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64;
-constexpr int THREADS = 256;
 constexpr int GROUP_M = 8;
 
 typedef const void __attribute__((address_space(1)))* gptr_t;
@@ -38,17 +38,17 @@ typedef void __attribute__((address_space(3)))* lptr_t;
 // per-lane SOURCE address (rule: linear dest + permuted source + same permutation on read).
 // With two 128-B rows per 256-B bank row, lanes 0-15 of a ds_read_b128 (rows r..r+15,
 // same logical chunk) then hit 16 distinct 16-B slots: conflict-free.
-template <int ROWS>
+template <int ROWS, int NT>
 __device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld, int r0, int k0,
                                            char* lds_tile, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < ROWS * BK * 2 / 16 / THREADS; ++i) {
-    const int chunk = i * THREADS + wave * 64 + lane;
+  for (int i = 0; i < ROWS * BK * 2 / 16 / NT; ++i) {
+    const int chunk = i * NT + wave * 64 + lane;
     const int r = chunk >> 3;
     const int p = chunk & 7;
     const int kc = p ^ ((r >> 1) & 7);
     const __bf16* src = g + (size_t)(r0 + r) * ld + k0 + kc * 8;
-    char* dst = lds_tile + (i * THREADS + wave * 64) * 16;  // wave-uniform base
+    char* dst = lds_tile + (i * NT + wave * 64) * 16;  // wave-uniform base
     __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
   }
 }
@@ -58,15 +58,27 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds_tile, int row, int kc
   return *reinterpret_cast<const bf16x8*>(lds_tile + row * (BK * 2) + phys * 16);
 }
 
-// Block tile BM x BN (64 or 128 each), 4 waves as 2x2, each wave (BM/2) x (BN/2) =
-// MI x NJ MFMA 16x16 tiles.  Small tiles exist so that the small-M GEMMs of the workload
-// catalog still launch >= 256 workgroups (one per CU) instead of idling half the chip.
-template <int BM, int BN, bool RELU, bool BIAS>
-__global__ void __launch_bounds__(THREADS, 2)
+// Block tile BM x BN, WGM x WGN waves, each wave (BM/WGM) x (BN/WGN) = MI x NJ MFMA 16x16
+// tiles.  Register reuse (LDS read bytes per FLOP) is set by the WAVE tile and global->LDS
+// traffic per FLOP by the BLOCK tile, so the large variant (256x256, 8 waves of 128x64)
+// cuts LDS demand ~40 % per FLOP against 128x128 -- the LDS port, not the MFMA, bounds
+// the 128x128 loop (reads + LDS-DMA writes ~= 1 LDS cycle per MFMA cycle at full rate).
+// Small tiles exist so that the small-M GEMMs of the workload catalog still launch
+// >= 256 workgroups (one per CU) instead of idling half the chip.
+//
+// The MFMA is issued with the B fragment as its first operand, so each lane's 4
+// accumulator registers are 4 CONSECUTIVE output columns of one row (D = C^T layout:
+// col = lane&15 -> m, row = (lane>>4)*4 + r -> n): the epilogue stores 8-byte packed bf16x4
+// (4x fewer store instructions than one bf16 per register) and loads bias as float4.
+template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS>
+__global__ void __launch_bounds__(WGM * WGN * 64, OCC)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int NT = WGM * WGN * 64;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int MI = BM / 32, NJ = BN / 32;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;       // wave tile
+  constexpr int MI = WTM / 16, NJ = WTN / 16;
+  static_assert(BM * BK * 2 / 16 % NT == 0 && BN * BK * 2 / 16 % NT == 0, "stage split");
   __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
 
   // ---- XCD-aware bijective remap, then grouped (GROUP_M) tile order ----------------
@@ -86,7 +98,7 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x & (kWave - 1);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
 
   f32x4 acc[MI][NJ];
 #pragma unroll
@@ -98,8 +110,8 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   auto tileB = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES) + A_BYTES; };
 
   const int nt = K / BK;
-  stage_tile<BM>(A, lda, m0, 0, tileA(0), wave, lane);
-  stage_tile<BN>(Bt, ldb, n0, 0, tileB(0), wave, lane);
+  stage_tile<BM, NT>(A, lda, m0, 0, tileA(0), wave, lane);
+  stage_tile<BN, NT>(Bt, ldb, n0, 0, tileB(0), wave, lane);
   __syncthreads();
 
   const int frow = lane & 15;
@@ -107,8 +119,8 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   int buf = 0;
   for (int t = 0; t < nt; ++t) {
     if (t + 1 < nt) {   // issue tile t+1 before the MFMAs of tile t
-      stage_tile<BM>(A, lda, m0, (t + 1) * BK, tileA(buf ^ 1), wave, lane);
-      stage_tile<BN>(Bt, ldb, n0, (t + 1) * BK, tileB(buf ^ 1), wave, lane);
+      stage_tile<BM, NT>(A, lda, m0, (t + 1) * BK, tileA(buf ^ 1), wave, lane);
+      stage_tile<BN, NT>(Bt, ldb, n0, (t + 1) * BK, tileB(buf ^ 1), wave, lane);
     }
     const char* a_t = tileA(buf);
     const char* b_t = tileB(buf);
@@ -116,35 +128,35 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 af[MI], bf[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = lds_frag(a_t, wm * (BM / 2) + i * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < NJ; ++j) bf[j] = lds_frag(b_t, wn * WTN + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[j] = lds_frag(b_t, wn * (BN / 2) + j * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < MI; ++i) af[i] = lds_frag(a_t, wm * WTM + i * 16 + frow, kk * 4 + fk);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();   // tile t+1 landed (vmcnt(0) before the barrier) and tile t fully read
     buf ^= 1;
   }
 
-  // ---- epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r; fused bias + ReLU --
+  // ---- epilogue (D = C^T layout): row m = lane&15, cols n..n+3 = (lane>>4)*4 + r ----
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
+  for (int j = 0; j < NJ; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + fk * 4;
+    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + col);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = n0 + wn * (BN / 2) + j * 16 + frow;
-      const float bv = BIAS ? bias[col] : 0.f;
+    for (int i = 0; i < MI; ++i) {
+      const int row = m0 + wm * WTM + i * 16 + frow;
+      f32x4 v = acc[i][j] + bv;
+      bf16x4 o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 16 + fk * 4 + r;
-        float v = acc[i][j][r] + bv;
-        if (RELU) v = v > 0.f ? v : 0.f;
-        C[(size_t)row * ldc + col] = (__bf16)v;
-      }
+      for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+      *reinterpret_cast<bf16x4*>(C + (size_t)row * ldc + col) = o;
     }
   }
 }
@@ -214,39 +226,55 @@ static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WGM, int WGN, int OCC>
 static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                         int ldb, int ldc, bool relu, hipStream_t s) {
-  const dim3 grid((M / BM) * (N / BN)), block(THREADS);
+  const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
   if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
+                       K, lda, ldb, ldc);
   else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false>), grid, block, 0, s, A, B, Cp, bp, M, N,
+                       K, lda, ldb, ldc);
   else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
+                       K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false>), grid, block, 0, s, A, B, Cp, bp, M,
+                       N, K, lda, ldb, ldc);
 }
 
-static int g_gemm_tile = 0;   // 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 64x64
+// 0 = auto, 1 = 128x128 (4 waves, 2/CU), 2 = 64x128, 3 = 64x64,
+// 4 = 256x256 (8 waves of 128x64, 1/CU), 5 = 256x128 (8 waves of 64x64, 1/CU)
+static int g_gemm_tile = 0;
+static const int kTileBM[6] = {0, 128, 64, 64, 256, 256};
+static const int kTileBN[6] = {0, 128, 128, 64, 256, 128};
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 3) throw std::runtime_error("gemm tile must be 0..3");
+  if (t < 0 || t > 5) throw std::runtime_error("gemm tile must be 0..5");
   g_gemm_tile = t;
 }
 
-int pick_gemm_tile(int M, int N) {
+int pick_gemm_tile(int M, int N, int cu_budget) {
   if (g_gemm_tile) return g_gemm_tile;
-  // Largest tile that still launches >= 2 workgroups per CU (the kernel fits 2 per CU:
-  // 126 VGPRs, <= 64 KiB LDS); else the smallest.  Measured on the 24 catalog shapes
-  // (profiles/r01_kernel_bench.json): picks the best or within 4% of the best tile.
-  if ((M / 128) * (N / 128) >= 2 * kCus) return 1;
-  if ((M / 64) * (N / 128) >= 2 * kCus && N % 128 == 0) return 2;
+  // cu_budget = CUs this GEMM can expect to own: the whole chip for a lone kernel, the
+  // pod's CU share when pods run side by side (0 = whole chip).  Measured
+  // (profiles/r01_gemm_tiles.json): a lone kernel wants >= 2 workgroups per CU of the
+  // 64/128-wide tiles (fill beats per-block efficiency) and the 256x256 tile only when it
+  // still fills every CU (4096^3: 1172 vs 1089 TF); co-running pods want the largest
+  // tile that gives one workgroup per CU of their share -- the other pods' kernels fill
+  // the rest of the chip -- 128x128 on the whole catalog mix: 784 vs 715 TF aggregate.
+  const bool alone = cu_budget <= 0 || cu_budget >= kCus;
+  const int budget = alone ? kCus : cu_budget;
+  const int per_cu = alone ? 2 : 1;
+  if (alone && (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget) return 4;
+  if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
+  if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
 }
 
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
-                  int ldc, bool relu, uintptr_t stream) {
+                  int ldc, bool relu, uintptr_t stream, int cu_budget) {
   // Host-side shape checks: the kernel has no bounds checks by design.
   if (M <= 0 || N <= 0 || K <= 0) throw std::runtime_error("gemm: empty shape");
   if (M % 64 || N % 64 || K % BK) throw std::runtime_error("gemm: M,N must be multiples of 64 and K of 64");
@@ -258,15 +286,17 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
   auto B = reinterpret_cast<const __bf16*>(bt);
   auto Cp = reinterpret_cast<__bf16*>(c);
   auto bp = reinterpret_cast<const float*>(bias);
-  int t = pick_gemm_tile(M, N);
-  if (t == 1 && (M % 128 || N % 128)) t = 3;
-  if (t == 2 && N % 128) t = 3;
-  if (t == 1)
-    launch_gemm<128, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
-  else if (t == 2)
-    launch_gemm<64, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
-  else
-    launch_gemm<64, 64>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
+  if (ldc % 4 || reinterpret_cast<uintptr_t>(c) % 8) throw std::runtime_error("gemm: C rows must be 8-byte aligned");
+  if (bias) check_align(reinterpret_cast<void*>(bias), "bias");
+  int t = pick_gemm_tile(M, N, cu_budget);
+  if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
+  switch (t) {
+    case 1: launch_gemm<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 2: launch_gemm<64, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 4: launch_gemm<256, 256, 2, 4, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 5: launch_gemm<256, 128, 4, 2, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    default: launch_gemm<64, 64, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+  }
   HIP_CHECK(hipGetLastError());
 }
 

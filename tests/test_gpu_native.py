@@ -38,14 +38,14 @@ def test_gemm_matches_fp32_reference(M, N, K, relu, bias):
     assert err <= 0.01 * ref.abs().max().item() + 1e-2, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
 def test_gemm_every_tile_variant(tile):
     from k8s_gpu_scheduler_amd import _native
     from k8s_gpu_scheduler_amd.ops import loadgen
     h = _native.hip()
     h.set_gemm_tile(tile)
     try:
-        for (M, N, K) in [(256, 256, 128), (384, 640, 320), (1024, 1536, 1536)]:
+        for (M, N, K) in [(256, 256, 128), (384, 640, 320), (1024, 1536, 1536), (512, 768, 2048)]:
             a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
             bt = torch.randn(N, K, device="cuda").to(torch.bfloat16)
             b = torch.randn(N, device="cuda")
