@@ -106,14 +106,34 @@ class SmiSource(DeviceSource):
         if not self.smi.init():
             raise RuntimeError(f"amd-smi init failed: {self.smi.error()}")
 
+    @staticmethod
+    def _rocr_ids() -> Dict[str, List[str]]:
+        """PCI BDF -> ROCr device ids ("GPU-<16 hex>", what ROCR_VISIBLE_DEVICES accepts) from
+        the HIP runtime, in enumeration order; empty when HIP is unavailable."""
+        try:
+            from .. import _native
+            h = _native.hip(required=False)
+            if h is None:
+                return {}
+            ids: Dict[str, List[str]] = {}
+            for d in h.query_all():
+                if d.get("rocr_uuid"):
+                    ids.setdefault(d.get("pci", "").lower(), []).append(d["rocr_uuid"])
+            return ids
+        except Exception:
+            return {}
+
     def devices(self):
         out = []
         raw = self.smi.devices()
+        rocr = self._rocr_ids()
         # partitions of one physical GPU share a BDF bus/device; count them per bus
         for d in raw:
             mode = (d.get("compute_partition") or "SPX").upper()
             parts = C.COMPUTE_PARTITIONS.get(mode, 1)
-            out.append({"uuid": "GPU-" + d.get("uuid", f"idx{d['index']}"), "gpu": d["index"] // parts,
+            ids = rocr.get(str(d.get("bdf", "")).lower()) or []
+            uuid = ids.pop(0) if ids else "GPU-" + d.get("uuid", f"idx{d['index']}")
+            out.append({"uuid": uuid, "smi_uuid": d.get("uuid", ""), "gpu": d["index"] // parts,
                         "partition": d["index"] % parts, "partitions": parts,
                         "cus": int(d.get("num_cu") or C.MI355X_CUS // parts),
                         "hbm_gib": float(d.get("vram_total_mb", C.MI355X_HBM_GIB * 1024 / parts)) / 1024.0,
@@ -145,7 +165,8 @@ class HipSource(DeviceSource):
     def devices(self):
         out = []
         for d in self.hip.query_all():
-            out.append({"uuid": "GPU-" + (d.get("uuid") or f"idx{d['index']}"), "gpu": d["index"], "partition": 0,
+            uuid = d.get("rocr_uuid") or "GPU-" + (d.get("uuid") or f"idx{d['index']}")
+            out.append({"uuid": uuid, "gpu": d["index"], "partition": 0,
                         "partitions": 1, "cus": d["cus"], "hbm_gib": d["total_mem"] / 2**30,
                         "numa": 0, "model": C.MI355X if d["arch"].startswith("gfx950") else d["arch"],
                         "first_xcd": 0, "bdf": d.get("pci", "")})

@@ -1,0 +1,138 @@
+"""Pod launcher: a minimal kubelet for one node.
+
+The reference relies on the real kubelet to read the pod's envFrom ConfigMaps at container
+creation (its PostBind writes CUDA_VISIBLE_DEVICES there, reference
+pkg/plugins/gpu_plugin/gpu_plugins.go:910-920) and on the NVIDIA runtime to expose the
+device.  This launcher plays both roles for tests, the fake cluster and bare-metal runs: it
+picks up pods bound to its node, builds the container environment the way the kubelet does
+(container `env`, then `envFrom` ConfigMaps, then the device plugin's allocation, which here
+is the scheduler's assignment annotations: devices -> ROCR_VISIBLE_DEVICES, cu-mask ->
+HSA_CU_MASK) and runs the container command as a child process, then reports the pod phase
+(Succeeded / Failed) through the API.
+
+The default command is `agent.container_probe`, which prints what the process sees of the
+GPU (visible devices, CUs its kernels ran on): SURVEY §7.4's "the pod saw exactly the one
+assigned device".
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import subprocess
+import sys
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+from ..api import constants as C
+from ..api import objects as O
+from ..kube.client import KubeClient, NotFound
+
+log = logging.getLogger(__name__)
+Obj = Dict[str, object]
+
+DEFAULT_COMMAND = [sys.executable, "-m", "k8s_gpu_scheduler_amd.agent.container_probe"]
+# environment of the launcher that a container must not inherit (it would override or
+# contradict the pod's device assignment)
+_SCRUB = (C.ENV_ROCR_VISIBLE, C.ENV_HIP_VISIBLE, C.ENV_CU_MASK, C.ENV_CUDA_VISIBLE, "GPU_DEVICE_ORDINAL",
+          "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "RANK", "WORLD_SIZE")
+
+
+@dataclass
+class LaunchResult:
+    pod_key: str
+    rc: int
+    stdout: str = ""
+    stderr: str = ""
+    env: Dict[str, str] = field(default_factory=dict)
+
+    def json(self) -> Optional[dict]:
+        for line in reversed(self.stdout.strip().splitlines()):
+            try:
+                return json.loads(line)
+            except json.JSONDecodeError:
+                continue
+        return None
+
+
+class PodLauncher:
+    def __init__(self, client: KubeClient, node_name: str, command: Optional[List[str]] = None,
+                 timeout_s: float = 120.0, base_env: Optional[Dict[str, str]] = None,
+                 command_for: Optional[Callable[[Obj], List[str]]] = None):
+        self.client = client
+        self.node = node_name
+        self.command = command or DEFAULT_COMMAND
+        self.command_for = command_for
+        self.timeout_s = timeout_s
+        base = dict(os.environ if base_env is None else base_env)
+        for k in _SCRUB:
+            base.pop(k, None)
+        self.base_env = base
+        self.launched: Dict[str, LaunchResult] = {}
+
+    # ------------------------------------------------------------------ env
+    def env_for(self, pod: Obj) -> Dict[str, str]:
+        """Container env, kubelet order: env entries, then envFrom ConfigMaps (a key from env
+        wins), then the device allocation from the assignment annotations."""
+        ns = O.namespace(pod)
+        env: Dict[str, str] = {}
+        ctr = O.containers(pod)[0] if O.containers(pod) else {}
+        from_cms: Dict[str, str] = {}
+        for ref in ctr.get("envFrom") or []:
+            name = (ref.get("configMapRef") or {}).get("name")
+            if not name:
+                continue
+            try:
+                cm = self.client.get("configmaps", name, ns)
+            except NotFound:
+                if (ref.get("configMapRef") or {}).get("optional"):
+                    continue
+                raise
+            from_cms.update({k: str(v) for k, v in (cm.get("data") or {}).items()})
+        env.update(from_cms)
+        for e in ctr.get("env") or []:
+            if "value" in e:
+                env[e["name"]] = str(e["value"])
+        ann = O.annotations(pod)
+        devices = ann.get(C.ANNOT_DEVICES, "")
+        if devices:
+            uuids = [u for u in devices.split(",") if u]
+            env.setdefault(C.ENV_ROCR_VISIBLE, ",".join(uuids))
+            env.setdefault(C.ENV_HIP_VISIBLE, ",".join(str(i) for i in range(len(uuids))))
+            if ann.get(C.ANNOT_CU_MASK):
+                env.setdefault(C.ENV_CU_MASK, ann[C.ANNOT_CU_MASK])
+        return env
+
+    # ------------------------------------------------------------------ run
+    def run(self, pod: Obj) -> LaunchResult:
+        key = O.key(pod)
+        env = self.env_for(pod)
+        ctr = O.containers(pod)[0] if O.containers(pod) else {}
+        argv = (self.command_for(pod) if self.command_for else None) or \
+            (list(ctr.get("command") or []) + list(ctr.get("args") or [])) or self.command
+        full_env = dict(self.base_env)
+        full_env.update(env)
+        try:
+            p = subprocess.run(argv, env=full_env, capture_output=True, text=True, timeout=self.timeout_s)
+            res = LaunchResult(key, p.returncode, p.stdout, p.stderr, env)
+        except subprocess.TimeoutExpired as e:
+            res = LaunchResult(key, -9, e.stdout or "", (e.stderr or "") + "\ntimeout", env)
+        except OSError as e:
+            res = LaunchResult(key, 127, "", str(e), env)
+        self.launched[key] = res
+        phase = "Succeeded" if res.rc == 0 else "Failed"
+        try:
+            self.client.patch("pods", O.name(pod), {"status": {"phase": phase}}, "merge", O.namespace(pod))
+        except NotFound:
+            pass
+        return res
+
+    def run_bound(self) -> List[LaunchResult]:
+        """Launch every pod bound to this node that has not run yet (one pass)."""
+        pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        out = []
+        for pod in pods:
+            if O.key(pod) in self.launched or O.is_terminal(pod):
+                continue
+            out.append(self.run(pod))
+        return out

@@ -110,6 +110,23 @@ def cu_slice_mask(first_unit: int, n_units: int, cus: int = C.MI355X_CUS) -> Lis
 xcd_cu_mask = cu_slice_mask
 
 
+def hsa_cu_mask_ranges(words: List[int]) -> str:
+    """Set bits of a CU mask as ROCr's HSA_CU_MASK range list ("0-31,64-95")."""
+    bits = [32 * wi + b for wi, w in enumerate(words) for b in range(32) if (w >> b) & 1]
+    out, start, prev = [], None, None
+    for b in bits:
+        if start is None:
+            start = prev = b
+        elif b == prev + 1:
+            prev = b
+        else:
+            out.append(f"{start}-{prev}" if prev > start else str(start))
+            start = prev = b
+    if start is not None:
+        out.append(f"{start}-{prev}" if prev > start else str(start))
+    return ",".join(out)
+
+
 def mask_to_hex(words: List[int]) -> str:
     """HSA_CU_MASK style: 0x<hex> with word 0 least significant."""
     v = 0

@@ -40,7 +40,8 @@ from ...framework.interface import (CycleState, FilterPlugin, NodeScore, PostBin
 from ...kube.resources import Resources
 from ...recommender.client import CachedPredictions, PredictionProvider, RecommenderClient, RpcPredictions
 from ...telemetry.cache import TelemetryCache
-from .devices import CUS_PER_XCD, Device, DeviceLedger, DeviceState, devices_for_node, mask_to_hex, cu_slice_mask
+from .devices import (CUS_PER_XCD, Device, DeviceLedger, DeviceState, cu_slice_mask, devices_for_node,
+                      hsa_cu_mask_ranges)
 from .scoring import DeviceSummary, Resident, build_device_summary, fast_device_score, workload_column
 from .topology import Topology, select_gpu_set
 
@@ -341,17 +342,22 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
 
     # ------------------------------------------------------------------ env
     def device_env(self, choice: Choice) -> Dict[str, str]:
+        """Container env for a placement.  ROCR_VISIBLE_DEVICES filters the devices the ROCm
+        runtime enumerates, so every index after it is RELATIVE to that list: HIP sees the
+        pod's devices as 0..n-1, and HSA_CU_MASK addresses its (single) fractional device as
+        GPU 0, in ROCr's `<gpu>:<cu ranges>` syntax.  The physical GPU indices stay in the
+        device-indices annotation."""
         devs = {d.uuid: d for d in choice.devices}
         uuids = [a[0] for a in choice.allocs]
-        idx = [str(devs[u].gpu) if u in devs else "" for u in uuids]
-        env = {C.ENV_ROCR_VISIBLE: ",".join(uuids), C.ENV_HIP_VISIBLE: ",".join(i for i in idx if i)}
+        env = {C.ENV_ROCR_VISIBLE: ",".join(uuids), C.ENV_HIP_VISIBLE: ",".join(str(i) for i in range(len(uuids)))}
         frac = [a for a in choice.allocs if not a[4]]
-        if frac and not choice.burstable:
+        if frac:
             u, u0, n, hbm, _ = frac[0]
-            d = devs.get(u)
-            first = (d.first_xcd if d else 0) + u0
-            env[C.ENV_CU_MASK] = f"{idx[0] or 0}:{mask_to_hex(cu_slice_mask(first, n))}"
             env[C.ENV_HBM_LIMIT] = f"{hbm:g}"
+            if not choice.burstable:
+                d = devs.get(u)
+                first = (d.first_xcd if d else 0) + u0
+                env[C.ENV_CU_MASK] = f"{uuids.index(u)}:{hsa_cu_mask_ranges(cu_slice_mask(first, n))}"
         if self.args.compat_env:
             env[C.ENV_CUDA_VISIBLE] = env[C.ENV_ROCR_VISIBLE]
             if frac:

@@ -8,7 +8,7 @@
 namespace gs {
 struct DevInfo {
   int index = 0;
-  std::string name, arch, uuid, pci;
+  std::string name, arch, uuid, rocr_uuid, pci;
   int cus = 0, clock_khz = 0, mem_clock_khz = 0, warp = 0, l2_bytes = 0, max_threads = 0;
   size_t lds_per_block = 0, total_mem = 0, free_mem = 0;
   size_t heap_limit = 0, fifo_limit = 0, stack_limit = 0;

@@ -25,6 +25,7 @@ PYBIND11_MODULE(_hip, m) {
       x["name"] = d.name;
       x["arch"] = d.arch;
       x["uuid"] = d.uuid;
+      x["rocr_uuid"] = d.rocr_uuid;
       x["pci"] = d.pci;
       x["cus"] = d.cus;
       x["clock_khz"] = d.clock_khz;

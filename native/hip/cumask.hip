@@ -4,8 +4,11 @@
 // pinned memory limit, pkg/plugins/gpu_plugin/gpu_plugins.go:896-917) and an A30 through
 // MIG.  The MI355X analog inside one process is a HIP stream whose hardware queue is
 // restricted to a CU mask (hipExtStreamCreateWithCUMask): the GPU plugin hands each
-// fractional pod a run of whole XCDs, and the executor runs the pod's kernels on a stream
-// masked to exactly those XCDs' CUs, so co-located pods do not share an L2.
+// fractional pod a run of CU-slice units (one 32-bit mask word = 4 CUs on each of the 8
+// XCDs -- a mask that leaves an XCD empty is ignored by the driver, measured), and the
+// executor runs a Guaranteed pod's kernels on a stream masked to exactly those CUs.  A
+// container gets the same restriction process-wide from HSA_CU_MASK="0:<cu ranges>"
+// (verified in-container: profiles/r01_e2e_container_view.json).
 //
 // `probe_xcd` launches one workgroup per slot that records HW_REG_XCC_ID and HW_REG_HW_ID;
 // the host uses it to verify which XCDs / CUs a mask really maps to.

@@ -28,6 +28,19 @@ static std::string hex_uuid(const hipUUID& u) {
   return s;
 }
 
+// ROCm fills hipUUID with the ASCII of the agent's unique id (16 hex digits); rocminfo,
+// amd-smi's ROCm id and ROCR_VISIBLE_DEVICES all name the device "GPU-<those digits>".
+static std::string rocr_uuid(const hipUUID& u) {
+  std::string s;
+  for (int i = 0; i < 16; ++i) {
+    const char c = u.bytes[i];
+    const bool hexdig = (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+    if (!hexdig) return "";
+    s += c;
+  }
+  return "GPU-" + s;
+}
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -61,7 +74,10 @@ std::vector<DevInfo> query_all() {
     std::snprintf(bdf, sizeof(bdf), "%04x:%02x:%02x.0", p.pciDomainID, p.pciBusID, p.pciDeviceID);
     di.pci = bdf;
     hipUUID u;
-    if (hipDeviceGetUuid(&u, d) == hipSuccess) di.uuid = hex_uuid(u);
+    if (hipDeviceGetUuid(&u, d) == hipSuccess) {
+      di.uuid = hex_uuid(u);
+      di.rocr_uuid = rocr_uuid(u);
+    }
     HIP_CHECK(hipSetDevice(d));
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) {

@@ -165,3 +165,39 @@ def test_scheduler_over_rest_with_threaded_informers(api, tmp_path):
         assert ann[C.ANNOT_DEVICES].startswith("GPU-")
     finally:
         s.stop()
+
+
+def _sched_with_agent(src, node="mi355x-0"):
+    fc = FakeCluster()
+    r = rds()
+    NodeAgent(node, r, src).publish()
+    fc.create("nodes", O.make_node(node, gpus=len(src.devices())))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, seed=0, extras={"redis": r})
+    s.start_informers()
+    return fc, s
+
+
+def test_launcher_builds_kubelet_env_from_assignment():
+    """Mini-kubelet: container env = env + envFrom ConfigMaps + the device allocation from the
+    scheduler's annotations (ROCR_VISIBLE_DEVICES / HSA_CU_MASK), launched as a child."""
+    import sys
+    from k8s_gpu_scheduler_amd.agent.launcher import PodLauncher
+    fc, s = _sched_with_agent(synthetic_node(8, node="mi355x-0"))
+    fc.create("configmaps", O.make_config_map("cm-g", {"FROM_CM": "1"}))
+    fc.create("pods", O.make_pod("guar", gpu_cu=64, gpu_mem_gib=8, slo=50, config_maps=["cm-g"]))
+    fc.create("pods", O.make_pod("burst", gpu_cu=64, gpu_limits=False))
+    fc.create("pods", O.make_pod("whole", gpus=1))
+    assert all(r.status.ok for r in s.schedule_pending())
+    keys = ["ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "HSA_CU_MASK", "SLO", "FROM_CM", "LOCAL_RANK"]
+    cmd = [sys.executable, "-c", f"import os, json; print(json.dumps({{k: os.environ.get(k) for k in {keys!r}}}))"]
+    la = PodLauncher(fc, "mi355x-0", command=cmd, base_env={"PATH": "/usr/bin:/bin", "LOCAL_RANK": "3"})
+    res = {r.pod_key: r for r in la.run_bound()}
+    assert set(res) == {"default/guar", "default/burst", "default/whole"}
+    g, b, w = (res[f"default/{n}"].json() for n in ("guar", "burst", "whole"))
+    ann = O.annotations(fc.get("pods", "guar", "default"))
+    assert g["ROCR_VISIBLE_DEVICES"] == ann[C.ANNOT_DEVICES] and g["HIP_VISIBLE_DEVICES"] == "0"
+    assert g["HSA_CU_MASK"].startswith("0:") and g["SLO"] == "50" and g["FROM_CM"] == "1"
+    assert g["LOCAL_RANK"] is None                       # launcher-side rank env is scrubbed
+    assert b["HSA_CU_MASK"] is None and b["ROCR_VISIBLE_DEVICES"]       # Burstable: no hard mask
+    assert w["HSA_CU_MASK"] is None and w["ROCR_VISIBLE_DEVICES"].startswith("GPU-")
+    assert O.phase(fc.get("pods", "whole", "default")) == "Succeeded"

@@ -179,3 +179,67 @@ def test_peer_matrix_and_smi():
     topo = s.topology()
     assert topo["n"] == s.count()
     s.shutdown()
+
+
+def test_pod_sees_only_its_assignment_end_to_end():
+    """SURVEY §7.4 slice: HIP-enumerated devices -> node agent -> Redis -> scheduler ->
+    assignment annotations -> launcher (mini-kubelet) -> container process.  The container
+    sees exactly its device (by ROCr id), and a Guaranteed fractional pod's kernels run only
+    on its CU slice (HSA_CU_MASK); a Burstable one is not masked."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import HipSource
+    from k8s_gpu_scheduler_amd.agent.launcher import PodLauncher
+    from k8s_gpu_scheduler_amd.api import constants as C
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+    from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.plugins import full_registry
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    node = "mi355x-box"
+    src = HipSource()
+    devs = src.devices()
+    assert devs and all(d["uuid"].startswith("GPU-") and len(d["uuid"]) == 20 for d in devs), devs
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    NodeAgent(node, r, src).publish()
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node(node, gpus=len(devs)))
+    s = Scheduler(fc, default_gpu_config({"compat_env": False}), full_registry(), bind_async=False, seed=0,
+                  extras={"redis": r})
+    s.start_informers()
+    la = PodLauncher(fc, node, timeout_s=240)
+    res = {}
+    # the box has one GPU: two fractional pods share it, then (after they finish and are
+    # deleted) one whole-GPU pod
+    for batch in ([O.make_pod("guar", gpu_cu=64, gpu_mem_gib=8), O.make_pod("burst", gpu_cu=64, gpu_limits=False)],
+                  [O.make_pod("whole", gpus=1)]):
+        for p in batch:
+            fc.create("pods", p)
+        sr = s.schedule_pending()
+        assert all(x.status.ok for x in sr), [x.status.message() for x in sr]
+        res.update({x.pod_key.split("/")[1]: x for x in la.run_bound()})
+        keep = {k: O.annotations(fc.get("pods", k, "default")) for k in [O.name(p) for p in batch]}
+        for p in batch:
+            fc.delete("pods", O.name(p), "default")
+        res.update({k + "/ann": v for k, v in keep.items()})
+    names = ("whole", "guar", "burst")
+    out = {k: (res[k].json() or {"rc": res[k].rc, "stderr": res[k].stderr[-2000:]}) for k in names}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/e2e_container_view.json", "w") as f:
+        json.dump({k: {"env": res[k].env, "seen": out[k]} for k in names}, f, indent=1)
+    for k in names:
+        assert res[k].rc == 0, out[k]
+        ann = res[k + "/ann"]
+        assert out[k]["count"] == 1 and out[k]["devices"][0]["rocr_uuid"] == ann[C.ANNOT_DEVICES], out[k]
+    assert out["whole"]["cus_used"] == 256 and out["burst"]["cus_used"] == 256, out
+    assert out["guar"]["cus_used"] == 64 and set(out["guar"]["cus_per_xcc"].values()) == {8}, out["guar"]
+    # a device id that is not on the node hides every GPU (the env really filters)
+    env = dict(os.environ, ROCR_VISIBLE_DEVICES="GPU-0000000000000000")
+    p = subprocess.run([sys.executable, "-m", "k8s_gpu_scheduler_amd.agent.container_probe"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert json.loads(p.stdout.strip().splitlines()[-1]).get("count", 0) == 0, p.stdout + p.stderr

@@ -125,7 +125,9 @@ def test_config3_fractional_binpack_and_env():
     ann = O.annotations(fc.get("pods", "p0", "default"))
     assert d[C.ENV_ROCR_VISIBLE] == ann[C.ANNOT_DEVICES]
     u0 = json.loads(ann[C.ANNOT_DEVICE_INDICES])[0][1]
-    assert d[C.ENV_CU_MASK].endswith(mask_to_hex(cu_slice_mask(u0, 2)))
+    # ROCr syntax, GPU index relative to ROCR_VISIBLE_DEVICES: "0:<cu ranges>"
+    assert d[C.ENV_CU_MASK] == f"0:{32 * u0}-{32 * u0 + 63}"
+    assert d[C.ENV_HIP_VISIBLE] == "0" and ann[C.ANNOT_CU_MASK] == d[C.ENV_CU_MASK]
     assert d[C.ENV_CUDA_VISIBLE] == d[C.ENV_ROCR_VISIBLE]          # compat keys
     assert d[C.ENV_MPS_THREADS] == "25"
 
