@@ -29,6 +29,7 @@ mask (measured ~24% lower node throughput on this mix, in exchange for isolation
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import math
 import os
@@ -272,8 +273,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="torch.distributed backend (default: nccl = RCCL on GPU, gloo on CPU)")
     ap.add_argument("--control-plane", default="process", choices=["process", "inline"],
                     help="run apiserver+scheduler in a separate process (default) or inside rank 0")
+    ap.add_argument("--lookahead", type=int, default=2,
+                    help="epochs kept in flight per GPU before collecting (>= 1)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
+    a.lookahead = max(1, a.lookahead)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -377,8 +381,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
 
     def run_epochs(count: int, timed: bool) -> None:
         """Launch-ahead pipeline: epoch e is enqueued (device-side ordered behind e-1),
-        rank 0 schedules e+1 while the GPU runs, then e-1 is collected."""
-        pending: Optional[Tuple[List[Any], np.ndarray]] = None
+        rank 0 schedules e+1 while the GPU runs, then epoch e-L is collected (L =
+        --lookahead).  With L >= 2 each GPU keeps up to L+1 epochs queued, so a rank whose
+        pods ran long in one epoch catches up in the next instead of stalling every rank at
+        the per-epoch placement broadcast (the ranks are coupled only through it)."""
+        pending: "collections.deque[Tuple[List[Any], np.ndarray]]" = collections.deque()
         for e in range(count):
             t0 = time.perf_counter()
             arr = bcast(state["next"])
@@ -397,16 +404,16 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                 host["comm"] += t1 - t0
                 host["launch"] += t2 - t1
                 host["schedule"] += time.perf_counter() - t2
-            if pending is not None:
-                collect(*pending, timed)
-            pending = (runs, arr)
+            pending.append((runs, arr))
+            while len(pending) > a.lookahead:
+                collect(*pending.popleft(), timed)
             if rank == 0 and async_cp:
                 t3 = time.perf_counter()
                 state["next"] = cp.get_schedule()
                 if timed:
                     host["schedule"] += time.perf_counter() - t3
-        if pending is not None:
-            collect(*pending, timed)
+        while pending:
+            collect(*pending.popleft(), timed)
 
     run_epochs(a.warmup, False)
     if world > 1:
