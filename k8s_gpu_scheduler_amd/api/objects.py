@@ -280,9 +280,17 @@ def _pod_requests(pod: Obj) -> Dict[str, float]:
     return tot
 
 
-def gpu_request(pod: Obj) -> Tuple[int, int, float]:
+def forget_requests(pod: Obj) -> None:
+    """Drop the memoised request parse of a pod (admission mutated its resources before
+    the object was persisted)."""
+    u = pod.get("metadata", {}).get("uid")
+    if u:
+        _REQ_CACHE.pop(u, None)
+
+
+def gpu_request(pod: Obj, cached: bool = True) -> Tuple[int, int, float]:
     """(whole GPUs, CUs, HBM GiB) requested by a pod."""
-    r = pod_requests(pod)
+    r = pod_requests(pod) if cached else _pod_requests(pod)
     return (int(r.get(C.RESOURCE_GPU, 0)), int(r.get(C.RESOURCE_GPU_CU, 0)),
             float(r.get(C.RESOURCE_GPU_MEM, 0.0)))
 

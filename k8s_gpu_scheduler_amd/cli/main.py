@@ -8,6 +8,7 @@
                          CONFIGURATIONS_DATA_PATH / INTERFERENCE_DATA_PATH / PORT / JOB_DELAY)
   gpu-sched agent       --node $NODE_NAME          (reference profiler DaemonSet)
   gpu-sched redisctl    -l/--list -f/--flush -c/--config   (reference redisCtl.go:22-26)
+  gpu-sched resize-webhook --redis host:port --port 8443 --tls-cert c --tls-key k  (config 5)
   gpu-sched devquery                               (reference gpu_profiling.cpp, all devices)
   gpu-sched profile     (measure the MI355X configuration/interference tables)
   gpu-sched bench       (pod-arrival benchmark; same as bench.py)
@@ -120,6 +121,31 @@ def cmd_recommender(args) -> int:
     server, bound = svc.make_server(port, args.workers)
     logging.info("recommender serving on :%d", bound)
     server.wait_for_termination()
+    return 0
+
+
+def cmd_resize_webhook(args) -> int:
+    """Mutating admission webhook that right-sizes fractional GPU requests from the
+    per-workload history in Redis (BASELINE config 5; recommender/admission.py)."""
+    from ..recommender.admission import AdmissionServer, RedisHistory, ResizeAdmission
+    from ..store.resp import Redis
+    if not args.redis:
+        logging.error("--redis is required (history store)")
+        return 2
+    hist = RedisHistory(Redis.connect(args.redis, args.redis_password))
+    preds = None
+    if args.recommender:
+        from ..recommender.client import CachedPredictions, RecommenderClient
+        cp = CachedPredictions(RecommenderClient(args.recommender))
+        preds = cp.configurations
+    adm = ResizeAdmission(hist.read, preds, min_samples=args.min_samples, shrink_only=args.shrink_only)
+    srv = AdmissionServer(adm, "0.0.0.0", args.port, args.tls_cert, args.tls_key).start()
+    logging.info("resize webhook on %s", srv.url)
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        srv.stop()
     return 0
 
 
@@ -246,6 +272,16 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--redis", default="")
     s.add_argument("--redis-password", default=C.REDIS_PASSWORD)
     s.set_defaults(fn=cmd_recommender)
+    s = sub.add_parser("resize-webhook")
+    s.add_argument("--redis", default="")
+    s.add_argument("--redis-password", default=C.REDIS_PASSWORD)
+    s.add_argument("--recommender", default="")
+    s.add_argument("--port", type=int, default=8443)
+    s.add_argument("--tls-cert", default="")
+    s.add_argument("--tls-key", default="")
+    s.add_argument("--min-samples", type=int, default=3)
+    s.add_argument("--shrink-only", action="store_true")
+    s.set_defaults(fn=cmd_resize_webhook)
     s = sub.add_parser("agent")
     common(s)
     s.add_argument("--node", default="")

@@ -125,6 +125,7 @@ class FakeCluster(KubeClient):
         self._rv = itertools.count(1)
         self._cur_rv = 0
         self._subs: Dict[str, List[Callable[[WatchEvent], None]]] = {r: [] for r in NAMESPACED}
+        self._admission: Dict[str, List[Callable[[Obj], Obj]]] = {}
         self._queues: Dict[str, List[Tuple[Optional[str], "queue.Queue[Optional[WatchEvent]]"]]] = {
             r: [] for r in NAMESPACED}
         self._history: Dict[str, List[Tuple[int, WatchEvent]]] = {r: [] for r in NAMESPACED}
@@ -206,6 +207,11 @@ class FakeCluster(KubeClient):
                 raise NotFound(f"{resource} {namespace}/{name}")
             return O.deepcopy(obj)
 
+    def add_admission(self, resource: str, fn: Callable[[Obj], Obj]) -> None:
+        """Mutating admission hook on CREATE (the in-process analog of a
+        MutatingWebhookConfiguration): fn(obj) -> obj, run in registration order."""
+        self._admission.setdefault(resource, []).append(fn)
+
     def create(self, resource, obj, namespace=None, owned=False):
         """owned=True: the caller hands the object over (never touches it again) and does
         not need the stored copy back -- skips both defensive copies (bulk arrivals)."""
@@ -213,6 +219,8 @@ class FakeCluster(KubeClient):
             self._maybe_fail("create", resource)
             if not owned:
                 obj = O.deepcopy(obj)
+            for fn in self._admission.get(resource, ()):
+                obj = fn(obj)
             md = O.meta(obj)
             if NAMESPACED[resource]:
                 md["namespace"] = namespace or md.get("namespace") or "default"

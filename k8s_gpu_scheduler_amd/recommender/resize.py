@@ -8,7 +8,8 @@ Policy, per pod (history = samples the node agent appended to `gpusched:hist:<po
   never below `min_hbm_gib`.
 * CUs: the smallest partition share s in {32, 64, 128, 256} whose throughput
   (measured at that share if sampled, else scaled from the configuration predictions
-  `<P>P_MI355X`, else from the observed throughput x share ratio) still meets
+  `<P>P_MI355X`, else from the observed throughput x share ratio; observed throughput
+  = its `tput_quantile` quantile) still meets
   SLO x (1 + slo_margin).  No SLO -> keep p95 CU-busy x allotment, rounded to a share.
 """
 from __future__ import annotations
@@ -40,7 +41,10 @@ def _pct(xs: List[float], q: float) -> float:
 def recommend(history: List[Dict[str, Any]], requested_cu: int, requested_hbm_gib: float, slo: float = 0.0,
               conf_predictions: Optional[Dict[str, float]] = None, model: str = "MI355X",
               headroom: float = 0.15, slo_margin: float = 0.05, hbm_quantum_gib: float = 1.0,
-              min_hbm_gib: float = 1.0, min_samples: int = 3) -> ResizeAdvice:
+              min_hbm_gib: float = 1.0, min_samples: int = 3, tput_quantile: float = 0.25) -> ResizeAdvice:
+    """tput_quantile: which quantile of the throughputs observed at a share counts as that
+    share's throughput -- below the median, so a share is only picked when most of its
+    observed runs (under whatever co-runners they had) met the SLO."""
     if len(history) < min_samples:
         return ResizeAdvice(requested_cu, requested_hbm_gib, len(history), "insufficient history")
     hbm = [float(h.get("hbm_gib", 0.0)) for h in history]
@@ -54,7 +58,7 @@ def recommend(history: List[Dict[str, Any]], requested_cu: int, requested_hbm_gi
     if slo > 0:
         def tput(share: int) -> Optional[float]:
             if share in by_share:
-                return sorted(by_share[share])[len(by_share[share]) // 2]
+                return _pct(by_share[share], tput_quantile)
             if conf_predictions:
                 v = conf_predictions.get(f"{SHARE_TO_P[share]}P_{model}")
                 if v is not None and v > 0:
@@ -62,7 +66,7 @@ def recommend(history: List[Dict[str, Any]], requested_cu: int, requested_hbm_gi
             if by_share:
                 # sub-linear extrapolation from the nearest observed share
                 s0 = min(by_share, key=lambda s: abs(math.log2(s / share)))
-                t0 = sorted(by_share[s0])[len(by_share[s0]) // 2]
+                t0 = _pct(by_share[s0], tput_quantile)
                 return t0 * (share / s0) ** 0.85
             return None
         for s in SHARES:

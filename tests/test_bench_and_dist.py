@@ -44,3 +44,14 @@ def test_bench_two_ranks_gloo(tmp_path):
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 8
     assert json.loads(out.read_text())["value"] == r["value"]
+
+
+def test_resize_loop_clears_backlog_sim():
+    """Config 5 (simulated executor): with the admission loop the over-requested pods are
+    shrunk to what their SLO needs, so the backlog that builds without it disappears."""
+    from k8s_gpu_scheduler_amd.parallel import resize_loop
+    on = resize_loop.run(n_gpus=2, epochs=15, rate=3.0, sim=True, resize=True)
+    off = resize_loop.run(n_gpus=2, epochs=15, rate=3.0, sim=True, resize=False)
+    assert on["created"] == off["created"]
+    assert on["completed"] > off["completed"] and on["final_backlog"] < off["final_backlog"]
+    assert on["mean_cu_request_placed"] < 128 and on["admission"]["resized"] > 0

@@ -132,3 +132,77 @@ def test_resize_rpc(server):
     cl = RecommenderClient(addr)
     r = cl.recommend_resources("mlperf-gpu-onnx-resnet50-1024", 128, 64.0, 150.0)
     assert r.samples == 5 and r.recommended_hbm_gib == 23.0 and r.recommended_cu == 64
+
+
+def test_resize_admission_loop_on_fake_cluster():
+    """Config 5 loop: measured history per workload -> admission rewrites a NEW pod's GPU
+    request (QoS class kept), the scheduler packs the smaller pods; the webhook form emits
+    the same change as an AdmissionReview JSONPatch."""
+    import base64
+    import json as _json
+    from k8s_gpu_scheduler_amd.api import constants as C
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+    from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.kube.patch import apply_json_patch
+    from k8s_gpu_scheduler_amd.plugins import full_registry
+    from k8s_gpu_scheduler_amd.plugins.gpu.devices import DeviceLedger
+    from k8s_gpu_scheduler_amd.recommender.admission import (RedisHistory, ResizeAdmission, webhook_handler,
+                                                             workload_key)
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    hist = RedisHistory(Redis(FakeRedisBackend(FakeRedisEngine())))
+    adm = ResizeAdmission(hist.read)
+    fc = FakeCluster()
+    fc.add_admission("pods", adm)
+    fc.create("nodes", O.make_node("n", gpus=1))
+    ledger = DeviceLedger()
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, extras={"ledger": ledger})
+    s.start_informers()
+    # no history yet: requests untouched, only 2 of 4 128-CU pods fit one GPU
+    for i in range(4):
+        fc.create("pods", O.make_pod(f"onnx-resnet50-1024-a{i}", gpu_cu=128, gpu_mem_gib=20, slo=100))
+    assert sum(r.status.ok for r in s.schedule_pending()) == 2
+    assert workload_key(fc.get("pods", "onnx-resnet50-1024-a0", "default")) == "onnx_resnet50_1024"
+    # the executor / agent measured this workload: 64 CUs already give 150 q/s, 8 GiB used
+    for _ in range(8):
+        hist.append("onnx_resnet50_1024", {"cu": 64, "throughput": 150.0, "hbm_gib": 8.0})
+    for i in range(4):
+        fc.delete("pods", f"onnx-resnet50-1024-a{i}", "default")
+    for i in range(4):
+        fc.create("pods", O.make_pod(f"onnx-resnet50-1024-b{i}", gpu_cu=128, gpu_mem_gib=20, slo=100))
+    p = fc.get("pods", "onnx-resnet50-1024-b0", "default")
+    assert O.gpu_request(p) == (0, 64, 10.0)                       # 64 CUs, p95 8 GiB * 1.15 -> 10
+    assert O.gpu_qos(p) == "Guaranteed"                             # limits rewritten with requests
+    assert _json.loads(O.annotations(p)[C.ANNOT_RESIZED])["from"]["cu"] == 128
+    assert sum(r.status.ok for r in s.schedule_pending()) == 4      # all four now fit
+    # webhook front-end: same decision as a JSONPatch
+    pod = O.make_pod("onnx-resnet50-1024-c", gpu_cu=128, gpu_mem_gib=20, slo=100, gpu_limits=False)
+    out = webhook_handler(adm, {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                                "request": {"uid": "u1", "kind": {"kind": "Pod"}, "operation": "CREATE",
+                                            "object": pod}})
+    r = out["response"]
+    assert r["uid"] == "u1" and r["allowed"] and r["patchType"] == "JSONPatch"
+    patched = apply_json_patch(pod, _json.loads(base64.b64decode(r["patch"])))
+    assert O.gpu_request(patched, cached=False)[1] == 64 and O.gpu_qos(patched) == "Burstable"
+
+
+def test_resize_webhook_http_server():
+    import json as _json
+    import urllib.request
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.recommender.admission import AdmissionServer, ResizeAdmission
+    hist = {"onnx_mobilenet_1024": [{"cu": 32, "throughput": 400.0, "hbm_gib": 2.0}] * 5}
+    srv = AdmissionServer(ResizeAdmission(lambda k: hist.get(k, [])), "127.0.0.1", 0).start()
+    try:
+        pod = O.make_pod("mlperf-gpu-onnx-mobilenet-1024", gpu_cu=128, gpu_mem_gib=16, slo=300)
+        body = _json.dumps({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                            "request": {"uid": "x", "kind": {"kind": "Pod"}, "operation": "CREATE",
+                                        "object": pod}}).encode()
+        req = urllib.request.Request(srv.url + "/mutate", data=body, headers={"Content-Type": "application/json"})
+        out = _json.loads(urllib.request.urlopen(req, timeout=5).read())
+        assert out["response"]["allowed"] and out["response"]["patchType"] == "JSONPatch"
+        assert urllib.request.urlopen(srv.url + "/healthz", timeout=5).read() == b"ok"
+    finally:
+        srv.stop()
