@@ -127,16 +127,22 @@ class Framework:
                 return s
         return Status.success()
 
-    def find_feasible(self, state: CycleState, pod: Obj, nodes: List[Any]) -> Tuple[List[Any], Dict[str, Status]]:
+    def find_feasible(self, state: CycleState, pod: Obj, nodes: List[Any],
+                      limit: int = 0) -> Tuple[List[Any], Dict[str, Status]]:
+        """Filter nodes in order; with limit > 0 stop once that many are feasible (the
+        scheduler passes a rotated node list, kube-scheduler's nextStartNodeIndex)."""
         t0 = time.perf_counter_ns()
         feasible, failed = [], {}
         for ni in nodes:
             s = self.run_filter(state, pod, ni)
             if s.ok:
                 feasible.append(ni)
+                if limit and len(feasible) >= limit:
+                    break
             else:
                 failed[ni.name] = s
         self.metrics.add("filter", time.perf_counter_ns() - t0)
+        state.write("framework/nodes-processed", len(feasible) + len(failed))
         return feasible, failed
 
     def run_post_filter(self, state: CycleState, pod: Obj, failed: Dict[str, Status]) -> Tuple[Optional[str], Status]:

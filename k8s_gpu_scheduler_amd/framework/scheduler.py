@@ -91,6 +91,7 @@ class Scheduler:
         self.handle = Handle(self)
         self.frameworks: Dict[str, Framework] = {}
         self._snapshot: Optional[Snapshot] = None
+        self._next_start = 0
         for prof in config.profiles:
             self.frameworks[prof.scheduler_name] = Framework(prof, registry, self.handle, config.parallelism)
         first = next(iter(self.frameworks.values()))
@@ -171,6 +172,20 @@ class Scheduler:
             self._snapshot = self.cache.snapshot()
         return self._snapshot
 
+    # kube-scheduler's adaptive sampling (pkg/scheduler/schedule_one.go numFeasibleNodesToFind)
+    MIN_FEASIBLE_NODES = 100
+    MIN_FEASIBLE_PERCENT = 5
+
+    def num_feasible_nodes_to_find(self, n: int) -> int:
+        if n < self.MIN_FEASIBLE_NODES:
+            return n
+        pct = self.config.percentage_of_nodes_to_score
+        if pct <= 0:
+            pct = max(self.MIN_FEASIBLE_PERCENT, 50 - n // 125)
+        if pct >= 100:
+            return n
+        return max(self.MIN_FEASIBLE_NODES, n * pct // 100)
+
     def _select_host(self, scores: List[Any]) -> str:
         best, cnt, sel = None, 0, ""
         for ns in scores:
@@ -193,11 +208,18 @@ class Scheduler:
         self._snapshot = self.cache.snapshot()
         state = CycleState()
         nodes = self._snapshot.list()
-        res.evaluated = len(nodes)
         st = fw.run_pre_filter(state, pod)
         if not st.ok:
             return self._fail(pi, fw, state, res, st, t0)
-        feasible, failed = fw.find_feasible(state, pod, nodes)
+        limit = self.num_feasible_nodes_to_find(len(nodes))
+        if limit < len(nodes):
+            start = self._next_start % len(nodes)
+            nodes = nodes[start:] + nodes[:start]
+        feasible, failed = fw.find_feasible(state, pod, nodes, limit if limit < len(nodes) else 0)
+        processed = state.read("framework/nodes-processed") or len(nodes)
+        if nodes:
+            self._next_start = (self._next_start + processed) % len(nodes)
+        res.evaluated = processed
         res.feasible = len(feasible)
         if not feasible:
             _, pst = fw.run_post_filter(state, pod, failed)

@@ -234,3 +234,21 @@ def test_slo_objective_prefers_tight_fit():
     s.schedule_pending()
     assert plugin.ledger.placement("default/wl-a-2")[1][0] == g["default/wl-b-1"] != g["default/wl-a-1"] \
         or g["default/wl-a-1"] == g["default/wl-b-1"]
+
+
+def test_adaptive_node_sampling_large_cluster():
+    """kube-scheduler's numFeasibleNodesToFind: with 1000 nodes only 42 % are filtered to
+    feasibility per cycle (50 - 1000/125), starting where the previous cycle stopped, so
+    consecutive pods spread over the cluster; percentageOfNodesToScore=100 scores all."""
+    fc, s, ledger, _ = world(nodes=[f"n{i:04d}" for i in range(1000)], gpus=8)
+    assert s.num_feasible_nodes_to_find(1000) == 420 and s.num_feasible_nodes_to_find(50) == 50
+    assert s.num_feasible_nodes_to_find(100000) == 5000          # 5 % floor
+    s.keep_results = True
+    for i in range(3):
+        fc.create("pods", O.make_pod(f"p{i}", gpu_cu=64))
+    res = s.schedule_pending()
+    assert all(r.status.ok for r in res) and all(r.evaluated == 420 for r in res)
+    s.config.percentage_of_nodes_to_score = 100
+    fc.create("pods", O.make_pod("q", gpu_cu=64))
+    (r,) = s.schedule_pending()
+    assert r.status.ok and r.evaluated == 1000

@@ -112,6 +112,7 @@ def main():
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     res = {"busybox_2nodes": busybox(a.pods), "fractional_4x8gpu": fractional(a.pods),
+           "fractional_1000x8gpu_adaptive_sampling": fractional(a.pods, nodes=1000),
            "reference_algorithm_parity_rpc": parity_rpc(min(a.pods, 40))}
     print(json.dumps(res, indent=1))
     if a.out:
