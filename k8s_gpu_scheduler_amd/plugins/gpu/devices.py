@@ -206,6 +206,7 @@ class DeviceLedger:
         self.nodes: Dict[str, Dict[str, DeviceState]] = {}
         self.pod_index: Dict[str, Tuple[str, List[str]]] = {}     # pod key -> (node, uuids)
         self.generation = 0
+        self.node_gen: Dict[str, int] = {}      # per-node change counter (Score memo key)
 
     def set_devices(self, node: str, devices: Iterable[Device]) -> None:
         with self._lock:
@@ -220,6 +221,7 @@ class DeviceLedger:
                     new[d.uuid] = DeviceState(d)
             self.nodes[node] = new
             self.generation += 1
+            self.node_gen[node] = self.node_gen.get(node, 0) + 1
 
     def devices(self, node: str) -> List[DeviceState]:
         with self._lock:
@@ -250,6 +252,7 @@ class DeviceLedger:
                 st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole)
             self.pod_index[pod_key] = (node, [a[0] for a in allocs])
             self.generation += 1
+            self.node_gen[node] = self.node_gen.get(node, 0) + 1
             return True
 
     def release(self, pod_key: str) -> bool:
@@ -271,6 +274,7 @@ class DeviceLedger:
                     st.used_units[u] = False
                 st.hbm_used = max(0.0, st.hbm_used - use.hbm_gib)
             self.generation += 1
+            self.node_gen[node] = self.node_gen.get(node, 0) + 1
             return True
 
     def placement(self, pod_key: str) -> Optional[Tuple[str, List[str]]]:

@@ -24,11 +24,13 @@ Reference: `type GPU` implementing Score + NormalizeScore + PostBind
 """
 from __future__ import annotations
 
+import dataclasses
 import json
 import logging
 import math
 import random
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -52,6 +54,7 @@ _REQ = "GPU/request"
 _PRED = "GPU/predictions"
 _CHOICE = "GPU/choice"
 _CANDS = "GPU/candidates"
+_SIG = "GPU/signature"
 BIND_ANNOTATIONS = "bind/annotations"
 
 
@@ -128,6 +131,8 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
         self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
         self._col_memo: Dict[str, Optional[str]] = {}
+        self._cands_memo: Dict[str, Tuple[Any, List[Tuple[DeviceState, int]]]] = {}
+        self._score_memo: Dict[str, Tuple[Any, Optional[Choice]]] = {}
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)
         self._client: Optional[RecommenderClient] = None
@@ -420,25 +425,34 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
 
     def _best_choice(self, state: CycleState, pod: Obj, req: GpuRequest, node: str,
                      scoring: bool) -> Optional[Choice]:
-        states = self.ledger.devices(node)
-        if not states:
-            return None
         if req.whole:
-            return self._whole_choice(req, node, states)
+            states = self.ledger.devices(node)
+            return self._whole_choice(req, node, states) if states else None
         memo = state.read(_CANDS)
         if memo is None:
             memo = {}
             state.write(_CANDS, memo)
         cands = memo.get(node)
+        # Across cycles a node's candidates and best choice only change when its ledger
+        # entry (node_gen) or its telemetry changes, so large clusters -- where almost
+        # every node is untouched between two pods -- reuse them (the equivalence-cache
+        # idea of kube-scheduler, keyed by node version x request signature).
+        ckey = (self.ledger.node_gen.get(node, 0), req.units, req.hbm_gib)
         if cands is None:
-            cands = []
-            for st in states:
-                if st.hbm_free + 1e-6 < req.hbm_gib:
-                    continue
-                u0 = st.find_units(req.units)
-                if u0 is None:
-                    continue
-                cands.append((st, u0))
+            hit = self._cands_memo.get(node)
+            if hit is not None and hit[0] == ckey:
+                cands = hit[1]
+            else:
+                states = self.ledger.devices(node)
+                cands = []
+                for st in states:
+                    if st.hbm_free + 1e-6 < req.hbm_gib:
+                        continue
+                    u0 = st.find_units(req.units)
+                    if u0 is None:
+                        continue
+                    cands.append((st, u0))
+                self._cands_memo[node] = (ckey, cands)
             memo[node] = cands      # Filter computes, Score reuses (same cycle snapshot)
         if not cands:
             return None
@@ -448,6 +462,34 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         a = self.args
         name = O.name(pod)
         conf, intf = state.read(_PRED) or self._pod_predictions(name)
+        skey = None
+        if a.pack != "random":
+            tv = self.telemetry.node_version(node) if a.w_telemetry else 0
+            tkey = (tv, int(time.monotonic()) if (tv and self.telemetry.stale_s) else 0)
+            sig = state.read(_SIG)
+            if sig is None:
+                # everything the score depends on besides the node: the request, the
+                # incoming pod's predictions (its workload row) -- not its name
+                x_col = self._workload_col(name, intf) if intf else None
+                sig = (req.units, req.hbm_gib, req.slo, x_col,
+                       tuple(sorted(conf.items())) if conf else (),
+                       () if x_col is not None or not intf else tuple(sorted(intf.items())))
+                state.write(_SIG, sig)
+            skey = (ckey, tkey, sig)
+            hit = self._score_memo.get(node)
+            if hit is not None and hit[0] == skey:
+                return dataclasses.replace(hit[1]) if hit[1] is not None else None
+        best = self._score_cands(node, cands, req, name, conf, intf)
+        if skey is not None:
+            self._score_memo[node] = (skey, best)
+            if best is not None:
+                best = dataclasses.replace(best)
+        return best
+
+    def _score_cands(self, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest, name: str,
+                     conf: Dict[str, float], intf: Dict[str, float]) -> Optional[Choice]:
+        a = self.args
+        states = self.ledger.devices(node)
         slo_scores: List[Optional[float]] = [None] * len(cands)
         if a.w_slo and req.slo > 0 and conf:
             x_col = self._workload_col(name, intf)

@@ -38,11 +38,18 @@ class TelemetryCache:
         self._d: Dict[Tuple[str, str], DeviceSample] = {}
         self.stale_s = stale_s
         self.updates = 0
+        self._node_ver: Dict[str, int] = {}
 
     def update(self, node: str, uuid: str, sample: DeviceSample) -> None:
         with self._lock:
             self._d[(node, uuid)] = sample
             self.updates += 1
+            self._node_ver[node] = self._node_ver.get(node, 0) + 1
+
+    def node_version(self, node: str) -> int:
+        """Bumped on every sample for the node (0 = never sampled): lets Score memoise
+        per-node results until the node's telemetry changes."""
+        return self._node_ver.get(node, 0)
 
     def get(self, node: str, uuid: str) -> Optional[DeviceSample]:
         with self._lock:
