@@ -134,10 +134,27 @@ class _ResourceScore(ScorePlugin):
 
     def __init__(self, args=None, handle=None):
         self.handle = handle
+        self._memo = {}
 
-    def _fractions(self, pod, node_name):
+    def score(self, state, pod, node_name):
+        # a node's score only changes with its NodeInfo generation and the request
         ni = self.handle.snapshot().get(node_name)
         req = O.pod_requests(pod)
+        key = (ni.generation if ni else -1, id(ni.node) if ni else 0) + tuple(req.get(r, 0.0) for r in self.RES)
+        hit = self._memo.get(node_name)
+        if hit is not None and hit[0] == key:
+            return hit[1], None
+        v = self._score(self._fractions(pod, node_name, ni, req))
+        if len(self._memo) > 100000:
+            self._memo.clear()
+        self._memo[node_name] = (key, v)
+        return v, None
+
+    def _fractions(self, pod, node_name, ni=None, req=None):
+        if ni is None:
+            ni = self.handle.snapshot().get(node_name)
+        if req is None:
+            req = O.pod_requests(pod)
         fr = []
         for r in self.RES:
             alloc = ni.allocatable.get(r, 0.0) if ni else 0.0
@@ -150,23 +167,21 @@ class _ResourceScore(ScorePlugin):
 class NodeResourcesLeastAllocated(_ResourceScore):
     NAME = "NodeResourcesLeastAllocated"
 
-    def score(self, state, pod, node_name):
-        fr = self._fractions(pod, node_name)
+    def _score(self, fr):
         if not fr:
-            return 0, None
-        return int(sum((1 - f) * C.MAX_NODE_SCORE for f in fr) / len(fr)), None
+            return 0
+        return int(sum((1 - f) * C.MAX_NODE_SCORE for f in fr) / len(fr))
 
 
 class NodeResourcesBalancedAllocation(_ResourceScore):
     NAME = "NodeResourcesBalancedAllocation"
 
-    def score(self, state, pod, node_name):
-        fr = self._fractions(pod, node_name)
+    def _score(self, fr):
         if len(fr) < 2:
-            return C.MAX_NODE_SCORE, None
+            return C.MAX_NODE_SCORE
         mean = sum(fr) / len(fr)
         var = sum((f - mean) ** 2 for f in fr) / len(fr)
-        return int((1 - var ** 0.5) * C.MAX_NODE_SCORE), None
+        return int((1 - var ** 0.5) * C.MAX_NODE_SCORE)
 
 
 class DefaultBinder(BindPlugin):
