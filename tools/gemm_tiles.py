@@ -72,18 +72,23 @@ def main():
 
     budget = {"b": 0}
 
+    bias16 = {k: v[3].to(torch.bfloat16) for k, v in bufs.items()}
+
     def run_mix():
         for st, seq in zip(streams, seqs):
             with torch.cuda.stream(st):
                 for (M, N, K) in seq:
                     a, bt, c, bias = bufs[(M, N, K)]
-                    loadgen.gemm(a, bt, out=c, bias=bias, relu=True, stream=st, cu_budget=budget["b"])
+                    if budget["b"] < 0:       # hipBLASLt (torch.addmm) + separate ReLU
+                        torch.relu_(torch.addmm(bias16[(M, N, K)], a, bt.T, out=c))
+                    else:
+                        loadgen.gemm(a, bt, out=c, bias=bias, relu=True, stream=st, cu_budget=budget["b"])
         for st in streams:
             torch.cuda.current_stream().wait_stream(st)
     for rnd in range(3):
-        for tile in ("budget64", 0) + TILES:
-            budget["b"] = 64 if tile == "budget64" else 0
-            h.set_gemm_tile(0 if tile == "budget64" else tile)
+        for tile in ("torch", "budget64", 0) + TILES:
+            budget["b"] = 64 if tile == "budget64" else (-1 if tile == "torch" else 0)
+            h.set_gemm_tile(tile if isinstance(tile, int) else 0)
             ms = t_ms(run_mix, iters=5, warm=1)
             if rnd:
                 out["concurrent"].append({"tile": tile, "round": rnd, "tflops": round(flops / ms / 1e9, 1)})
