@@ -65,6 +65,9 @@ class DeviceExecutor:
     #   triad_blocks -- workgroups per stream-kernel launch (0 = the kernel's default)
     gemm_share = True
     triad_blocks = 0
+    #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
+    #                   HIP graph on the pod's stream (captured once per workload/slot)
+    use_graphs = False
 
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
         self.device = device
@@ -76,6 +79,7 @@ class DeviceExecutor:
         self._last_events: List[torch.cuda.Event] = []
         self._unit_last: Dict[int, Tuple[Tuple[int, int], torch.cuda.Event]] = {}
         self.epoch_runs: List[List[PodRun]] = []
+        self._graphs: Dict[Tuple, "torch.cuda.CUDAGraph"] = {}
         self.flops_done = 0.0
         self.bytes_done = 0.0
 
@@ -100,11 +104,41 @@ class DeviceExecutor:
         return b
 
     def warm(self, placements: List[PodRun]) -> None:
-        """Pre-create streams/buffers (outside any timed region)."""
+        """Pre-create streams/buffers -- and, with use_graphs, capture the pods' graphs --
+        outside any timed region."""
         for p in placements:
-            self.stream_for(p.first_unit, p.n_units, p.masked)
-            self.buffers(CATALOG[p.workload], p.first_unit, p.n_units)
+            st = self.stream_for(p.first_unit, p.n_units, p.masked)
+            bufs = self.buffers(CATALOG[p.workload], p.first_unit, p.n_units)
+            if self.use_graphs:
+                self._graph_for(p, bufs, st.stream, self._budget(p))
         torch.cuda.synchronize(self.device)
+
+    def _budget(self, r: PodRun) -> int:
+        return r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
+
+    def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:
+        for _ in range(r.iters):
+            for o, t in bufs.ops:
+                if o.kind == "gemm":
+                    a, bt, bias, c = t
+                    loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+                else:
+                    x, y, z = t
+                    loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
+
+    def _graph_for(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> "torch.cuda.CUDAGraph":
+        """One HIP graph per (workload, unit slot, QoS, iters): captured on the pod's own
+        stream, so replaying it there keeps the stream's CU mask and its ordering."""
+        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks)
+        g = self._graphs.get(k)
+        if g is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                self._enqueue_ops(r, bufs, st, budget)
+            torch.cuda.synchronize(self.device)
+            self._graphs[k] = g
+        return g
 
     def launch_epoch(self, runs: List[PodRun]) -> None:
         """Enqueue one epoch's pods; returns immediately (async).
@@ -126,18 +160,16 @@ class DeviceExecutor:
                     waited.add(id(last[1]))
             w = CATALOG[r.workload]
             bufs = self.buffers(w, r.first_unit, r.n_units)
-            budget = r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
+            budget = self._budget(r)
             r.start = torch.cuda.Event(enable_timing=True)
             r.end = torch.cuda.Event(enable_timing=True)
             r.start.record(st)
-            for _ in range(r.iters):
-                for o, t in bufs.ops:
-                    if o.kind == "gemm":
-                        a, bt, bias, c = t
-                        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
-                    else:
-                        x, y, z = t
-                        loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
+            if self.use_graphs:
+                g = self._graph_for(r, bufs, st, budget)
+                with torch.cuda.stream(st):
+                    g.replay()
+            else:
+                self._enqueue_ops(r, bufs, st, budget)
             r.end.record(st)
             for u in range(r.first_unit, r.first_unit + r.n_units):
                 self._unit_last[u] = (key, r.end)
@@ -180,6 +212,7 @@ class DeviceExecutor:
 
     def close(self) -> None:
         torch.cuda.synchronize(self.device)
+        self._graphs.clear()
         for s in self._streams.values():
             s.close()
         self._streams.clear()

@@ -273,6 +273,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="torch.distributed backend (default: nccl = RCCL on GPU, gloo on CPU)")
     ap.add_argument("--control-plane", default="process", choices=["process", "inline"],
                     help="run apiserver+scheduler in a separate process (default) or inside rank 0")
+    ap.add_argument("--graphs", type=int, default=1, choices=[0, 1],
+                    help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
     ap.add_argument("--out", default="")
@@ -311,6 +313,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         from .executor import DeviceExecutor
         ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
+        ex.use_graphs = bool(a.graphs)
     else:
         ex = SimExecutor()
     gpus_here = [rank] if world > 1 else list(range(n_gpus))
@@ -337,7 +340,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     # warm-up placements: build every (workload, slot) buffer/stream once, untimed
     if use_gpu:
         from .executor import PodRun
-        ex.warm([PodRun(0, wl, u, 2, 1, masked=a.qos == "guaranteed") for wl in W.NAMES for u in (0, 2, 4, 6)])
+        ex.warm([PodRun(0, wl, u, 2, a.iters, masked=a.qos == "guaranteed") for wl in W.NAMES for u in (0, 2, 4, 6)])
 
     totals = {"pods": 0.0, "busy_unit_ms": 0.0, "slo_ok": 0.0}
     state: Dict[str, Any] = {"next": cp.schedule_epoch() if rank == 0 else None}
