@@ -106,9 +106,6 @@ def cu_slice_mask(first_unit: int, n_units: int, cus: int = C.MI355X_CUS) -> Lis
     return words
 
 
-# backwards-compatible name used by earlier tools
-xcd_cu_mask = cu_slice_mask
-
 
 def hsa_cu_mask_ranges(words: List[int]) -> str:
     """Set bits of a CU mask as ROCr's HSA_CU_MASK range list ("0-31,64-95")."""

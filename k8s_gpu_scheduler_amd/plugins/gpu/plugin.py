@@ -44,7 +44,7 @@ from ...recommender.client import CachedPredictions, PredictionProvider, Recomme
 from ...telemetry.cache import TelemetryCache
 from .devices import (CUS_PER_XCD, Device, DeviceLedger, DeviceState, cu_slice_mask, devices_for_node,
                       hsa_cu_mask_ranges)
-from .scoring import DeviceSummary, Resident, build_device_summary, fast_device_score, workload_column
+from .scoring import DeviceSummary, build_device_summary, fast_device_score, workload_column
 from .topology import Topology, select_gpu_set
 
 log = logging.getLogger(__name__)
@@ -414,14 +414,6 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             conf, intf = self._pod_predictions(use.name)
             res.append((use.name, use.slo, conf.get(self._col(use.units[1], st.device.units)), intf))
         return build_device_summary(res)
-
-    def _residents(self, st: DeviceState) -> List[Resident]:
-        out = []
-        for use in st.pods.values():
-            conf, intf = self._pod_predictions(use.name)
-            col = self._col(use.units[1], st.device.units)
-            out.append(Resident(use.name, use.slo, conf, intf, col))
-        return out
 
     def _best_choice(self, state: CycleState, pod: Obj, req: GpuRequest, node: str,
                      scoring: bool) -> Optional[Choice]:

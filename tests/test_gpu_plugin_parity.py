@@ -198,3 +198,25 @@ def test_parity_over_grpc_matches_cache(trained, ref_data):
         assert plugin.predictions.calls >= 4          # the reference's RPC-per-lookup pattern
     finally:
         srv.stop(0)
+
+
+def test_fast_device_score_matches_reference_terms(trained):
+    """Fixed mode's incremental per-device summary gives the reference objective
+    (device_score's terms and aggregation) up to float32-vs-float64 rounding."""
+    import random
+    conf, intf = trained
+    names = [RES, MOB, "mlperf-gpu-tensorflow-ssd-mobilenet-2048", "mlperf-gpu-onnx-ssd-mobilenet-4096",
+             "mlperf-gpu-tensorflow-resnet50-1024"]
+    rng = random.Random(7)
+    for _ in range(200):
+        k = rng.randrange(0, 5)
+        res = [S.Resident(n, rng.choice([0, 40, 90, 150, 400]), conf.lookup(n), intf.lookup(n + "_V100"), "1P_V100")
+               for n in rng.sample(names, k)]
+        inc = rng.choice(names) + "-x"
+        x_intf = intf.lookup(inc[:-2] + "_V100")
+        pred = rng.choice([-1.0, 95.5, 300.0])
+        slo = rng.choice([50.0, 120.0, 600.0])
+        ref = S.device_score(res, inc, slo, pred, x_intf, "1P_V100")
+        summ = S.build_device_summary([(r.name, r.slo, r.conf.get("1P_V100"), r.intf) for r in res])
+        fast = S.fast_device_score(summ, inc, S.workload_column(inc, x_intf) if x_intf else None, slo, pred, x_intf)
+        assert fast == pytest.approx(ref, rel=1e-4, abs=1e-3), (res, inc, slo, pred)
