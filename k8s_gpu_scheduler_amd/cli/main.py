@@ -72,6 +72,12 @@ def cmd_scheduler(args) -> int:
     from ..kube.leader import LeaderElector
     client = _client(args.kubeconfig, args.fake_apiserver)
     cfg, sched = _build_scheduler(args, client)
+    if args.metrics_port:
+        from ..telemetry.exporter import GpuExporter, attach_scheduler_metrics
+        exp = GpuExporter(os.getenv("NODE_NAME", socket.gethostname()), exporter_pod=os.getenv("POD_NAME", ""))
+        attach_scheduler_metrics(exp, sched)
+        exp.serve(args.metrics_port)
+        logging.info("scheduler metrics on :%d/metrics", args.metrics_port)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: stop.set())
     if cfg.leader_election.leader_elect:
@@ -259,6 +265,8 @@ def build_parser() -> argparse.ArgumentParser:
     s = sub.add_parser("scheduler")
     common(s)
     s.add_argument("--config", default="")
+    s.add_argument("--metrics-port", type=int, default=10251,
+                   help="Prometheus /metrics (pods scheduled, latency, per-extension-point means); 0 = off")
     s.set_defaults(fn=cmd_scheduler)
     s = sub.add_parser("extender")
     common(s)

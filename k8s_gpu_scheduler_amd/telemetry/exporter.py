@@ -81,3 +81,30 @@ class GpuExporter:
 
     def serve(self, port: int = 9400, addr: str = "0.0.0.0") -> None:
         start_http_server(port, addr, registry=self.registry)
+
+
+def attach_scheduler_metrics(exporter: "GpuExporter", sched, period_s: float = 5.0):
+    """Feed a Scheduler's results into the exporter's scheduler series: every result
+    (bound / unschedulable, latency) as it happens, per-extension-point mean latency every
+    `period_s`.  Returns a stop() callable."""
+    import threading
+    prev = sched.on_result
+
+    def on_result(res):
+        if res.status.ok and res.node:
+            exporter.observe_scheduler(scheduled=1, latencies=(res.latency_s,))
+        else:
+            exporter.observe_scheduler(failed=1, latencies=(res.latency_s,))
+        if prev is not None:
+            prev(res)
+    sched.on_result = on_result
+    stop = threading.Event()
+
+    def loop():
+        while not stop.wait(period_s):
+            ext = {}
+            for fw in sched.frameworks.values():
+                ext.update(fw.metrics.summary())
+            exporter.observe_scheduler(ext=ext)
+    threading.Thread(target=loop, daemon=True, name="sched-metrics").start()
+    return stop.set

@@ -84,3 +84,29 @@ def test_query_timeout_is_bounded():
     t = time.time()
     assert instant_query("http://127.0.0.1:9", "", timeout_s=0.2) == []
     assert time.time() - t < 3
+
+
+def test_scheduler_metrics_exporter():
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+    from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.plugins import full_registry
+    from k8s_gpu_scheduler_amd.telemetry.exporter import GpuExporter, attach_scheduler_metrics
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n", gpus=1))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False)
+    s.start_informers()
+    exp = GpuExporter("n")
+    stop = attach_scheduler_metrics(exp, s, period_s=0.05)
+    for i in range(3):
+        fc.create("pods", O.make_pod(f"p{i}", gpu_cu=128))
+    s.schedule_pending()
+    import time
+    time.sleep(0.2)
+    stop()
+    txt = exp.render().decode()
+    assert 'gpusched_pods_scheduled_total{result="scheduled"} 2.0' in txt
+    assert 'gpusched_pods_scheduled_total{result="unschedulable"} 1.0' in txt
+    assert "gpusched_scheduling_latency_seconds_count 3.0" in txt
+    assert 'gpusched_extension_point_mean_us{point="score"}' in txt
