@@ -34,9 +34,13 @@ def _py_includes() -> List[str]:
     return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
 
 
-def _targets(asan: bool = False) -> List[Tuple[str, List[str], List[str]]]:
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
+              "tsan": ["-fsanitize=thread", "-fno-omit-frame-pointer"]}
+
+
+def _targets(asan: bool = False, san_kind: str = "") -> List[Tuple[str, List[str], List[str]]]:
     inc = _py_includes()
-    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"] if asan else []
+    san = SANITIZERS.get(san_kind or ("asan" if asan else ""), [])
     core_src = sorted(glob.glob(os.path.join(NATIVE, "core", "*.cpp")))
     smi_src = sorted(glob.glob(os.path.join(NATIVE, "smi", "*.cpp")))
     hip_src = sorted(glob.glob(os.path.join(NATIVE, "hip", "*.hip")) + glob.glob(os.path.join(NATIVE, "hip", "*.cpp")))
@@ -58,13 +62,18 @@ def _stale(out: str, srcs: List[str]) -> bool:
     return any(os.path.getmtime(s) > mt for s in deps)
 
 
-def build(force: bool = False, asan: bool = False, only: Tuple[str, ...] = (), verbose: bool = False) -> List[str]:
+def build(force: bool = False, asan: bool = False, only: Tuple[str, ...] = (), verbose: bool = False,
+          san_kind: str = "") -> List[str]:
+    """san_kind: "" | "asan" (address+undefined) | "tsan" (thread) -- host modules only."""
     built = []
     jobs = []
-    for name, srcs, cmd in _targets(asan):
+    kind = san_kind or ("asan" if asan else "")
+    for name, srcs, cmd in _targets(asan, kind):
         if only and name not in only:
             continue
-        out = os.path.join(HERE, name + ("_asan" if asan else "") + EXT)
+        if kind and name == "_hip":
+            continue                # GPU code is never built with a host sanitizer
+        out = os.path.join(HERE, name + (f"_{kind}" if kind else "") + EXT)
         if not force and not _stale(out, srcs):
             continue
         jobs.append((name, out, cmd + ["-o", out + ".tmp"]))
@@ -88,8 +97,22 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--asan", action="store_true")
+    ap.add_argument("--tsan", action="store_true")
     ap.add_argument("--only", nargs="*", default=[])
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
-    for p in build(a.force, a.asan, tuple(a.only), a.verbose):
+    for p in build(a.force, a.asan, tuple(a.only), a.verbose, "tsan" if a.tsan else ""):
         print("built", p)
+
+
+def sampler_tsan_test(workdir: str) -> Tuple[int, str]:
+    """Build and run native/tests/sampler_tsan.cpp under ThreadSanitizer (host)."""
+    exe = os.path.join(workdir, "sampler_tsan")
+    src = os.path.join(NATIVE, "tests", "sampler_tsan.cpp")
+    p = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                        f"-I{os.path.join(NATIVE, 'smi')}", src, "-o", exe], capture_output=True, text=True)
+    if p.returncode != 0:
+        return p.returncode, p.stderr
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    return r.returncode, r.stdout + r.stderr

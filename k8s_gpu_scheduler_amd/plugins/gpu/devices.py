@@ -164,17 +164,26 @@ class DeviceState:
 
     def find_units(self, n: int) -> Optional[int]:
         """Best-fit aligned run of n free units (alignment = next pow2 >= n); memoised
-        until the unit map changes (the ledger invalidates on reserve/release)."""
-        cache = self.__dict__.setdefault("_fit", {})
-        if n in cache:
-            return cache[n]
+        until the unit map changes.  The memo is tagged with the state's version, which the
+        ledger bumps before AND after every change, so a search that overlapped a
+        concurrent reserve/release is never served from the memo afterwards."""
+        d = self.__dict__
+        ver = d.get("_ver", 0)
+        cache = d.get("_fit")
+        if cache is not None and cache[0] == ver and n in cache[1]:
+            return cache[1][n]
         r = self._find_units(n)
-        cache[n] = r
+        if cache is None or cache[0] != ver:
+            cache = (ver, {})
+            d["_fit"] = cache
+        cache[1][n] = r
         return r
 
     def invalidate(self) -> None:
-        self.__dict__.pop("_fit", None)
-        self.__dict__.pop("_slo", None)     # plugin's resident summary (scoring.DeviceSummary)
+        d = self.__dict__
+        d["_ver"] = d.get("_ver", 0) + 1
+        d.pop("_fit", None)
+        d.pop("_slo", None)     # plugin's resident summary (scoring.DeviceSummary)
 
     def _find_units(self, n: int) -> Optional[int]:
         if n > len(self.used_units):
@@ -247,6 +256,7 @@ class DeviceLedger:
                     st.used_units[u] = True
                 st.hbm_used += hbm
                 st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole)
+                st.invalidate()
             self.pod_index[pod_key] = (node, [a[0] for a in allocs])
             self.generation += 1
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
@@ -270,6 +280,7 @@ class DeviceLedger:
                 for u in range(u0, u0 + n):
                     st.used_units[u] = False
                 st.hbm_used = max(0.0, st.hbm_used - use.hbm_gib)
+                st.invalidate()
             self.generation += 1
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
             return True

@@ -486,9 +486,14 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         if a.w_slo and req.slo > 0 and conf:
             x_col = self._workload_col(name, intf)
             for i, (st, _) in enumerate(cands):
-                summ = st.__dict__.get("_slo")
-                if summ is None:
-                    summ = st.__dict__["_slo"] = self._device_summary(st)
+                d = st.__dict__
+                ver = d.get("_ver", 0)
+                hit = d.get("_slo")
+                if hit is not None and hit[0] == ver:
+                    summ = hit[1]
+                else:                           # version-tagged like find_units' memo
+                    summ = self._device_summary(st)
+                    d["_slo"] = (ver, summ)
                 slo_scores[i] = fast_device_score(summ, name, x_col, req.slo,
                                                   conf.get(self._col(req.units, st.device.units), -1.0), intf)
         best: Optional[Choice] = None

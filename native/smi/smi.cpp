@@ -25,6 +25,8 @@
 #include <thread>
 #include <vector>
 
+#include "sampler.h"
+
 namespace py = pybind11;
 
 namespace {
@@ -235,37 +237,14 @@ class Smi {
     return s == AMDSMI_STATUS_SUCCESS ? "" : status_str(s);
   }
 
-  // ---- background sampler with a ring buffer ---------------------------------------
+  // ---- background sampler with a ring buffer (sampler.h; TSan-tested on the host) -----
   void start(double period_s, int capacity) {
-    stop();
-    running_ = true;
-    cap_ = capacity > 0 ? capacity : 600;
-    th_ = std::thread([this, period_s]() {
-      while (running_) {
-        auto v = sample();
-        {
-          std::lock_guard<std::mutex> g(ring_mu_);
-          ring_.push_back(v);
-          while ((int)ring_.size() > cap_) ring_.pop_front();
-        }
-        auto until = std::chrono::steady_clock::now() + std::chrono::duration<double>(period_s);
-        while (running_ && std::chrono::steady_clock::now() < until)
-          std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      }
-    });
+    sampler_.start([this]() { return sample(); }, period_s, capacity);
   }
 
-  void stop() {
-    running_ = false;
-    if (th_.joinable()) th_.join();
-  }
+  void stop() { sampler_.stop(); }
 
-  std::vector<std::vector<Sample>> drain() {
-    std::lock_guard<std::mutex> g(ring_mu_);
-    std::vector<std::vector<Sample>> out(ring_.begin(), ring_.end());
-    ring_.clear();
-    return out;
-  }
+  std::vector<std::vector<Sample>> drain() { return sampler_.drain(); }
 
   void shutdown() {
     stop();
@@ -276,15 +255,12 @@ class Smi {
   }
 
  private:
-  std::mutex mu_, ring_mu_;
+  std::mutex mu_;
   bool inited_ = false;
   std::string err_;
   std::vector<amdsmi_processor_handle> gpus_;
   std::vector<Sample> prev_;
-  std::thread th_;
-  std::atomic<bool> running_{false};
-  std::deque<std::vector<Sample>> ring_;
-  int cap_ = 600;
+  gs::PeriodicSampler<std::vector<Sample>> sampler_;   // last member: joined first on destruction
 };
 
 py::dict to_dict(const Sample& s) {

@@ -116,3 +116,19 @@ def test_host_modules_build_with_sanitizers(tmp_path):
     out = B.build(force=True, asan=True, only=("_core",))
     assert out and out[0].endswith(".so") and "_asan" in out[0]
     os.remove(out[0])
+
+
+def test_sampler_thread_is_race_free_under_tsan(tmp_path):
+    """The amd-smi sampler's thread/ring contract (native/smi/sampler.h) under
+    ThreadSanitizer: start/stop/drain from several threads."""
+    from k8s_gpu_scheduler_amd._native import build as B
+    rc, out = B.sampler_tsan_test(str(tmp_path))
+    assert rc == 0 and "ok drained=" in out, out[-3000:]
+
+
+@pytest.mark.slow
+def test_host_modules_build_with_tsan():
+    from k8s_gpu_scheduler_amd._native import build as B
+    out = B.build(force=True, only=("_core",), san_kind="tsan")
+    assert out and "_tsan" in out[0]
+    os.remove(out[0])
