@@ -247,6 +247,9 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
 // 0 = auto, 1 = 128x128 (4 waves, 2/CU), 2 = 64x128, 3 = 64x64,
 // 4 = 256x256 (8 waves of 128x64, 1/CU), 5 = 256x128 (8 waves of 64x64, 1/CU)
 static int g_gemm_tile = 0;
+// (Measured and dropped: 128x128 with 2 waves of 128x64 and 128x256 with 4 waves of
+// 64x128 -- fewer LDS bytes per FLOP, but 753 / 670 TF vs 783 TF for 128x128 on the co-run
+// mix: profiles/r01_gemm_tiles_with_2wave_variants.json.)
 static const int kTileBM[6] = {0, 128, 64, 64, 256, 256};
 static const int kTileBN[6] = {0, 128, 128, 64, 256, 128};
 
