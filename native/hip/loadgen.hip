@@ -60,17 +60,26 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds_tile, int row, int kc
 
 // Block tile BM x BN, WGM x WGN waves, each wave (BM/WGM) x (BN/WGN) = MI x NJ MFMA 16x16
 // tiles.  Register reuse (LDS read bytes per FLOP) is set by the WAVE tile and global->LDS
-// traffic per FLOP by the BLOCK tile, so the large variant (256x256, 8 waves of 128x64)
-// cuts LDS demand ~40 % per FLOP against 128x128 -- the LDS port, not the MFMA, bounds
-// the 128x128 loop (reads + LDS-DMA writes ~= 1 LDS cycle per MFMA cycle at full rate).
-// Small tiles exist so that the small-M GEMMs of the workload catalog still launch
-// >= 256 workgroups (one per CU) instead of idling half the chip.
+// traffic per FLOP by the BLOCK tile (the 256x256 variant, 8 waves of 128x64, moves ~40 %
+// fewer LDS bytes per FLOP than 128x128).  Counters at 8192^3 (profiles/r01_gemm_pmc.json):
+// no LDS bank conflicts, LDS array ~30 % busy, waves waiting ~26 % of their cycles -- the
+// 2-stage loop is bound by the wait for the next tile, which STAGES >= 3 (counted vmcnt,
+// raw s_barrier, glds issued two tiles ahead) attacks.  Small tiles exist so that the
+// small-M GEMMs of the workload catalog still launch >= 256 workgroups (one per CU).
 //
 // The MFMA is issued with the B fragment as its first operand, so each lane's 4
 // accumulator registers are 4 CONSECUTIVE output columns of one row (D = C^T layout:
 // col = lane&15 -> m, row = (lane>>4)*4 + r -> n): the epilogue stores 8-byte packed bf16x4
 // (4x fewer store instructions than one bf16 per register) and loads bias as float4.
-template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS>
+// s_waitcnt with only the vmcnt field constrained (expcnt = 7, lgkmcnt = 15 = no wait);
+// gfx9 encoding: vmcnt[3:0] -> bits 3:0, vmcnt[5:4] -> bits 15:14.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int STAGES = 2>
 __global__ void __launch_bounds__(WGM * WGN * 64, OCC)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -79,7 +88,9 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   constexpr int WTM = BM / WGM, WTN = BN / WGN;       // wave tile
   constexpr int MI = WTM / 16, NJ = WTN / 16;
   static_assert(BM * BK * 2 / 16 % NT == 0 && BN * BK * 2 / 16 % NT == 0, "stage split");
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+  constexpr int LOADS = (BM + BN) * BK * 2 / 16 / NT;    // glds per thread per K-tile
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
 
   // ---- XCD-aware bijective remap, then grouped (GROUP_M) tile order ----------------
   const int nwg = gridDim.x;
@@ -110,20 +121,9 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   auto tileB = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES) + A_BYTES; };
 
   const int nt = K / BK;
-  stage_tile<BM, NT>(A, lda, m0, 0, tileA(0), wave, lane);
-  stage_tile<BN, NT>(Bt, ldb, n0, 0, tileB(0), wave, lane);
-  __syncthreads();
-
   const int frow = lane & 15;
   const int fk = lane >> 4;
-  int buf = 0;
-  for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) {   // issue tile t+1 before the MFMAs of tile t
-      stage_tile<BM, NT>(A, lda, m0, (t + 1) * BK, tileA(buf ^ 1), wave, lane);
-      stage_tile<BN, NT>(Bt, ldb, n0, (t + 1) * BK, tileB(buf ^ 1), wave, lane);
-    }
-    const char* a_t = tileA(buf);
-    const char* b_t = tileB(buf);
+  auto compute = [&](const char* a_t, const char* b_t) {
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 af[MI], bf[NJ];
@@ -139,8 +139,45 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    __syncthreads();   // tile t+1 landed (vmcnt(0) before the barrier) and tile t fully read
-    buf ^= 1;
+  };
+  auto stage = [&](int t, int buf) {
+    stage_tile<BM, NT>(A, lda, m0, t * BK, tileA(buf), wave, lane);
+    stage_tile<BN, NT>(Bt, ldb, n0, t * BK, tileB(buf), wave, lane);
+  };
+
+  if constexpr (STAGES == 2) {
+    stage(0, 0);
+    __syncthreads();
+    int buf = 0;
+    for (int t = 0; t < nt; ++t) {
+      if (t + 1 < nt) stage(t + 1, buf ^ 1);   // issue tile t+1 before the MFMAs of tile t
+      compute(tileA(buf), tileB(buf));
+      __syncthreads();   // tile t+1 landed (vmcnt(0) before the barrier) and tile t fully read
+      buf ^= 1;
+    }
+  } else {
+    // Prologue: tiles 0 .. STAGES-2 in flight.  Iteration t: wait until only the tiles
+    // after t are outstanding (counted vmcnt -- loads retire in order), barrier (every
+    // thread's part of tile t landed AND every wave finished reading tile t-1, whose
+    // buffer tile t+STAGES-1 reuses), issue tile t+STAGES-1, compute tile t.
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; ++p)
+      if (p < nt) stage(p, p);
+    for (int t = 0; t < nt; ++t) {
+      const int ahead = nt - 1 - t;             // tiles after t already issued (<= STAGES-2)
+      if (ahead >= STAGES - 2) {
+        wait_vmcnt<LOADS * (STAGES - 2)>();
+      } else if (STAGES == 4 && ahead == 1) {
+        wait_vmcnt<LOADS>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + STAGES - 1 < nt) stage(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      compute(tileA(t % STAGES), tileB(t % STAGES));
+    }
   }
 
   // ---- epilogue (D = C^T layout): row m = lane&15, cols n..n+3 = (lane>>4)*4 + r ----
@@ -226,21 +263,21 @@ static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
 
-template <int BM, int BN, int WGM, int WGN, int OCC>
+template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES = 2>
 static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                         int ldb, int ldc, bool relu, hipStream_t s) {
   const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
   if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false>), grid, block, 0, s, A, B, Cp, bp, M,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES>), grid, block, 0, s, A, B, Cp, bp, M,
                        N, K, lda, ldb, ldc);
 }
 
@@ -250,11 +287,15 @@ static int g_gemm_tile = 0;
 // (Measured and dropped: 128x128 with 2 waves of 128x64 and 128x256 with 4 waves of
 // 64x128 -- fewer LDS bytes per FLOP, but 753 / 670 TF vs 783 TF for 128x128 on the co-run
 // mix: profiles/r01_gemm_tiles_with_2wave_variants.json.)
-static const int kTileBM[6] = {0, 128, 64, 64, 256, 256};
-static const int kTileBN[6] = {0, 128, 128, 64, 256, 128};
+// 6 = 128x128, 3 stages (1/CU); 7 = 64x128, 3 stages (2/CU); 8 = 256x128 8 waves, 3 stages.
+// Measured (profiles/r01_gemm_tiles.json): correct, but none beats 128x128 / 2 stages / 2 per CU
+// (4096x2048x2048: 697 / 783 / 898 vs 954 TF; co-run mix 659 / 682 / 733 vs 795 TF): the extra
+// stage costs the second resident block, which hid the tile wait just as well.
+static const int kTileBM[9] = {0, 128, 64, 64, 256, 256, 128, 64, 256};
+static const int kTileBN[9] = {0, 128, 128, 64, 256, 128, 128, 128, 128};
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 5) throw std::runtime_error("gemm tile must be 0..5");
+  if (t < 0 || t > 8) throw std::runtime_error("gemm tile must be 0..8");
   g_gemm_tile = t;
 }
 
@@ -298,6 +339,9 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 2: launch_gemm<64, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 4: launch_gemm<256, 256, 2, 4, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 5: launch_gemm<256, 128, 4, 2, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 6: launch_gemm<128, 128, 2, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 7: launch_gemm<64, 128, 2, 2, 2, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 8: launch_gemm<256, 128, 4, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     default: launch_gemm<64, 64, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
   HIP_CHECK(hipGetLastError());

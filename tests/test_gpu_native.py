@@ -38,7 +38,7 @@ def test_gemm_matches_fp32_reference(M, N, K, relu, bias):
     assert err <= 0.01 * ref.abs().max().item() + 1e-2, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_gemm_every_tile_variant(tile):
     from k8s_gpu_scheduler_amd import _native
     from k8s_gpu_scheduler_amd.ops import loadgen

@@ -15,7 +15,7 @@ from k8s_gpu_scheduler_amd import _native  # noqa: E402
 from k8s_gpu_scheduler_amd.models import workloads as W  # noqa: E402
 from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
 
-TILES = (1, 2, 3, 4, 5)
+TILES = (1, 2, 3, 4, 5, 6, 7, 8)
 
 
 def t_ms(fn, iters=20, warm=3):
