@@ -22,7 +22,6 @@ from __future__ import annotations
 
 import json
 import logging
-import os
 import threading
 import time
 from typing import Any, Callable, Dict, List, Optional

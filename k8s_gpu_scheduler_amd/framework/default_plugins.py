@@ -6,12 +6,11 @@ resource fit, default binder) stay on.  These are the subset that matters for GP
 """
 from __future__ import annotations
 
-from typing import Any, Dict, Optional, Tuple
+from typing import Any, Dict
 
 from ..api import constants as C
 from ..api import objects as O
-from .interface import (BindPlugin, CycleState, FilterPlugin, NodeScore, PreFilterPlugin, QueueSortPlugin,
-                        ScoreExtensions, ScorePlugin, Status)
+from .interface import BindPlugin, FilterPlugin, PreFilterPlugin, QueueSortPlugin, ScorePlugin, Status
 from .runtime import Registry
 
 Obj = Dict[str, Any]

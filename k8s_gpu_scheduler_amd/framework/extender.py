@@ -20,7 +20,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional
 
 from ..api import objects as O
-from .interface import CycleState, Status
+from .interface import CycleState
 from .scheduler import Scheduler
 
 MAX_EXTENDER_PRIORITY = 10

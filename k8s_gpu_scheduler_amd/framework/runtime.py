@@ -15,9 +15,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..api.constants import MAX_NODE_SCORE, MIN_NODE_SCORE
 from .config import Profile
-from .interface import (EXTENSION_POINTS, BindPlugin, Code, CycleState, FilterPlugin, NodeScore,
-                        PermitPlugin, PostBindPlugin, PostFilterPlugin, PreBindPlugin, PreFilterPlugin,
-                        PreScorePlugin, QueueSortPlugin, ReservePlugin, ScorePlugin, Status, as_status)
+from .interface import EXTENSION_POINTS, Code, CycleState, NodeScore, Status, as_status
 
 log = logging.getLogger(__name__)
 Obj = Dict[str, Any]

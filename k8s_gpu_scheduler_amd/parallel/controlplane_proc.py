@@ -16,7 +16,7 @@ Protocol (multiprocessing Pipe, in order):
 from __future__ import annotations
 
 import multiprocessing as mp
-from typing import Any, Optional
+from typing import Any
 
 import numpy as np
 

@@ -13,12 +13,12 @@ Working buffers are allocated once per (workload, slot) and reused -- a warm con
 from __future__ import annotations
 
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from ..models.workloads import CATALOG, NAMES, Op, Workload
+from ..models.workloads import CATALOG, Op, Workload
 from ..ops import loadgen
 from ..plugins.gpu.devices import CUS_PER_XCD as CUS_PER_UNIT, cu_slice_mask
 

@@ -31,7 +31,6 @@ from __future__ import annotations
 import argparse
 import collections
 import json
-import math
 import os
 import random
 import time

@@ -9,12 +9,11 @@ Redis/Prometheus returns an error instead of `klog.Fatal` killing the process.
 """
 from __future__ import annotations
 
-import json
 import logging
 import random
 import threading
 import time
-from typing import TYPE_CHECKING, Any, Dict, List, Optional
+from typing import TYPE_CHECKING, Any, Dict, List
 
 from ...api import constants as C
 from ...api import objects as O

@@ -21,7 +21,7 @@ import logging
 import os
 import threading
 from concurrent import futures
-from typing import Any, Callable, Dict, Optional
+from typing import Any, Callable, Optional
 
 import grpc
 

@@ -16,7 +16,7 @@ import socket
 import socketserver
 import threading
 import time
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Dict, List, Optional
 
 from .resp import Parser, RedisError, encode_reply
 

@@ -6,7 +6,6 @@ import sys
 import time
 import urllib.request
 
-import pytest
 
 from k8s_gpu_scheduler_amd.api import constants as C
 from k8s_gpu_scheduler_amd.api import objects as O

@@ -1,10 +1,7 @@
 """Smaller components: recommender smoke client/helpers, metrics logger, host-sanitizer
 build of the native host modules, discovery helpers, workload catalog, C++ core
 unit-fit search."""
-import math
 import os
-import subprocess
-import sys
 
 import numpy as np
 import pytest

@@ -10,7 +10,7 @@ import time
 import numpy as np
 import pytest
 
-from k8s_gpu_scheduler_amd.models.imputers import ALSImputer, IterativeImputerModel, SVDImputer, make_imputer
+from k8s_gpu_scheduler_amd.models.imputers import make_imputer
 from k8s_gpu_scheduler_amd.recommender import proto as P
 from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, RecommenderClient, RpcPredictions, reply_to_map
 from k8s_gpu_scheduler_amd.recommender.resize import recommend

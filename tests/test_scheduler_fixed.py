@@ -19,7 +19,7 @@ from k8s_gpu_scheduler_amd.framework.interface import NodeScore, min_max_normali
 from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
 from k8s_gpu_scheduler_amd.kube.client import Conflict, FakeCluster
 from k8s_gpu_scheduler_amd.plugins import full_registry
-from k8s_gpu_scheduler_amd.plugins.gpu.devices import DeviceLedger, cu_slice_mask, mask_to_hex
+from k8s_gpu_scheduler_amd.plugins.gpu.devices import DeviceLedger
 from k8s_gpu_scheduler_amd.plugins.gpu.topology import Topology, select_gpu_set
 from k8s_gpu_scheduler_amd.telemetry.cache import DeviceSample, TelemetryCache
 
