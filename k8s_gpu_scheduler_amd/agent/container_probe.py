@@ -3,7 +3,7 @@ pod's env (ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES) and the CUs its kernels a
 on (HSA_CU_MASK).  The default command of `agent.launcher.PodLauncher` -- the in-container
 check of SURVEY §7.4 ("the pod saw exactly the one assigned device").
 
-  python -m k8s_gpu_scheduler_amd.agent.container_probe      -> one JSON line on stdout
+  python -m k8s_gpu_scheduler_amd.agent.container_probe [--work N]   -> one JSON line on stdout
 """
 from __future__ import annotations
 
@@ -39,9 +39,30 @@ def probe(blocks: int = 4096) -> dict:
     return out
 
 
+def work(iters: int) -> dict:
+    """A little real load (MFMA GEMM + HBM stream) so a profiled pod has kernels to trace."""
+    import torch
+    from ..ops import loadgen
+    # operands generated on the host: device-side RNG kernels (hiprand, shipped with the torch
+    # wheel's ROCm) crashed under the system rocprofv3's kernel tracer on the box
+    g = torch.Generator().manual_seed(0)
+    a = (torch.rand(2048, 2048, generator=g) - 0.5).to(torch.bfloat16).cuda()
+    bt = (torch.rand(2048, 2048, generator=g) - 0.5).to(torch.bfloat16).cuda()
+    x, y, z = (torch.ones(1 << 22).cuda() for _ in range(3))
+    for _ in range(iters):
+        loadgen.gemm(a, bt, relu=True)
+        loadgen.triad(x, y, z, 1.5)
+    torch.cuda.synchronize()
+    return {"work_iters": iters}
+
+
 def main() -> int:
     try:
-        print(json.dumps(probe()), flush=True)
+        out = probe()
+        n = int(sys.argv[sys.argv.index("--work") + 1]) if "--work" in sys.argv else 0
+        if n > 0:
+            out.update(work(n))
+        print(json.dumps(out), flush=True)
         return 0
     except Exception as e:  # report, do not crash silently
         print(json.dumps({"error": str(e)}), flush=True)

@@ -69,6 +69,8 @@ class PodLauncher:
             base.pop(k, None)
         self.base_env = base
         self.launched: Dict[str, LaunchResult] = {}
+        self.cwd: Optional[str] = None              # container working directory (None = ours)
+        self.extra_env: Dict[str, str] = {}         # runtime-injected env (not the pod's)
 
     # ------------------------------------------------------------------ env
     def env_for(self, pod: Obj) -> Dict[str, str]:
@@ -111,9 +113,11 @@ class PodLauncher:
         argv = (self.command_for(pod) if self.command_for else None) or \
             (list(ctr.get("command") or []) + list(ctr.get("args") or [])) or self.command
         full_env = dict(self.base_env)
+        full_env.update(self.extra_env)
         full_env.update(env)
         try:
-            p = subprocess.run(argv, env=full_env, capture_output=True, text=True, timeout=self.timeout_s)
+            p = subprocess.run(argv, env=full_env, capture_output=True, text=True, timeout=self.timeout_s,
+                               cwd=self.cwd)
             res = LaunchResult(key, p.returncode, p.stdout, p.stderr, env)
         except subprocess.TimeoutExpired as e:
             res = LaunchResult(key, -9, e.stdout or "", (e.stderr or "") + "\ntimeout", env)

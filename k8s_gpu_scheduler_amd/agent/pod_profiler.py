@@ -1,0 +1,118 @@
+"""Per-pod GPU profiling sidecar: rocprofv3 around the container, summary into Redis.
+
+BASELINE's north star: "the profiler sidecar samples rocprof counters per pod into Redis
+and the recommender resizes GPU requests from that history".  The reference's profiler only
+enumerates UUIDs (pkg/profiler/profile_gpu.sh:3-13); its per-workload throughput matrices were
+measured offline.  Here a launched pod (agent.launcher.PodLauncher) can run under
+
+  rocprofv3 --kernel-trace --stats --output-format csv -d <dir> -o run -- <container argv>
+
+(the program directly after `--`, no shell or env hop), or, in a separate mode, under
+`rocprofv3 --pmc <counters>` (counters are never combined with trace domains).  The CSVs are
+summarised -- GPU busy time, kernel count, the top kernels, busy fraction of the pod's wall
+time, counter totals -- and appended to the pod's workload history
+(`schema.history_key(<workload>)`), next to the CU share it ran on, which is exactly what
+`recommender.resize.recommend` / the resize admission webhook read.
+"""
+from __future__ import annotations
+
+import csv
+import os
+import shutil
+import tempfile
+import time
+from typing import Any, Dict, List, Optional
+
+from ..api import constants as C
+from ..api import objects as O
+from ..recommender.admission import RedisHistory, workload_key
+from .launcher import LaunchResult, PodLauncher
+
+ROCPROF = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+
+
+def summarize_kernel_stats(path: str, top: int = 5) -> Dict[str, Any]:
+    rows = list(csv.DictReader(open(path)))
+    tot_ns = sum(float(r.get("TotalDurationNs", 0) or 0) for r in rows)
+    calls = sum(int(float(r.get("Calls", 0) or 0)) for r in rows)
+    rows.sort(key=lambda r: -float(r.get("TotalDurationNs", 0) or 0))
+    return {"gpu_busy_ms": tot_ns / 1e6, "kernels": calls,
+            "top": [{"name": r["Name"][:120], "calls": int(float(r["Calls"])),
+                     "ms": float(r["TotalDurationNs"]) / 1e6} for r in rows[:top]]}
+
+
+def summarize_counters(path: str) -> Dict[str, float]:
+    tot: Dict[str, float] = {}
+    for r in csv.DictReader(open(path)):
+        k = r.get("Counter_Name", "")
+        tot[k] = tot.get(k, 0.0) + float(r.get("Counter_Value", 0) or 0)
+    return tot
+
+
+class ProfiledLauncher(PodLauncher):
+    """PodLauncher whose containers run under rocprofv3; each finished pod appends one
+    profile sample to its workload's history."""
+
+    def __init__(self, *a: Any, history: Optional[RedisHistory] = None, mode: str = "trace",
+                 counters: Optional[List[str]] = None, keep_dir: str = "", **kw: Any):
+        super().__init__(*a, **kw)
+        if mode not in ("trace", "pmc"):
+            raise ValueError("mode must be 'trace' or 'pmc'")
+        self.history = history
+        self.mode = mode
+        self.counters = counters or ["SQ_WAVES", "SQ_BUSY_CU_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16"]
+        self.keep_dir = keep_dir
+        self.samples: Dict[str, Dict[str, Any]] = {}
+
+    def run(self, pod: Dict[str, Any]) -> LaunchResult:
+        work = tempfile.mkdtemp(prefix="podprof-", dir=os.environ.get("TMPDIR") or None)
+        out_dir = os.path.join(work, "prof")
+        inner = self.command_for
+
+        def wrapped(p: Dict[str, Any]) -> List[str]:
+            ctr = O.containers(p)[0] if O.containers(p) else {}
+            argv = (inner(p) if inner else None) or \
+                (list(ctr.get("command") or []) + list(ctr.get("args") or [])) or self.command
+            prof = [ROCPROF, "--output-format", "csv", "-d", out_dir, "-o", "run"]
+            prof += ["--kernel-trace", "--stats"] if self.mode == "trace" else ["--pmc", *self.counters]
+            return prof + ["--"] + list(argv)
+        self.command_for = wrapped
+        # rocprofv3 keeps its scratch in the working directory and TMPDIR: both go to the
+        # per-pod temp dir; the package stays importable through PYTHONPATH
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        old_cwd, old_env = self.cwd, dict(self.extra_env)
+        self.cwd = work
+        self.extra_env.update({"TMPDIR": work, "PYTHONPATH": os.pathsep.join(
+            x for x in (pkg_root, self.base_env.get("PYTHONPATH", "")) if x)})
+        t0 = time.time()
+        try:
+            res = super().run(pod)
+        finally:
+            self.command_for = inner
+            self.cwd, self.extra_env = old_cwd, old_env
+        wall = time.time() - t0
+        sample: Dict[str, Any] = {"ts": t0, "wall_s": wall, "rc": res.rc}
+        try:
+            for root, _, files in os.walk(out_dir):
+                for f in files:
+                    if f.endswith("kernel_stats.csv"):
+                        sample.update(summarize_kernel_stats(os.path.join(root, f)))
+                    elif f.endswith("counter_collection.csv"):
+                        sample["counters"] = summarize_counters(os.path.join(root, f))
+            if "gpu_busy_ms" in sample:
+                sample["busy_frac"] = min(1.0, sample["gpu_busy_ms"] / 1e3 / max(wall, 1e-9))
+            g, cu, mem = O.gpu_request(pod)
+            sample["cu"] = cu or (g * C.MI355X_CUS)
+            if mem:
+                sample["hbm_gib"] = mem
+            self.samples[O.key(pod)] = sample
+            if self.history is not None:
+                self.history.append(workload_key(pod), sample)
+        finally:
+            if self.keep_dir:
+                dst = os.path.join(self.keep_dir, O.name(pod))
+                shutil.rmtree(dst, ignore_errors=True)
+                if os.path.isdir(out_dir):
+                    shutil.copytree(out_dir, dst)
+            shutil.rmtree(work, ignore_errors=True)
+        return res

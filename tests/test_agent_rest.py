@@ -201,3 +201,37 @@ def test_launcher_builds_kubelet_env_from_assignment():
     assert b["HSA_CU_MASK"] is None and b["ROCR_VISIBLE_DEVICES"]       # Burstable: no hard mask
     assert w["HSA_CU_MASK"] is None and w["ROCR_VISIBLE_DEVICES"].startswith("GPU-")
     assert O.phase(fc.get("pods", "whole", "default")) == "Succeeded"
+
+
+def test_profiled_launcher_records_history(tmp_path, monkeypatch):
+    """The rocprof sidecar wraps the container command (program right after `--`) and turns
+    the kernel statistics into a history sample for the pod's workload (CPU: a stand-in
+    profiler script writes a kernel_stats.csv)."""
+    import os
+    import stat
+    import sys
+    from k8s_gpu_scheduler_amd.agent import pod_profiler
+    from k8s_gpu_scheduler_amd.agent.pod_profiler import ProfiledLauncher
+    from k8s_gpu_scheduler_amd.recommender.admission import RedisHistory
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(
+        "#!" + sys.executable + "\n"
+        "import os, subprocess, sys\n"
+        "a = sys.argv[1:]; d = a[a.index('-d') + 1]; cmd = a[a.index('--') + 1:]\n"
+        "os.makedirs(d, exist_ok=True)\n"
+        "open(os.path.join(d, 'run_kernel_stats.csv'), 'w').write(\n"
+        "  'Name,Calls,TotalDurationNs,AverageNs,Percentage\\n'\n"
+        "  'gemm_bf16_nt_kernel,40,2000000,50000,80\\nstream_triad,40,500000,12500,20\\n')\n"
+        "sys.exit(subprocess.call(cmd))\n")
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    monkeypatch.setattr(pod_profiler, "ROCPROF", str(fake))
+    fc, s = _sched_with_agent(synthetic_node(8, node="mi355x-0"))
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-x", gpu_cu=64, gpu_mem_gib=8))
+    assert all(r.status.ok for r in s.schedule_pending())
+    hist = RedisHistory(rds())
+    la = ProfiledLauncher(fc, "mi355x-0", command=[sys.executable, "-c", "print('{}')"], history=hist)
+    (res,) = la.run_bound()
+    assert res.rc == 0
+    (h,) = hist.read("onnx_resnet50_1024")
+    assert h["gpu_busy_ms"] == 2.5 and h["kernels"] == 80 and h["cu"] == 64 and h["hbm_gib"] == 8
+    assert h["top"][0]["name"].startswith("gemm_bf16")

@@ -266,3 +266,38 @@ def test_executor_graph_replay_matches_eager():
         ex.close()
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
+
+
+def test_profiled_pod_writes_rocprof_history():
+    """Profiler sidecar on the box: the pod runs under rocprofv3 --kernel-trace --stats and
+    its kernel time lands in the workload's Redis history (what the resize loop reads)."""
+    import sys
+    from k8s_gpu_scheduler_amd.agent.devices import synthetic_node
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.pod_profiler import ProfiledLauncher
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+    from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.plugins import full_registry
+    from k8s_gpu_scheduler_amd.recommender.admission import RedisHistory
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    NodeAgent("box", r, synthetic_node(1, node="box")).publish()
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("box", gpus=1))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, extras={"redis": r})
+    s.start_informers()
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-prof", gpu_cu=256))
+    assert all(x.status.ok for x in s.schedule_pending())
+    hist = RedisHistory(r)
+    la = ProfiledLauncher(fc, "box", timeout_s=300, history=hist,
+                          command=[sys.executable, "-m", "k8s_gpu_scheduler_amd.agent.container_probe", "--work", "30"])
+    # the synthetic node's UUIDs are not this box's ROCr ids: run unfiltered
+    la.env_for = lambda pod: {}
+    (res,) = la.run_bound()
+    assert res.rc == 0, res.stderr[-3000:]
+    (h,) = hist.read("onnx_resnet50_1024")
+    assert h["gpu_busy_ms"] > 0 and h["kernels"] >= 60, h
+    assert any("gemm_bf16" in k["name"] for k in h["top"]), h["top"]
