@@ -45,7 +45,7 @@ from ...telemetry.cache import TelemetryCache
 from .devices import (CUS_PER_XCD, Device, DeviceLedger, DeviceState, cu_slice_mask, devices_for_node,
                       hsa_cu_mask_ranges)
 from .scoring import DeviceSummary, build_device_summary, fast_device_score, workload_column
-from .topology import Topology, select_gpu_set
+from .topology import XGMI_GPU_BPS, Topology, select_gpu_set
 
 log = logging.getLogger(__name__)
 Obj = Dict[str, Any]
@@ -546,7 +546,13 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                           [s.device for s in pick])
         topo = self.topologies.get(node) or Topology.fully_connected(max(s.device.gpu for s in states) + 1)
         by_gpu = {st.device.gpu: st for st in free}
-        sel = select_gpu_set(topo, list(by_gpu), req.whole)
+        load: Dict[int, float] = {}
+        if self.args.w_telemetry:
+            for g, st in by_gpu.items():
+                smp = self.telemetry.get(node, st.device.uuid)
+                if smp is not None:
+                    load[g] = max(smp.xgmi_tx_bps, smp.xgmi_rx_bps) / XGMI_GPU_BPS
+        sel = select_gpu_set(topo, list(by_gpu), req.whole, load)
         if sel is None:
             return None
         gpus, quality = sel

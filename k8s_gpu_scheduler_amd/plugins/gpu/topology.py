@@ -10,7 +10,9 @@ adjacency alone rarely discriminates; the selection therefore ranks candidate se
 2. NUMA locality: all GPUs on one NUMA node/socket (host staging stays local);
 3. best fit: take GPUs from the NUMA domain with the fewest free GPUs that still fits,
    so larger future requests keep a whole domain;
-4. lowest total link weight (amdsmi `topo_get_link_weight`), then lowest indices.
+4. least live xGMI traffic on the set's GPUs (telemetry: amd-smi per-link accumulators,
+   quantised to 10 % of a GPU's 7-link capacity so noise does not reorder equal sets);
+5. lowest total link weight (amdsmi `topo_get_link_weight`), then lowest indices.
 A set is only eligible if each GPU is entirely free (no fractional residents): RCCL
 rings of a multi-GPU pod are per-link bound and a co-located partition pod would share
 that GPU's links.
@@ -60,8 +62,13 @@ def is_clique(topo: Topology, gpus: Sequence[int]) -> bool:
     return all(topo.connected(a, b) for a, b in itertools.combinations(gpus, 2))
 
 
-def select_gpu_set(topo: Topology, free_gpus: Sequence[int], k: int) -> Optional[Tuple[List[int], float]]:
-    """Best k-GPU xGMI clique among `free_gpus`; returns (gpus, quality in [0,1]) or None."""
+XGMI_GPU_BPS = 7 * 153e9        # one MI355X: 7 xGMI links x ~153 GB/s per direction
+
+
+def select_gpu_set(topo: Topology, free_gpus: Sequence[int], k: int,
+                   link_load: Optional[Dict[int, float]] = None) -> Optional[Tuple[List[int], float]]:
+    """Best k-GPU xGMI clique among `free_gpus`; returns (gpus, quality in [0,1]) or None.
+    link_load: per-GPU xGMI utilisation in [0, 1] (live telemetry), optional."""
     free = sorted(set(free_gpus))
     if k <= 0 or len(free) < k:
         return None
@@ -78,7 +85,8 @@ def select_gpu_set(topo: Topology, free_gpus: Sequence[int], k: int) -> Optional
         same_numa = len(domains) == 1
         fit = min(free_per_numa[d] for d in domains) if same_numa else 99
         wsum = sum(topo.weight[a][b] if topo.weight else 0 for a, b in itertools.combinations(combo, 2))
-        key = (0 if same_numa else 1, fit, wsum, combo)
+        load = sum(round(10 * min(1.0, max(0.0, (link_load or {}).get(g, 0.0)))) for g in combo)
+        key = (0 if same_numa else 1, fit, load, wsum, combo)
         if best is None or key < best[0]:
             best = (key, list(combo))
     if best is None:

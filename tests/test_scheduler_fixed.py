@@ -180,6 +180,22 @@ def test_topology_selection_rules():
     assert select_gpu_set(t, [0, 1], 2) is None
 
 
+def test_quad_avoids_busy_xgmi_links():
+    """Two equally good NUMA-local quads: live xGMI traffic on one GPU of the first steers
+    the 4-GPU pod to the other (telemetry-aware topology Filter/Score, BASELINE config 4)."""
+    t = Topology.fully_connected(8)
+    assert select_gpu_set(t, range(8), 4, {1: 0.8})[0] == [4, 5, 6, 7]
+    assert select_gpu_set(t, range(8), 4, {1: 0.04})[0] == [0, 1, 2, 3]     # below the 10 % quantum
+    fc, s, ledger, tele = world()
+    for st in ledger.devices("node-a"):
+        tele.update("node-a", st.device.uuid,
+                    DeviceSample(xgmi_tx_bps=600e9 if st.device.gpu == 2 else 0.0))
+    fc.create("pods", O.make_pod("quad", gpus=4))
+    (r,) = s.schedule_pending()
+    assert r.status.ok
+    assert sorted(st.device.gpu for st in ledger.devices("node-a") if st.pods) == [4, 5, 6, 7]
+
+
 def test_bind_failure_unreserves_and_requeues():
     fc, s, ledger, _ = world()
     fc.fail_next("bind", "pods", Conflict("apiserver says no"))
