@@ -122,7 +122,7 @@ class FakeApiServer:
                     return self._send(404, {"code": 404})
                 body = self._body()
                 try:
-                    if r["sub"] == "binding":
+                    if r.get("sub") == "binding":
                         outer.cluster.bind(r["ns"], r["name"], body["target"]["name"],
                                            body.get("metadata", {}).get("uid", ""),
                                            body.get("metadata", {}).get("annotations"))

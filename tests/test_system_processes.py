@@ -1,0 +1,103 @@
+"""System test of the shipped entry points as separate processes (CPU): the HTTP fake
+apiserver (`fake-cluster`), the node agent (`agent --synthetic`) publishing to a Redis
+server, and the scheduler (`scheduler` with our deploy/scheduler.yaml config, leader
+election on a Lease) -- pods created over REST get bound with their device assignment, and
+the scheduler's /metrics counts them."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+import pytest
+
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.kube.rest import RestClient, RestConfig
+from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisEngine, FakeRedisServer
+from k8s_gpu_scheduler_amd.store.resp import Redis
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(args, **kw):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.Popen([sys.executable, "-m", "k8s_gpu_scheduler_amd", *args], cwd=ROOT, env=env,
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, **kw)
+
+
+def _wait(pred, timeout=60.0, every=0.2):
+    t = time.time()
+    while time.time() - t < timeout:
+        v = pred()
+        if v:
+            return v
+        time.sleep(every)
+    return None
+
+
+@pytest.mark.timeout(240)
+def test_scheduler_agent_apiserver_as_processes(tmp_path):
+    procs = []
+    redis = FakeRedisServer(FakeRedisEngine(password=C.REDIS_PASSWORD)).start()
+    try:
+        api_port = _free_port()
+        fc = _spawn(["fake-cluster", "--port", str(api_port), "--nodes", "1", "--gpus", "8"])
+        procs.append(fc)
+        url = fc.stdout.readline().strip()
+        assert url.startswith("http"), url
+        client = RestClient(RestConfig(url))
+        node = O.name(client.list("nodes")[0][0])
+        raddr = redis.addr
+        ag = _spawn(["agent", "--fake-apiserver", url, "--redis", raddr, "--node", node, "--synthetic", "8",
+                     "--once", "--no-discovery", "--metrics-port", "0"])
+        assert ag.wait(120) == 0, ag.stdout.read()
+        mport = _free_port()
+        sc = _spawn(["scheduler", "--fake-apiserver", url, "--redis", raddr, "--no-discovery",
+                     "--config", os.path.join(ROOT, "deploy", "scheduler.yaml"), "--metrics-port", str(mport)])
+        procs.append(sc)
+        client.create("configmaps", O.make_config_map("env-a"))
+        for i in range(4):
+            client.create("pods", O.make_pod(f"onnx-resnet50-1024-{i}", gpu_cu=64, gpu_mem_gib=8, slo=100,
+                                             config_maps=["env-a"] if i == 0 else []))
+        client.create("pods", O.make_pod("whole", gpus=2))
+
+        def all_bound():
+            pods = client.list("pods", "default")[0]
+            return pods if len(pods) == 5 and all(O.node_name_of(p) for p in pods) else None
+        pods = _wait(all_bound, 120)
+        assert pods, [(O.name(p), O.node_name_of(p)) for p in client.list("pods", "default")[0]]
+        by = {O.name(p): p for p in pods}
+        uuids = json.loads(Redis.connect(raddr, C.REDIS_PASSWORD).get(node) or "[]")
+        ann = O.annotations(by["onnx-resnet50-1024-0"])
+        assert ann[C.ANNOT_DEVICES].startswith("GPU-") and ann[C.ANNOT_CU_MASK].startswith("0:")
+        if uuids:
+            assert ann[C.ANNOT_DEVICES] in uuids
+        assert len(O.annotations(by["whole"])[C.ANNOT_DEVICES].split(",")) == 2
+        env = client.get("configmaps", "env-a", "default")["data"]
+        assert env[C.ENV_ROCR_VISIBLE] == ann[C.ANNOT_DEVICES]
+        # the leader holds the Lease named in the config
+        lease = client.get("leases", "gpu-scheduler", "kube-system")
+        assert lease["spec"]["holderIdentity"]
+        txt = _wait(lambda: (lambda t: t if 'result="scheduled"} 5.0' in t else None)(
+            urllib.request.urlopen(f"http://127.0.0.1:{mport}/metrics", timeout=5).read().decode()), 30)
+        assert txt, "scheduler metrics missing"
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        redis.stop()
