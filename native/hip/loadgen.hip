@@ -31,31 +31,36 @@ constexpr int GROUP_M = 8;
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
-// Issue the glds for one ROWSx64 bf16 tile (rows [r0, r0+ROWS), k [k0, k0+64)) of a
-// row-major matrix with leading dimension ld (elements).  Logical 16-byte chunk kc of row
-// r lands at physical chunk kc ^ ((r >> 1) & 7) of that row's 128-byte LDS line; the LDS
-// image itself is lane-linear (glds requirement), so the swizzle is applied on the
+// Issue the glds for one ROWS x KT bf16 tile (rows [r0, r0+ROWS), k [k0, k0+KT)) of a
+// row-major matrix with leading dimension ld (elements).  A row is KT*2 bytes = KT/8 16-byte
+// chunks; logical chunk kc of row r lands at physical chunk kc ^ ((r >> 1) & (KT/8 - 1)).
+// The LDS image itself is lane-linear (glds requirement), so the swizzle is applied on the
 // per-lane SOURCE address (rule: linear dest + permuted source + same permutation on read).
-// With two 128-B rows per 256-B bank row, lanes 0-15 of a ds_read_b128 (rows r..r+15,
-// same logical chunk) then hit 16 distinct 16-B slots: conflict-free.
-template <int ROWS, int NT>
+// For KT = 64 (128-B rows) and KT = 32 (64-B rows) this makes every 16-lane group of a
+// ds_read_b128 fragment read (rows r..r+15, one logical chunk) hit 16 distinct 16-B bank
+// slots: conflict-free (checked against the gfx950 ds_read_b128 lane groups; PMC
+// SQ_LDS_BANK_CONFLICT = 0, profiles/r01_gemm_pmc.json).
+template <int ROWS, int NT, int KT = BK>
 __device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld, int r0, int k0,
                                            char* lds_tile, int wave, int lane) {
+  constexpr int CH = KT / 8;          // 16-byte chunks per row
+  constexpr int SH = CH == 8 ? 3 : 2;
 #pragma unroll
-  for (int i = 0; i < ROWS * BK * 2 / 16 / NT; ++i) {
+  for (int i = 0; i < ROWS * KT * 2 / 16 / NT; ++i) {
     const int chunk = i * NT + wave * 64 + lane;
-    const int r = chunk >> 3;
-    const int p = chunk & 7;
-    const int kc = p ^ ((r >> 1) & 7);
+    const int r = chunk >> SH;
+    const int p = chunk & (CH - 1);
+    const int kc = p ^ ((r >> 1) & (CH - 1));
     const __bf16* src = g + (size_t)(r0 + r) * ld + k0 + kc * 8;
     char* dst = lds_tile + (i * NT + wave * 64) * 16;  // wave-uniform base
     __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
   }
 }
 
+template <int KT = BK>
 __device__ __forceinline__ bf16x8 lds_frag(const char* lds_tile, int row, int kchunk) {
-  const int phys = kchunk ^ ((row >> 1) & 7);
-  return *reinterpret_cast<const bf16x8*>(lds_tile + row * (BK * 2) + phys * 16);
+  const int phys = kchunk ^ ((row >> 1) & (KT / 8 - 1));
+  return *reinterpret_cast<const bf16x8*>(lds_tile + row * (KT * 2) + phys * 16);
 }
 
 // Block tile BM x BN, WGM x WGN waves, each wave (BM/WGM) x (BN/WGN) = MI x NJ MFMA 16x16
@@ -79,17 +84,18 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int STAGES = 2>
+template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int STAGES = 2, int KT = BK>
 __global__ void __launch_bounds__(WGM * WGN * 64, OCC)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
   constexpr int NT = WGM * WGN * 64;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static_assert(KT == 32 || KT == 64, "K tile");
+  constexpr int A_BYTES = BM * KT * 2, B_BYTES = BN * KT * 2;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;       // wave tile
   constexpr int MI = WTM / 16, NJ = WTN / 16;
-  static_assert(BM * BK * 2 / 16 % NT == 0 && BN * BK * 2 / 16 % NT == 0, "stage split");
+  static_assert(BM * KT * 2 / 16 % NT == 0 && BN * KT * 2 / 16 % NT == 0, "stage split");
   static_assert(STAGES >= 2 && STAGES <= 4, "stages");
-  constexpr int LOADS = (BM + BN) * BK * 2 / 16 / NT;    // glds per thread per K-tile
+  constexpr int LOADS = (BM + BN) * KT * 2 / 16 / NT;    // glds per thread per K-tile
   __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
 
   // ---- XCD-aware bijective remap, then grouped (GROUP_M) tile order ----------------
@@ -120,17 +126,17 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   auto tileA = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES); };
   auto tileB = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES) + A_BYTES; };
 
-  const int nt = K / BK;
+  const int nt = K / KT;
   const int frow = lane & 15;
   const int fk = lane >> 4;
   auto compute = [&](const char* a_t, const char* b_t) {
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+    for (int kk = 0; kk < KT / 32; ++kk) {
       bf16x8 af[MI], bf[NJ];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[j] = lds_frag(b_t, wn * WTN + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < NJ; ++j) bf[j] = lds_frag<KT>(b_t, wn * WTN + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = lds_frag(a_t, wm * WTM + i * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < MI; ++i) af[i] = lds_frag<KT>(a_t, wm * WTM + i * 16 + frow, kk * 4 + fk);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -141,8 +147,8 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
     }
   };
   auto stage = [&](int t, int buf) {
-    stage_tile<BM, NT>(A, lda, m0, t * BK, tileA(buf), wave, lane);
-    stage_tile<BN, NT>(Bt, ldb, n0, t * BK, tileB(buf), wave, lane);
+    stage_tile<BM, NT, KT>(A, lda, m0, t * KT, tileA(buf), wave, lane);
+    stage_tile<BN, NT, KT>(Bt, ldb, n0, t * KT, tileB(buf), wave, lane);
   };
 
   if constexpr (STAGES == 2) {
@@ -263,21 +269,21 @@ static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
 
-template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES = 2>
+template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES = 2, int KT = BK>
 static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                         int ldb, int ldc, bool relu, hipStream_t s) {
   const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
   if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES>), grid, block, 0, s, A, B, Cp, bp, M,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M,
                        N, K, lda, ldb, ldc);
 }
 
@@ -291,6 +297,9 @@ static int g_gemm_tile = 0;
 // Measured (profiles/r01_gemm_tiles.json): correct, but none beats 128x128 / 2 stages / 2 per CU
 // (4096x2048x2048: 697 / 783 / 898 vs 954 TF; co-run mix 659 / 682 / 733 vs 795 TF): the extra
 // stage costs the second resident block, which hid the tile wait just as well.
+// (Also measured and dropped: 128x128 with a 32-deep K tile, 2 and 3 stages -- 4 / 3 blocks
+// per CU, 687 / 704 TF on the co-run mix: twice the barriers per FLOP cost more than the
+// extra residency hides; profiles/r01_gemm_tiles_bk32.json.)
 static const int kTileBM[9] = {0, 128, 64, 64, 256, 256, 128, 64, 256};
 static const int kTileBN[9] = {0, 128, 128, 64, 256, 128, 128, 128, 128};
 
