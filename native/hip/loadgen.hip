@@ -84,7 +84,8 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int STAGES = 2, int KT = BK>
+template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int STAGES = 2, int KT = BK,
+          bool HOIST = false>
 __global__ void __launch_bounds__(WGM * WGN * 64, OCC)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -130,6 +131,28 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   const int frow = lane & 15;
   const int fk = lane >> 4;
   auto compute = [&](const char* a_t, const char* b_t) {
+    if constexpr (HOIST) {
+      // every fragment of the K tile is read before the first MFMA: the MFMAs of k-step 0
+      // wait only for their own reads (counted lgkmcnt), k-step 1's reads fly under them
+      bf16x8 af[KT / 32][MI], bf[KT / 32][NJ];
+#pragma unroll
+      for (int kk = 0; kk < KT / 32; ++kk) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bf[kk][j] = lds_frag<KT>(b_t, wn * WTN + j * 16 + frow, kk * 4 + fk);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[kk][i] = lds_frag<KT>(a_t, wm * WTM + i * 16 + frow, kk * 4 + fk);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < KT / 32; ++kk)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < KT / 32; ++kk) {
       bf16x8 af[MI], bf[NJ];
@@ -269,21 +292,21 @@ static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
 
-template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES = 2, int KT = BK>
+template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES = 2, int KT = BK, bool HOIST = false>
 static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                         int ldb, int ldc, bool relu, hipStream_t s) {
   const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
   if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M, N,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M, N,
                        K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES, KT>), grid, block, 0, s, A, B, Cp, bp, M,
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M,
                        N, K, lda, ldb, ldc);
 }
 
@@ -293,13 +316,18 @@ static int g_gemm_tile = 0;
 // (Measured and dropped: 128x128 with 2 waves of 128x64 and 128x256 with 4 waves of
 // 64x128 -- fewer LDS bytes per FLOP, but 753 / 670 TF vs 783 TF for 128x128 on the co-run
 // mix: profiles/r01_gemm_tiles_with_2wave_variants.json.)
-// 6 = 128x128, 3 stages (1/CU); 7 = 64x128, 3 stages (2/CU); 8 = 256x128 8 waves, 3 stages.
+// 6 = 128x128 without hoisted reads (A/B reference); 7 = 64x128, 3 stages (2/CU);
+// 8 = 256x128 8 waves, 3 stages.
 // Measured (profiles/r01_gemm_tiles.json): correct, but none beats 128x128 / 2 stages / 2 per CU
 // (4096x2048x2048: 697 / 783 / 898 vs 954 TF; co-run mix 659 / 682 / 733 vs 795 TF): the extra
 // stage costs the second resident block, which hid the tile wait just as well.
 // (Also measured and dropped: 128x128 with a 32-deep K tile, 2 and 3 stages -- 4 / 3 blocks
 // per CU, 687 / 704 TF on the co-run mix: twice the barriers per FLOP cost more than the
 // extra residency hides; profiles/r01_gemm_tiles_bk32.json.)
+// Tiles 1, 3 and 4 read all fragments of a K tile before its first MFMA (HOIST): +0-7 % over
+// the per-k-step reads on the catalog shapes, 4096^3 1105 vs 1047 TF; for 64x128 it is mixed
+// (profiles/r01_gemm_tiles_hoist.json), so that tile keeps per-k-step reads.  Tile 6 is the
+// non-hoisted 128x128 kept as the A/B reference.
 static const int kTileBM[9] = {0, 128, 64, 64, 256, 256, 128, 64, 256};
 static const int kTileBN[9] = {0, 128, 128, 64, 256, 128, 128, 128, 128};
 
@@ -344,14 +372,14 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
   int t = pick_gemm_tile(M, N, cu_budget);
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
   switch (t) {
-    case 1: launch_gemm<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 1: launch_gemm<128, 128, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 2: launch_gemm<64, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    case 4: launch_gemm<256, 256, 2, 4, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 4: launch_gemm<256, 256, 2, 4, 1, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 5: launch_gemm<256, 128, 4, 2, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    case 6: launch_gemm<128, 128, 2, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 6: launch_gemm<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 7: launch_gemm<64, 128, 2, 2, 2, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 8: launch_gemm<256, 128, 4, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    default: launch_gemm<64, 64, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
   HIP_CHECK(hipGetLastError());
 }
