@@ -23,7 +23,7 @@ DEFAULT_PLUGINS: Dict[str, List[Dict[str, Any]]] = {
     "preFilter": [{"name": "NodeResourcesFit"}],
     "filter": [{"name": "NodeUnschedulable"}, {"name": "NodeName"}, {"name": "TaintToleration"},
                {"name": "NodeAffinity"}, {"name": "NodeResourcesFit"}],
-    "postFilter": [],
+    "postFilter": [{"name": "DefaultPreemption"}],
     "preScore": [],
     "score": [{"name": "NodeResourcesBalancedAllocation", "weight": 1},
               {"name": "NodeResourcesLeastAllocated", "weight": 1}],

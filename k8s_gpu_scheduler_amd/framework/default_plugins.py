@@ -199,8 +199,9 @@ class DefaultBinder(BindPlugin):
 
 
 def default_registry() -> Registry:
+    from .preemption import DefaultPreemption
     r = Registry()
     for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
-                NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder):
+                NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption):
         r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
     return r

@@ -27,6 +27,7 @@ class QueuedPodInfo:
     attempts: int = 0
     initial_attempt: float = 0.0
     unschedulable_plugins: set = field(default_factory=set)
+    cycle: int = 0                  # scheduling cycle in which it was last popped
 
 
 class SchedulingQueue:
@@ -46,6 +47,11 @@ class SchedulingQueue:
         self.max_backoff_s = max_backoff_s
         self.unschedulable_timeout_s = unschedulable_timeout_s
         self._closed = False
+        # upstream's schedulingCycle / moveRequestCycle: a move request (cluster event) that
+        # happens WHILE a pod is being scheduled must not be lost when that pod then fails --
+        # e.g. preemption deletes victims inside the preemptor's own cycle
+        self._cycle = 0
+        self._move_request_cycle = -1
         less_fn = self._less
 
         @functools.total_ordering
@@ -143,6 +149,8 @@ class SchedulingQueue:
                     if self._active_keys.get(k) is pi:
                         del self._active_keys[k]
                         pi.attempts += 1
+                        self._cycle += 1
+                        pi.cycle = self._cycle
                         if not pi.initial_attempt:
                             pi.initial_attempt = time.monotonic()
                         self._in_flight.add(k)
@@ -168,7 +176,12 @@ class SchedulingQueue:
             k = O.key(pi.pod)
             self._in_flight.discard(k)
             pi.timestamp = time.monotonic()
-            if backoff:
+            if backoff and self._move_request_cycle >= pi.cycle > 0:
+                exp = pi.timestamp + self._backoff_duration(pi)
+                self._backoff_keys[k] = pi
+                heapq.heappush(self._backoff, (exp, next(self._seq), pi))
+                self._cv.notify()
+            elif backoff:
                 self._unsched[k] = pi
             else:
                 self._push_active(pi)
@@ -176,6 +189,7 @@ class SchedulingQueue:
 
     def move_all_to_active_or_backoff(self, event: str = "") -> None:
         with self._cv:
+            self._move_request_cycle = self._cycle
             now = time.monotonic()
             for k, pi in list(self._unsched.items()):
                 del self._unsched[k]

@@ -144,11 +144,14 @@ class Framework:
         return feasible, failed
 
     def run_post_filter(self, state: CycleState, pod: Obj, failed: Dict[str, Status]) -> Tuple[Optional[str], Status]:
+        """First plugin that nominates a node (or declares the pod unresolvable) wins."""
+        last = Status.unschedulable("no postFilter plugin made the pod schedulable")
         for p in self.points["postFilter"]:
             nominated, s = p.post_filter(state, pod, failed)
-            if s.ok or s.code == Code.UNSCHEDULABLE_AND_UNRESOLVABLE:
+            if nominated or s.ok or s.code == Code.UNSCHEDULABLE_AND_UNRESOLVABLE:
                 return nominated, s
-        return None, Status.unschedulable("no postFilter plugin made the pod schedulable")
+            last = s
+        return None, last
 
     # ---------------------------------------------------------------- score
     def run_pre_score(self, state: CycleState, pod: Obj, nodes: List[Any]) -> Status:

@@ -45,6 +45,7 @@ class ScheduleResult:
     feasible: int = 0
     latency_s: float = 0.0
     bound: bool = False
+    nominated: str = ""         # node nominated by a PostFilter (preemption)
 
 
 class Handle:
@@ -75,6 +76,9 @@ class Handle:
     @property
     def extras(self) -> Dict[str, Any]:
         return self._s.extras
+
+    def framework_for(self, pod: Obj) -> Optional["Framework"]:
+        return self._s.frameworks.get(O.scheduler_name(pod))
 
 
 class Scheduler:
@@ -222,9 +226,12 @@ class Scheduler:
         res.evaluated = processed
         res.feasible = len(feasible)
         if not feasible:
-            _, pst = fw.run_post_filter(state, pod, failed)
+            nominated, pst = fw.run_post_filter(state, pod, failed)
             reasons = sorted({m for s in failed.values() for m in s.reasons})
             msg = f"0/{len(nodes)} nodes are available: " + ", ".join(reasons) if nodes else "no nodes available"
+            if pst.message():
+                msg += f"; postFilter: {pst.message()}"
+            res.nominated = nominated or ""
             return self._fail(pi, fw, state, res, Status.unschedulable(msg), t0)
         if len(feasible) == 1 and not fw.points["score"]:
             host = feasible[0].name

@@ -249,6 +249,11 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             return Status.unschedulable("node is being re-partitioned", self.NAME)
         if not self.ledger.has_node(node_info.name):
             self._on_node(node)
+        removed = getattr(node_info, "removed", None)
+        if removed:                 # preemption what-if: victims' units/HBM released
+            if self._fits_without(req, node_info.name, removed):
+                return None
+            return Status.unschedulable("insufficient free GPU units/HBM even without lower-priority pods", self.NAME)
         choice = self._best_choice(state, pod, req, node_info.name, scoring=False)
         if choice is None and not req.implicit:
             return Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME)
@@ -526,6 +531,24 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             if best is None or sc > best.score:
                 best = Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], sc, [st.device])
         return best
+
+    def _fits_without(self, req: GpuRequest, node: str, removed: Any) -> bool:
+        """Would the request fit if the pods in `removed` released their devices?  Works on
+        copies of the node's device states; the ledger itself is untouched."""
+        sim: List[DeviceState] = []
+        for st in self.ledger.devices(node):
+            c = DeviceState(st.device, list(st.used_units), st.hbm_used, dict(st.pods))
+            for key in removed:
+                use = c.pods.pop(key, None)
+                if use is not None:
+                    u0, n = use.units
+                    for u in range(u0, u0 + n):
+                        c.used_units[u] = False
+                    c.hbm_used = max(0.0, c.hbm_used - use.hbm_gib)
+            sim.append(c)
+        if req.whole:
+            return self._whole_choice(req, node, sim) is not None
+        return any(c.hbm_free + 1e-6 >= req.hbm_gib and c._find_units(req.units) is not None for c in sim)
 
     def _whole_choice(self, req: GpuRequest, node: str, states: List[DeviceState]) -> Optional[Choice]:
         free = [st for st in states if not st.pods and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)]

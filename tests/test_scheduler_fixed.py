@@ -268,3 +268,35 @@ def test_adaptive_node_sampling_large_cluster():
     fc.create("pods", O.make_pod("q", gpu_cu=64))
     (r,) = s.schedule_pending()
     assert r.status.ok and r.evaluated == 1000
+
+
+def test_gpu_aware_preemption():
+    """DefaultPreemption (PostFilter, on by default as in kube-scheduler): a high-priority
+    pod that finds no free CU units evicts the minimal set of lower-priority pods on the best
+    node -- judged by the GPU plugin's what-if ledger -- is nominated there, and lands once
+    the victims are gone.  Equal/higher priority pods are never victims."""
+    cfg = default_gpu_config({})
+    cfg.pod_initial_backoff_s = 0.0
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("node-a", gpus=1))
+    ledger = DeviceLedger()
+    s = Scheduler(fc, cfg, full_registry(), bind_async=False, seed=0, extras={"ledger": ledger})
+    s.start_informers()
+    s.queue.initial_backoff_s = 0.0
+    fc.create("pods", O.make_pod("low-a", gpu_cu=128, priority=1))
+    fc.create("pods", O.make_pod("low-b", gpu_cu=64, priority=2))
+    fc.create("pods", O.make_pod("same", gpu_cu=64, priority=10))
+    assert all(r.status.ok for r in s.schedule_pending())            # GPU full: 128 + 64 + 64
+    fc.create("pods", O.make_pod("high", gpu_cu=128, priority=10))
+    # cycle 1 fails and preempts; the victim's delete requeues the preemptor at once (the
+    # move request arrived during its own cycle), cycle 2 binds it
+    r, r2 = s.schedule_pending()
+    assert not r.status.ok and "preempt" in r.status.message() and r.nominated == "node-a"
+    names = {O.name(p) for p in fc.list("pods")[0]}
+    assert names == {"low-b", "same", "high"}                          # one victim: the 128-CU low-a
+    assert fc.get("pods", "high", "default")["status"]["nominatedNodeName"] == "node-a"
+    assert r2.pod_key == "default/high" and r2.status.ok and r2.node == "node-a"
+    # a pod that cannot preempt anything (no lower priority left to evict) stays pending
+    fc.create("pods", O.make_pod("never", gpu_cu=128, priority=10))
+    (r3,) = s.schedule_pending()
+    assert not r3.status.ok and {O.name(p) for p in fc.list("pods")[0]} >= {"low-b", "same", "high"}
