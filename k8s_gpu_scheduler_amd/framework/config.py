@@ -20,9 +20,11 @@ from ..api import constants as C
 
 DEFAULT_PLUGINS: Dict[str, List[Dict[str, Any]]] = {
     "queueSort": [{"name": "PrioritySort"}],
-    "preFilter": [{"name": "NodeResourcesFit"}],
+    "preFilter": [{"name": "NodeResourcesFit"}, {"name": "NodePorts"}, {"name": "InterPodAffinity"},
+                  {"name": "PodTopologySpread"}],
     "filter": [{"name": "NodeUnschedulable"}, {"name": "NodeName"}, {"name": "TaintToleration"},
-               {"name": "NodeAffinity"}, {"name": "NodeResourcesFit"}],
+               {"name": "NodeAffinity"}, {"name": "NodePorts"}, {"name": "NodeResourcesFit"},
+               {"name": "InterPodAffinity"}, {"name": "PodTopologySpread"}],
     "postFilter": [{"name": "DefaultPreemption"}],
     "preScore": [],
     "score": [{"name": "NodeResourcesBalancedAllocation", "weight": 1},

@@ -199,9 +199,11 @@ class DefaultBinder(BindPlugin):
 
 
 def default_registry() -> Registry:
+    from .placement_plugins import InterPodAffinity, NodePorts, PodTopologySpread
     from .preemption import DefaultPreemption
     r = Registry()
     for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
-                NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption):
+                NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption,
+                NodePorts, InterPodAffinity, PodTopologySpread):
         r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
     return r

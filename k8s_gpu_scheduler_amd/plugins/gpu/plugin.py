@@ -196,6 +196,12 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         except json.JSONDecodeError:
             return
         if allocs:
+            if not self.ledger.has_node(node):
+                # informers may deliver pods before their node (start order): load the node
+                try:
+                    self._on_node(self.handle.client.get("nodes", node))
+                except Exception as e:
+                    log.debug("recovery: node %s of %s unavailable: %s", node, O.key(pod), e)
             self.ledger.reserve(node, O.key(pod), O.name(pod), O.pod_slo(pod), allocs)
 
     def _on_pod_delete(self, pod: Obj) -> None:

@@ -300,3 +300,64 @@ def test_gpu_aware_preemption():
     fc.create("pods", O.make_pod("never", gpu_cu=128, priority=10))
     (r3,) = s.schedule_pending()
     assert not r3.status.ok and {O.name(p) for p in fc.list("pods")[0]} >= {"low-b", "same", "high"}
+
+
+def test_default_placement_filters_ports_affinity_spread():
+    """kube-scheduler default filters the reference inherited: hostPort conflicts (NodePorts),
+    required pod anti-affinity / affinity (InterPodAffinity, incl. symmetry) and
+    DoNotSchedule topology spreading (PodTopologySpread)."""
+    fc = FakeCluster()
+    for n, zone in (("n1", "z1"), ("n2", "z1"), ("n3", "z2")):
+        fc.create("nodes", O.make_node(n, gpus=0, labels_={"topology.kubernetes.io/zone": zone}))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, seed=0)
+    s.start_informers()
+
+    def pod(name, **spec):
+        p = O.make_pod(name, labels_=spec.pop("labels", {}))
+        p["spec"].update(spec)
+        return p
+    # NodePorts: three pods on hostPort 8080 fill three nodes, the fourth cannot fit
+    for i in range(4):
+        p = pod(f"web-{i}")
+        p["spec"]["containers"][0]["ports"] = [{"containerPort": 80, "hostPort": 8080}]
+        fc.create("pods", p)
+    res = s.schedule_pending()
+    assert [r.status.ok for r in res] == [True, True, True, False]
+    assert len({r.node for r in res if r.status.ok}) == 3
+    assert "free ports" in res[3].status.message()
+    for i in range(4):
+        fc.delete("pods", f"web-{i}", "default")
+    # anti-affinity across zones: one per zone, the third has nowhere to go
+    anti = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"app": "kv"}}, "topologyKey": "topology.kubernetes.io/zone"}]}}
+    for i in range(3):
+        fc.create("pods", pod(f"kv-{i}", labels={"app": "kv"}, affinity=anti))
+    res = s.schedule_pending()
+    assert [r.status.ok for r in res] == [True, True, False]
+    zones = {O.labels(fc.get("nodes", r.node))["topology.kubernetes.io/zone"] for r in res if r.status.ok}
+    assert zones == {"z1", "z2"}
+    # symmetry: a plain pod labelled app=kv is repelled by the existing pods' anti-affinity
+    fc.delete("pods", "kv-2", "default")
+    fc.create("pods", pod("kv-plain", labels={"app": "kv"}))
+    (r,) = s.schedule_pending()
+    assert not r.status.ok and "anti-affinity" in r.status.message()
+    fc.delete("pods", "kv-plain", "default")
+    # affinity: co-locate with the db pod's node
+    fc.create("pods", pod("db", labels={"app": "db"}, nodeName="n2"))
+    aff = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "kubernetes.io/hostname"}]}}
+    fc.create("pods", pod("cache", affinity=aff))
+    (r,) = s.schedule_pending()
+    assert r.status.ok and r.node == "n2"
+    # topology spread over zones, maxSkew 1
+    spread = [{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule",
+               "labelSelector": {"matchLabels": {"app": "sp"}}}]
+    for i in range(4):
+        fc.create("pods", pod(f"sp-{i}", labels={"app": "sp"}, topologySpreadConstraints=spread))
+    res = s.schedule_pending()
+    assert all(r.status.ok for r in res)
+    per_zone = {}
+    for r in res:
+        z = O.labels(fc.get("nodes", r.node))["topology.kubernetes.io/zone"]
+        per_zone[z] = per_zone.get(z, 0) + 1
+    assert per_zone == {"z1": 2, "z2": 2}
