@@ -20,7 +20,7 @@ from ...api import objects as O
 from ...kube.resources import Resources
 from ...store import schema
 from ...utils import discovery
-from .scoring import Resident, device_score, mps_env, pick_mps_config, reconfigure_choice
+from .scoring import Resident, mps_env, pick_mps_config, reconfigure_choice, score_devices
 
 if TYPE_CHECKING:
     from .plugin import GPUPlugin
@@ -158,10 +158,16 @@ class ParityLogic:
         if model:
             if self.p.args.parity_shuffle:
                 self.rng.shuffle(uuids)
+            # The reference scores UUID by UUID with the recommender calls and the V100
+            # ConfigMap write inside the loop (:558-757); the calls and side effects are
+            # kept per UUID here, and the scores are then computed as one batch
+            # (scoring.score_devices -> the native C++ core on busy nodes), identical numerics.
+            col = f"{len(uuids)}P_{model}"
+            per_uuid = []
+            pred, intf = -1.0, {}
             for uuid in uuids:
                 residents = [Resident(n, s, self._conf(n), self._intf(f"{n}_{model}"))
                              for n, s in (slos.get(uuid) or {}).items()]
-                col = f"{len(uuids)}P_{model}"
                 conf = self._conf(O.name(pod))
                 pred = -1.0
                 if model == "A30":
@@ -172,7 +178,9 @@ class ParityLogic:
                 intf = self._intf(f"{O.name(pod)}_{model}") if pred != -1 else {}
                 # residents are excluded from their own interference sum; the incoming pod
                 # is never a resident here (it is not Running on this UUID).
-                tmp = device_score(residents, O.name(pod), cur_slo, pred, intf, col)
+                per_uuid.append((uuid, residents))
+            scores = score_devices([r for _, r in per_uuid], O.name(pod), cur_slo, pred, intf, col)
+            for (uuid, _), tmp in zip(per_uuid, scores):
                 if int(tmp) > score:
                     score = int(tmp)
                     selected = uuid
