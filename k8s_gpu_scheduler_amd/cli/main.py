@@ -121,6 +121,7 @@ def cmd_recommender(args) -> int:
         from ..store.resp import Redis
         r = Redis.connect(args.redis, args.redis_password)
         svc.history_source = lambda pod: schema.read_history(r, pod)
+        svc.store = r                   # persist / restore trained model versions
     svc.train()
     svc.start_retrain_loop()
     port = int(os.getenv("PORT", args.port))

@@ -17,6 +17,7 @@ Redis history), Version.
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
@@ -45,18 +46,48 @@ class ModelSlot:
         self.current: Optional[TrainedTable] = None
         self.version: Optional[str] = None
 
-    def load_if_changed(self) -> bool:
+    def load_if_changed(self, store: Any = None) -> bool:
+        """Re-fit when the training file's md5 changed.  With a Redis `store`, every newly
+        trained version is persisted (`schema.model_key(name)`: version + training table),
+        and a missing training file falls back to the last persisted version -- so a
+        restarted recommender serves immediately."""
         v = file_version(self.path)
         if v is None:
+            if store is not None and self.version is None:
+                return self._load_persisted(store)
             log.info("%s: train data not found at %s", self.name, self.path)
             return False
         if v == self.version:
             return False
-        trained = TrainedTable.fit(Table.read_tsv(self.path), self.kind, v, **self.model_kw)
+        table = Table.read_tsv(self.path)
+        trained = TrainedTable.fit(table, self.kind, v, **self.model_kw)
         with self._lock:
             self.current, self.version = trained, v
+        if store is not None:
+            try:
+                from ..store import schema
+                store.set(schema.model_key(self.name), json.dumps(
+                    {"version": v, "kind": self.kind, "table": table.to_json()}, separators=(",", ":")))
+            except Exception as e:
+                log.warning("%s: persisting model version %s failed: %s", self.name, v[:8], e)
         log.info("%s: trained version %s (%d x %d)", self.name, v[:8], len(trained.table.index),
                  len(trained.table.columns))
+        return True
+
+    def _load_persisted(self, store: Any) -> bool:
+        from ..store import schema
+        try:
+            raw = store.get(schema.model_key(self.name))
+        except Exception as e:
+            log.info("%s: no persisted model (%s)", self.name, e)
+            return False
+        if not raw:
+            return False
+        d = json.loads(raw)
+        trained = TrainedTable.fit(Table.from_json(d["table"]), self.kind, d["version"], **self.model_kw)
+        with self._lock:
+            self.current, self.version = trained, d["version"]
+        log.info("%s: restored persisted version %s", self.name, d["version"][:8])
         return True
 
     def set_table(self, table: Table, version: str = "mem") -> None:
@@ -78,6 +109,7 @@ class RecommenderService:
         self.job_delay_s = job_delay_s
         self.history_source = history_source
         self.model = model
+        self.store: Any = None          # Redis: persisted model versions (set by the CLI / tests)
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.calls = 0
@@ -92,7 +124,7 @@ class RecommenderService:
     def train(self) -> None:
         for slot in (self.conf, self.intf):
             try:
-                slot.load_if_changed()
+                slot.load_if_changed(self.store)
             except Exception as e:
                 log.warning("%s: training failed: %s", slot.name, e)
 

@@ -11,7 +11,7 @@ import hashlib
 import os
 import threading
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -69,6 +69,15 @@ class Table:
             for i, r in zip(self.index, self.values):
                 f.write("\t".join([i] + ["" if np.isnan(v) else repr(float(v)) for v in r]) + "\n")
         os.replace(tmp, path)
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"index": list(self.index), "columns": list(self.columns),
+                "values": [[None if np.isnan(v) else float(v) for v in r] for r in self.values]}
+
+    @classmethod
+    def from_json(cls, d: Dict[str, Any]) -> "Table":
+        vals = np.asarray([[np.nan if v is None else float(v) for v in r] for r in d["values"]], dtype=float)
+        return cls(list(d["index"]), list(d["columns"]), vals)
 
     def row(self, label: str) -> np.ndarray:
         return self.values[self.index.index(label)]

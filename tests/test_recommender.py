@@ -206,3 +206,28 @@ def test_resize_webhook_http_server():
         assert urllib.request.urlopen(srv.url + "/healthz", timeout=5).read() == b"ok"
     finally:
         srv.stop()
+
+
+def test_model_versions_persist_in_redis(tmp_path, ref_data):
+    """A trained version is persisted to Redis; a restarted recommender whose training file
+    is gone serves the persisted version."""
+    import shutil
+    from k8s_gpu_scheduler_amd.recommender.service import RecommenderService
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    conf_p, intf_p = ref_data
+    c, i = tmp_path / "c.tsv", tmp_path / "i.tsv"
+    shutil.copy(conf_p, c)
+    shutil.copy(intf_p, i)
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    a = RecommenderService(str(c), str(i))
+    a.store = r
+    a.train()
+    want = a.conf.get().lookup("mlperf-gpu-onnx-mobilenet-1024")
+    c.unlink()
+    i.unlink()
+    b = RecommenderService(str(c), str(i))
+    b.store = r
+    b.train()
+    assert b.conf.version == a.conf.version and b.intf.version == a.intf.version
+    assert b.conf.get().lookup("mlperf-gpu-onnx-mobilenet-1024") == pytest.approx(want)
