@@ -15,6 +15,7 @@
 """
 from __future__ import annotations
 
+import logging
 import threading
 import time
 from typing import Any, Dict, List, Optional
@@ -23,6 +24,8 @@ import grpc
 
 from . import proto as P
 from .tables import TrainedTable, find_index_for_request
+
+log = logging.getLogger(__name__)
 
 
 class RecommenderClient:
@@ -112,15 +115,22 @@ class _Tab:
 
 
 class CachedPredictions(PredictionProvider):
-    """In-process, zero-I/O predictions.  Source: a RecommenderClient (ExportTable,
-    refreshed when `refresh()` sees a new version) or local TrainedTables."""
+    """In-process, zero-I/O predictions.  Source: a RecommenderClient (ExportTable, pulled
+    again every `refresh_s` by a background thread so a retrained model version reaches the
+    scheduler -- the reference sees new versions because it calls the recommender per
+    prediction) or local TrainedTables.  An unreachable recommender (it may start after the
+    scheduler) is not fatal: lookups return no predictions until the first pull succeeds,
+    retried every `retry_s`."""
 
     def __init__(self, client: Optional[RecommenderClient] = None,
                  conf: Optional[TrainedTable] = None, intf: Optional[TrainedTable] = None,
-                 refresh_s: float = 30.0):
+                 refresh_s: float = 30.0, retry_s: float = 2.0, background: bool = True):
         self.client = client
         self.refresh_s = refresh_s
+        self.retry_s = retry_s
         self._last = 0.0
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
         self._conf: Optional[_Tab] = None
         self._intf: Optional[_Tab] = None
         if conf is not None:
@@ -128,7 +138,26 @@ class CachedPredictions(PredictionProvider):
         if intf is not None:
             self._intf = _Tab(intf.table.index, intf.table.columns, intf.completed().tolist(), intf.version)
         if client is not None:
-            self.refresh(force=True)
+            ok = self.try_refresh(force=True)
+            if background:
+                self._thread = threading.Thread(target=self._loop, args=(ok,), name="predictions-refresh",
+                                                daemon=True)
+                self._thread.start()
+
+    def _loop(self, ok: bool) -> None:
+        while not self._stop.wait(self.refresh_s if ok else self.retry_s):
+            ok = self.try_refresh(force=True)
+
+    def close(self) -> None:
+        self._stop.set()
+
+    def try_refresh(self, force: bool = False) -> bool:
+        try:
+            self.refresh(force)
+            return self._conf is not None and self._intf is not None
+        except Exception as e:
+            log.warning("predictions refresh failed (keeping the previous tables): %s", e)
+            return False
 
     def refresh(self, force: bool = False) -> None:
         if self.client is None:

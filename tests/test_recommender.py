@@ -231,3 +231,42 @@ def test_model_versions_persist_in_redis(tmp_path, ref_data):
     b.train()
     assert b.conf.version == a.conf.version and b.intf.version == a.intf.version
     assert b.conf.get().lookup("mlperf-gpu-onnx-mobilenet-1024") == pytest.approx(want)
+
+
+def test_cached_predictions_survive_late_recommender_and_follow_new_versions(ref_data, tmp_path):
+    """The scheduler may start before the recommender: the cache comes up empty instead of
+    failing, fills once the server answers, and a retrained version reaches it without a
+    restart (the reference sees new versions because it calls per prediction)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cl = RecommenderClient(f"127.0.0.1:{port}", timeout_s=0.5)
+    cache = CachedPredictions(cl, refresh_s=0.3, retry_s=0.1)
+    assert cache.configurations("mlperf-gpu-onnx-mobilenet-1024") == {}
+    conf, intf = ref_data
+    c, i = tmp_path / "c.tsv", tmp_path / "i.tsv"
+    shutil.copy(conf, c)
+    shutil.copy(intf, i)
+    svc = RecommenderService(str(c), str(i), job_delay_s=0.2)
+    svc.train()
+    srv, _ = svc.make_server(port, 2, "127.0.0.1")
+    try:
+        deadline = time.time() + 15
+        while not cache.configurations("mlperf-gpu-onnx-mobilenet-1024") and time.time() < deadline:
+            time.sleep(0.1)
+        assert cache.configurations("mlperf-gpu-onnx-mobilenet-1024")["1P_A30"] == pytest.approx(624.9)
+        t = Table.read_tsv(str(c))
+        t.set("new_workload_1", "1P_A30", 77.0)
+        t.write_tsv(str(c))
+        svc.start_retrain_loop()
+        deadline = time.time() + 15
+        while not cache.configurations("new-workload-1") and time.time() < deadline:
+            time.sleep(0.1)
+        assert cache.configurations("new-workload-1")["1P_A30"] == pytest.approx(77.0)
+    finally:
+        cache.close()
+        svc.stop()
+        srv.stop(0)
+        cl.close()
