@@ -276,6 +276,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
+    ap.add_argument("--gemm-policy", type=int, default=0, choices=[0, 1, 2],
+                    help="GEMM tile policy (A/B knob): 0 default, 1 8-phase 256x256 also for co-running pods")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     a.lookahead = max(1, a.lookahead)
@@ -313,6 +315,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         from .executor import DeviceExecutor
         ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
         ex.use_graphs = bool(a.graphs)
+        if a.gemm_policy:
+            from .. import _native
+            _native.hip(required=True).set_gemm_policy(a.gemm_policy)
     else:
         ex = SimExecutor()
     gpus_here = [rank] if world > 1 else list(range(n_gpus))

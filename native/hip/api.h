@@ -26,6 +26,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
 void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream);
 void set_triad_variant(int v);
 void set_gemm_tile(int t);
+void set_gemm_policy(int p);
 int pick_gemm_tile(int M, int N, int cu_budget);
 std::vector<int> peer_access_matrix();
 double peer_copy_gbps(int src, int dst, size_t bytes, int iters);

@@ -12,7 +12,9 @@
 //    global_load_lds (no VGPR round trip) into a double-buffered, XOR-swizzled LDS image
 //    (bank-conflict-free ds_read_b128 fragment reads); stage of tile t+1 is issued before
 //    the MFMAs of tile t; XCD-aware bijective block remap + grouped tile order for L2 reuse.
-//    Epilogue fuses bias + ReLU and stores packed bf16x4.
+//    Epilogue fuses bias + ReLU and stores packed bf16x4.  Lone large GEMMs use a separate
+//    256x256 "8-phase" kernel (gemm_bf16_nt_256_8ph: two staggered wave groups, one
+//    half-tile of glds per phase, counted vmcnt).
 //  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
 #include <cstdint>
 
@@ -227,6 +229,179 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x256 "8-phase" GEMM for lone, large GEMMs (a whole-GPU Guaranteed pod): 8 waves as
+// 2 (M) x 4 (N) groups, one block per CU, 128 KiB LDS = 2 K-tile buffers x {A0, A1, B0, B1}
+// half-tiles of 128 rows x 64 k.  Wave (wr, wc) owns rows h*128 + wr*64 + [0, 64) and
+// columns g*128 + wc*32 + [0, 32) for h, g in {0, 1}, so a (h, g) output quadrant touches
+// only half-tiles A_h and B_g.  Each K-tile is 4 phases, each phase = its fragment reads,
+// ONE half-tile of glds (2 x 16 B per thread), a barrier, 16 MFMAs, a barrier:
+//
+//   phase 1: quadrant (0,0)  reads A0 (8 x ds_read_b128) + B0 (4, kept in registers)
+//   phase 2: quadrant (0,1)  reads B1 (4)
+//   phase 3: quadrant (1,1)  reads A1 (8)
+//   phase 4: quadrant (1,0)  no reads (A1 and B0 already in registers)
+//
+// Half-tile j (A0, B0, B1, A1 = 0..3) of K-tile u is staged in global phase 4u - 5 + j
+// (K-tile u runs phases 4u+1 .. 4u+4; the prologue covers the phases <= 0), so every half-tile
+// is restaged >= 2 phases after its last read of K-tile u-2 (WAR with the two wave groups
+// staggered by one barrier) and is retired by a counted vmcnt at phase 2 or 4 at least one
+// phase before its first read (RAW): three half-tiles stay in flight (vmcnt(6)) in steady
+// state, fewer as the K loop drains.  The wr = 1 group runs one barrier behind the wr = 0
+// group, so on every SIMD (one wave of each group) one wave issues its reads and glds
+// while the other runs MFMAs.
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  // s_waitcnt takes an immediate: n (loads allowed in flight) is 0, 2, 4 or 6
+  if (n >= 6) wait_vmcnt<6>();
+  else if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) wait_vmcnt<2>();
+  else wait_vmcnt<0>();
+}
+
+template <bool RELU, bool BIAS>
+__global__ void __launch_bounds__(512, 1)
+gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
+                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int HALF = 128 * 64 * 2;               // bytes of one half-tile image
+  constexpr int BUF = 4 * HALF;                    // one K-tile: A0 A1 B0 B1
+  constexpr int OA0 = 0, OA1 = HALF, OB0 = 2 * HALF, OB1 = 3 * HALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int nwg = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b % kXcds;
+  const int q = nwg / kXcds, rem = nwg % kXcds;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
+  const int tiles_m = M / 256, tiles_n = N / 256;
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int m0 = (first_m + (wgid % per_group) % gsize) * 256;
+  const int n0 = ((wgid % per_group) / gsize) * 256;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int frow = lane & 15, fk = lane >> 4;
+
+  f32x4 acc[2][4][2][2];                           // [h][mi][g][nj]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[h][i][g][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ar[2][4], b0r[2][2], b1r[2][2];            // [kk][mi], [kk][nj]
+
+  const int T = K / 64;
+  const int last_stage = 4 * T - 6;                // global phase of the last glds
+  // half-tile j of K-tile u: A rows (j = 0, 3) or B rows (j = 1, 2)
+  auto stage = [&](int u, int j) {
+    char* dst = smem + (u & 1) * BUF + (j == 0 ? OA0 : j == 3 ? OA1 : j == 1 ? OB0 : OB1);
+    if (j == 0 || j == 3)
+      stage_tile<128, 512, 64>(A, lda, m0 + (j == 3 ? 128 : 0), u * 64, dst, wave, lane);
+    else
+      stage_tile<128, 512, 64>(Bt, ldb, n0 + (j == 2 ? 128 : 0), u * 64, dst, wave, lane);
+  };
+  auto read_a = [&](const char* half) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ar[kk][i] = lds_frag<64>(half, wr * 64 + i * 16 + frow, kk * 4 + fk);
+  };
+  auto read_b = [&](const char* half, bf16x8 (&br)[2][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) br[kk][j] = lds_frag<64>(half, wc * 32 + j * 16 + frow, kk * 4 + fk);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma_quadrant = [&](int h, int g, bf16x8 (&br)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[h][i][g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(br[kk][j], ar[kk][i], acc[h][i][g][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // loads allowed in flight at the wait of global phase p: the glds of phases p-2 .. p
+  // that exist (2 per phase)
+  auto inflight = [&](int p) { return 2 * max(0, min(3, last_stage - p + 3)); };
+
+  // prologue: K-tile 0 and half-tiles A0, B0 of K-tile 1 (phases -5 .. 0)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) stage(0, j);
+  stage(1, 0);
+  stage(1, 1);
+  wait_vmcnt<4>();                                 // K-tile 0 landed; K-tile 1's A0/B0 in flight
+  barrier();
+  if (wr == 1) barrier();                          // group 1 runs one barrier behind
+
+  for (int t = 0; t < T; ++t) {
+    const char* cur = smem + (t & 1) * BUF;
+    const int p0 = 4 * t;
+    // phase 1: (0,0)
+    read_b(cur + OB0, b0r);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(cur + OA0);
+    if (t + 1 < T) stage(t + 1, 2);
+    barrier();
+    mfma_quadrant(0, 0, b0r);
+    barrier();
+    // phase 2: (0,1)
+    read_b(cur + OB1, b1r);
+    if (t + 1 < T) stage(t + 1, 3);
+    wait_vmcnt_rt(inflight(p0 + 2));
+    barrier();
+    mfma_quadrant(0, 1, b1r);
+    barrier();
+    // phase 3: (1,1)
+    read_a(cur + OA1);
+    if (t + 2 < T) stage(t + 2, 0);
+    barrier();
+    mfma_quadrant(1, 1, b1r);
+    barrier();
+    // phase 4: (1,0)
+    if (t + 2 < T) stage(t + 2, 1);
+    wait_vmcnt_rt(inflight(p0 + 4));
+    barrier();
+    mfma_quadrant(1, 0, b0r);
+    barrier();
+  }
+  if (wr == 0) barrier();                          // balance the barrier count
+
+  // epilogue (D = C^T layout, as in gemm_bf16_nt_kernel): lane holds 4 consecutive columns
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + g * 128 + wc * 32 + j * 16 + fk * 4;
+      f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + col);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + h * 128 + wr * 64 + i * 16 + frow;
+          f32x4 v = acc[h][i][g][j] + bv;
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+          *reinterpret_cast<bf16x4*>(C + (size_t)row * ldc + col) = o;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) stream_triad_kernel(float4* __restrict__ a, const float4* __restrict__ b,
                                                            const float4* __restrict__ c, float s, size_t n4) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -328,11 +503,26 @@ static int g_gemm_tile = 0;
 // the per-k-step reads on the catalog shapes, 4096^3 1105 vs 1047 TF; for 64x128 it is mixed
 // (profiles/r01_gemm_tiles_hoist.json), so that tile keeps per-k-step reads.  Tile 6 is the
 // non-hoisted 128x128 kept as the A/B reference.
-static const int kTileBM[9] = {0, 128, 64, 64, 256, 256, 128, 64, 256};
-static const int kTileBN[9] = {0, 128, 128, 64, 256, 128, 128, 128, 128};
+// 9 = 256x256 8-phase (gemm_bf16_nt_256_8ph; needs K >= 128).
+static const int kTileBM[10] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256};
+static const int kTileBN[10] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256};
+
+// Study knob.  0 = default: the 8-phase 256x256 (tile 9) for lone GEMMs that still get one
+// block per CU (4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs 1211;
+// profiles/r01_gemm_big.json).  1 = also for co-running pods whose CU share it fills: +8 % on
+// a GEMM-only 4-stream mix (855 vs 794 TF, profiles/r01_gemm_corun_8ph.json) but no gain in
+// the bench, where the pods' GEMMs share the chip with HBM-streaming phases (508 vs 510 pods/s,
+// interleaved A/B, profiles/r01_gemm_policy_ab.txt) -- so co-running pods keep the
+// 128x128 / 2-per-CU picker.  2 = tile 4 instead of tile 9 for lone GEMMs.
+static int g_gemm_policy = 0;
+
+void set_gemm_policy(int p) {
+  if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");
+  g_gemm_policy = p;
+}
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 8) throw std::runtime_error("gemm tile must be 0..8");
+  if (t < 0 || t > 9) throw std::runtime_error("gemm tile must be 0..9");
   g_gemm_tile = t;
 }
 
@@ -348,7 +538,9 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const bool alone = cu_budget <= 0 || cu_budget >= kCus;
   const int budget = alone ? kCus : cu_budget;
   const int per_cu = alone ? 2 : 1;
-  if (alone && (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget) return 4;
+  const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
+  if (alone && fits256) return g_gemm_policy == 2 ? 4 : 9;
+  if (!alone && fits256 && g_gemm_policy == 1) return 9;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
@@ -370,6 +562,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
   if (ldc % 4 || reinterpret_cast<uintptr_t>(c) % 8) throw std::runtime_error("gemm: C rows must be 8-byte aligned");
   if (bias) check_align(reinterpret_cast<void*>(bias), "bias");
   int t = pick_gemm_tile(M, N, cu_budget);
+  if (t == 9 && K < 128) t = 4;                  // the 8-phase prologue stages two K-tiles
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
   switch (t) {
     case 1: launch_gemm<128, 128, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
@@ -379,6 +572,18 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 6: launch_gemm<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 7: launch_gemm<64, 128, 2, 2, 2, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 8: launch_gemm<256, 128, 4, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 9: {
+      const dim3 grid((M / 256) * (N / 256)), block(512);
+      if (relu && bp)
+        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+      else if (relu)
+        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+      else if (bp)
+        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+      else
+        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+      break;
+    }
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
   HIP_CHECK(hipGetLastError());

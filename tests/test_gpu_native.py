@@ -56,6 +56,39 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
+def test_gemm_256_8phase_numerics_and_race_screen():
+    """The 8-phase 256x256 kernel (tile 9): every K-tile count from the minimum (2) through odd
+    counts (the buffer parity flips) to long loops, several grid sizes, each shape run
+    repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
+    (guide §5 'A sync-structure edit makes a NEW template'), so every run is checked against
+    an fp32 reference, and A = I with an asymmetric B pins the C layout."""
+    from k8s_gpu_scheduler_amd import _native
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    h = _native.hip()
+    h.set_gemm_tile(9)
+    try:
+        for (M, N, K) in [(256, 256, 128), (256, 512, 192), (512, 256, 320), (768, 1024, 1024),
+                          (2048, 2048, 4096), (4096, 4096, 640)]:
+            g = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K)
+            a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+            bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+            b = torch.randn(N, device="cuda", generator=g)
+            ref = torch.relu(a.float() @ bt.float().T + b)
+            tol = 0.01 * ref.abs().max().item() + 1e-2
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            for _ in range(6):
+                out.fill_(float("nan"))
+                loadgen.gemm(a, bt, out=out, bias=b, relu=True)
+                err = (out.float() - ref).abs().max().item()
+                assert err <= tol, (M, N, K, err)
+        n = 256
+        eye = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+        asym = (torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n) % 97).to(torch.bfloat16)
+        assert torch.equal(loadgen.gemm(eye, asym).float(), asym.float().T)
+    finally:
+        h.set_gemm_tile(0)
+
+
 def test_gemm_layout_identity_asymmetric():
     """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
     from k8s_gpu_scheduler_amd.ops import loadgen

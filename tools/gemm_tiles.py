@@ -15,7 +15,7 @@ from k8s_gpu_scheduler_amd import _native  # noqa: E402
 from k8s_gpu_scheduler_amd.models import workloads as W  # noqa: E402
 from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
 
-TILES = (1, 2, 3, 4, 5, 6, 7, 8)
+TILES = (1, 2, 3, 4, 5, 6, 7, 8, 9)
 
 
 def t_ms(fn, iters=20, warm=3):
@@ -42,6 +42,8 @@ def main():
     out = {"isolated": [], "concurrent": []}
     shapes = sorted({(o.M, o.N, o.K) for w in W.CATALOG.values() for o in w.ops if o.kind == "gemm"})
     shapes += [(4096, 4096, 4096), (8192, 8192, 8192)]
+    if os.environ.get("GEMM_TILES_CONCURRENT_ONLY"):
+        shapes = []
     for (M, N, K) in shapes:
         a, bt, c, bias = operands(M, N, K)
         res = {}
@@ -86,14 +88,16 @@ def main():
         for st in streams:
             torch.cuda.current_stream().wait_stream(st)
     for rnd in range(3):
-        for tile in ("torch", "budget64", 0) + TILES:
-            budget["b"] = 64 if tile == "budget64" else (-1 if tile == "torch" else 0)
+        for tile in ("torch", "budget64", "budget64_8ph", 0) + TILES:
+            budget["b"] = {"torch": -1, "budget64": 64, "budget64_8ph": 64}.get(tile, 0)
             h.set_gemm_tile(tile if isinstance(tile, int) else 0)
+            h.set_gemm_policy(1 if tile == "budget64_8ph" else 0)
             ms = t_ms(run_mix, iters=5, warm=1)
             if rnd:
                 out["concurrent"].append({"tile": tile, "round": rnd, "tflops": round(flops / ms / 1e9, 1)})
                 print(out["concurrent"][-1], flush=True)
     h.set_gemm_tile(0)
+    h.set_gemm_policy(0)
     os.makedirs("gpurun_out", exist_ok=True)
     json.dump(out, open("gpurun_out/gemm_tiles.json", "w"), indent=1)
 
