@@ -61,6 +61,8 @@ ANNOT_RESIZED = ANNOT_PREFIX + "resized-request"
 ANNOT_NODE_SCORE = ANNOT_PREFIX + "score"
 
 ENV_SLO = "SLO"
+# batch pods: query batches the pod will run (the scheduler predicts its GPU time from it)
+ENV_ITERATIONS = "ITERATIONS"
 # Device env written before the container starts (PreBind) -- MI355X-native keys.
 ENV_ROCR_VISIBLE = "ROCR_VISIBLE_DEVICES"
 ENV_HIP_VISIBLE = "HIP_VISIBLE_DEVICES"

@@ -210,6 +210,16 @@ def pod_slo(pod: Obj) -> float:
         return 0.0
 
 
+def pod_iterations(pod: Obj) -> float:
+    """Declared iteration count of a batch pod (env ITERATIONS on Containers[0]); 0 = a
+    long-running service (its load is its SLO rate instead)."""
+    raw = get_env(pod, C.ENV_ITERATIONS)
+    try:
+        return max(0.0, float(raw)) if raw != "" else 0.0
+    except ValueError:
+        return 0.0
+
+
 def env_from_config_maps(pod: Obj, first_container_only: bool = False) -> List[str]:
     """ConfigMap names referenced by envFrom (all containers, like
     reference pkg/resources/pods.go:162-171; or just Containers[0])."""

@@ -183,9 +183,11 @@ def load_config(path_or_text: str) -> SchedulerConfig:
     raise ValueError("no KubeSchedulerConfiguration found")
 
 
-def default_gpu_config(gpu_args: Optional[Dict[str, Any]] = None, disable_defaults: bool = False) -> SchedulerConfig:
+def default_gpu_config(gpu_args: Optional[Dict[str, Any]] = None, disable_defaults: bool = False,
+                       queue_sort: bool = False) -> SchedulerConfig:
     """The deployed profile: GPU at score (weight 10100) + every extension point the
-    fixed-mode plugin implements (filter/reserve/preBind/postBind)."""
+    fixed-mode plugin implements (filter/reserve/preBind/postBind); `queue_sort` also makes
+    GPU the queueSort plugin (longest predicted work first within an arrival window)."""
     score: Dict[str, Any] = {"enabled": [{"name": C.PLUGIN_NAME, "weight": C.DEFAULT_SCORE_WEIGHT}]}
     if disable_defaults:
         score["disabled"] = [{"name": "*"}]
@@ -196,6 +198,7 @@ def default_gpu_config(gpu_args: Optional[Dict[str, Any]] = None, disable_defaul
         "profiles": [{
             "schedulerName": C.SCHEDULER_NAME,
             "plugins": {
+                **({"queueSort": {"enabled": [{"name": C.PLUGIN_NAME}]}} if queue_sort else {}),
                 "preFilter": {"enabled": [{"name": C.PLUGIN_NAME}]},
                 "filter": {"enabled": [{"name": C.PLUGIN_NAME}]},
                 "preScore": {"enabled": [{"name": C.PLUGIN_NAME}]},

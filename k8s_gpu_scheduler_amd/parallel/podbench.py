@@ -50,9 +50,12 @@ from ..plugins import full_registry
 from ..plugins.gpu.devices import DeviceLedger
 from ..recommender.client import CachedPredictions, _Tab
 from ..telemetry.cache import DeviceSample, TelemetryCache
+from ..telemetry.workcost import WorkCostModel
 
 NODE = "mi355x-node-0"
 FIELDS = 7    # gpu, first_unit, n_units, workload_id, iters, slo_milli, masked
+TELE = 4 + 2 * len(W.NAMES)   # busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods)
+UNITS_PER_GPU = 8
 
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
@@ -86,7 +89,8 @@ class ControlPlane:
     """Rank 0: apiserver + scheduler + arrivals."""
 
     def __init__(self, n_gpus: int, pods_per_gpu: int, iters: int, seed: int, policy: str = "gpu",
-                 cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable"):
+                 cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
+                 balance: float = 1.0):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -95,15 +99,22 @@ class ControlPlane:
         self.fc = FakeCluster(sync_watch=True, auto_run=True)
         self.fc.create("nodes", O.make_node(NODE, gpus=n_gpus))
         self.telemetry = TelemetryCache(stale_s=0)
+        self.workcost = WorkCostModel()
         self.ledger = DeviceLedger()
         self.predictions = predictions or measured_predictions() or analytic_predictions()
-        args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "pack": "binpack", "compat_env": False}
+        args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
+                "compat_env": False}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
-        self.sched = Scheduler(self.fc, default_gpu_config(args, disable_defaults=True), full_registry(),
+        # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
+        # predicted work first) and the least-predicted-load term spreads each epoch's
+        # work evenly over the GPUs (the ranks are coupled through the per-epoch broadcast,
+        # so the busiest GPU sets the pace)
+        cfg = default_gpu_config(args, disable_defaults=True, queue_sort=balance > 0 and policy != "random")
+        self.sched = Scheduler(self.fc, cfg, full_registry(),
                                bind_async=False, record_events=False, seed=seed,
                                extras={"telemetry": self.telemetry, "ledger": self.ledger,
-                                       "predictions": self.predictions})
+                                       "predictions": self.predictions, "workcost": self.workcost})
         self.sched.keep_results = False
         self.sched.start_informers()
         self.plugin = self.sched.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
@@ -141,7 +152,8 @@ class ControlPlane:
         for p in pods:
             w = W.CATALOG[p["workload"]]
             pod = O.make_pod(p["name"], gpu_cu=self.cu_per_pod, gpu_mem_gib=round(w.hbm_gib, 1),
-                             slo=round(p["slo"], 3), gpu_limits=self.qos == "guaranteed")
+                             slo=round(p["slo"], 3), gpu_limits=self.qos == "guaranteed",
+                             env={C.ENV_ITERATIONS: str(self.iters)})
             self.fc.create("pods", pod, owned=True)
         results = self.sched.schedule_pending()
         arr = np.full((len(pods), FIELDS), -1, dtype=np.int32)
@@ -179,7 +191,14 @@ class ControlPlane:
                 pass
 
     def update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
-        """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib)."""
+        """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib[, per-workload
+        (sum of observed GPU-seconds per iteration, pods) x len(W.NAMES)])."""
+        per_gpu = np.asarray(per_gpu, dtype=np.float64)
+        if per_gpu.shape[1] >= TELE:
+            cost = per_gpu[:, 4:TELE].sum(axis=0).reshape(len(W.NAMES), 2)
+            for wid, (tot, n) in enumerate(cost):
+                if n > 0:
+                    self.workcost.observe(W.NAMES[wid], float(tot / n), int(n))
         for st in self.ledger.devices(NODE):
             g = st.device.gpu
             if g >= len(per_gpu):
@@ -190,22 +209,56 @@ class ControlPlane:
 
 
 class SimExecutor:
-    """CPU stand-in for DeviceExecutor (tests / no-GPU runs): pod time from the roofline."""
+    """CPU stand-in for DeviceExecutor (tests / no-GPU runs).
 
-    def __init__(self) -> None:
+    Untimed (default): pod time from the roofline at the pod's share, nothing waits.
+    Timed (`--sim-timed`): a modelled device per rank -- an epoch occupies the GPU for the
+    sum of its pods' whole-GPU co-run cost (GEMM FLOPs at the measured co-run GEMM rate +
+    HBM bytes at the measured co-run stream rate, profiles/r01_overlap_study.json) x
+    `scale`, epochs run back to back, and wait_epoch sleeps until the epoch's modelled
+    completion -- so multi-rank CPU rehearsals (gloo) reproduce the coupling of the ranks
+    through the per-epoch placement broadcast, and load imbalance costs wall time."""
+
+    CORUN_TFLOPS = 750.0
+    CORUN_TBPS = 6.3
+
+    def __init__(self, timed: bool = False, scale: float = 1.0) -> None:
         self.flops_done = 0.0
         self.pending: List[Any] = []
+        self.timed, self.scale = timed, scale
+        self._dev_free = 0.0
+
+    @classmethod
+    def corun_cost_s(cls, w: "W.Workload") -> float:
+        t = 0.0
+        for o in w.ops:
+            t += o.flops / (cls.CORUN_TFLOPS * 1e12) if o.kind == "gemm" else o.bytes / (cls.CORUN_TBPS * 1e12)
+        return t
 
     def warm(self, runs) -> None:
         pass
 
     def wait_epoch(self, runs) -> None:
-        pass
+        if self.timed and runs:
+            dt = max(getattr(r, "done_at", 0.0) for r in runs) - time.perf_counter()
+            if dt > 0:
+                time.sleep(dt)
 
     def launch_epoch(self, runs) -> None:
+        if self.timed:
+            now = time.perf_counter()
+            cost = [self.corun_cost_s(W.CATALOG[r.workload]) * r.iters * self.scale for r in runs]
+            start = max(now, self._dev_free)
+            self._dev_free = start + sum(cost)
+            for r, c in zip(runs, cost):
+                # processor sharing: a pod holding n of the GPU's units is charged c of
+                # whole-GPU time, i.e. it runs c x units/n of wall time at its share
+                r.ms = c * UNITS_PER_GPU / max(r.n_units, 1) * 1e3
+                r.done_at = self._dev_free
         for r in runs:
             w = W.CATALOG[r.workload]
-            r.ms = W.roofline_seconds(w, r.n_units / 8.0) * r.iters * 1e3
+            if not self.timed:
+                r.ms = W.roofline_seconds(w, r.n_units / 8.0) * r.iters * 1e3
             self.flops_done += w.flops * r.iters
         self.pending = runs
 
@@ -217,6 +270,19 @@ class SimExecutor:
 
     def close(self) -> None:
         pass
+
+
+def _cost_rows(runs: List[Any]) -> np.ndarray:
+    """Per-workload (sum of observed GPU-seconds per iteration, pods) of finished pods:
+    a pod holding n of the GPU's units for ms is charged ms x n / units (its share of the
+    GPU's busy time), divided by its iterations."""
+    out = np.zeros((len(W.NAMES), 2), dtype=np.float64)
+    for r in runs:
+        if r.ms > 0 and r.iters > 0:
+            wid = W.INDEX[r.workload]
+            out[wid, 0] += r.ms / 1e3 * r.n_units / UNITS_PER_GPU / r.iters
+            out[wid, 1] += 1
+    return out
 
 
 def _union_ms(iv: List[Tuple[float, float]]) -> float:
@@ -264,6 +330,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--policy", default="gpu", choices=["gpu", "random"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--sim", action="store_true", help="no GPU: simulated executor")
+    ap.add_argument("--sim-timed", action="store_true",
+                    help="simulated executor sleeps out a modelled device time per epoch (multi-rank CPU rehearsal)")
+    ap.add_argument("--sim-scale", type=float, default=1.0, help="modelled device-time multiplier (--sim-timed)")
+    ap.add_argument("--balance", type=float, default=1.0,
+                    help="weight of the GPU plugin's least-predicted-load term (0 = off; >0 also sorts the "
+                         "queue longest-predicted-work first)")
     ap.add_argument("--no-cu-mask", action="store_true")
     ap.add_argument("--qos", default="burstable", choices=["burstable", "guaranteed"],
                     help="burstable: CU request is an accounted share, kernels may use idle CUs; "
@@ -289,7 +361,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     # (torch.cuda.is_available() initialises HIP; a GPU-initialised process must not exec).
     n_gpus_planned = world if world > 1 else max(1, a.gpus if a.sim else 1)
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
-                     policy=a.policy, qos=a.qos)
+                     policy=a.policy, qos=a.qos, balance=a.balance)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -319,7 +391,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             from .. import _native
             _native.hip(required=True).set_gemm_policy(a.gemm_policy)
     else:
-        ex = SimExecutor()
+        ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
     gpus_here = [rank] if world > 1 else list(range(n_gpus))
 
     # Control traffic (placements, telemetry) runs on a NON-blocking side stream: the
@@ -329,7 +401,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     side = torch.cuda.Stream(device=dev) if use_gpu else None
     cdev = dev if (world > 1 and backend == "nccl") else torch.device("cpu")
     assign = torch.zeros((P, FIELDS), dtype=torch.int32, device=cdev)
-    tele = torch.zeros((4,), dtype=torch.float64, device=cdev)
+    tele = torch.zeros((TELE,), dtype=torch.float64, device=cdev)
     tele_all = [torch.zeros_like(tele) for _ in range(world)]
 
     def bcast(arr: Optional[np.ndarray]) -> np.ndarray:
@@ -363,7 +435,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     intervals.append((ref["ev"].elapsed_time(r.start), ref["ev"].elapsed_time(r.end)))
         st = ex.collect(runs)
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
-        vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm]
+        vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm] + _cost_rows(runs).ravel().tolist()
         if world > 1:
             with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
                 tele.copy_(torch.tensor(vec, dtype=torch.float64))
@@ -371,17 +443,18 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                 per_gpu = torch.stack(tele_all).cpu().numpy()
         elif not use_gpu and n_gpus > 1:
             # single-process simulation of several GPUs: split by gpu id
-            per_gpu = np.zeros((n_gpus, 4))
+            per_gpu = np.zeros((n_gpus, TELE))
             for r in runs:
                 g = int(arr[r.pod_id][0])
-                per_gpu[g] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
-                               W.CATALOG[r.workload].hbm_gib)
+                per_gpu[g, :4] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
+                                   W.CATALOG[r.workload].hbm_gib)
+                per_gpu[g, 4:] += _cost_rows([r]).ravel()
         else:
             per_gpu = np.asarray(vec, dtype=np.float64)[None, :]
         if rank == 0:
             cp.update_telemetry(per_gpu, max(st["span_ms"], 1e-3))
         if timed:
-            tot = per_gpu.sum(axis=0)
+            tot = per_gpu[:, :4].sum(axis=0)
             totals["pods"] += tot[1]
             totals["busy_unit_ms"] += tot[0]
             totals["slo_ok"] += tot[2]
@@ -472,6 +545,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "config": {"model": "bin-pack fractional-GPU pods onto MI355X by live HBM/CU-util (Score path)",
                        "global_batch": P, "seq_len": a.iters, "parallelism": f"dp{n_gpus}",
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
+                       "balance": a.balance,
                        "note": "global_batch = pods per scheduling epoch; seq_len = query batches per pod"},
             "gpu_util_pct": round(util, 2),
             "cu_share_occupancy_pct": round(occ, 2),

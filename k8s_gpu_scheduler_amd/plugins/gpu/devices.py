@@ -141,6 +141,7 @@ class PodUse:
     hbm_gib: float
     units: Tuple[int, int]       # (first unit, count) inside the device
     whole: bool = False
+    work: float = 0.0            # predicted whole-GPU seconds of this pod on this device
 
 
 @dataclass
@@ -149,6 +150,7 @@ class DeviceState:
     used_units: List[bool] = field(default_factory=list)
     hbm_used: float = 0.0
     pods: Dict[str, PodUse] = field(default_factory=dict)
+    work: float = 0.0            # sum of the residents' predicted GPU time (PodUse.work)
 
     def __post_init__(self) -> None:
         if not self.used_units:
@@ -237,8 +239,10 @@ class DeviceLedger:
         return node in self.nodes
 
     def reserve(self, node: str, pod_key: str, pod_name: str, slo: float,
-                allocs: List[Tuple[str, int, int, float, bool]]) -> bool:
-        """allocs: (uuid, first_unit, n_units, hbm_gib, whole).  All-or-nothing."""
+                allocs: List[Tuple[str, int, int, float, bool]], work: float = 0.0) -> bool:
+        """allocs: (uuid, first_unit, n_units, hbm_gib, whole).  All-or-nothing.  `work` is
+        the pod's predicted GPU time (split evenly over its devices), summed per device for
+        the plugin's load-balance term."""
         with self._lock:
             if pod_key in self.pod_index:
                 self.release(pod_key)
@@ -255,7 +259,9 @@ class DeviceLedger:
                 for u in range(u0, u0 + n):
                     st.used_units[u] = True
                 st.hbm_used += hbm
-                st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole)
+                share = work / max(len(allocs), 1)
+                st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole, share)
+                st.work += share
                 st.invalidate()
             self.pod_index[pod_key] = (node, [a[0] for a in allocs])
             self.generation += 1
@@ -280,10 +286,20 @@ class DeviceLedger:
                 for u in range(u0, u0 + n):
                     st.used_units[u] = False
                 st.hbm_used = max(0.0, st.hbm_used - use.hbm_gib)
+                st.work = max(0.0, st.work - use.work) if st.pods else 0.0
                 st.invalidate()
             self.generation += 1
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
             return True
+
+    def gpu_work(self, node: str) -> Dict[int, float]:
+        """Predicted GPU time of the pods resident on each physical GPU of a node (its
+        partitions / fractional shares summed)."""
+        with self._lock:
+            out: Dict[int, float] = {}
+            for st in self.nodes.get(node, {}).values():
+                out[st.device.gpu] = out.get(st.device.gpu, 0.0) + st.work
+            return out
 
     def placement(self, pod_key: str) -> Optional[Tuple[str, List[str]]]:
         with self._lock:

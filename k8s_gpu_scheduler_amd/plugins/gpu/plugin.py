@@ -37,8 +37,8 @@ from typing import Any, Dict, List, Optional, Tuple
 from ...api import constants as C
 from ...api import objects as O
 from ...framework.interface import (CycleState, FilterPlugin, NodeScore, PostBindPlugin, PreBindPlugin,
-                                    PreFilterPlugin, PreScorePlugin, ReservePlugin, ScoreExtensions, ScorePlugin,
-                                    Status, min_max_normalize)
+                                    PreFilterPlugin, PreScorePlugin, QueueSortPlugin, ReservePlugin, ScoreExtensions,
+                                    ScorePlugin, Status, min_max_normalize)
 from ...kube.resources import Resources
 from ...recommender.client import CachedPredictions, PredictionProvider, RecommenderClient, RpcPredictions
 from ...telemetry.cache import TelemetryCache
@@ -85,6 +85,12 @@ class GPUArgs:
     w_slo: float = 1.0
     w_pack: float = 1.0
     w_telemetry: float = 0.5
+    # least-predicted-load across a node's GPUs: each resident pod's predicted GPU time
+    # (ITERATIONS / predicted whole-GPU throughput, or SLO / throughput for services)
+    w_balance: float = 0.0
+    # queueSort (when GPU is the profile's queueSort plugin): pods arriving in the same
+    # window are popped longest-predicted-work first (LPT), older windows first
+    lpt_window_s: float = 1.0
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
@@ -104,6 +110,7 @@ class GPUArgs:
     def from_dict(cls, d: Dict[str, Any]) -> "GPUArgs":
         a = cls()
         alias = {"weightSLO": "w_slo", "weightPack": "w_pack", "weightTelemetry": "w_telemetry",
+                 "weightBalance": "w_balance", "lptWindowSeconds": "lpt_window_s",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle"}
@@ -114,7 +121,7 @@ class GPUArgs:
         return a
 
 
-class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, ScoreExtensions, ReservePlugin,
+class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, ScoreExtensions, ReservePlugin,
                 PreBindPlugin, PostBindPlugin):
     NAME = C.PLUGIN_NAME
 
@@ -128,6 +135,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         self.ledger = ledger or extras.get("ledger") or DeviceLedger()
         self.redis = redis if redis is not None else extras.get("redis")
         self.predictions = predictions or extras.get("predictions")
+        self.workcost = extras.get("workcost")      # telemetry.workcost.WorkCostModel (optional)
         self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
         self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
         self._col_memo: Dict[str, Optional[str]] = {}
@@ -202,7 +210,8 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                     self._on_node(self.handle.client.get("nodes", node))
                 except Exception as e:
                     log.debug("recovery: node %s of %s unavailable: %s", node, O.key(pod), e)
-            self.ledger.reserve(node, O.key(pod), O.name(pod), O.pod_slo(pod), allocs)
+            work = self.pod_work(pod, self._pod_predictions(O.name(pod))[0])
+            self.ledger.reserve(node, O.key(pod), O.name(pod), O.pod_slo(pod), allocs, work=work)
 
     def _on_pod_delete(self, pod: Obj) -> None:
         self.ledger.release(O.key(pod))
@@ -312,7 +321,10 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             choice.burstable = req.burstable
         elif req.implicit:
             return None                 # no free GPU share: runs without one
-        if choice is None or not self.ledger.reserve(node_name, O.key(pod), O.name(pod), req.slo, choice.allocs):
+        work = self.pod_work(pod, (state.read(_PRED) or self._pod_predictions(O.name(pod)))[0]) \
+            if choice is not None else 0.0
+        if choice is None or not self.ledger.reserve(node_name, O.key(pod), O.name(pod), req.slo, choice.allocs,
+                                                     work=work):
             return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
         state.write(_CHOICE + "/reserved", choice)
         return None
@@ -384,6 +396,45 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                 env[C.ENV_MPS_THREADS] = ""
                 env[C.ENV_MPS_MEM] = ""
         return env
+
+    # ------------------------------------------------------------------ queue sort
+    def less(self, a: Any, b: Any) -> bool:
+        """QueueSort: priority first (PrioritySort), then arrival window, then the longest
+        predicted work first inside a window -- longest-processing-time-first list
+        scheduling, which with the least-loaded balance term keeps a burst of pods evenly
+        spread over a node's GPUs.  Windows keep the order a strict weak ordering and
+        bound how long a short pod can be overtaken (one window)."""
+        ka, kb = self._sort_key(a), self._sort_key(b)
+        return ka < kb
+
+    def _sort_key(self, pi: Any) -> Tuple[int, int, float, float]:
+        d = pi.__dict__
+        hit = d.get("_gpu_sort")
+        if hit is not None and hit[0] is pi.pod:
+            return hit[1]
+        pod = pi.pod
+        w = self.args.lpt_window_s
+        window = int(pi.timestamp // w) if w > 0 else 0
+        work = self.pod_work(pod, self._pod_predictions(O.name(pod))[0]) if w > 0 else 0.0
+        key = (-O.priority(pod), window, -work, pi.timestamp)
+        d["_gpu_sort"] = (pod, key)
+        return key
+
+    def pod_work(self, pod: Obj, conf: Dict[str, float]) -> float:
+        """Predicted whole-GPU time of a pod: ITERATIONS x seconds per iteration for a
+        batch pod, SLO x seconds per iteration (the GPU fraction it needs) for a service;
+        0 without a prediction.  Seconds per iteration come from the observed co-run cost
+        of the pod's workload (telemetry.workcost, fed by the executors) when there is
+        one, else 1 / the predicted whole-GPU throughput (Burstable co-running pods share
+        every CU, so the whole-GPU rate is the denominator for the load they add)."""
+        spi = self.workcost.seconds_per_iter(O.name(pod)) if self.workcost is not None else None
+        if spi is None:
+            tput = (conf.get(f"1P_{self.args.model}") or 0.0) if conf else 0.0
+            if tput <= 0:
+                return 0.0
+            spi = 1.0 / tput
+        iters = O.pod_iterations(pod)
+        return (iters if iters > 0 else O.pod_slo(pod)) * spi
 
     # ------------------------------------------------------------------ predictions
     def _pod_predictions(self, name: str) -> Tuple[Dict[str, float], Dict[str, float]]:
@@ -465,6 +516,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         a = self.args
         name = O.name(pod)
         conf, intf = state.read(_PRED) or self._pod_predictions(name)
+        work = self.pod_work(pod, conf) if a.w_balance else 0.0
         skey = None
         if a.pack != "random":
             tv = self.telemetry.node_version(node) if a.w_telemetry else 0
@@ -474,7 +526,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                 # everything the score depends on besides the node: the request, the
                 # incoming pod's predictions (its workload row) -- not its name
                 x_col = self._workload_col(name, intf) if intf else None
-                sig = (req.units, req.hbm_gib, req.slo, x_col,
+                sig = (req.units, req.hbm_gib, req.slo, work, x_col,
                        tuple(sorted(conf.items())) if conf else (),
                        () if x_col is not None or not intf else tuple(sorted(intf.items())))
                 state.write(_SIG, sig)
@@ -482,7 +534,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             hit = self._score_memo.get(node)
             if hit is not None and hit[0] == skey:
                 return dataclasses.replace(hit[1]) if hit[1] is not None else None
-        best = self._score_cands(node, cands, req, name, conf, intf)
+        best = self._score_cands(node, cands, req, name, conf, intf, work)
         if skey is not None:
             self._score_memo[node] = (skey, best)
             if best is not None:
@@ -490,7 +542,7 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
         return best
 
     def _score_cands(self, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest, name: str,
-                     conf: Dict[str, float], intf: Dict[str, float]) -> Optional[Choice]:
+                     conf: Dict[str, float], intf: Dict[str, float], work: float = 0.0) -> Optional[Choice]:
         a = self.args
         states = self.ledger.devices(node)
         slo_scores: List[Optional[float]] = [None] * len(cands)
@@ -512,6 +564,11 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
             st, u0 = cands[self._rng.randrange(len(cands))]
             return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], 50.0, [st.device])
         gpu_fill: Optional[Dict[int, List[int]]] = None
+        loads: Optional[Dict[int, float]] = None
+        top = 0.0
+        if a.w_balance:
+            loads = self.ledger.gpu_work(node)
+            top = max(loads.values(), default=0.0) + work
         for i, (st, u0) in enumerate(cands):
             parts: List[Tuple[float, float]] = []
             if slo_scores[i] is not None:
@@ -527,6 +584,11 @@ class GPUPlugin(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin, Scor
                 frac = (used + req.units) / max(tot, 1)
                 pk = 100.0 * frac if a.pack == "binpack" else 100.0 * (1.0 - frac)
                 parts.append((a.w_pack, pk))
+            if loads is not None:
+                # 100 on the least-loaded GPU after placement relative to the node's
+                # busiest; equal loads (or no prediction) tie
+                bal = 100.0 * (1.0 - (loads.get(st.device.gpu, 0.0) + work) / top) if top > 0 else 100.0
+                parts.append((a.w_balance, bal))
             if a.w_telemetry:
                 smp = self.telemetry.get(node, st.device.uuid)
                 if smp is not None:

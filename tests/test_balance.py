@@ -1,0 +1,163 @@
+"""Least-predicted-load balancing across a node's GPUs, longest-work-first queue sort and
+the observed work-cost model (telemetry.workcost).
+
+The ranks of a multi-GPU job are coupled (here: the bench's per-epoch placement broadcast),
+so the busiest GPU sets the pace; the GPU plugin's balance term spreads predicted GPU time
+evenly, the queueSort orders a burst longest-first (LPT list scheduling)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+from k8s_gpu_scheduler_amd.framework.queue import QueuedPodInfo
+from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+from k8s_gpu_scheduler_amd.plugins import full_registry
+from k8s_gpu_scheduler_amd.plugins.gpu.devices import DeviceLedger, synth_uuid
+from k8s_gpu_scheduler_amd.plugins.gpu.plugin import GPUPlugin
+from k8s_gpu_scheduler_amd.telemetry.cache import TelemetryCache
+from k8s_gpu_scheduler_amd.telemetry.workcost import WorkCostModel
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _Pred:
+    """Predictions: 'big' workloads run 1 iteration/s on a whole GPU, 'small' 10/s."""
+
+    def configurations(self, name):
+        tput = 1.0 if "big" in name else 10.0
+        return {f"{p}P_{C.MI355X}": tput / p for p in (1, 2, 4, 8)}
+
+    def interference(self, name):
+        return {}
+
+
+def _world(args, queue_sort=True, workcost=None):
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n0", gpus=4))
+    ledger = DeviceLedger()
+    extras = {"ledger": ledger, "telemetry": TelemetryCache(stale_s=0), "predictions": _Pred()}
+    if workcost is not None:
+        extras["workcost"] = workcost
+    s = Scheduler(fc, default_gpu_config(args, disable_defaults=True, queue_sort=queue_sort), full_registry(),
+                  bind_async=False, seed=0, extras=extras)
+    s.start_informers()
+    return fc, s, ledger
+
+
+def _pod(name, iters=10):
+    return O.make_pod(name, gpu_cu=64, env={C.ENV_ITERATIONS: str(iters)})
+
+
+def _loads(ledger):
+    return ledger.gpu_work("n0")
+
+
+def test_ledger_tracks_predicted_work_per_gpu():
+    led = DeviceLedger()
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n0", gpus=2))
+    from k8s_gpu_scheduler_amd.plugins.gpu.devices import devices_for_node
+    led.set_devices("n0", devices_for_node(fc.get("nodes", "n0")))
+    u0, u1 = synth_uuid("n0", 0), synth_uuid("n0", 1)
+    assert led.reserve("n0", "ns/a", "a", 0, [(u0, 0, 2, 1.0, False)], work=3.0)
+    assert led.reserve("n0", "ns/b", "b", 0, [(u0, 2, 2, 1.0, False)], work=1.5)
+    assert led.reserve("n0", "ns/c", "c", 0, [(u0, 4, 2, 0.0, False), (u1, 0, 2, 0.0, False)], work=2.0)
+    assert led.gpu_work("n0") == {0: 5.5, 1: 1.0}
+    led.release("ns/a")
+    assert led.gpu_work("n0") == {0: 2.5, 1: 1.0}
+    led.release("ns/b")
+    led.release("ns/c")
+    assert led.gpu_work("n0") == {0: 0.0, 1: 0.0}
+
+
+def test_pod_work_from_predictions_and_observed_cost():
+    p = GPUPlugin({"w_balance": 1.0}, None, predictions=_Pred())
+    conf = _Pred().configurations("big-x")
+    assert p.pod_work(_pod("big-x", iters=20), conf) == pytest.approx(20.0)
+    svc = O.make_pod("big-svc", gpu_cu=64, slo=0.25)            # service: SLO x s/iter
+    assert p.pod_work(svc, conf) == pytest.approx(0.25)
+    assert p.pod_work(_pod("nothing"), {}) == 0.0
+    wc = WorkCostModel(alpha=0.5)
+    wc.observe("big", 0.2)
+    p.workcost = wc                                           # observed co-run cost wins
+    assert p.pod_work(_pod("big-x", iters=20), conf) == pytest.approx(4.0)
+    wc.observe("big", 0.4)                                    # EWMA
+    assert p.pod_work(_pod("big-x", iters=20), conf) == pytest.approx(20 * 0.3)
+
+
+def test_workcost_label_resolution_prefers_longest_label():
+    wc = WorkCostModel()
+    wc.observe("onnx_resnet50_1024", 1.0)
+    wc.observe("onnx_resnet50_10240", 2.0)
+    assert wc.seconds_per_iter("onnx-resnet50-10240-e1-p3") == 2.0
+    assert wc.seconds_per_iter("onnx-resnet50-1024-e1-p3") == 1.0
+    assert wc.seconds_per_iter("busybox-abc") is None
+    wc.observe("x", -1.0)                                     # ignored
+    assert "x" not in wc.snapshot()
+
+
+def test_balance_spreads_predicted_work_over_gpus():
+    """4 big (10 s) + 12 small (1 s) pods, 4 GPUs x 4 slots: least-loaded + LPT puts one
+    big pod on each GPU; without the term bin-packing stacks the big pods."""
+    fc, s, ledger = _world({"w_slo": 0.0, "w_pack": 0.25, "w_telemetry": 0.0, "w_balance": 1.0})
+    names = [f"small-{i}" for i in range(12)] + [f"big-{i}" for i in range(4)]
+    for n in names:
+        fc.create("pods", _pod(n))
+    s.schedule_pending()
+    loads = _loads(ledger)
+    assert sorted(loads.values()) == pytest.approx([13.0] * 4)
+    fc2, s2, ledger2 = _world({"w_slo": 0.0, "w_pack": 0.25, "w_telemetry": 0.0, "w_balance": 0.0},
+                              queue_sort=False)
+    for n in names:
+        fc2.create("pods", _pod(n))
+    s2.schedule_pending()
+    assert max(_loads(ledger2).values()) >= 31.0              # 3 big + 1 small on one GPU
+
+
+def test_lpt_queue_sort_orders_burst_longest_first_with_windows():
+    p = GPUPlugin({"lpt_window_s": 1.0}, None, predictions=_Pred())
+    a = QueuedPodInfo(_pod("small-a"), timestamp=10.1)
+    b = QueuedPodInfo(_pod("big-b"), timestamp=10.5)
+    c = QueuedPodInfo(_pod("big-c"), timestamp=11.2)          # next window
+    hi = QueuedPodInfo(O.make_pod("small-hi", gpu_cu=64, priority=5), timestamp=12.0)
+    order = sorted([a, b, c, hi], key=p._sort_key)
+    assert [O.name(x.pod) for x in order] == ["small-hi", "big-b", "small-a", "big-c"]
+    assert p.less(b, a) and not p.less(a, b)
+
+
+def test_bench_sim_balance_flag_and_cost_learning():
+    from k8s_gpu_scheduler_amd.parallel.podbench import ControlPlane, main
+    r = main(["--sim", "--gpus", "4", "--steps", "3", "--warmup", "1", "--balance", "1"])
+    assert r["config"]["balance"] == 1.0 and r["unscheduled"] == 0
+    cp = ControlPlane(n_gpus=2, pods_per_gpu=4, iters=20, seed=0, balance=1.0)
+    import numpy as np
+    from k8s_gpu_scheduler_amd.parallel.podbench import TELE
+    per_gpu = np.zeros((2, TELE))
+    per_gpu[0, 4:6] = (0.5, 2)                                # workload 0: 2 pods, 0.25 s/iter mean
+    cp.update_telemetry(per_gpu, 10.0)
+    from k8s_gpu_scheduler_amd.models import workloads as W
+    assert cp.workcost.snapshot()[W.NAMES[0]] == pytest.approx(0.25)
+
+
+@pytest.mark.slow
+def test_bench_timed_sim_four_ranks_balance_improves_throughput(tmp_path):
+    """Rehearsal of the coupled multi-rank run (gloo, modelled device time): spreading
+    predicted work must not lose throughput against plain bin-packing."""
+    res = {}
+    for bal in (0, 1):
+        env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+               "--master-addr", "127.0.0.1", "--master-port", str(29621 + bal), os.path.join(ROOT, "bench.py"),
+               "--sim-timed", "--sim-scale", "2", "--gpus", "4", "--steps", "16", "--warmup", "3",
+               "--balance", str(bal)]
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+        assert p.returncode == 0, p.stderr[-3000:]
+        res[bal] = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert res[1]["unscheduled"] == 0
+    assert res[1]["value"] >= 0.97 * res[0]["value"]
