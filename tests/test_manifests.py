@@ -1,0 +1,96 @@
+"""Deploy manifests keep the reference's names, namespaces, ports and RBAC surface
+("same ... deploy manifests"; reference deploy/*.yaml), with the MI355X
+changes (ROCm device access, no NVIDIA runtime) and a loadable scheduler profile."""
+import glob
+import os
+
+import yaml
+
+from k8s_gpu_scheduler_amd.framework.config import load_config
+from k8s_gpu_scheduler_amd.framework.runtime import Framework
+from k8s_gpu_scheduler_amd.plugins import full_registry
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEPLOY = os.path.join(ROOT, "deploy")
+
+
+def _docs():
+    out = []
+    for f in sorted(glob.glob(os.path.join(DEPLOY, "**", "*.yaml"), recursive=True)):
+        with open(f) as fh:
+            for d in yaml.safe_load_all(fh):
+                if d:
+                    out.append((os.path.relpath(f, DEPLOY), d))
+    return out
+
+
+def _find(kind, name, ns=None):
+    for f, d in _docs():
+        md = d.get("metadata", {})
+        if d.get("kind") == kind and md.get("name") == name and (ns is None or md.get("namespace") == ns):
+            return d
+    raise AssertionError(f"{kind} {ns}/{name} not in deploy/")
+
+
+def test_every_manifest_parses_and_has_kind():
+    docs = _docs()
+    assert len(docs) >= 15
+    for f, d in docs:
+        assert d.get("apiVersion") and d.get("kind"), f
+
+
+def test_reference_service_ports_and_namespaces():
+    redis = _find("Service", "redis", "redis")
+    assert any(p.get("nodePort") == 32767 and p.get("port") == 6379 for p in redis["spec"]["ports"])
+    rec = _find("Service", "recommender", "recommender") if any(
+        d.get("kind") == "Service" and d["metadata"].get("name") == "recommender" for _, d in _docs()) else None
+    if rec is None:
+        rec = next(d for _, d in _docs() if d.get("kind") == "Service"
+                   and d["metadata"].get("namespace") == "recommender")
+    assert any(p.get("nodePort") == 32700 and p.get("targetPort") in (50051, "50051") for p in rec["spec"]["ports"])
+    _find("StatefulSet", "redis", "redis")
+
+
+def test_scheduler_profile_loads_and_instantiates():
+    cfg = load_config(os.path.join(DEPLOY, "scheduler.yaml"))
+    prof = cfg.profile("gpu-scheduler")
+    assert prof is not None and cfg.leader_election.leader_elect
+    assert cfg.leader_election.resource_name == "gpu-scheduler"
+    assert {r.name: r.weight for r in prof.enabled("score")}["GPU"] == 10100
+    assert prof.args("GPU")["mode"] == "fixed"
+    fw = Framework(prof, full_registry(), handle=None)
+    gpu = fw.plugin("GPU")
+    assert gpu.args.w_balance == 0.5 and gpu.args.model == "MI355X"
+    dep = _find("Deployment", "gpu-scheduler", "kube-system")
+    spec = dep["spec"]["template"]["spec"]
+    assert (spec.get("serviceAccountName") or spec.get("serviceAccount")) == "sample-sa"   # reference SA name
+
+
+def test_rbac_covers_what_the_scheduler_does():
+    rules = [r for _, d in _docs() if d.get("kind") == "ClusterRole" for r in d.get("rules", [])]
+
+    def allowed(resource, verb):
+        return any(resource in r.get("resources", []) and (verb in r.get("verbs", []) or "*" in r.get("verbs", []))
+                   for r in rules)
+    for res, verb in [("pods", "list"), ("pods", "watch"), ("pods", "delete"), ("pods/binding", "create"),
+                      ("bindings", "create"), ("configmaps", "update"), ("configmaps", "create"),
+                      ("nodes", "patch"), ("leases", "update"), ("events", "create")]:
+        assert allowed(res, verb) or (res == "pods/binding" and allowed("bindings", verb)), (res, verb)
+
+
+def test_node_agent_daemonset_uses_rocm_devices_not_nvidia():
+    ds = next(d for _, d in _docs() if d.get("kind") == "DaemonSet")
+    text = yaml.safe_dump(ds)
+    assert "/dev/kfd" in text and "/dev/dri" in text
+    assert "nvidia" not in text.lower()
+    env = {e["name"] for c in ds["spec"]["template"]["spec"]["containers"] for e in c.get("env", [])}
+    assert {"NODE_NAME", "POD_NAME", "POD_NAMESPACE"} <= env     # downward API, as the reference
+
+
+def test_busybox_fixture_matches_reference_shape():
+    dep = next(d for f, d in _docs() if f.startswith("busybox") and d.get("kind") == "Deployment")
+    spec = dep["spec"]["template"]["spec"]
+    assert spec["schedulerName"] == "gpu-scheduler"
+    c = spec["containers"][0]
+    assert any(e["name"] == "SLO" for e in c.get("env", []))
+    assert any("configMapRef" in ef for ef in c.get("envFrom", []))
