@@ -45,6 +45,21 @@ class NodeUnschedulable(FilterPlugin):
             return Status.unschedulable("node(s) were not ready", self.NAME, True)
         return None
 
+    def filter_nodes(self, state, pod, node_infos):
+        tol = None
+        out = []
+        for ni in node_infos:
+            node = ni.node
+            if O.node_unschedulable(node):
+                if tol is None:
+                    tol = O.tolerates(pod, {"key": "node.kubernetes.io/unschedulable", "effect": "NoSchedule"})
+                if not tol:
+                    out.append(Status.unschedulable("node(s) were unschedulable", self.NAME, True))
+                    continue
+            out.append(None if O.node_ready(node) else
+                       Status.unschedulable("node(s) were not ready", self.NAME, True))
+        return out
+
 
 class NodeName(FilterPlugin):
     NAME = "NodeName"
@@ -57,6 +72,12 @@ class NodeName(FilterPlugin):
         if want and want != node_info.name:
             return Status.unschedulable("node(s) didn't match the requested node name", self.NAME, True)
         return None
+
+    def filter_nodes(self, state, pod, node_infos):
+        want = pod.get("spec", {}).get("nodeName")
+        if not want:
+            return [None] * len(node_infos)
+        return [None if ni.name == want else self.filter(state, pod, ni) for ni in node_infos]
 
 
 class TaintToleration(FilterPlugin):
@@ -73,6 +94,10 @@ class TaintToleration(FilterPlugin):
                 return Status.unschedulable(f"node(s) had untolerated taint {{{t.get('key')}: {t.get('value', '')}}}",
                                             self.NAME, True)
         return None
+
+    def filter_nodes(self, state, pod, node_infos):
+        # untainted nodes (the common case) need no per-node work
+        return [self.filter(state, pod, ni) if O.node_taints(ni.node) else None for ni in node_infos]
 
 
 class NodeAffinity(FilterPlugin):
@@ -97,6 +122,12 @@ class NodeAffinity(FilterPlugin):
             if not ok:
                 return Status.unschedulable("node(s) didn't match Pod's node affinity/selector", self.NAME, True)
         return None
+
+    def filter_nodes(self, state, pod, node_infos):
+        spec = pod.get("spec", {})
+        if not spec.get("nodeSelector") and not ((spec.get("affinity") or {}).get("nodeAffinity")):
+            return [None] * len(node_infos)
+        return [self.filter(state, pod, ni) for ni in node_infos]
 
 
 _FIT_KEY = "NodeResourcesFit/req"
@@ -127,6 +158,32 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
                 return Status.unschedulable(f"Insufficient {r}", self.NAME)
         return None
 
+    def filter_nodes(self, state, pod, node_infos):
+        req = state.read(_FIT_KEY)
+        if req is None:
+            req = O.pod_requests(pod)
+        want = [(r, v - 1e-9, r.startswith(("amd.com/", "nvidia.com/"))) for r, v in req.items()
+                if v > 0 and r not in self.ignored]
+        pods_key = C.RESOURCE_PODS
+        out = []
+        for ni in node_infos:
+            alloc, used = ni.allocatable, ni.requested
+            st = None
+            if pods_key in alloc and alloc[pods_key] - used.get(pods_key, 0.0) < 1:
+                st = Status.unschedulable("Too many pods", self.NAME)
+            else:
+                for r, v, ext in want:
+                    a = alloc.get(r)
+                    if a is None:
+                        if ext:
+                            st = Status.unschedulable(f"Insufficient {r}", self.NAME)
+                            break
+                    elif a - used.get(r, 0.0) < v:
+                        st = Status.unschedulable(f"Insufficient {r}", self.NAME)
+                        break
+            out.append(st)
+        return out
+
 
 class _ResourceScore(ScorePlugin):
     RES = (C.RESOURCE_CPU, C.RESOURCE_MEMORY)
@@ -148,6 +205,26 @@ class _ResourceScore(ScorePlugin):
             self._memo.clear()
         self._memo[node_name] = (key, v)
         return v, None
+
+    def score_nodes(self, state, pod, names):
+        snap = self.handle.snapshot()
+        req = O.pod_requests(pod)
+        rq = tuple(req.get(r, 0.0) for r in self.RES)
+        memo = self._memo
+        if len(memo) > 100000:
+            memo.clear()
+        out = []
+        for nn in names:
+            ni = snap.get(nn)
+            key = (ni.generation if ni else -1, id(ni.node) if ni else 0) + rq
+            hit = memo.get(nn)
+            if hit is not None and hit[0] == key:
+                out.append(hit[1])
+                continue
+            v = self._score(self._fractions(pod, nn, ni, req))
+            memo[nn] = (key, v)
+            out.append(v)
+        return out, None
 
     def _fractions(self, pod, node_name, ni=None, req=None):
         if ni is None:

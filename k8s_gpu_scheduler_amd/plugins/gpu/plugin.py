@@ -274,6 +274,37 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME)
         return None
 
+    def filter_nodes(self, state: CycleState, pod: Obj, node_infos: List[Any]) -> List[Optional[Status]]:
+        """Batch Filter (framework chunked filtering): the request is parsed once; nodes
+        under a preemption what-if or not yet in the ledger take the per-node path."""
+        if self.parity is not None:
+            return [None] * len(node_infos)
+        req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
+        out: List[Optional[Status]] = []
+        memo = state.read(_CANDS)
+        if memo is None:
+            memo = {}
+            state.write(_CANDS, memo)
+        node_gen, cmemo, has_node = self.ledger.node_gen, self._cands_memo, self.ledger.has_node
+        frac = not req.whole
+        for ni in node_infos:
+            nn = ni.name
+            if getattr(ni, "removed", None) or not has_node(nn) or O.node_taints(ni.node):
+                out.append(self.filter(state, pod, ni))
+                continue
+            if frac:                    # inline memo hit of _best_choice(scoring=False)
+                hit = cmemo.get(nn)
+                if hit is not None and hit[0] == (node_gen.get(nn, 0), req.units, req.hbm_gib):
+                    memo[nn] = hit[1]
+                    ok = bool(hit[1])
+                else:
+                    ok = self._best_choice(state, pod, req, nn, scoring=False) is not None
+            else:
+                ok = self._best_choice(state, pod, req, nn, scoring=False) is not None
+            out.append(None if ok or req.implicit else
+                       Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME))
+        return out
+
     def pre_score(self, state: CycleState, pod: Obj, nodes: List[Any]) -> Optional[Status]:
         if self.parity is not None:
             return None
@@ -301,6 +332,36 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         choices[node_name] = choice
         return max(C.MIN_NODE_SCORE, min(C.MAX_NODE_SCORE, int(choice.score))), None
 
+    def score_nodes(self, state: CycleState, pod: Obj, names: List[str]) -> Tuple[List[int], Optional[Status]]:
+        """Batch Score over every feasible node (fixed mode; parity mode does I/O per node
+        and keeps the per-node path)."""
+        req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
+        choices = state.read(_CHOICE)
+        if choices is None:
+            choices = {}
+            state.write(_CHOICE, choices)
+        out = []
+        lo, hi = C.MIN_NODE_SCORE, C.MAX_NODE_SCORE
+        sig = self._pod_ctx(state, pod, req)[4] if not req.whole else None
+        node_gen, smemo, tele = self.ledger.node_gen, self._score_memo, self.telemetry
+        use_t, stale = bool(self.args.w_telemetry), tele.stale_s
+        for nn in names:
+            choice = None
+            hit = smemo.get(nn) if sig is not None else None
+            if hit is not None:         # inline memo hit of _best_choice(scoring=True)
+                tv = tele.node_version(nn) if use_t else 0
+                skey = ((node_gen.get(nn, 0), req.units, req.hbm_gib),
+                        (tv, int(time.monotonic()) if (tv and stale) else 0), sig)
+                if hit[0] != skey:
+                    hit = None
+            choice = hit[1] if hit is not None else self._best_choice(state, pod, req, nn, scoring=True)
+            if choice is None:
+                out.append(0)
+                continue
+            choices[nn] = choice
+            out.append(max(lo, min(hi, int(choice.score))))
+        return out, None
+
     def score_extensions(self) -> ScoreExtensions:
         return self
 
@@ -318,7 +379,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if choice is None:
             choice = self._best_choice(state, pod, req, node_name, scoring=True)
         if choice is not None:
-            choice.burstable = req.burstable
+            choice = dataclasses.replace(choice, burstable=req.burstable)   # memoised object: copy
         elif req.implicit:
             return None                 # no free GPU share: runs without one
         work = self.pod_work(pod, (state.read(_PRED) or self._pod_predictions(O.name(pod)))[0]) \
@@ -479,6 +540,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
 
     def _best_choice(self, state: CycleState, pod: Obj, req: GpuRequest, node: str,
                      scoring: bool) -> Optional[Choice]:
+        """Best device choice on one node.  The returned Choice may be the memoised
+        object itself (never mutated before Reserve, which copies it)."""
         if req.whole:
             states = self.ledger.devices(node)
             return self._whole_choice(req, node, states) if states else None
@@ -513,33 +576,42 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if not scoring:
             st, u0 = cands[0]
             return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], 0.0, [st.device])
+        name, conf, intf, work, sig = self._pod_ctx(state, pod, req)
+        skey = None
+        if sig is not None:
+            tv = self.telemetry.node_version(node) if self.args.w_telemetry else 0
+            tkey = (tv, int(time.monotonic()) if (tv and self.telemetry.stale_s) else 0)
+            skey = (ckey, tkey, sig)
+            hit = self._score_memo.get(node)
+            if hit is not None and hit[0] == skey:
+                return hit[1]
+        best = self._score_cands(node, cands, req, name, conf, intf, work)
+        if skey is not None:
+            self._score_memo[node] = (skey, best)
+        return best
+
+    def _pod_ctx(self, state: CycleState, pod: Obj, req: GpuRequest) -> Tuple[str, Dict[str, float],
+                                                                              Dict[str, float], float, Any]:
+        """Pod-level inputs of Score, computed once per cycle: predictions, predicted work
+        and the memo signature -- everything the score depends on besides the node (the
+        request and the incoming pod's workload row, not its name); None = no memo
+        (random packing)."""
+        ctx = state.read(_SIG)
+        if ctx is not None:
+            return ctx
         a = self.args
         name = O.name(pod)
         conf, intf = state.read(_PRED) or self._pod_predictions(name)
         work = self.pod_work(pod, conf) if a.w_balance else 0.0
-        skey = None
+        sig = None
         if a.pack != "random":
-            tv = self.telemetry.node_version(node) if a.w_telemetry else 0
-            tkey = (tv, int(time.monotonic()) if (tv and self.telemetry.stale_s) else 0)
-            sig = state.read(_SIG)
-            if sig is None:
-                # everything the score depends on besides the node: the request, the
-                # incoming pod's predictions (its workload row) -- not its name
-                x_col = self._workload_col(name, intf) if intf else None
-                sig = (req.units, req.hbm_gib, req.slo, work, x_col,
-                       tuple(sorted(conf.items())) if conf else (),
-                       () if x_col is not None or not intf else tuple(sorted(intf.items())))
-                state.write(_SIG, sig)
-            skey = (ckey, tkey, sig)
-            hit = self._score_memo.get(node)
-            if hit is not None and hit[0] == skey:
-                return dataclasses.replace(hit[1]) if hit[1] is not None else None
-        best = self._score_cands(node, cands, req, name, conf, intf, work)
-        if skey is not None:
-            self._score_memo[node] = (skey, best)
-            if best is not None:
-                best = dataclasses.replace(best)
-        return best
+            x_col = self._workload_col(name, intf) if intf else None
+            sig = (req.units, req.hbm_gib, req.slo, work, x_col,
+                   tuple(sorted(conf.items())) if conf else (),
+                   () if x_col is not None or not intf else tuple(sorted(intf.items())))
+        ctx = (name, conf, intf, work, sig)
+        state.write(_SIG, ctx)
+        return ctx
 
     def _score_cands(self, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest, name: str,
                      conf: Dict[str, float], intf: Dict[str, float], work: float = 0.0) -> Optional[Choice]:
