@@ -161,3 +161,73 @@ def test_bench_timed_sim_four_ranks_balance_improves_throughput(tmp_path):
         res[bal] = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
     assert res[1]["unscheduled"] == 0
     assert res[1]["value"] >= 0.97 * res[0]["value"]
+
+
+def test_batch_filter_and_score_match_node_at_a_time():
+    """framework.runtime.find_feasible/run_score with the plugins' batch forms give the
+    same feasible set, first-failure statuses and scores as the node-at-a-time loop."""
+    from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+    from k8s_gpu_scheduler_amd.framework.interface import CycleState
+    fc = FakeCluster()
+    for i in range(40):
+        kw = {}
+        if i % 7 == 3:
+            kw["taints"] = [{"key": "dedicated", "value": "x", "effect": "NoSchedule"}]
+        if i % 5 == 1:
+            kw["labels_"] = {"zone": "b"}
+        node = O.make_node(f"n{i:02d}", gpus=2 if i % 3 else 1, cpu="4" if i % 4 == 2 else "64")
+        if kw.get("taints"):
+            node["spec"]["taints"] = kw["taints"]
+        if kw.get("labels_"):
+            node["metadata"]["labels"].update(kw["labels_"])
+        if i % 11 == 5:
+            node["spec"]["unschedulable"] = True
+        fc.create("nodes", node)
+    s = Scheduler(fc, default_gpu_config({"w_balance": 1.0}), full_registry(), bind_async=False, seed=0,
+                  extras={"ledger": DeviceLedger(), "telemetry": TelemetryCache(stale_s=0), "predictions": _Pred()})
+    s.start_informers()
+    for i in range(30):                              # load some GPUs
+        fc.create("pods", O.make_pod(f"warm-{i}", gpu_cu=128, cpu="1"))
+    s.schedule_pending()
+    fw = s.frameworks[C.SCHEDULER_NAME]
+    seen_plugins = set()
+    pods = [O.make_pod("q1", gpu_cu=64, cpu="8"), O.make_pod("q2", gpu_cu=256, node_selector={"zone": "b"}),
+            O.make_pod("q3", gpus=2), O.make_pod("q4", gpu_cu=64, tolerations=[{"key": "dedicated",
+                                                                                 "operator": "Exists"}])]
+    for pod in pods:
+        for limit in (0, 3, 7):
+            nodes = s.cache.snapshot().list()
+            s._snapshot = s.cache.snapshot()
+            st1 = CycleState()
+            fw.run_pre_filter(st1, pod)
+            feas1, failed1 = fw.find_feasible(st1, pod, nodes, limit)
+            st2 = CycleState()
+            fw.run_pre_filter(st2, pod)
+            feas2, failed2 = [], {}
+            for ni in nodes:                         # reference: one node at a time
+                r = fw.run_filter(st2, pod, ni)
+                if r.ok:
+                    feas2.append(ni)
+                    if limit and len(feas2) >= limit:
+                        break
+                else:
+                    failed2[ni.name] = r
+            assert [n.name for n in feas1] == [n.name for n in feas2], (O.name(pod), limit)
+            assert {k: (v.code, v.plugin, v.reasons) for k, v in failed1.items()} == \
+                   {k: (v.code, v.plugin, v.reasons) for k, v in failed2.items()}
+            seen_plugins |= {v.plugin for v in failed1.values()}
+            if len(feas1) > 1 and limit == 0:
+                fw.run_pre_score(st1, pod, feas1)
+                batch, ok = fw.run_score(st1, pod, feas1)
+                assert ok.ok
+                per_node = {}
+                for p in fw.points["score"]:
+                    if p.name() in st1.skip_score_plugins:
+                        continue
+                    per_node[p.name()] = [p.score(st1, pod, n.name)[0] for n in feas1]
+                got = st1.read("framework/per-plugin-scores")
+                for name, vals in per_node.items():
+                    raw = [ns.score for ns in got[name]]
+                    if name != "GPU":                # GPU's list is normalized in place
+                        assert raw == vals, name
+    assert {"TaintToleration", "NodeResourcesFit", "NodeAffinity", "NodeUnschedulable"} <= seen_plugins, seen_plugins
