@@ -70,9 +70,32 @@ def main():
     os.makedirs("gpurun_out", exist_ok=True)
     json.dump(out, open("gpurun_out/overlap.json", "w"), indent=1)
     print(json.dumps(out, indent=1))
-    # stream-kernel launch shape sweep under co-run: (triad variant, blocks)
+    # phase staggering: slot k starts its op cycle at op k (same ops, rotated order)
+    def rotated(keep_all):
+        saved = {k: b.ops for k, b in ex._bufs.items()}
+        for (wl, u0, n), b in ex._bufs.items():
+            r = (u0 // 2) % max(len(b.ops), 1)
+            b.ops = b.ops[r:] + b.ops[:r]
+        try:
+            return run(ex, epochs, keep_all)
+        finally:
+            for k, b in ex._bufs.items():
+                b.ops = saved[k]
+    rot = []
+    for rnd in range(4):
+        f = run(ex, epochs, lambda o: True)
+        g = rotated(lambda o: True)
+        if rnd:
+            rot.append((round(f, 3), round(g, 3)))
+    out["rotation_full_vs_rotated_ms"] = rot
+    print("rotation", rot, flush=True)
     from k8s_gpu_scheduler_amd import _native
     hip = _native.hip(required=True)
+    json.dump(out, open("gpurun_out/overlap.json", "w"), indent=1)
+    if os.environ.get("OVERLAP_SHORT"):
+        ex.close()
+        return
+    # stream-kernel launch shape sweep under co-run: (triad variant, blocks)
     sweep = {}
     configs = [(6, 0), (3, 256), (3, 1024), (4, 256)]
     for rnd in range(3):
