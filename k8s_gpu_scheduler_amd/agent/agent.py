@@ -33,6 +33,7 @@ from ..kube.resources import Resources
 from ..store import schema
 from ..store.resp import Redis
 from .devices import DeviceSource
+from .health import HealthMonitor
 
 log = logging.getLogger(__name__)
 
@@ -52,7 +53,8 @@ def pod_of_pid(pid: int, proc: str = "/proc") -> Optional[str]:
 class NodeAgent:
     def __init__(self, node: str, redis: Redis, source: DeviceSource, client: Optional[KubeClient] = None,
                  poll_s: float = C.PROFILER_POLL_S, exporter: Any = None, telemetry: Any = None,
-                 apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None):
+                 apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None,
+                 health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -64,10 +66,18 @@ class NodeAgent:
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.partition_state = "idle"
+        self.health = health or HealthMonitor()
+        # Evict the pods of a device that turned unhealthy (their controllers recreate them
+        # and the scheduler places them elsewhere -- the elastic-recovery path); off by
+        # default, as with Kubernetes device plugins
+        self.evict_unhealthy = evict_unhealthy
+        self.evicted: List[str] = []
 
     # ------------------------------------------------------------------ publish
     def publish(self, force: bool = False) -> bool:
         devs = self.source.devices()
+        for d in devs:
+            d["healthy"] = self.health.healthy(d["uuid"])
         uuids = [d["uuid"] for d in devs]
         if not force and uuids == self.prev_uuids:
             return False
@@ -101,6 +111,49 @@ class NodeAgent:
                         power_w=float(s.get("power_w", 0)), temp_c=float(s.get("temp_c", 0)),
                         xgmi_tx_bps=float(s.get("xgmi_write_bps", 0)), xgmi_rx_bps=float(s.get("xgmi_read_bps", 0))))
         return samples
+
+    def check_health(self, samples: Optional[List[Dict[str, Any]]] = None) -> bool:
+        """Health verdicts from the latest samples; on a transition republish the
+        descriptors, update the node annotation (the schedulers' change trigger) and,
+        with evict_unhealthy, delete the pods assigned to newly failed devices."""
+        if samples is None:
+            samples = self.source.samples()
+        before = self.health.unhealthy()
+        devs = self.source.devices()
+        changed = self.health.update(samples, devs)
+        if self.exporter is not None:
+            self.exporter.observe_health({i: self.health.healthy(d["uuid"]) for i, d in enumerate(devs)},
+                                         {i: d["uuid"] for i, d in enumerate(devs)})
+        if not changed:
+            return False
+        bad = self.health.unhealthy()
+        self.publish(force=True)
+        if self.client is not None:
+            try:
+                self.client.patch("nodes", self.node, {"metadata": {"annotations": {
+                    C.ANNOT_UNHEALTHY: json.dumps(bad, sort_keys=True, separators=(",", ":"))}}}, "merge")
+            except Exception as e:
+                log.warning("health annotation on %s failed: %s", self.node, e)
+            newly = set(bad) - set(before)
+            if self.evict_unhealthy and newly:
+                self._evict_on(newly)
+        log.warning("device health on %s changed: %s", self.node, bad or "all healthy")
+        return True
+
+    def _evict_on(self, uuids: set) -> None:
+        try:
+            pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        except Exception as e:
+            log.warning("listing pods for eviction failed: %s", e)
+            return
+        for p in pods:
+            assigned = set(filter(None, O.annotations(p).get(C.ANNOT_DEVICES, "").split(",")))
+            if assigned & uuids and not O.is_terminal(p):
+                try:
+                    self.client.delete("pods", O.name(p), O.namespace(p))
+                    self.evicted.append(O.key(p))
+                except Exception as e:
+                    log.warning("evicting %s failed: %s", O.key(p), e)
 
     def record_history(self, uid_to_pod: Optional[Dict[str, str]] = None) -> int:
         """Per-pod usage samples from the per-process list (VRAM, CU occupancy)."""
@@ -168,7 +221,11 @@ class NodeAgent:
         except Exception as e:
             log.warning("partition reconcile failed: %s", e)
         self.publish()
-        self.sample()
+        samples = self.sample()
+        try:
+            self.check_health(samples)
+        except Exception as e:
+            log.warning("health check failed: %s", e)
 
     def run(self) -> None:
         while not self._stop.is_set():

@@ -59,6 +59,9 @@ ANNOT_SLO = ANNOT_PREFIX + "slo"
 ANNOT_WORKLOAD = ANNOT_PREFIX + "workload"
 ANNOT_RESIZED = ANNOT_PREFIX + "resized-request"
 ANNOT_NODE_SCORE = ANNOT_PREFIX + "score"
+# node annotation kept by the agent: JSON {uuid: reason} of unhealthy devices ("{}" when
+# all are healthy) -- also the change trigger that makes schedulers re-read the inventory
+ANNOT_UNHEALTHY = ANNOT_PREFIX + "unhealthy-devices"
 
 ENV_SLO = "SLO"
 # batch pods: query batches the pod will run (the scheduler predicts its GPU time from it)

@@ -12,6 +12,7 @@ ConfigMap walk of `GetSLOs` / `AppendToExistingConfigMapsInPod`
 from __future__ import annotations
 
 import copy
+import json
 import re
 import time
 import uuid as _uuid
@@ -208,6 +209,18 @@ def pod_slo(pod: Obj) -> float:
         return float(raw) if raw != "" else 0.0
     except ValueError:
         return 0.0
+
+
+def node_unhealthy_devices(node: Obj) -> Dict[str, str]:
+    """{uuid: reason} from the agent's unhealthy-devices node annotation ({} if none / bad)."""
+    raw = annotations(node).get(C.ANNOT_UNHEALTHY, "")
+    if not raw:
+        return {}
+    try:
+        v = json.loads(raw)
+    except ValueError:
+        return {}
+    return {str(k): str(r) for k, r in v.items()} if isinstance(v, dict) else {}
 
 
 def pod_iterations(pod: Obj) -> float:

@@ -47,6 +47,7 @@ class Device:
     model: str = C.MI355X
     units: int = 0              # XCD units (32 CUs each)
     first_xcd: int = 0          # first CU-slice unit of the GPU owned by this device
+    healthy: bool = True        # agent health verdict (agent/health.py); unhealthy = not allocatable
 
     def __post_init__(self) -> None:
         if not self.units:
@@ -55,14 +56,15 @@ class Device:
     def to_json(self) -> Dict[str, Any]:
         return {"uuid": self.uuid, "gpu": self.gpu, "partition": self.partition, "partitions": self.partitions,
                 "cus": self.cus, "hbm_gib": self.hbm_gib, "numa": self.numa, "model": self.model,
-                "first_xcd": self.first_xcd}
+                "first_xcd": self.first_xcd, "healthy": self.healthy}
 
     @classmethod
     def from_json(cls, node: str, d: Dict[str, Any]) -> "Device":
         return cls(uuid=d["uuid"], node=node, gpu=int(d.get("gpu", 0)), partition=int(d.get("partition", 0)),
                    partitions=int(d.get("partitions", 1)), cus=int(d.get("cus", C.MI355X_CUS)),
                    hbm_gib=float(d.get("hbm_gib", C.MI355X_HBM_GIB)), numa=int(d.get("numa", 0)),
-                   model=d.get("model", C.MI355X), first_xcd=int(d.get("first_xcd", 0)))
+                   model=d.get("model", C.MI355X), first_xcd=int(d.get("first_xcd", 0)),
+                   healthy=bool(d.get("healthy", True)))
 
 
 def devices_for_node(node: Obj, uuids: Optional[List[str]] = None,
@@ -71,8 +73,13 @@ def devices_for_node(node: Obj, uuids: Optional[List[str]] = None,
     node labels (GPU count + compute partition), with Redis UUIDs (reference schema)
     assigned in order when given."""
     nm = O.name(node)
+    bad = O.node_unhealthy_devices(node)
     if descriptors:
-        return [Device.from_json(nm, d) for d in descriptors]
+        out = [Device.from_json(nm, d) for d in descriptors]
+        for d in out:
+            if d.uuid in bad:
+                d.healthy = False
+        return out
     gpus = O.node_gpu_count(node)
     parts = O.node_partitions_per_gpu(node)
     model = O.node_gpu_model(node) or C.MI355X
@@ -92,6 +99,9 @@ def devices_for_node(node: Obj, uuids: Optional[List[str]] = None,
     if uuids and len(uuids) > len(out) and not gpus:
         # Unlabelled node with UUIDs (reference-style): one device per UUID.
         out = [Device(u, nm, k, 0, 1) for k, u in enumerate(uuids)]
+    for d in out:
+        if d.uuid in bad:
+            d.healthy = False
     return out
 
 

@@ -563,7 +563,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                 states = self.ledger.devices(node)
                 cands = []
                 for st in states:
-                    if st.hbm_free + 1e-6 < req.hbm_gib:
+                    if not st.device.healthy or st.hbm_free + 1e-6 < req.hbm_gib:
                         continue
                     u0 = st.find_units(req.units)
                     if u0 is None:
@@ -688,10 +688,12 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             sim.append(c)
         if req.whole:
             return self._whole_choice(req, node, sim) is not None
-        return any(c.hbm_free + 1e-6 >= req.hbm_gib and c._find_units(req.units) is not None for c in sim)
+        return any(c.device.healthy and c.hbm_free + 1e-6 >= req.hbm_gib and c._find_units(req.units) is not None
+                   for c in sim)
 
     def _whole_choice(self, req: GpuRequest, node: str, states: List[DeviceState]) -> Optional[Choice]:
-        free = [st for st in states if not st.pods and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)]
+        free = [st for st in states if st.device.healthy and not st.pods
+                and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)]
         if len(free) < req.whole:
             return None
         per = req.hbm_gib / max(req.whole, 1)

@@ -10,6 +10,8 @@ pkg/prom/fetch_prom_metrics/prom_metrics.go:63-70) and exports nothing of its ow
   amd_gpu_temperature_hotspot                 (C,  DCGM_FI_DEV_GPU_TEMP)
   amd_gpu_vram_used_mb / amd_gpu_vram_free_mb (MB, DCGM_FI_DEV_FB_USED / _FREE)
   amd_gpu_power_watts, amd_gpu_xgmi_{tx,rx}_bytes (rate, B/s)
+  amd_gpu_ecc_uncorrectable_total, amd_gpu_ecc_correctable_total (accumulated counts)
+  amd_gpu_healthy                             (1/0, the agent's health verdict, agent/health.py)
 
 optionally the same values under the DCGM names (`dcgm_compat=True`), and scheduler
 series: pods scheduled, scheduling latency histogram, SLO attainment, per-extension-point
@@ -42,6 +44,10 @@ class GpuExporter:
         self.slo = Gauge("gpusched_slo_attainment", "fraction of pods meeting their SLO", registry=self.registry)
         self.ext = Gauge("gpusched_extension_point_mean_us", "mean latency per extension point", ["point"],
                          registry=self.registry)
+        self.ecc = {k: Gauge(f"amd_gpu_ecc_{k}_total", f"accumulated {k} ECC errors", lab, registry=self.registry)
+                    for k in ("uncorrectable", "correctable")}
+        self.healthy = Gauge("amd_gpu_healthy", "1 if the node agent considers the device healthy", lab,
+                             registry=self.registry)
 
     def observe_samples(self, samples: Iterable[Dict[str, float]], uuids: Dict[int, str]) -> None:
         for s in samples:
@@ -59,9 +65,17 @@ class GpuExporter:
                     "amd_gpu_xgmi_rx_bytes": float(s.get("xgmi_read_bps", 0.0))}
             for m, v in vals.items():
                 self.g[m].labels(*lv).set(v)
+            for k, gauge in self.ecc.items():
+                v = float(s.get(f"ecc_{k}", -1))
+                if v >= 0:
+                    gauge.labels(*lv).set(v)
             if self.dcgm:
                 for dm, am in C.DCGM_TO_AMD.items():
                     self.dcgm[dm].labels(*lv).set(vals[am])
+
+    def observe_health(self, healthy: Dict[int, bool], uuids: Dict[int, str]) -> None:
+        for idx, ok in healthy.items():
+            self.healthy.labels(str(idx), uuids.get(idx, ""), self.node, self.pod).set(1.0 if ok else 0.0)
 
     def observe_scheduler(self, scheduled: int = 0, failed: int = 0, latencies=(), slo: Optional[float] = None,
                           ext: Optional[Dict[str, Dict[str, float]]] = None) -> None:

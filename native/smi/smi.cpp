@@ -39,6 +39,10 @@ struct Sample {
   double power_w = -1, temp_c = -1;
   double xgmi_read_kb = 0, xgmi_write_kb = 0;       // accumulators (sum over links)
   double xgmi_read_bps = 0, xgmi_write_bps = 0;     // rates since previous sample
+  // accumulated ECC error counts (-1 = not reported by this device/driver); the node
+  // agent's health monitor marks a GPU unhealthy when the uncorrectable count grows
+  double ecc_correctable = -1, ecc_uncorrectable = -1, ecc_deferred = -1;
+  bool responsive = false;                          // the activity/VRAM queries answered
 };
 
 const char* status_str(amdsmi_status_t s) {
@@ -133,11 +137,19 @@ class Smi {
       s.gfx = u.gfx_activity;
       s.umc = u.umc_activity;
       s.mm = u.mm_activity;
+      s.responsive = true;
     }
     amdsmi_vram_usage_t v;
     if (amdsmi_get_gpu_vram_usage(h, &v) == AMDSMI_STATUS_SUCCESS) {
       s.vram_used_mb = v.vram_used;
       s.vram_total_mb = v.vram_total;
+      s.responsive = true;
+    }
+    amdsmi_error_count_t ec;
+    if (amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS) {
+      s.ecc_correctable = static_cast<double>(ec.correctable_count);
+      s.ecc_uncorrectable = static_cast<double>(ec.uncorrectable_count);
+      s.ecc_deferred = static_cast<double>(ec.deferred_count);
     }
     amdsmi_power_info_t p;
     if (amdsmi_get_power_info(h, &p) == AMDSMI_STATUS_SUCCESS)
@@ -276,6 +288,10 @@ py::dict to_dict(const Sample& s) {
   d["temp_c"] = s.temp_c;
   d["xgmi_read_bps"] = s.xgmi_read_bps;
   d["xgmi_write_bps"] = s.xgmi_write_bps;
+  d["ecc_correctable"] = s.ecc_correctable;
+  d["ecc_uncorrectable"] = s.ecc_uncorrectable;
+  d["ecc_deferred"] = s.ecc_deferred;
+  d["responsive"] = s.responsive;
   return d;
 }
 

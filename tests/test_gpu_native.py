@@ -209,6 +209,13 @@ def test_peer_matrix_and_smi():
     assert s.count() >= 1
     samples = s.sample()
     assert samples and samples[0]["vram_total_mb"] > 0
+    # health inputs: the device answers; ECC counts are reported (or -1 if unsupported)
+    assert samples[0]["responsive"] is True
+    assert all(samples[0][k] >= -1 for k in ("ecc_correctable", "ecc_uncorrectable", "ecc_deferred"))
+    from k8s_gpu_scheduler_amd.agent.health import HealthMonitor
+    hm = HealthMonitor()
+    hm.update(samples, [{"uuid": f"dev{i}"} for i in range(len(samples))])
+    assert hm.unhealthy() == {}, hm.unhealthy()         # a working box is healthy
     topo = s.topology()
     assert topo["n"] == s.count()
     s.shutdown()
