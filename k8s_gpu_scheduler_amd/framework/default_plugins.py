@@ -277,10 +277,11 @@ class DefaultBinder(BindPlugin):
 
 def default_registry() -> Registry:
     from .placement_plugins import InterPodAffinity, NodePorts, PodTopologySpread
+    from .coscheduling import Coscheduling
     from .preemption import DefaultPreemption
     r = Registry()
     for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
                 NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption,
-                NodePorts, InterPodAffinity, PodTopologySpread):
+                NodePorts, InterPodAffinity, PodTopologySpread, Coscheduling):
         r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
     return r

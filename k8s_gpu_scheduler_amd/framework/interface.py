@@ -50,6 +50,10 @@ class Status:
     def skip(cls) -> "Status":
         return cls(Code.SKIP)
 
+    @classmethod
+    def wait(cls, msg: str = "") -> "Status":
+        return cls(Code.WAIT, [msg] if msg else [])
+
     @property
     def ok(self) -> bool:
         return self.code == Code.SUCCESS

@@ -267,17 +267,23 @@ class Framework:
                 log.warning("unreserve %s failed: %s", p.name(), e)
 
     def run_permit(self, state: CycleState, pod: Obj, node: str) -> Tuple[Status, float]:
+        """Upstream semantics: any rejection wins; otherwise, if some plugins asked to wait,
+        the pod becomes a waiting pod until each of them allows it (handle.allow) or the
+        longest of their timeouts passes; their names are left in the cycle state."""
         wait = 0.0
+        waiting: List[str] = []
         for p in self.points["permit"]:
             s, timeout = p.permit(state, pod, node)
             s = as_status(s)
             if s.code == Code.WAIT:
                 wait = max(wait, timeout)
+                waiting.append(p.name())
                 continue
             if not s.ok:
                 s.plugin = s.plugin or p.name()
                 return s, 0.0
-        return (Status(Code.WAIT) if wait else Status.success()), wait
+        state.write("framework/permit-waiting", waiting)
+        return (Status(Code.WAIT) if waiting else Status.success()), wait
 
     def run_pre_bind(self, state: CycleState, pod: Obj, node: str) -> Status:
         for p in self.points["preBind"]:

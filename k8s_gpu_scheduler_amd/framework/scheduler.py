@@ -80,6 +80,32 @@ class Handle:
     def framework_for(self, pod: Obj) -> Optional["Framework"]:
         return self._s.frameworks.get(O.scheduler_name(pod))
 
+    # waiting pods (Permit -> WAIT), upstream framework.Handle's WaitingPod API
+    def get_waiting_pod(self, pod_key: str) -> Optional["WaitingPod"]:
+        return self._s.waiting_pods().get(pod_key)
+
+    def iterate_over_waiting_pods(self) -> List["WaitingPod"]:
+        return list(self._s.waiting_pods().values())
+
+    def allow(self, pod_key: str, plugin: str) -> bool:
+        return self._s.allow_waiting(pod_key, plugin)
+
+    def reject(self, pod_key: str, plugin: str, message: str) -> bool:
+        return self._s.reject_waiting(pod_key, plugin, message)
+
+
+@dataclass
+class WaitingPod:
+    """A reserved pod held at Permit until every waiting plugin allows it (then its binding
+    cycle runs) or one rejects it / the deadline passes (then it is unreserved and
+    requeued).  `ctx` = (framework, state, queued pod info, host, result, t0)."""
+    key: str
+    pod: Obj
+    node: str
+    pending: set
+    deadline: float
+    ctx: tuple = ()
+
 
 class Scheduler:
     def __init__(self, client: KubeClient, config: SchedulerConfig, registry: Registry,
@@ -114,6 +140,8 @@ class Scheduler:
         self._pending_binds = 0
         self._bind_cv = threading.Condition()
         self._started = False
+        self._waiting: Dict[str, WaitingPod] = {}
+        self._waiting_lock = threading.RLock()
 
     @staticmethod
     def _queue_less(fw: Framework):
@@ -258,13 +286,67 @@ class Scheduler:
             return self._fail(pi, fw, state, res, st, t0)
         res.node = host
         self._snapshot = None
+        if st.code == Code.WAIT:
+            pending = set(state.read("framework/permit-waiting") or [])
+            key = O.key(pod)
+            wp = WaitingPod(key, pod, host, pending, time.monotonic() + max(0.0, wait),
+                            (fw, state, pi, host, res, t0))
+            with self._waiting_lock:
+                self._waiting[key] = wp
+            res.status = Status(Code.WAIT, ["waiting on permit: " + ",".join(sorted(pending))])
+            return res
+        self._start_binding(fw, state, pi, host, res, t0)
+        return res
+
+    # ---------------------------------------------------------------- waiting pods
+    def waiting_pods(self) -> Dict[str, WaitingPod]:
+        with self._waiting_lock:
+            return dict(self._waiting)
+
+    def allow_waiting(self, pod_key: str, plugin: str) -> bool:
+        with self._waiting_lock:
+            wp = self._waiting.get(pod_key)
+            if wp is None:
+                return False
+            wp.pending.discard(plugin)
+            if wp.pending:
+                return True
+            del self._waiting[pod_key]
+        fw, state, pi, host, res, t0 = wp.ctx
+        res.status = Status.success()
+        self._start_binding(fw, state, pi, host, res, t0)
+        return True
+
+    def reject_waiting(self, pod_key: str, plugin: str, message: str) -> bool:
+        with self._waiting_lock:
+            wp = self._waiting.pop(pod_key, None)
+        if wp is None:
+            return False
+        fw, state, pi, host, res, t0 = wp.ctx
+        fw.run_unreserve(state, wp.pod, host)
+        self.cache.forget_pod(wp.pod)
+        res.node = ""
+        st = Status.unschedulable(f"rejected at permit by {plugin}: {message}", plugin)
+        self._fail(pi, fw, state, res, st, t0)
+        return True
+
+    def expire_waiting(self) -> int:
+        """Reject waiting pods whose permit deadline passed (called by the loops)."""
+        now = time.monotonic()
+        with self._waiting_lock:
+            late = [wp for wp in self._waiting.values() if wp.deadline <= now]
+        for wp in late:
+            self.reject_waiting(wp.key, ",".join(sorted(wp.pending)) or "permit", "timed out waiting on permit")
+        return len(late)
+
+    def _start_binding(self, fw: Framework, state: CycleState, pi: QueuedPodInfo, host: str,
+                       res: ScheduleResult, t0: float) -> None:
         if self._bind_pool is not None:
             with self._bind_cv:
                 self._pending_binds += 1
             self._bind_pool.submit(self._binding_cycle, fw, state, pi, host, res, t0)
         else:
             self._binding_cycle(fw, state, pi, host, res, t0)
-        return res
 
     def _binding_cycle(self, fw: Framework, state: CycleState, pi: QueuedPodInfo, host: str,
                        res: ScheduleResult, t0: float) -> None:
@@ -329,6 +411,8 @@ class Scheduler:
         """Drain the active queue synchronously (tests / bench)."""
         out = []
         while max_pods is None or len(out) < max_pods:
+            if self._waiting:
+                self.expire_waiting()
             pi = self.queue.pop(timeout_s)
             if pi is None:
                 break
@@ -350,6 +434,8 @@ class Scheduler:
         last_cleanup = time.monotonic()
         while not self._stop.is_set():
             pi = self.queue.pop(0.2)
+            if self._waiting:
+                self.expire_waiting()
             if time.monotonic() - last_cleanup > 1.0:
                 self.cache.cleanup_expired()
                 last_cleanup = time.monotonic()
