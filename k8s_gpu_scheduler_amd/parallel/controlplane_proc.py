@@ -60,7 +60,15 @@ class ControlPlaneProc:
 
     def get_schedule(self) -> np.ndarray:
         while True:
-            msg = self._conn.recv()
+            # never block forever on a dead child: torchrun then tears the job down
+            # instead of every rank hanging at the next placement broadcast
+            while not self._conn.poll(1.0):
+                if not self._p.is_alive():
+                    raise RuntimeError(f"control-plane process exited (code {self._p.exitcode})")
+            try:
+                msg = self._conn.recv()
+            except (EOFError, OSError) as e:
+                raise RuntimeError(f"control-plane process connection lost: {e}") from e
             if msg[0] == "placements":
                 self._outstanding -= 1
                 _, arr, self.sched_s, self.unscheduled = msg

@@ -55,3 +55,22 @@ def test_resize_loop_clears_backlog_sim():
     assert on["created"] == off["created"]
     assert on["completed"] > off["completed"] and on["final_backlog"] < off["final_backlog"]
     assert on["mean_cu_request_placed"] < 128 and on["admission"]["resized"] > 0
+
+
+def test_dead_control_plane_raises_instead_of_hanging():
+    """A crashed control-plane process must fail the bench (torchrun then stops every
+    rank), never leave rank 0 blocked at the next schedule forever."""
+    from k8s_gpu_scheduler_amd.parallel.controlplane_proc import ControlPlaneProc
+    cp = ControlPlaneProc(n_gpus=1, pods_per_gpu=2, iters=2, seed=0)
+    try:
+        assert cp.schedule_epoch().shape == (2, 7)
+        cp.request_schedule()
+        cp._p.kill()
+        cp._p.join()
+        with pytest.raises((RuntimeError, OSError)):
+            cp.get_schedule()
+        with pytest.raises((RuntimeError, OSError)):
+            cp.schedule_epoch()
+    finally:
+        cp._outstanding = 0
+        cp.close()
