@@ -72,12 +72,19 @@ class NodeAgent:
         # default, as with Kubernetes device plugins
         self.evict_unhealthy = evict_unhealthy
         self.evicted: List[str] = []
+        self.on_inventory_change: List[Callable[[], None]] = []    # e.g. the device plugin's changed()
 
     # ------------------------------------------------------------------ publish
-    def publish(self, force: bool = False) -> bool:
+    def inventory(self) -> List[Dict[str, Any]]:
+        """Device descriptors with the current health verdicts (what publish() writes and
+        what the kubelet device plugin advertises)."""
         devs = self.source.devices()
         for d in devs:
             d["healthy"] = self.health.healthy(d["uuid"])
+        return devs
+
+    def publish(self, force: bool = False) -> bool:
+        devs = self.inventory()
         uuids = [d["uuid"] for d in devs]
         if not force and uuids == self.prev_uuids:
             return False
@@ -88,6 +95,11 @@ class NodeAgent:
             self.redis.set(schema.topology_key(self.node), json.dumps(topo, separators=(",", ":")))
         self.prev_uuids = uuids
         self.publishes += 1
+        for cb in self.on_inventory_change:
+            try:
+                cb()
+            except Exception as e:
+                log.warning("inventory-change callback failed: %s", e)
         log.info("published %d devices for %s", len(uuids), self.node)
         return True
 

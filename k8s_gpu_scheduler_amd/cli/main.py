@@ -177,9 +177,19 @@ def cmd_agent(args) -> int:
     exp = GpuExporter(node, os.getenv("POD_NAME", "amd-gpu-exporter"), dcgm_compat=args.dcgm_compat)
     if args.metrics_port:
         exp.serve(args.metrics_port)
-    agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp)
+    agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy)
+    mgr = None
+    if args.device_plugin:
+        # kubelet device plugin for amd.com/gpu, amd.com/gpu-cu, amd.com/gpu-memory
+        from ..agent.deviceplugin import DevicePluginManager
+        agent.publish(force=True)
+        mgr = DevicePluginManager(node, agent.inventory, client=client, plugin_dir=args.device_plugin_dir).start()
+        agent.on_inventory_change.append(mgr.changed)
+        threading.Thread(target=mgr.run_forever, name="device-plugin", daemon=True).start()
     if args.once:
         agent.step()
+        if mgr is not None:
+            mgr.stop()
         return 0
     agent.run()
     return 0
@@ -299,6 +309,11 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--dcgm-compat", action="store_true")
     s.add_argument("--synthetic", type=int, default=0, help="fake N GPUs (no hardware)")
     s.add_argument("--once", action="store_true")
+    s.add_argument("--device-plugin", action="store_true",
+                   help="also serve the kubelet device plugin (amd.com/gpu, gpu-cu, gpu-memory)")
+    s.add_argument("--device-plugin-dir", default="/var/lib/kubelet/device-plugins")
+    s.add_argument("--evict-unhealthy", action="store_true",
+                   help="delete pods assigned to a GPU that turns unhealthy (controllers reschedule them)")
     s.set_defaults(fn=cmd_agent)
     s = sub.add_parser("redisctl")
     s.add_argument("-l", "--list", action="store_true", help="List redis' data")

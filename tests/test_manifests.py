@@ -94,3 +94,14 @@ def test_busybox_fixture_matches_reference_shape():
     c = spec["containers"][0]
     assert any(e["name"] == "SLO" for e in c.get("env", []))
     assert any("configMapRef" in ef for ef in c.get("envFrom", []))
+
+
+def test_agent_daemonset_serves_the_device_plugin():
+    ds = next(d for _, d in _docs() if d.get("kind") == "DaemonSet")
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+    assert "--device-plugin" in c["args"]
+    assert any(m["mountPath"] == "/var/lib/kubelet/device-plugins" for m in c["volumeMounts"])
+    rules = [r for f, d in _docs() if f.startswith("profiler") and d.get("kind") == "ClusterRole"
+             for r in d["rules"]]
+    pod_verbs = {v for r in rules if "pods" in r["resources"] for v in r["verbs"]}
+    assert {"patch", "delete", "list"} <= pod_verbs
