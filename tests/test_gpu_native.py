@@ -341,3 +341,27 @@ def test_profiled_pod_writes_rocprof_history():
     (h,) = hist.read("onnx_resnet50_1024")
     assert h["gpu_busy_ms"] > 0 and h["kernels"] >= 60, h
     assert any("gemm_bf16" in k["name"] for k in h["top"]), h["top"]
+
+
+def test_device_plugin_allocates_real_device_nodes():
+    """Device plugin on the real inventory (amd-smi / HIP): every advertised GPU resolves to
+    its own /dev/dri/renderD* through sysfs, and Allocate hands a container /dev/kfd plus
+    that node."""
+    import os
+    from k8s_gpu_scheduler_amd.agent import deviceplugin as dp
+    from k8s_gpu_scheduler_amd.agent.devices import best_source
+    inv = best_source().devices()
+    assert inv, "no devices enumerated"
+    for d in inv:
+        d["healthy"] = True
+    nodes = [dp.render_nodes(str(d.get("bdf", ""))) for d in inv]
+    assert all(n and all(os.path.exists(p) for p in n) for n in nodes), nodes
+    if all(d.get("bdf") for d in inv):
+        assert all(len(n) == 1 for n in nodes) and len({n[0] for n in nodes}) == len(nodes)
+    plugin = dp.DevicePlugin("amd.com/gpu", "box", lambda: inv)
+    req = dp.AllocateRequest()
+    req.container_requests.add(devices_ids=[inv[0]["uuid"]])
+    resp = plugin.Allocate(req, None).container_responses[0]
+    paths = [x.host_path for x in resp.devices]
+    assert paths[0] == "/dev/kfd" and nodes[0][0] in paths
+    assert resp.envs["ROCR_VISIBLE_DEVICES"] == inv[0]["uuid"]
