@@ -141,6 +141,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self._col_memo: Dict[str, Optional[str]] = {}
         self._cands_memo: Dict[str, Tuple[Any, List[Tuple[DeviceState, int]]]] = {}
         self._score_memo: Dict[str, Tuple[Any, Optional[Choice]]] = {}
+        self._col_cache: Dict[Tuple[int, int], str] = {}
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)
         self._client: Optional[RecommenderClient] = None
@@ -519,8 +520,11 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
 
     # ------------------------------------------------------------------ device choice
     def _col(self, units: int, dev_units: int) -> str:
-        p = max(1, dev_units // max(units, 1))
-        return f"{p}P_{self.args.model}"
+        k = (units, dev_units)
+        c = self._col_cache.get(k)
+        if c is None:
+            c = self._col_cache[k] = f"{max(1, dev_units // max(units, 1))}P_{self.args.model}"
+        return c
 
     def _workload_col(self, name: str, intf: Dict[str, float]) -> Optional[str]:
         hit = self._col_memo.get(name, False)
@@ -631,46 +635,53 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                     d["_slo"] = (ver, summ)
                 slo_scores[i] = fast_device_score(summ, name, x_col, req.slo,
                                                   conf.get(self._col(req.units, st.device.units), -1.0), intf)
-        best: Optional[Choice] = None
         if a.pack == "random":
             st, u0 = cands[self._rng.randrange(len(cands))]
             return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], 50.0, [st.device])
-        gpu_fill: Optional[Dict[int, List[int]]] = None
+        # per-GPU inputs once per call (a node has <= 8 GPUs; candidates share them)
+        fill: Dict[int, Tuple[int, int]] = {}
+        if a.w_pack:
+            for s2 in states:
+                t, u = fill.get(s2.device.gpu, (0, 0))
+                fill[s2.device.gpu] = (t + s2.device.units, u + s2.device.units - s2.free_units)
         loads: Optional[Dict[int, float]] = None
         top = 0.0
         if a.w_balance:
             loads = self.ledger.gpu_work(node)
             top = max(loads.values(), default=0.0) + work
+        samples = self.telemetry.node(node) if a.w_telemetry else {}
+        binpack = a.pack == "binpack"
+        hbm_mb = req.hbm_gib * 1024
+        best_i, best_sc = -1, 0.0
         for i, (st, u0) in enumerate(cands):
-            parts: List[Tuple[float, float]] = []
+            num = den = 0.0
             if slo_scores[i] is not None:
-                parts.append((a.w_slo, slo_scores[i]))
+                num += a.w_slo * slo_scores[i]
+                den += a.w_slo
+            g = st.device.gpu
             if a.w_pack:
-                if gpu_fill is None:
-                    gpu_fill = {}
-                    for s2 in states:
-                        t_u = gpu_fill.setdefault(s2.device.gpu, [0, 0])
-                        t_u[0] += s2.device.units
-                        t_u[1] += s2.device.units - s2.free_units
-                tot, used = gpu_fill[st.device.gpu]
+                tot, used = fill[g]
                 frac = (used + req.units) / max(tot, 1)
-                pk = 100.0 * frac if a.pack == "binpack" else 100.0 * (1.0 - frac)
-                parts.append((a.w_pack, pk))
+                num += a.w_pack * (100.0 * frac if binpack else 100.0 * (1.0 - frac))
+                den += a.w_pack
             if loads is not None:
                 # 100 on the least-loaded GPU after placement relative to the node's
                 # busiest; equal loads (or no prediction) tie
-                bal = 100.0 * (1.0 - (loads.get(st.device.gpu, 0.0) + work) / top) if top > 0 else 100.0
-                parts.append((a.w_balance, bal))
-            if a.w_telemetry:
-                smp = self.telemetry.get(node, st.device.uuid)
+                num += a.w_balance * (100.0 * (1.0 - (loads.get(g, 0.0) + work) / top) if top > 0 else 100.0)
+                den += a.w_balance
+            if samples:
+                smp = samples.get(st.device.uuid)
                 if smp is not None:
-                    hbm_ok = 1.0 if smp.vram_total_mb - smp.vram_used_mb >= req.hbm_gib * 1024 else 0.0
-                    parts.append((a.w_telemetry, 100.0 * (1.0 - min(1.0, smp.gfx_activity)) * hbm_ok))
-            wsum = sum(w for w, _ in parts)
-            sc = sum(w * v for w, v in parts) / wsum if wsum > 0 else 0.0
-            if best is None or sc > best.score:
-                best = Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], sc, [st.device])
-        return best
+                    hbm_ok = 1.0 if smp.vram_total_mb - smp.vram_used_mb >= hbm_mb else 0.0
+                    num += a.w_telemetry * 100.0 * (1.0 - min(1.0, smp.gfx_activity)) * hbm_ok
+                    den += a.w_telemetry
+            sc = num / den if den > 0 else 0.0
+            if best_i < 0 or sc > best_sc:
+                best_i, best_sc = i, sc
+        if best_i < 0:
+            return None
+        st, u0 = cands[best_i]
+        return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], best_sc, [st.device])
 
     def _fits_without(self, req: GpuRequest, node: str, removed: Any) -> bool:
         """Would the request fit if the pods in `removed` released their devices?  Works on

@@ -12,7 +12,7 @@ from __future__ import annotations
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional
 
 
 @dataclass
@@ -35,14 +35,14 @@ class DeviceSample:
 class TelemetryCache:
     def __init__(self, stale_s: float = 10.0):
         self._lock = threading.Lock()
-        self._d: Dict[Tuple[str, str], DeviceSample] = {}
+        self._d: Dict[str, Dict[str, DeviceSample]] = {}      # node -> uuid -> latest sample
         self.stale_s = stale_s
         self.updates = 0
         self._node_ver: Dict[str, int] = {}
 
     def update(self, node: str, uuid: str, sample: DeviceSample) -> None:
         with self._lock:
-            self._d[(node, uuid)] = sample
+            self._d.setdefault(node, {})[uuid] = sample
             self.updates += 1
             self._node_ver[node] = self._node_ver.get(node, 0) + 1
 
@@ -53,13 +53,16 @@ class TelemetryCache:
 
     def get(self, node: str, uuid: str) -> Optional[DeviceSample]:
         with self._lock:
-            s = self._d.get((node, uuid))
+            s = self._d.get(node, {}).get(uuid)
         if s is None or (self.stale_s and time.monotonic() - s.ts > self.stale_s):
             return None
         return s
 
     def node(self, node: str) -> Dict[str, DeviceSample]:
-        now = time.monotonic()
+        """Fresh samples of one node, uuid -> sample (one lock, O(devices of the node))."""
         with self._lock:
-            return {u: s for (n, u), s in self._d.items()
-                    if n == node and (not self.stale_s or now - s.ts <= self.stale_s)}
+            d = dict(self._d.get(node, {}))
+        if not self.stale_s:
+            return d
+        now = time.monotonic()
+        return {u: s for u, s in d.items() if now - s.ts <= self.stale_s}
