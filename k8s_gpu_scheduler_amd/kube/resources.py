@@ -13,7 +13,10 @@ Same operations as the reference's `resources.Descriptor` and `PatchNodeParam`
 from __future__ import annotations
 
 import json
-from typing import Any, Dict, List, Optional
+import random
+import threading
+import time
+from typing import Any, Dict, List, Optional, Tuple
 
 from ..api import objects as O
 from .client import Conflict, KubeClient, NotFound
@@ -79,9 +82,19 @@ class Resources:
                                   self.namespace)
 
     def update_config_map(self, cm_name: str, data: Dict[str, str], overwrite: bool = True,
-                          retries: int = 5) -> Optional[Obj]:
-        """Merge `data` into a ConfigMap (reference pods.go:98-121); optimistic retries."""
-        for _ in range(retries):
+                          retries: int = 10) -> Optional[Obj]:
+        """Merge `data` into a ConfigMap (reference pods.go:98-121).  Writers in this
+        process are serialised per ConfigMap (concurrent binding cycles of pods that share
+        one -- the reference's busybox replicas share `game-demo`, SURVEY §2.9 #6 -- would
+        otherwise mostly conflict with each other); other writers are handled with
+        optimistic retries and a short jittered backoff."""
+        with _cm_lock(self.namespace, cm_name):
+            return self._update_config_map(cm_name, data, overwrite, retries)
+
+    def _update_config_map(self, cm_name: str, data: Dict[str, str], overwrite: bool, retries: int) -> Optional[Obj]:
+        for attempt in range(retries):
+            if attempt:
+                time.sleep(random.uniform(0.0, 0.002 * (2 ** min(attempt, 6))))
             try:
                 cm = self.client.get("configmaps", cm_name, self.namespace)
             except NotFound:
@@ -154,6 +167,18 @@ class Resources:
         node = self.client.get("nodes", node_name)
         taints = [t for t in O.node_taints(node) if t.get("key") != key]
         return self.client.patch("nodes", node_name, {"spec": {"taints": taints}}, "merge")
+
+
+_CM_LOCKS: Dict[Tuple[str, str], threading.Lock] = {}
+_CM_LOCKS_GUARD = threading.Lock()
+
+
+def _cm_lock(namespace: str, name: str) -> threading.Lock:
+    with _CM_LOCKS_GUARD:
+        lk = _CM_LOCKS.get((namespace, name))
+        if lk is None:
+            lk = _CM_LOCKS[(namespace, name)] = threading.Lock()
+        return lk
 
 
 def patch_payload(op: str, path: str, data: Dict[str, Any]) -> bytes:

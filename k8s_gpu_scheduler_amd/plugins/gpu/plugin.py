@@ -347,7 +347,6 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         node_gen, smemo, tele = self.ledger.node_gen, self._score_memo, self.telemetry
         use_t, stale = bool(self.args.w_telemetry), tele.stale_s
         for nn in names:
-            choice = None
             hit = smemo.get(nn) if sig is not None else None
             if hit is not None:         # inline memo hit of _best_choice(scoring=True)
                 tv = tele.node_version(nn) if use_t else 0

@@ -175,3 +175,39 @@ def test_concurrent_configmap_updates_retry():
     [t.join() for t in ts]
     assert not errs
     assert len(fc.get("configmaps", "cm", "default")["data"]) == 80
+
+
+def test_shared_configmap_writers_over_http_never_give_up():
+    """16 concurrent binding-cycle-like writers over the REST client (HTTP fake apiserver)
+    on one shared ConfigMap -- the reference's busybox replicas sharing `game-demo` -- plus
+    an out-of-process-style writer bypassing the in-process lock: every update lands."""
+    from k8s_gpu_scheduler_amd.kube.fake_apiserver import FakeApiServer
+    from k8s_gpu_scheduler_amd.kube.rest import RestClient, RestConfig
+    fc = FakeCluster()
+    fc.create("configmaps", O.make_config_map("game-demo"))
+    srv = FakeApiServer(fc).start()
+    try:
+        rc = RestClient(RestConfig(srv.url))
+        r = Resources(rc, "default")
+        errs = []
+
+        def worker(i):
+            try:
+                for j in range(5):
+                    r.update_config_map("game-demo", {f"pod{i}-{j}": "GPU-x"})
+            except Exception as e:
+                errs.append(e)
+
+        def rogue():                        # another process's writer: optimistic retries only
+            try:
+                for j in range(10):
+                    r._update_config_map("game-demo", {f"rogue-{j}": "1"}, True, 10)
+            except Exception as e:
+                errs.append(e)
+        ts = [threading.Thread(target=worker, args=(i,)) for i in range(16)] + [threading.Thread(target=rogue)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert not errs, errs[:3]
+        assert len(fc.get("configmaps", "game-demo", "default")["data"]) == 16 * 5 + 10
+    finally:
+        srv.stop()

@@ -110,6 +110,14 @@ def main() -> int:
             p = pods.get(n, {})
             ann = O.annotations(p)
             print(f"{n:40s} {O.node_name_of(p) or '-':18s} {ann.get(C.ANNOT_DEVICES, '')[:60]} {ann.get(C.ANNOT_CU_MASK, '')}")
+        unbound = [n for n in names if not O.node_name_of(pods.get(n, {}))]
+        if unbound:                      # why: the scheduler's FailedScheduling events
+            try:
+                for ev in client.list("events", "default")[0]:
+                    if ev.get("involvedObject", {}).get("name") in unbound:
+                        print(f"event {ev['involvedObject']['name']}: {ev.get('reason')}: {ev.get('message')}")
+            except Exception as e:
+                print(f"(events unavailable: {e})")
         print(json.dumps({"bound": sum(1 for n in names if O.node_name_of(pods.get(n, {}))), "pods": len(names),
                           "seconds": round(time.time() - t0, 2)}))
         print(f"component logs: {LOGDIR}")
