@@ -471,14 +471,14 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
     def _sort_key(self, pi: Any) -> Tuple[int, int, float, float]:
         d = pi.__dict__
         hit = d.get("_gpu_sort")
-        if hit is not None and hit[0] is pi.pod:
+        if hit is not None and hit[0] is pi.pod and hit[2] == pi.timestamp:
             return hit[1]
         pod = pi.pod
         w = self.args.lpt_window_s
         window = int(pi.timestamp // w) if w > 0 else 0
         work = self.pod_work(pod, self._pod_predictions(O.name(pod))[0]) if w > 0 else 0.0
         key = (-O.priority(pod), window, -work, pi.timestamp)
-        d["_gpu_sort"] = (pod, key)
+        d["_gpu_sort"] = (pod, key, pi.timestamp)    # requeueing restamps the pod: recompute
         return key
 
     def pod_work(self, pod: Obj, conf: Dict[str, float]) -> float:

@@ -231,3 +231,12 @@ def test_batch_filter_and_score_match_node_at_a_time():
                     if name != "GPU":                # GPU's list is normalized in place
                         assert raw == vals, name
     assert {"TaintToleration", "NodeResourcesFit", "NodeAffinity", "NodeUnschedulable"} <= seen_plugins, seen_plugins
+
+
+def test_lpt_sort_key_follows_requeue_timestamp():
+    p = GPUPlugin({"lpt_window_s": 1.0}, None, predictions=_Pred())
+    a = QueuedPodInfo(_pod("big-a"), timestamp=10.0)
+    b = QueuedPodInfo(_pod("small-b"), timestamp=20.0)
+    assert p.less(a, b)
+    a.timestamp = 30.0                       # a was requeued after b arrived
+    assert p.less(b, a)
