@@ -11,6 +11,7 @@ Protocol (multiprocessing Pipe, in order):
                                   epoch, reply ("placements", arr, sched_s, unscheduled)
   ("telemetry", per_gpu, ms)   -> child: update the TelemetryCache (no reply)
   ("reset_stats",)             -> child: zero sched_s / unscheduled counters
+  ("interference_mae",)        -> child: reply ("interference_mae", online-model error summary)
   ("stop",)                    -> child exits
 """
 from __future__ import annotations
@@ -36,6 +37,8 @@ def _serve(conn: Any, kwargs: dict) -> None:
         elif kind == "reset_stats":
             cp.sched_s = 0.0
             cp.unscheduled = 0
+        elif kind == "interference_mae":
+            conn.send(("interference_mae", cp.interference_mae()))
         elif kind == "stop":
             conn.close()
             return
@@ -83,6 +86,16 @@ class ControlPlaneProc:
 
     def reset_stats(self) -> None:
         self._conn.send(("reset_stats",))
+
+    def interference_mae(self):
+        while self._outstanding > 0:           # drain pending placements first
+            self.get_schedule()
+        self._conn.send(("interference_mae",))
+        while not self._conn.poll(1.0):
+            if not self._p.is_alive():
+                raise RuntimeError(f"control-plane process exited (code {self._p.exitcode})")
+        msg = self._conn.recv()
+        return msg[1] if msg[0] == "interference_mae" else None
 
     def close(self) -> None:
         try:

@@ -54,8 +54,14 @@ from ..telemetry.workcost import WorkCostModel
 
 NODE = "mi355x-node-0"
 FIELDS = 7    # gpu, first_unit, n_units, workload_id, iters, slo_milli, masked
-TELE = 4 + 2 * len(W.NAMES)   # busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods)
 UNITS_PER_GPU = 8
+MAX_PODS_GPU = 8              # per-pod co-run records per GPU and epoch
+COST0 = 4
+POD0 = COST0 + 2 * len(W.NAMES)
+# busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods), then per pod of
+# this GPU's epoch: (workload id or -1, achieved iterations/s) -- the co-run observations the
+# online interference model learns from
+TELE = POD0 + 2 * MAX_PODS_GPU
 
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
@@ -90,7 +96,7 @@ class ControlPlane:
 
     def __init__(self, n_gpus: int, pods_per_gpu: int, iters: int, seed: int, policy: str = "gpu",
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
-                 balance: float = 1.0):
+                 balance: float = 1.0, learn_interference: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -121,6 +127,17 @@ class ControlPlane:
         self.uuid_to_gpu = {d.device.uuid: d.device.gpu for d in self.ledger.devices(NODE)}
         conf = self.predictions._conf
         self.quarter_tput = {n: conf.by_label[n][f"{C.MI355X_CUS // cu_per_pod}P_{C.MI355X}"] for n in W.NAMES}
+        self.online = None
+        if learn_interference and self.predictions._intf is not None:
+            from ..recommender.online import OnlineInterference
+            from ..recommender.tables import find_index_for_request
+            tab = self.predictions._intf
+            rows = [find_index_for_request(n, tab.index) for n in W.NAMES]
+            cols = [next((c for c in tab.columns if c == n), None) for n in W.NAMES]
+            if all(rows) and all(cols):
+                prior = np.array([[tab.by_label[r][c] for c in cols] for r in rows], dtype=np.float64)
+                self.online = OnlineInterference(W.NAMES, W.NAMES, prior)
+                self._online_rows = rows
         self.epoch = 0
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -190,15 +207,38 @@ class ControlPlane:
             except Exception:
                 pass
 
+    def _learn_interference(self, pods: np.ndarray) -> None:
+        """pods[g] = MAX_PODS_GPU x (workload id, achieved iterations/s) of GPU g's epoch:
+        each pod's loss against its predicted alone-throughput at its share is one
+        observation of the additive interference model (recommender.online)."""
+        refit = False
+        for g in range(pods.shape[0]):
+            rec = pods[g].reshape(MAX_PODS_GPU, 2)
+            wids = [int(w) for w, _ in rec if w >= 0]
+            for i, (w, tput) in enumerate(rec):
+                if w < 0:
+                    continue
+                w = int(w)
+                others = wids[:i] + wids[i + 1:]
+                refit |= self.online.observe(w, others, self.quarter_tput[W.NAMES[w]] - float(tput))
+        if refit:       # serve the refitted table to the scheduler (next cycles' predictions)
+            self.predictions.install_interference(self._online_rows, W.NAMES, self.online.rows(),
+                                                  f"online-{self.online.version}")
+
+    def interference_mae(self) -> Optional[Dict[str, Any]]:
+        return self.online.mae() if self.online is not None else None
+
     def update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
         """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib[, per-workload
         (sum of observed GPU-seconds per iteration, pods) x len(W.NAMES)])."""
         per_gpu = np.asarray(per_gpu, dtype=np.float64)
         if per_gpu.shape[1] >= TELE:
-            cost = per_gpu[:, 4:TELE].sum(axis=0).reshape(len(W.NAMES), 2)
+            cost = per_gpu[:, COST0:POD0].sum(axis=0).reshape(len(W.NAMES), 2)
             for wid, (tot, n) in enumerate(cost):
                 if n > 0:
                     self.workcost.observe(W.NAMES[wid], float(tot / n), int(n))
+            if self.online is not None:
+                self._learn_interference(per_gpu[:, POD0:TELE])
         for st in self.ledger.devices(NODE):
             g = st.device.gpu
             if g >= len(per_gpu):
@@ -270,6 +310,15 @@ class SimExecutor:
 
     def close(self) -> None:
         pass
+
+
+def _pod_rows(runs: List[Any]) -> List[float]:
+    """(workload id, achieved iterations/s) of up to MAX_PODS_GPU pods of one GPU's epoch;
+    (-1, 0) pads."""
+    out: List[float] = []
+    for r in runs[:MAX_PODS_GPU]:
+        out += [float(W.INDEX[r.workload]), float(r.throughput)]
+    return out + [-1.0, 0.0] * (MAX_PODS_GPU - min(len(runs), MAX_PODS_GPU))
 
 
 def _cost_rows(runs: List[Any]) -> np.ndarray:
@@ -435,7 +484,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     intervals.append((ref["ev"].elapsed_time(r.start), ref["ev"].elapsed_time(r.end)))
         st = ex.collect(runs)
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
-        vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm] + _cost_rows(runs).ravel().tolist()
+        vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm] + _cost_rows(runs).ravel().tolist() + \
+            _pod_rows(runs)
         if world > 1:
             with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
                 tele.copy_(torch.tensor(vec, dtype=torch.float64))
@@ -448,7 +498,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                 g = int(arr[r.pod_id][0])
                 per_gpu[g, :4] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
                                    W.CATALOG[r.workload].hbm_gib)
-                per_gpu[g, 4:] += _cost_rows([r]).ravel()
+                per_gpu[g, COST0:POD0] += _cost_rows([r]).ravel()
+            for g in range(n_gpus):
+                per_gpu[g, POD0:] = _pod_rows([r for r in runs if int(arr[r.pod_id][0]) == g])
         else:
             per_gpu = np.asarray(vec, dtype=np.float64)[None, :]
         if rank == 0:
@@ -553,6 +605,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "achieved_tflops": round(flops_tot / elapsed / 1e12, 1),
             "slo_attainment_pct": round(100.0 * totals["slo_ok"] / max(totals["pods"], 1), 2),
             "sched_ms_per_pod": round(cp.sched_s / max(totals["pods"], 1) * 1e3, 4),
+            "interference_mae": cp.interference_mae(),
             "unscheduled": cp.unscheduled,
             "host_ms_per_step_rank0": {k: round(v / a.steps * 1e3, 3) for k, v in host.items()},
             "simulated": not use_gpu,

@@ -302,6 +302,13 @@ class DeviceLedger:
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
             return True
 
+    def invalidate_summaries(self) -> None:
+        """Drop every device's cached scoring summary (new prediction tables)."""
+        with self._lock:
+            for states in self.nodes.values():
+                for st in states.values():
+                    st.__dict__.pop("_slo", None)
+
     def gpu_work(self, node: str) -> Dict[int, float]:
         """Predicted GPU time of the pods resident on each physical GPU of a node (its
         partitions / fractional shares summed)."""

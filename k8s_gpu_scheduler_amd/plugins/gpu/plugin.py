@@ -142,6 +142,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self._cands_memo: Dict[str, Tuple[Any, List[Tuple[DeviceState, int]]]] = {}
         self._score_memo: Dict[str, Tuple[Any, Optional[Choice]]] = {}
         self._col_cache: Dict[Tuple[int, int], str] = {}
+        self._pred_version: Any = None
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)
         self._client: Optional[RecommenderClient] = None
@@ -501,7 +502,15 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
     def _pod_predictions(self, name: str) -> Tuple[Dict[str, float], Dict[str, float]]:
         if self.predictions is None:
             return {}, {}
+        ver_fn = getattr(self.predictions, "version", None)
+        ver = ver_fn() if ver_fn is not None else None
         with self._lock:
+            if ver != self._pred_version:       # a new model version: forget memoised lookups
+                self._pred_version = ver
+                self._resident_memo.clear()
+                self._col_memo.clear()
+                self._score_memo.clear()
+                self.ledger.invalidate_summaries()
             hit = self._resident_memo.get(name)
         if hit is not None:
             return hit

@@ -185,3 +185,14 @@ class CachedPredictions(PredictionProvider):
 
     def tables(self) -> "tuple[Optional[_Tab], Optional[_Tab]]":
         return self._conf, self._intf
+
+    def version(self) -> tuple:
+        """Changes whenever a new configurations / interference table is installed (callers
+        memoising per-pod lookups key their memo by it)."""
+        c, i = self._conf, self._intf
+        return (id(c), c.version if c else None, id(i), i.version if i else None)
+
+    def install_interference(self, index: List[str], columns: List[str], rows: List[List[float]],
+                             version: str) -> None:
+        """Swap in a new interference table (e.g. the online-learned one)."""
+        self._intf = _Tab(list(index), list(columns), rows, version)

@@ -1,0 +1,91 @@
+"""Pairwise interference learned online from what co-running pods actually achieved.
+
+The reference's interference matrix is measured offline and only re-read when its file
+changes (reference pkg/recommender/recom_server.py:74-134, interference_train.ods); its
+Score sums the matrix entries of a pod's co-residents to predict the throughput it loses
+(gpu_plugins.go:589-612).  Here the same additive model is *fitted* to live observations:
+a pod of workload `a` that achieved throughput `t` while sharing a GPU with pods of
+workloads `b_1..b_k` lost `loss = predicted_alone(a) - t`, modelled as
+`sum_j intf[a][b_j]`.  Each row `a` is a ridge regression over the 18 (or however many)
+co-runner columns, shrunk toward the prior (offline / imputed) row, so rows with few
+observations keep the measured table and well-observed rows follow the hardware.
+
+`prequential` error bookkeeping (predict each observation with the current model before
+learning from it) measures whether the online table predicts better than the prior.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+
+class OnlineInterference:
+    def __init__(self, labels: Sequence[str], columns: Sequence[str], prior: np.ndarray, lam: float = 4.0,
+                 refit_every: int = 32):
+        self.labels, self.columns = list(labels), list(columns)
+        w, c = len(self.labels), len(self.columns)
+        prior = np.asarray(prior, dtype=np.float64)
+        if prior.shape != (w, c):
+            raise ValueError(f"prior shape {prior.shape} != ({w}, {c})")
+        fill = np.nanmean(prior) if np.isfinite(prior).any() else 0.0
+        self.prior = np.where(np.isfinite(prior), prior, fill)
+        self.lam = lam
+        self.refit_every = refit_every
+        self._ata = np.zeros((w, c, c))
+        self._atb = np.zeros((w, c))
+        self._n = np.zeros(w, dtype=np.int64)
+        self.matrix = self.prior.copy()
+        self.version = 0
+        self._since = 0
+        self._lock = threading.Lock()
+        self.err = {"prior": 0.0, "online": 0.0, "n": 0}
+
+    def _x(self, others: Sequence[int]) -> np.ndarray:
+        return np.bincount(np.asarray(others, dtype=np.int64), minlength=len(self.columns)).astype(np.float64)
+
+    def predict_loss(self, a: int, others: Sequence[int], prior: bool = False) -> float:
+        m = self.prior if prior else self.matrix
+        return float(m[a] @ self._x(others)) if len(others) else 0.0
+
+    def observe(self, a: int, others: Sequence[int], loss: float) -> bool:
+        """Learn from one pod; returns True when the matrix was refitted."""
+        if not len(others) or not np.isfinite(loss):
+            return False
+        x = self._x(others)
+        with self._lock:
+            self.err["prior"] += abs(float(self.prior[a] @ x) - loss)
+            self.err["online"] += abs(float(self.matrix[a] @ x) - loss)
+            self.err["n"] += 1
+            self._ata[a] += np.outer(x, x)
+            self._atb[a] += x * loss
+            self._n[a] += 1
+            self._since += 1
+            if self._since >= self.refit_every:
+                self._refit()
+                return True
+        return False
+
+    def _refit(self) -> None:
+        eye = np.eye(len(self.columns))
+        m = self.matrix.copy()
+        for a in np.nonzero(self._n)[0]:
+            lhs = self._ata[a] + self.lam * eye
+            rhs = self._atb[a] + self.lam * self.prior[a]
+            m[a] = np.maximum(np.linalg.solve(lhs, rhs), 0.0)    # a co-runner never adds throughput
+        self.matrix = m
+        self.version += 1
+        self._since = 0
+
+    def refit(self) -> None:
+        with self._lock:
+            self._refit()
+
+    def mae(self) -> Dict[str, Optional[float]]:
+        n = self.err["n"]
+        return {"n": n, "prior": self.err["prior"] / n if n else None,
+                "online": self.err["online"] / n if n else None}
+
+    def rows(self) -> List[List[float]]:
+        return self.matrix.tolist()

@@ -270,3 +270,41 @@ def test_cached_predictions_survive_late_recommender_and_follow_new_versions(ref
         svc.stop()
         srv.stop(0)
         cl.close()
+
+
+def test_online_interference_learns_additive_model():
+    """recommender.online: ridge toward the prior, converging to the true additive matrix
+    from co-run observations; prequential error of the online model beats the prior."""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.recommender.online import OnlineInterference
+    rng = np.random.default_rng(0)
+    w = 6
+    true = rng.uniform(0, 100, (w, w))
+    prior = true + rng.normal(0, 40, (w, w))
+    prior[0, 0] = np.nan                                  # unmeasured entry: filled, not fatal
+    m = OnlineInterference([f"w{i}" for i in range(w)], [f"w{i}" for i in range(w)], prior, lam=2.0, refit_every=16)
+    assert np.isfinite(m.matrix).all()
+    # few observations: row stays near the prior
+    m.observe(1, [2, 3, 4], float(true[1, [2, 3, 4]].sum()))
+    m.refit()
+    assert abs(m.matrix[1, 5] - m.prior[1, 5]) < 1e-9   # column never seen -> prior kept
+    for _ in range(3000):
+        a = int(rng.integers(w))
+        others = [int(x) for x in rng.integers(0, w, 3)]
+        m.observe(a, others, float(true[a, others].sum() + rng.normal(0, 2)))
+    m.refit()
+    assert np.abs(m.matrix - true).max() < 5.0
+    e = m.mae()
+    assert e["n"] == 3001 and e["online"] < 0.5 * e["prior"]
+
+
+def test_plugin_forgets_memoised_predictions_on_new_table():
+    from k8s_gpu_scheduler_amd.plugins.gpu.plugin import GPUPlugin
+    from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, _Tab
+    cp = CachedPredictions()
+    cp._conf = _Tab(["wl_a"], ["1P_MI355X"], [[10.0]], "v1")
+    cp._intf = _Tab(["wl_a"], ["wl_a"], [[1.0]], "v1")
+    p = GPUPlugin({}, None, predictions=cp)
+    assert p._pod_predictions("wl-a-0")[1] == {"wl_a": 1.0}
+    cp.install_interference(["wl_a"], ["wl_a"], [[5.0]], "online-1")
+    assert p._pod_predictions("wl-a-0")[1] == {"wl_a": 5.0}
