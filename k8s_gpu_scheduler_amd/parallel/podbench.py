@@ -136,7 +136,9 @@ class ControlPlane:
             cols = [next((c for c in tab.columns if c == n), None) for n in W.NAMES]
             if all(rows) and all(cols):
                 prior = np.array([[tab.by_label[r][c] for c in cols] for r in rows], dtype=np.float64)
-                self.online = OnlineInterference(W.NAMES, W.NAMES, prior)
+                # refit about every 4 epochs (each refit re-summarises the scheduler's devices)
+                self.online = OnlineInterference(W.NAMES, W.NAMES, prior,
+                                                 refit_every=max(32, 4 * n_gpus * pods_per_gpu))
                 self._online_rows = rows
         self.epoch = 0
         self.live: List[Tuple[str, str]] = []

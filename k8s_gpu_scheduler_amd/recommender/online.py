@@ -38,36 +38,51 @@ class OnlineInterference:
         self._n = np.zeros(w, dtype=np.int64)
         self.matrix = self.prior.copy()
         self.version = 0
-        self._since = 0
+        self._pending: List[tuple] = []
         self._lock = threading.Lock()
         self.err = {"prior": 0.0, "online": 0.0, "n": 0}
 
-    def _x(self, others: Sequence[int]) -> np.ndarray:
-        return np.bincount(np.asarray(others, dtype=np.int64), minlength=len(self.columns)).astype(np.float64)
-
     def predict_loss(self, a: int, others: Sequence[int], prior: bool = False) -> float:
-        m = self.prior if prior else self.matrix
-        return float(m[a] @ self._x(others)) if len(others) else 0.0
+        row = (self.prior if prior else self.matrix)[a]
+        return float(sum(row[b] for b in others))
 
     def observe(self, a: int, others: Sequence[int], loss: float) -> bool:
-        """Learn from one pod; returns True when the matrix was refitted."""
+        """Learn from one pod; returns True when the matrix was refitted.  Observations are
+        queued and folded into the per-row normal equations in one vectorised pass at refit
+        time, so the per-pod cost is a few dict/array lookups."""
         if not len(others) or not np.isfinite(loss):
             return False
-        x = self._x(others)
+        pr, on = self.prior[a], self.matrix[a]
         with self._lock:
-            self.err["prior"] += abs(float(self.prior[a] @ x) - loss)
-            self.err["online"] += abs(float(self.matrix[a] @ x) - loss)
+            self.err["prior"] += abs(sum(pr[b] for b in others) - loss)
+            self.err["online"] += abs(sum(on[b] for b in others) - loss)
             self.err["n"] += 1
-            self._ata[a] += np.outer(x, x)
-            self._atb[a] += x * loss
-            self._n[a] += 1
-            self._since += 1
-            if self._since >= self.refit_every:
+            self._pending.append((a, tuple(others), loss))
+            if len(self._pending) >= self.refit_every:
                 self._refit()
                 return True
         return False
 
+    def _fold(self) -> None:
+        if not self._pending:
+            return
+        n, c = len(self._pending), len(self.columns)
+        rows = np.fromiter((p[0] for p in self._pending), dtype=np.int64, count=n)
+        y = np.fromiter((p[2] for p in self._pending), dtype=np.float64, count=n)
+        x = np.zeros((n, c))
+        for i, (_, others, _) in enumerate(self._pending):
+            for b in others:
+                x[i, b] += 1.0
+        for a in np.unique(rows):
+            sel = rows == a
+            xa = x[sel]
+            self._ata[a] += xa.T @ xa
+            self._atb[a] += xa.T @ y[sel]
+            self._n[a] += int(sel.sum())
+        self._pending.clear()
+
     def _refit(self) -> None:
+        self._fold()
         eye = np.eye(len(self.columns))
         m = self.matrix.copy()
         for a in np.nonzero(self._n)[0]:
@@ -76,7 +91,6 @@ class OnlineInterference:
             m[a] = np.maximum(np.linalg.solve(lhs, rhs), 0.0)    # a co-runner never adds throughput
         self.matrix = m
         self.version += 1
-        self._since = 0
 
     def refit(self) -> None:
         with self._lock:
