@@ -18,7 +18,7 @@ from __future__ import annotations
 import logging
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 import grpc
 
@@ -62,6 +62,13 @@ class RecommenderClient:
 
     def version(self) -> Any:
         return self._call(f"/{P.EXT_SERVICE}/Version", P.Empty())
+
+    def observe_interference(self, observations: List[Tuple[str, List[str], float]]) -> Any:
+        """Send (pod, co-runner pods, throughput loss) observations for online learning."""
+        req = P.ObserveRequest()
+        for pod, others, loss in observations:
+            req.observations.add(pod=pod, co_runners=list(others), loss=float(loss))
+        return self._call(f"/{P.EXT_SERVICE}/ObserveInterference", req)
 
     def close(self) -> None:
         with self._lock:

@@ -14,7 +14,8 @@ Wire-identical to the reference's proto (reference pkg/recommender/protos/recom.
 FileDescriptorProto is assembled here and message classes come from the descriptor pool.
 A second service, `gpusched.recommender.Extended`, adds what the MI355X build needs
 (bulk table export for the in-process prediction cache, resource-resize advice, model
-version) without touching the reference API.
+version, co-run observations for online interference learning) without touching the
+reference API.
 """
 from __future__ import annotations
 
@@ -75,6 +76,16 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
     _field(ver, "model", 3, _F.TYPE_STRING)
     emp = fx.message_type.add(name="Empty")
     del emp
+    cr = fx.message_type.add(name="CoRun")                # one pod's co-run observation
+    _field(cr, "pod", 1, _F.TYPE_STRING)                 # pod (or workload) name
+    _field(cr, "co_runners", 2, _F.TYPE_STRING, _F.LABEL_REPEATED)
+    _field(cr, "loss", 3, _F.TYPE_FLOAT)                 # predicted-alone minus achieved throughput
+    orq = fx.message_type.add(name="ObserveRequest")
+    _field(orq, "observations", 1, _F.TYPE_MESSAGE, _F.LABEL_REPEATED, ".gpusched.recommender.CoRun")
+    orp = fx.message_type.add(name="ObserveReply")
+    _field(orp, "accepted", 1, _F.TYPE_INT32)
+    _field(orp, "interference", 2, _F.TYPE_STRING)       # interference table version now served
+    _field(orp, "observations", 3, _F.TYPE_INT32)        # total learned so far
     s2 = fx.service.add(name="Extended")
     s2.method.add(name="ExportTable", input_type=".gpusched.recommender.TableRequest",
                   output_type=".gpusched.recommender.Table")
@@ -82,6 +93,8 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
                   output_type=".gpusched.recommender.ResizeReply")
     s2.method.add(name="Version", input_type=".gpusched.recommender.Empty",
                   output_type=".gpusched.recommender.VersionReply")
+    s2.method.add(name="ObserveInterference", input_type=".gpusched.recommender.ObserveRequest",
+                  output_type=".gpusched.recommender.ObserveReply")
     pool.Add(fx)
     return pool
 
@@ -102,6 +115,9 @@ ResizeRequest = _cls("gpusched.recommender.ResizeRequest")
 ResizeReply = _cls("gpusched.recommender.ResizeReply")
 VersionReply = _cls("gpusched.recommender.VersionReply")
 Empty = _cls("gpusched.recommender.Empty")
+CoRun = _cls("gpusched.recommender.CoRun")
+ObserveRequest = _cls("gpusched.recommender.ObserveRequest")
+ObserveReply = _cls("gpusched.recommender.ObserveReply")
 
 SERVICE = "recommender.recommender"
 EXT_SERVICE = "gpusched.recommender.Extended"
@@ -111,6 +127,7 @@ METHODS: Dict[str, Any] = {
     f"/{EXT_SERVICE}/ExportTable": (TableRequest, Table),
     f"/{EXT_SERVICE}/RecommendResources": (ResizeRequest, ResizeReply),
     f"/{EXT_SERVICE}/Version": (Empty, VersionReply),
+    f"/{EXT_SERVICE}/ObserveInterference": (ObserveRequest, ObserveReply),
 }
 
 

@@ -25,6 +25,7 @@ from concurrent import futures
 from typing import Any, Callable, Optional
 
 import grpc
+import numpy as np
 
 from ..api import constants as C
 from . import proto as P
@@ -44,7 +45,8 @@ class ModelSlot:
         self.name, self.path, self.kind, self.model_kw = name, path, kind, model_kw
         self._lock = threading.Lock()
         self.current: Optional[TrainedTable] = None
-        self.version: Optional[str] = None
+        self.version: Optional[str] = None         # version served (file md5, or online-N)
+        self.file_version: Optional[str] = None    # md5 of the training file last fitted
 
     def load_if_changed(self, store: Any = None) -> bool:
         """Re-fit when the training file's md5 changed.  With a Redis `store`, every newly
@@ -57,12 +59,12 @@ class ModelSlot:
                 return self._load_persisted(store)
             log.info("%s: train data not found at %s", self.name, self.path)
             return False
-        if v == self.version:
+        if v == self.file_version:
             return False
         table = Table.read_tsv(self.path)
         trained = TrainedTable.fit(table, self.kind, v, **self.model_kw)
         with self._lock:
-            self.current, self.version = trained, v
+            self.current, self.version, self.file_version = trained, v, v
         if store is not None:
             try:
                 from ..store import schema
@@ -95,6 +97,11 @@ class ModelSlot:
         with self._lock:
             self.current, self.version = trained, version
 
+    def serve_table(self, table: Table, version: str) -> None:
+        """Serve a learned table (no NaN) without touching the file bookkeeping: a later
+        change of the training file still re-fits from the file."""
+        self.set_table(table, version)
+
     def get(self) -> Optional[TrainedTable]:
         with self._lock:
             return self.current
@@ -113,6 +120,9 @@ class RecommenderService:
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.calls = 0
+        self._online: Any = None            # recommender.online.OnlineInterference
+        self._online_base: Optional[str] = None
+        self._online_lock = threading.Lock()
 
     @classmethod
     def from_env(cls, **kw: Any) -> "RecommenderService":
@@ -184,6 +194,42 @@ class RecommenderService:
         return P.ResizeReply(recommended_cu=adv.cu, recommended_hbm_gib=adv.hbm_gib, samples=adv.samples,
                              reason=adv.reason)
 
+    def ObserveInterference(self, request: Any, context: Any) -> Any:
+        """Online interference learning (recommender.online): each observation is a pod's
+        throughput loss next to its co-runners; the refitted matrix becomes the served
+        interference table (version online-N) until the training file changes."""
+        from .online import OnlineInterference
+        from .tables import find_index_for_request
+        with self._online_lock:
+            t = self.intf.get()
+            if t is None:
+                return P.ObserveReply(accepted=0, interference="", observations=0)
+            base = self.intf.file_version or self.intf.version
+            if self._online is None or self._online_base != base:
+                self._online = OnlineInterference(t.table.index, t.table.columns, t.completed(),
+                                                  refit_every=max(1, int(os.getenv("ONLINE_REFIT_EVERY", "32"))))
+                self._online_base = base
+            on = self._online
+            cols = list(t.table.columns)
+            accepted, refit = 0, False
+            for ob in request.observations:
+                lab = find_index_for_request(ob.pod.replace("-", "_"), t.table.index)
+                others = []
+                for c in ob.co_runners:
+                    nm = c.replace("-", "_")
+                    j = next((k for k, col in enumerate(cols) if col in nm), None)
+                    if j is not None:
+                        others.append(j)
+                if not lab or not others:
+                    continue
+                refit |= on.observe(t.table.index.index(lab), others, float(ob.loss))
+                accepted += 1
+            if refit:
+                self.intf.serve_table(Table(list(t.table.index), cols, np.asarray(on.rows())),
+                                      f"online-{on.version}")
+            return P.ObserveReply(accepted=accepted, interference=self.intf.version or "",
+                                  observations=int(on.mae()["n"]))
+
     def Version(self, request: Any, context: Any) -> Any:
         return P.VersionReply(configurations=self.conf.version or "", interference=self.intf.version or "",
                               model=self.conf.kind)
@@ -197,7 +243,8 @@ class RecommenderService:
                                           "ImputeInterference": self.ImputeInterference}),
             P.generic_handler(P.EXT_SERVICE, {"ExportTable": self.ExportTable,
                                               "RecommendResources": self.RecommendResources,
-                                              "Version": self.Version}),
+                                              "Version": self.Version,
+                                              "ObserveInterference": self.ObserveInterference}),
         ))
         bound = server.add_insecure_port(f"{host}:{port}")
         server.start()

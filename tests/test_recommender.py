@@ -308,3 +308,25 @@ def test_plugin_forgets_memoised_predictions_on_new_table():
     assert p._pod_predictions("wl-a-0")[1] == {"wl_a": 1.0}
     cp.install_interference(["wl_a"], ["wl_a"], [[5.0]], "online-1")
     assert p._pod_predictions("wl-a-0")[1] == {"wl_a": 5.0}
+
+
+def test_observe_interference_rpc_serves_learned_table(server):
+    """Extended.ObserveInterference: co-run observations refit the interference row and the
+    learned table is served (version online-N) until the training file changes."""
+    svc, addr, (c, i) = server
+    cl = RecommenderClient(addr)
+    before = reply_to_map(cl.impute_interference("mlperf-gpu-onnx-resnet50-1024_A30"))
+    col = "onnx_mobilenet_1024"
+    target = before[col] + 50.0
+    obs = [("mlperf-gpu-onnx-resnet50-1024_A30", ["pod-onnx-mobilenet-1024-7"], target)] * 40
+    rep = cl.observe_interference(obs + [("busybox-abc", ["x"], 1.0)])
+    assert rep.accepted == 40 and rep.interference.startswith("online-") and rep.observations == 40
+    assert cl.version().interference == rep.interference
+    after = reply_to_map(cl.impute_interference("mlperf-gpu-onnx-resnet50-1024_A30"))
+    assert abs(after[col] - target) < abs(before[col] - target) * 0.25     # moved to the observations
+    assert after["onnx_resnet50_1024"] == pytest.approx(before["onnx_resnet50_1024"], rel=1e-6)  # unseen column
+    # a new training file wins again (and restarts the learner from it)
+    with open(i, "a") as f:
+        f.write("\n")
+    svc.train()
+    assert not cl.version().interference.startswith("online-")
