@@ -33,7 +33,9 @@ class NodeUnschedulable(FilterPlugin):
     NAME = "NodeUnschedulable"
 
     def __init__(self, args=None, handle=None):
-        pass
+        # node name -> node object last seen schedulable and ready (objects are replaced,
+        # never mutated, on update, so identity means "unchanged")
+        self._plain: Dict[str, Any] = {}
 
     def filter(self, state, pod, node_info):
         node = node_info.node
@@ -48,8 +50,17 @@ class NodeUnschedulable(FilterPlugin):
     def filter_nodes(self, state, pod, node_infos):
         tol = None
         out = []
+        plain = self._plain
         for ni in node_infos:
             node = ni.node
+            if plain.get(ni.name) is node:          # schedulable and ready, node unchanged
+                out.append(None)
+                continue
+            if not O.node_unschedulable(node) and O.node_ready(node):
+                plain[ni.name] = node
+                out.append(None)
+                continue
+            plain.pop(ni.name, None)
             if O.node_unschedulable(node):
                 if tol is None:
                     tol = O.tolerates(pod, {"key": "node.kubernetes.io/unschedulable", "effect": "NoSchedule"})
@@ -138,6 +149,7 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
 
     def __init__(self, args=None, handle=None):
         self.ignored = set((args or {}).get("ignoredResources", []))
+        self._memo: Dict[str, tuple] = {}      # node -> (generation, node object, request sig, status)
 
     def pre_filter(self, state, pod):
         state.write(_FIT_KEY, O.pod_requests(pod))
@@ -164,9 +176,18 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
             req = O.pod_requests(pod)
         want = [(r, v - 1e-9, r.startswith(("amd.com/", "nvidia.com/"))) for r, v in req.items()
                 if v > 0 and r not in self.ignored]
+        sig = tuple(want)
         pods_key = C.RESOURCE_PODS
+        memo = self._memo
         out = []
         for ni in node_infos:
+            # a node's verdict only changes with its NodeInfo generation / object and the
+            # request; preemption what-if clones (pods removed, own generation count) bypass it
+            whatif = getattr(ni, "removed", None) is not None
+            hit = None if whatif else memo.get(ni.name)
+            if hit is not None and hit[0] == ni.generation and hit[1] is ni.node and hit[2] == sig:
+                out.append(hit[3])
+                continue
             alloc, used = ni.allocatable, ni.requested
             st = None
             if pods_key in alloc and alloc[pods_key] - used.get(pods_key, 0.0) < 1:
@@ -181,6 +202,8 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
                     elif a - used.get(r, 0.0) < v:
                         st = Status.unschedulable(f"Insufficient {r}", self.NAME)
                         break
+            if not whatif:
+                memo[ni.name] = (ni.generation, ni.node, sig, st)
             out.append(st)
         return out
 
