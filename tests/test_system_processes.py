@@ -101,3 +101,64 @@ def test_scheduler_agent_apiserver_as_processes(tmp_path):
             except subprocess.TimeoutExpired:
                 p.kill()
         redis.stop()
+
+
+@pytest.mark.timeout(240)
+def test_agent_serves_device_plugin_to_kubelet_as_process(tmp_path):
+    """The DaemonSet's command line (`agent --device-plugin`) as a process: it registers the
+    three resources with a (fake) kubelet and answers Allocate for a pod the scheduler
+    placed -- over Unix sockets, across processes."""
+    from concurrent import futures
+
+    import grpc
+
+    from k8s_gpu_scheduler_amd.agent import deviceplugin as dp
+    procs = []
+    redis = FakeRedisServer(FakeRedisEngine(password=C.REDIS_PASSWORD)).start()
+    regs = []
+    kubelet = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+    kubelet.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(dp.REG_SERVICE, {
+        "Register": grpc.unary_unary_rpc_method_handler(
+            lambda req, ctx: (regs.append(req.resource_name), dp.Empty())[1],
+            request_deserializer=dp.RegisterRequest.FromString, response_serializer=dp.Empty.SerializeToString)}),))
+    kubelet.add_insecure_port(f"unix://{tmp_path}/kubelet.sock")
+    kubelet.start()
+    try:
+        api_port = _free_port()
+        fc = _spawn(["fake-cluster", "--port", str(api_port), "--nodes", "1", "--gpus", "8"])
+        procs.append(fc)
+        url = fc.stdout.readline().strip()
+        client = RestClient(RestConfig(url))
+        node = O.name(client.list("nodes")[0][0])
+        ag = _spawn(["agent", "--fake-apiserver", url, "--redis", redis.addr, "--node", node, "--synthetic", "8",
+                     "--no-discovery", "--metrics-port", "0", "--poll", "0.5",
+                     "--device-plugin", "--device-plugin-dir", str(tmp_path)])
+        procs.append(ag)
+        assert _wait(lambda: len(regs) >= 3, 60), regs
+        assert sorted(regs) == sorted(dp.RESOURCES)
+        sc = _spawn(["scheduler", "--fake-apiserver", url, "--redis", redis.addr, "--no-discovery",
+                     "--config", os.path.join(ROOT, "deploy", "scheduler.yaml"), "--metrics-port", "0"])
+        procs.append(sc)
+        client.create("pods", O.make_pod("frac-0", gpu_cu=64, gpu_mem_gib=8, gpu_limits=True))
+        pod = _wait(lambda: (lambda p: p if O.node_name_of(p) else None)(client.get("pods", "frac-0", "default")), 90)
+        assert pod, "pod not bound"
+        ch = grpc.insecure_channel(f"unix://{tmp_path}/{dp.socket_name(C.RESOURCE_GPU_CU)}")
+        alloc = ch.unary_unary(f"/{dp.PLUGIN_SERVICE}/Allocate", request_serializer=dp.AllocateRequest.SerializeToString,
+                               response_deserializer=dp.AllocateResponse.FromString)
+        req = dp.AllocateRequest()
+        req.container_requests.add(devices_ids=[f"tok{k}" for k in range(64)])
+        resp = alloc(req, timeout=10).container_responses[0]
+        ann = O.annotations(pod)
+        assert resp.envs[C.ENV_ROCR_VISIBLE] == ann[C.ANNOT_DEVICES]
+        assert resp.envs[C.ENV_CU_MASK] == ann[C.ANNOT_CU_MASK]
+        ch.close()
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        kubelet.stop(0)
+        redis.stop()
