@@ -134,7 +134,9 @@ class RecommenderService:
     def train(self) -> None:
         for slot in (self.conf, self.intf):
             try:
-                slot.load_if_changed(self.store)
+                changed = slot.load_if_changed(self.store)
+                if changed and slot is self.intf and self.store is not None:
+                    self.restore_online()
             except Exception as e:
                 log.warning("%s: training failed: %s", slot.name, e)
 
@@ -225,10 +227,43 @@ class RecommenderService:
                 refit |= on.observe(t.table.index.index(lab), others, float(ob.loss))
                 accepted += 1
             if refit:
-                self.intf.serve_table(Table(list(t.table.index), cols, np.asarray(on.rows())),
-                                      f"online-{on.version}")
+                learned = Table(list(t.table.index), cols, np.asarray(on.rows()))
+                version = f"online-{on.version}"
+                self.intf.serve_table(learned, version)
+                self._persist_online(learned, version, base)
             return P.ObserveReply(accepted=accepted, interference=self.intf.version or "",
                                   observations=int(on.mae()["n"]))
+
+    def _persist_online(self, table: Table, version: str, base: Optional[str]) -> None:
+        """Keep the learned interference table in Redis so a restarted
+        recommender serves it again -- as long as the training file it was learned on top
+        of (`base` md5) is still the current one."""
+        if self.store is None:
+            return
+        try:
+            from ..store import schema
+            self.store.set(schema.model_key("interference-online"), json.dumps(
+                {"version": version, "base": base, "table": table.to_json()}, separators=(",", ":")))
+        except Exception as e:
+            log.warning("persisting the online interference table failed: %s", e)
+
+    def restore_online(self) -> bool:
+        """Serve a persisted online table learned on the current training file."""
+        if self.store is None or self.intf.get() is None:
+            return False
+        from ..store import schema
+        try:
+            raw = self.store.get(schema.model_key("interference-online"))
+        except Exception:
+            return False
+        if not raw:
+            return False
+        d = json.loads(raw)
+        if d.get("base") != (self.intf.file_version or self.intf.version):
+            return False
+        self.intf.serve_table(Table.from_json(d["table"]), d["version"])
+        log.info("interference: restored online table %s", d["version"])
+        return True
 
     def Version(self, request: Any, context: Any) -> Any:
         return P.VersionReply(configurations=self.conf.version or "", interference=self.intf.version or "",

@@ -330,3 +330,35 @@ def test_observe_interference_rpc_serves_learned_table(server):
         f.write("\n")
     svc.train()
     assert not cl.version().interference.startswith("online-")
+
+
+def test_online_table_survives_recommender_restart(ref_data, tmp_path):
+    import shutil as _sh
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    from k8s_gpu_scheduler_amd.recommender import proto as P
+    conf, intf = ref_data
+    c, i = tmp_path / "c.tsv", tmp_path / "i.tsv"
+    _sh.copy(conf, c)
+    _sh.copy(intf, i)
+    store = Redis(FakeRedisBackend(FakeRedisEngine()))
+    a = RecommenderService(str(c), str(i))
+    a.store = store
+    a.train()
+    req = P.ObserveRequest()
+    for _ in range(40):
+        req.observations.add(pod="mlperf-gpu-onnx-resnet50-1024_A30", co_runners=["x-onnx-mobilenet-1024"], loss=500.0)
+    rep = a.ObserveInterference(req, None)
+    assert rep.interference.startswith("online-")
+    b = RecommenderService(str(c), str(i))        # restart with the same training file
+    b.store = store
+    b.train()
+    assert b.intf.version == rep.interference
+    learned = b.intf.get().lookup("mlperf-gpu-onnx-resnet50-1024_A30")["onnx_mobilenet_1024"]
+    assert learned == pytest.approx(a.intf.get().lookup("mlperf-gpu-onnx-resnet50-1024_A30")["onnx_mobilenet_1024"])
+    with open(i, "a") as f:                       # a new training file: the online table is stale
+        f.write("\n")
+    c2 = RecommenderService(str(c), str(i))
+    c2.store = store
+    c2.train()
+    assert not c2.intf.version.startswith("online-")
