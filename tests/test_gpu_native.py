@@ -365,3 +365,32 @@ def test_device_plugin_allocates_real_device_nodes():
     paths = [x.host_path for x in resp.devices]
     assert paths[0] == "/dev/kfd" and nodes[0][0] in paths
     assert resp.envs["ROCR_VISIBLE_DEVICES"] == inv[0]["uuid"]
+
+
+def test_agent_exports_real_telemetry_to_prometheus():
+    """BASELINE config 2: the node agent on the real MI355X (amd-smi source) publishes the
+    device to Redis and its telemetry to the Prometheus exporter under the AMD and the
+    DCGM-compatible names the reference queries (reference prom_metrics.go:64-70), with the
+    device UUID label; the health verdict gauge is 1."""
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import SmiSource
+    from k8s_gpu_scheduler_amd.store import schema
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    from k8s_gpu_scheduler_amd.telemetry.exporter import GpuExporter
+    try:
+        src = SmiSource()
+    except RuntimeError as e:
+        pytest.skip(f"amd-smi unavailable: {e}")
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    ex = GpuExporter("box", dcgm_compat=True)
+    ag = NodeAgent("box", r, src, exporter=ex)
+    ag.step()
+    uuids = schema.read_uuids(r, "box")
+    assert uuids and all(u.startswith("GPU-") for u in uuids)
+    text = ex.render().decode()
+    for m in ("amd_gpu_gfx_activity", "amd_gpu_vram_used_mb", "amd_gpu_temperature_hotspot",
+              "DCGM_FI_PROF_GR_ENGINE_ACTIVE", "DCGM_FI_DEV_FB_FREE", "amd_gpu_healthy"):
+        assert f"{m}{{" in text, m
+    assert f'UUID="{uuids[0]}"' in text
+    assert any(l.startswith("amd_gpu_healthy{") and l.endswith(" 1.0") for l in text.splitlines())
