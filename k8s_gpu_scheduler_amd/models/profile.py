@@ -36,7 +36,10 @@ def _time_pods(ex, runs) -> None:
     ex.collect(runs)
 
 
-def profile(iters: int = 8, pairs: Optional[int] = None, seed: int = 0, names: Optional[List[str]] = None):
+def profile(iters: int = 8, pairs: Optional[int] = None, seed: int = 0, names: Optional[List[str]] = None,
+            repeats: int = 3):
+    """Median of `repeats` timed runs per cell (alone and co-located alike, so interference
+    = median alone - median co-located is not biased by the estimator)."""
     import torch
     from ..parallel.executor import DeviceExecutor, PodRun
     from . import workloads as W
@@ -46,15 +49,16 @@ def profile(iters: int = 8, pairs: Optional[int] = None, seed: int = 0, names: O
     # warm every stream / buffer
     ex.warm([PodRun(0, n, u0, k, 1) for n in names for (u0, k) in list(shares.values()) + [(2, 2)]])
     conf = np.zeros((len(names), 4))
+    reps = max(1, repeats)
     for i, n in enumerate(names):
         for j, p in enumerate((1, 2, 4, 8)):
             u0, k = shares[p]
-            best = 0.0
-            for _ in range(2):
+            samples = []
+            for _ in range(reps):
                 r = [PodRun(0, n, u0, k, iters)]
                 _time_pods(ex, r)
-                best = max(best, r[0].throughput)
-            conf[i, j] = best
+                samples.append(r[0].throughput)
+            conf[i, j] = float(np.median(samples))
     alone4 = conf[:, 2]
     intf = np.full((len(names), len(names)), np.nan)
     todo = list(itertools.product(range(len(names)), range(len(names))))
@@ -62,10 +66,13 @@ def profile(iters: int = 8, pairs: Optional[int] = None, seed: int = 0, names: O
         random.Random(seed).shuffle(todo)
         todo = todo[:pairs]
     for i, j in todo:
-        a = PodRun(0, names[i], 0, 2, iters)
-        b = PodRun(1, names[j], 2, 2, iters * 4)          # co-runner outlives the victim
-        _time_pods(ex, [b, a])
-        intf[i, j] = max(0.0, alone4[i] - a.throughput)
+        samples = []
+        for _ in range(reps):
+            a = PodRun(0, names[i], 0, 2, iters)
+            b = PodRun(1, names[j], 2, 2, iters * 4)      # co-runner outlives the victim
+            _time_pods(ex, [b, a])
+            samples.append(a.throughput)
+        intf[i, j] = max(0.0, alone4[i] - float(np.median(samples)))
     ex.close()
     return names, conf, intf
 
@@ -85,11 +92,12 @@ def write_tables(out_dir: str, names: List[str], conf: np.ndarray, intf: np.ndar
 def main(argv: Optional[List[str]] = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(__file__)), "data"))
-    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=16)
     ap.add_argument("--pairs", type=int, default=0, help="sample this many interference pairs (0 = all)")
+    ap.add_argument("--repeats", type=int, default=3, help="timed runs per cell (median)")
     a = ap.parse_args(argv)
     t = time.time()
-    names, conf, intf = profile(a.iters, a.pairs or None)
+    names, conf, intf = profile(a.iters, a.pairs or None, repeats=a.repeats)
     paths = write_tables(a.out, names, conf, intf)
     print(json.dumps({"paths": paths, "seconds": round(time.time() - t, 1),
                       "conf_1P_min_max": [float(conf[:, 0].min()), float(conf[:, 0].max())]}))
