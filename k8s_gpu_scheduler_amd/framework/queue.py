@@ -206,6 +206,11 @@ class SchedulingQueue:
             self._closed = True
             self._cv.notify_all()
 
+    def active_pods(self) -> List[Obj]:
+        """Pods waiting in the active queue (not the one being scheduled), in no order."""
+        with self._cv:
+            return [pi.pod for pi in self._active_keys.values()]
+
     def pending(self) -> Dict[str, int]:
         with self._cv:
             return {"active": len(self._active_keys), "backoff": len(self._backoff_keys),

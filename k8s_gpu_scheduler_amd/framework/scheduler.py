@@ -77,6 +77,10 @@ class Handle:
     def extras(self) -> Dict[str, Any]:
         return self._s.extras
 
+    def pending_pods(self) -> List[Obj]:
+        """Pods in the active queue -- what a plugin may plan jointly with the current one."""
+        return self._s.queue.active_pods()
+
     def framework_for(self, pod: Obj) -> Optional["Framework"]:
         return self._s.frameworks.get(O.scheduler_name(pod))
 

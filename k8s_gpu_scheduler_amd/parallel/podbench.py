@@ -96,7 +96,7 @@ class ControlPlane:
 
     def __init__(self, n_gpus: int, pods_per_gpu: int, iters: int, seed: int, policy: str = "gpu",
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
-                 balance: float = 1.0, learn_interference: bool = True):
+                 balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -109,7 +109,7 @@ class ControlPlane:
         self.ledger = DeviceLedger()
         self.predictions = predictions or measured_predictions() or analytic_predictions()
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
-                "compat_env": False}
+                "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random"}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
         # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
@@ -384,6 +384,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--sim-timed", action="store_true",
                     help="simulated executor sleeps out a modelled device time per epoch (multi-rank CPU rehearsal)")
     ap.add_argument("--sim-scale", type=float, default=1.0, help="modelled device-time multiplier (--sim-timed)")
+    ap.add_argument("--plan-bursts", type=int, default=1, choices=[0, 1],
+                    help="1: plan each epoch's burst of pods jointly (SLO-aware pairing under predicted "
+                         "interference, within 5%% of the balanced load)")
     ap.add_argument("--balance", type=float, default=1.0,
                     help="weight of the GPU plugin's least-predicted-load term (0 = off; >0 also sorts the "
                          "queue longest-predicted-work first)")
@@ -412,7 +415,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     # (torch.cuda.is_available() initialises HIP; a GPU-initialised process must not exec).
     n_gpus_planned = world if world > 1 else max(1, a.gpus if a.sim else 1)
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
-                     policy=a.policy, qos=a.qos, balance=a.balance)
+                     policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -599,7 +602,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "config": {"model": "bin-pack fractional-GPU pods onto MI355X by live HBM/CU-util (Score path)",
                        "global_batch": P, "seq_len": a.iters, "parallelism": f"dp{n_gpus}",
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
-                       "balance": a.balance,
+                       "balance": a.balance, "plan_bursts": a.plan_bursts,
                        "note": "global_batch = pods per scheduling epoch; seq_len = query batches per pod"},
             "gpu_util_pct": round(util, 2),
             "cu_share_occupancy_pct": round(occ, 2),

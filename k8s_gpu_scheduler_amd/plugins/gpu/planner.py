@@ -1,0 +1,190 @@
+"""Joint placement of a burst of fractional GPU pods ("plan bursts").
+
+The reference scores one pod at a time against the residents already on each device
+(reference pkg/plugins/gpu_plugin/gpu_plugins.go:558-757), so a burst of pods arriving
+together is placed greedily: whichever pod comes first takes the device that suits it,
+and later pods get what is left -- co-locating workloads whose predicted interference
+breaks their SLOs even when a different pairing would satisfy everyone.  On an 8-GPU
+MI355X node a burst of 32 quarter-GPU pods fills every slot, so the *pairing* is the
+whole decision.
+
+At the first cycle of a burst (PreScore of a pod with no plan), the GPU plugin plans the
+pod together with every pending fractional pod of the queue:
+
+1. an initial feasible assignment: longest predicted work first onto the least-loaded GPU
+   with free units / HBM (the balance objective);
+2. the native core (`_core.plan_assignment`) improves it with pairwise swaps that raise the
+   number of pods -- incoming and resident -- predicted to meet their SLO under the
+   interference of their co-residents (the reference's `SLO > pred - intf` test), never
+   letting a GPU's predicted load exceed the initial plan's busiest GPU by more than
+   `planTolerance`.
+
+The plan is a hint: each pod still runs the full Filter/Score/Reserve cycle; Score ranks
+the planned device first and every other choice after it, and a plan that no longer fits
+(capacity taken meanwhile) is simply ignored.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ...api import objects as O
+from ...recommender.tables import find_index_for_request
+from .scoring import workload_column
+
+Obj = Dict[str, Any]
+
+
+class BurstPlanner:
+    def __init__(self, plugin: Any, tolerance: float = 0.05, sweeps: int = 8):
+        self.plugin = plugin
+        self.tolerance = tolerance
+        self.sweeps = sweeps
+        self.plans: Dict[str, Tuple[str, str]] = {}      # pod key -> (node, device uuid)
+        self.planned_bursts = 0
+
+    # ---------------------------------------------------------------- inputs
+    def _matrix(self) -> Optional[Tuple[List[str], List[str], np.ndarray]]:
+        tables = getattr(self.plugin.predictions, "tables", None)
+        if tables is None:
+            return None
+        _, intf = tables()
+        if intf is None or not intf.index:
+            return None
+        key = (id(intf), intf.version)
+        hit = getattr(self, "_mcache", None)
+        if hit is None or hit[0] != key:
+            m = np.asarray([[intf.by_label[r].get(c, 0.0) for c in intf.columns] for r in intf.index], dtype=np.float64)
+            self._mcache = hit = (key, (list(intf.index), list(intf.columns), np.nan_to_num(m)))
+        return hit[1]
+
+    def _ids(self, name: str, index: List[str], columns: List[str]) -> Tuple[int, int]:
+        model = self.plugin.args.model
+        lab = find_index_for_request(f"{name}_{model}".replace("-", "_"), index)
+        r = index.index(lab) if lab else -1
+        c = workload_column(name, dict.fromkeys(columns))
+        return r, (columns.index(c) if c is not None else -1)
+
+    # ---------------------------------------------------------------- plan
+    def plan(self, pod: Obj, nodes: List[str]) -> Optional[Tuple[str, str]]:
+        """Plan `pod` with the pending fractional pods over the devices of `nodes` (the
+        pod's feasible nodes); returns its (node, device uuid)."""
+        key = O.key(pod)
+        hit = self.plans.get(key)
+        if hit is not None:
+            return hit
+        from ... import _native
+        core = _native.core()
+        mat = self._matrix()
+        if core is None or mat is None or not hasattr(core, "plan_assignment"):
+            return None
+        index, columns, M = mat
+        plugin = self.plugin
+        placed = [(nd, st) for nd in nodes for st in plugin.ledger.devices(nd) if st.device.healthy]
+        if not placed:
+            return None
+        states = [st for _, st in placed]
+        owner = [nd for nd, _ in placed]
+        # the burst: this pod + pending fractional pods of this scheduler not planned yet
+        burst, seen = [], {key}
+        for p in [pod] + list(plugin.handle.pending_pods() if plugin.handle is not None else []):
+            k = O.key(p)
+            if (k in seen and p is not pod) or k in self.plans or O.node_name_of(p):
+                continue
+            seen.add(k)
+            req = plugin.parse_request(p)
+            if req.units and not req.whole and req.gpu_pod:
+                burst.append((p, req))
+        if len(burst) < 2:
+            return None
+        dev_index = {(owner[d], st.device.uuid): d for d, st in enumerate(states)}
+        gkeys = sorted({(owner[d], st.device.gpu) for d, st in enumerate(states)})
+        gpos = {g: i for i, g in enumerate(gkeys)}
+        gof = [gpos[(owner[d], st.device.gpu)] for d, st in enumerate(states)]
+        free_units = [st.free_units for st in states]
+        free_hbm = [st.hbm_free for st in states]
+        load = [0.0] * len(gkeys)
+        res_dev, res_row, res_col, res_slo, res_pred = [], [], [], [], []
+        for d, st in enumerate(states):
+            load[gof[d]] += st.work
+            for use in st.pods.values():
+                conf, _ = plugin._pod_predictions(use.name)
+                r, c = self._ids(use.name, index, columns)
+                res_dev.append(d)
+                res_row.append(r)
+                res_col.append(c)
+                res_slo.append(use.slo)
+                res_pred.append(conf.get(plugin._col(use.units[1], st.device.units), -1.0) if conf else -1.0)
+        # pods planned earlier and still pending hold their capacity / interfere as residents
+        for k, (n, u) in self.plans.items():
+            d = dev_index.get((n, u))
+            if d is None:
+                continue
+            p = plugin._pending_by_key.get(k)
+            if p is None:
+                continue
+            req = plugin.parse_request(p)
+            free_units[d] -= req.units
+            free_hbm[d] -= req.hbm_gib
+            conf, _ = plugin._pod_predictions(O.name(p))
+            r, c = self._ids(O.name(p), index, columns)
+            res_dev.append(d)
+            res_row.append(r)
+            res_col.append(c)
+            res_slo.append(req.slo)
+            res_pred.append(conf.get(plugin._col(req.units, states[d].device.units), -1.0) if conf else -1.0)
+            load[gof[d]] += plugin.pod_work(p, conf)
+        base_load = list(load)
+        # 1. initial assignment: longest predicted work first, least-loaded GPU with room
+        items = []
+        for p, req in burst:
+            conf, _ = plugin._pod_predictions(O.name(p))
+            items.append((plugin.pod_work(p, conf), p, req, conf))
+        items.sort(key=lambda t: -t[0])
+        assign: List[Tuple[Any, Any, Any, int]] = []
+        for work, p, req, conf in items:
+            best = None
+            for d, st in enumerate(states):
+                if free_units[d] < req.units or free_hbm[d] + 1e-6 < req.hbm_gib:
+                    continue
+                k2 = (load[gof[d]], d)
+                if best is None or k2 < best[0]:
+                    best = (k2, d)
+            if best is None:
+                continue                      # does not fit now: left to the normal cycle
+            d = best[1]
+            free_units[d] -= req.units
+            free_hbm[d] -= req.hbm_gib
+            load[gof[d]] += work
+            assign.append((p, req, conf, d))
+        if len(assign) < 2:
+            return None
+        n = len(assign)
+        dev = np.array([a[3] for a in assign], dtype=np.int32)
+        units = np.array([a[1].units for a in assign], dtype=np.int32)
+        rows, cols, slo, pred, work = [], [], [], [], []
+        for p, req, conf, d in assign:
+            r, c = self._ids(O.name(p), index, columns)
+            rows.append(r)
+            cols.append(c)
+            slo.append(req.slo)
+            pred.append(conf.get(plugin._col(req.units, states[d].device.units), -1.0) if conf else -1.0)
+            work.append(plugin.pod_work(p, conf))
+        max_load = max(load) * (1.0 + self.tolerance)
+        out = core.plan_assignment(
+            dev, units, np.array(rows, dtype=np.int32), np.array(cols, dtype=np.int32),
+            np.array(slo, dtype=np.float64), np.array(pred, dtype=np.float64), np.array(work, dtype=np.float64),
+            np.array(gof, dtype=np.int32), np.array(base_load, dtype=np.float64),
+            np.array(res_dev, dtype=np.int32), np.array(res_row, dtype=np.int32), np.array(res_col, dtype=np.int32),
+            np.array(res_slo, dtype=np.float64), np.array(res_pred, dtype=np.float64), M, float(max_load),
+            self.sweeps)
+        for (p, _, _, _), d in zip(assign, out[:n]):
+            self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
+            plugin._pending_by_key[O.key(p)] = p
+        self.planned_bursts += 1
+        return self.plans.get(key)
+
+    def consume(self, pod_key: str) -> None:
+        self.plans.pop(pod_key, None)
+        self.plugin._pending_by_key.pop(pod_key, None)

@@ -55,6 +55,7 @@ _PRED = "GPU/predictions"
 _CHOICE = "GPU/choice"
 _CANDS = "GPU/candidates"
 _SIG = "GPU/signature"
+_PLAN = "GPU/plan"
 BIND_ANNOTATIONS = "bind/annotations"
 
 
@@ -91,6 +92,10 @@ class GPUArgs:
     # queueSort (when GPU is the profile's queueSort plugin): pods arriving in the same
     # window are popped longest-predicted-work first (LPT), older windows first
     lpt_window_s: float = 1.0
+    # plan a burst of pending fractional pods jointly (plugins.gpu.planner): pairings that
+    # keep predicted SLOs under interference, within planTolerance of the balanced load
+    plan_bursts: bool = False
+    plan_tolerance: float = 0.05
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
@@ -111,6 +116,7 @@ class GPUArgs:
         a = cls()
         alias = {"weightSLO": "w_slo", "weightPack": "w_pack", "weightTelemetry": "w_telemetry",
                  "weightBalance": "w_balance", "lptWindowSeconds": "lpt_window_s",
+                 "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle"}
@@ -142,6 +148,11 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self._cands_memo: Dict[str, Tuple[Any, List[Tuple[DeviceState, int]]]] = {}
         self._score_memo: Dict[str, Tuple[Any, Optional[Choice]]] = {}
         self._col_cache: Dict[Tuple[int, int], str] = {}
+        self._pending_by_key: Dict[str, Obj] = {}
+        self.planner = None
+        if self.args.plan_bursts:
+            from .planner import BurstPlanner
+            self.planner = BurstPlanner(self, self.args.plan_tolerance)
         self._pred_version: Any = None
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)
@@ -217,6 +228,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
 
     def _on_pod_delete(self, pod: Obj) -> None:
         self.ledger.release(O.key(pod))
+        if self.planner is not None:
+            self.planner.consume(O.key(pod))
 
     # ------------------------------------------------------------------ request
     def parse_request(self, pod: Obj) -> GpuRequest:
@@ -315,6 +328,13 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return Status.skip()
         state.write(_PRED, self._pod_predictions(O.name(pod)))
         state.write(_CHOICE, {})
+        if self.planner is not None and req.units and not req.whole:
+            try:
+                plan = self.planner.plan(pod, [n.name for n in nodes])
+            except Exception as e:          # planning is an optimisation: never fail the cycle
+                log.warning("burst planning failed: %s", e)
+                plan = None
+            state.write(_PLAN, plan)
         return None
 
     def score(self, state: CycleState, pod: Obj, node_name: str) -> Tuple[int, Optional[Status]]:
@@ -324,7 +344,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             except Exception as e:
                 return 0, Status.error(f"Error in Logic() in Score(): {e}", self.NAME)
         req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
-        choice = self._best_choice(state, pod, req, node_name, scoring=True)
+        choice = self._apply_plan(state, req, node_name, self._best_choice(state, pod, req, node_name, scoring=True))
         if choice is None:
             return 0, None
         choices = state.read(_CHOICE)
@@ -345,6 +365,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         out = []
         lo, hi = C.MIN_NODE_SCORE, C.MAX_NODE_SCORE
         sig = self._pod_ctx(state, pod, req)[4] if not req.whole else None
+        plan = state.read(_PLAN)
         node_gen, smemo, tele = self.ledger.node_gen, self._score_memo, self.telemetry
         use_t, stale = bool(self.args.w_telemetry), tele.stale_s
         for nn in names:
@@ -356,12 +377,33 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                 if hit[0] != skey:
                     hit = None
             choice = hit[1] if hit is not None else self._best_choice(state, pod, req, nn, scoring=True)
+            if plan is not None:
+                choice = self._apply_plan(state, req, nn, choice)
             if choice is None:
                 out.append(0)
                 continue
             choices[nn] = choice
             out.append(max(lo, min(hi, int(choice.score))))
         return out, None
+
+    def _apply_plan(self, state: CycleState, req: GpuRequest, node: str,
+                    choice: Optional[Choice]) -> Optional[Choice]:
+        """Burst plan (planner.BurstPlanner): the planned device on the planned node scores
+        100 and everything else below it; a stale plan (device no longer a candidate)
+        leaves the normal choice."""
+        plan = state.read(_PLAN)
+        if plan is None:
+            return choice
+        pnode, puuid = plan
+        if node == pnode:
+            for st, u0 in (state.read(_CANDS) or {}).get(node) or []:
+                if st.device.uuid == puuid:
+                    return Choice(node, [(puuid, u0, req.units, req.hbm_gib, False)], float(C.MAX_NODE_SCORE),
+                                  [st.device])
+            return choice
+        if choice is not None and choice.score > C.MAX_NODE_SCORE - 1:
+            choice = dataclasses.replace(choice, score=float(C.MAX_NODE_SCORE - 1))
+        return choice
 
     def score_extensions(self) -> ScoreExtensions:
         return self
@@ -389,12 +431,16 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                                                      work=work):
             return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
         state.write(_CHOICE + "/reserved", choice)
+        if self.planner is not None:
+            self.planner.consume(O.key(pod))
         return None
 
     def unreserve(self, state: CycleState, pod: Obj, node_name: str) -> None:
         if self.parity is not None:
             return
         self.ledger.release(O.key(pod))
+        if self.planner is not None:
+            self.planner.consume(O.key(pod))
 
     def pre_bind(self, state: CycleState, pod: Obj, node_name: str) -> Optional[Status]:
         if self.parity is not None:

@@ -14,7 +14,9 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
 #include <cmath>
+#include <stdexcept>
 #include <cstdint>
 #include <vector>
 
@@ -117,6 +119,135 @@ py::array_t<int32_t> find_units(py::array_t<uint64_t, py::array::c_style | py::a
   return out;
 }
 
+// Joint placement of a burst of pending fractional pods over a node's devices (the
+// reference scores one pod at a time, gpu_plugins.go:558-757; a burst placed greedily can
+// co-locate workloads that hurt each other).  Objective: number of pods -- incoming and
+// resident -- whose predicted throughput minus the summed interference of their
+// co-residents still meets their SLO (the reference's violation test, SLO > pred - intf,
+// :616,717), subject to every GPU's predicted load staying within `max_load`.
+// Deterministic first-improvement pairwise swaps between pods of equal units on
+// different devices, in sweeps, until no swap improves (or `sweeps` run out).
+//   dev[p]       initial device of incoming pod p (a feasible assignment)
+//   units[p]     its units (only equal-unit pods swap, so capacities stay valid)
+//   row[p], col[p]  its interference row / column (-1 = none), slo[p], pred[p], work[p]
+//   gpu[d]       physical GPU of device d (load is per GPU)
+//   res_*        residents: device, row, col, slo, pred (fixed), res_work per GPU via base_load
+//   M            interference matrix [rows x cols]
+py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | py::array::forcecast> dev_in,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> units,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> row,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> col,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> slo,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> pred,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> work,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> gpu,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> base_load,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> res_dev,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> res_row,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> res_col,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> res_slo,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> res_pred,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> M,
+                                     double max_load, int sweeps) {
+  const auto U = units.unchecked<1>();
+  const auto R = row.unchecked<1>();
+  const auto Cc = col.unchecked<1>();
+  const auto S = slo.unchecked<1>();
+  const auto Pd = pred.unchecked<1>();
+  const auto Wk = work.unchecked<1>();
+  const auto G = gpu.unchecked<1>();
+  const auto BL = base_load.unchecked<1>();
+  const auto RD = res_dev.unchecked<1>();
+  const auto RR = res_row.unchecked<1>();
+  const auto RC = res_col.unchecked<1>();
+  const auto RS = res_slo.unchecked<1>();
+  const auto RP = res_pred.unchecked<1>();
+  const auto Mx = M.unchecked<2>();
+  const py::ssize_t P = dev_in.shape(0), D = gpu.shape(0), NR = res_dev.shape(0);
+  if (U.shape(0) != P || R.shape(0) != P || Cc.shape(0) != P || S.shape(0) != P || Pd.shape(0) != P ||
+      Wk.shape(0) != P)
+    throw std::runtime_error("plan_assignment: pod array shapes differ");
+  if (RR.shape(0) != NR || RC.shape(0) != NR || RS.shape(0) != NR || RP.shape(0) != NR)
+    throw std::runtime_error("plan_assignment: resident array shapes differ");
+  int n_gpu = 0;
+  for (py::ssize_t d = 0; d < D; ++d) n_gpu = std::max(n_gpu, G(d) + 1);
+  if (BL.shape(0) < n_gpu) throw std::runtime_error("plan_assignment: base_load shorter than GPU count");
+  std::vector<int32_t> dev(dev_in.data(), dev_in.data() + P);
+  for (py::ssize_t p = 0; p < P; ++p)
+    if (dev[p] < 0 || dev[p] >= D) throw std::runtime_error("plan_assignment: device index out of range");
+  for (py::ssize_t r = 0; r < NR; ++r)
+    if (RD(r) < 0 || RD(r) >= D) throw std::runtime_error("plan_assignment: resident device out of range");
+  const py::ssize_t MR = Mx.shape(0), MC = Mx.shape(1);
+  auto m = [&](int r, int c) -> double { return (r >= 0 && c >= 0 && r < MR && c < MC) ? Mx(r, c) : 0.0; };
+
+  py::array_t<int32_t> out(P);
+  {
+    py::gil_scoped_release nogil;
+    // members of each device: incoming pods (>= 0) and residents (encoded -1 - r)
+    std::vector<std::vector<int>> mem(D);
+    for (py::ssize_t p = 0; p < P; ++p) mem[dev[p]].push_back((int)p);
+    for (py::ssize_t r = 0; r < NR; ++r) mem[RD(r)].push_back(-1 - (int)r);
+    std::vector<double> load(n_gpu, 0.0);
+    for (int g = 0; g < n_gpu; ++g) load[g] = BL(g);
+    for (py::ssize_t p = 0; p < P; ++p) load[G(dev[p])] += Wk(p);
+    // number of SLO-satisfied members of device d
+    auto ok_dev = [&](int d) {
+      int ok = 0;
+      const auto& v = mem[d];
+      for (int a : v) {
+        const int ra = a >= 0 ? R(a) : RR(-1 - a);
+        const double sa = a >= 0 ? S(a) : RS(-1 - a);
+        const double pa = a >= 0 ? Pd(a) : RP(-1 - a);
+        if (sa <= 0) { ++ok; continue; }
+        double intf = 0;
+        for (int b : v)
+          if (b != a) intf += m(ra, b >= 0 ? Cc(b) : RC(-1 - b));
+        ok += !(sa > pa - intf);
+      }
+      return ok;
+    };
+    auto swap_in = [&](int d, int from, int to) {
+      for (int& x : mem[d])
+        if (x == from) { x = to; return; }
+    };
+    for (int sw = 0; sw < sweeps; ++sw) {
+      bool improved = false;
+      for (py::ssize_t i = 0; i < P; ++i) {
+        for (py::ssize_t j = i + 1; j < P; ++j) {
+          const int di = dev[i], dj = dev[j];
+          if (di == dj || U(i) != U(j)) continue;
+          const int gi = G(di), gj = G(dj);
+          double li = load[gi], lj = load[gj];
+          if (gi != gj) {
+            li += Wk(j) - Wk(i);
+            lj += Wk(i) - Wk(j);
+            // never push a GPU over the cap (unless it was already over and this lowers it)
+            if ((li > max_load && li > load[gi]) || (lj > max_load && lj > load[gj])) continue;
+          }
+          const int before = ok_dev(di) + ok_dev(dj);
+          swap_in(di, (int)i, (int)j);
+          swap_in(dj, (int)j, (int)i);
+          const int after = ok_dev(di) + ok_dev(dj);
+          if (after > before) {
+            dev[i] = dj;
+            dev[j] = di;
+            load[gi] = li;
+            load[gj] = lj;
+            improved = true;
+          } else {
+            swap_in(di, (int)j, (int)i);
+            swap_in(dj, (int)i, (int)j);
+          }
+        }
+      }
+      if (!improved) break;
+    }
+  }
+  auto o = out.mutable_unchecked<1>();
+  for (py::ssize_t p = 0; p < P; ++p) o(p) = dev[p];
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_core, m) {
@@ -124,4 +255,8 @@ PYBIND11_MODULE(_core, m) {
   m.def("slo_scores", &slo_scores, py::arg("offsets"), py::arg("r_slo"), py::arg("r_pred"), py::arg("r_intf"),
         py::arg("inc_slo"), py::arg("inc_pred"), py::arg("inc_intf"));
   m.def("find_units", &find_units, py::arg("used"), py::arg("units"), py::arg("n"));
+  m.def("plan_assignment", &plan_assignment, py::arg("dev"), py::arg("units"), py::arg("row"), py::arg("col"),
+        py::arg("slo"), py::arg("pred"), py::arg("work"), py::arg("gpu"), py::arg("base_load"), py::arg("res_dev"),
+        py::arg("res_row"), py::arg("res_col"), py::arg("res_slo"), py::arg("res_pred"), py::arg("M"),
+        py::arg("max_load"), py::arg("sweeps") = 8);
 }
