@@ -15,8 +15,10 @@ pod together with every pending fractional pod of the queue:
    with free units / HBM (the balance objective);
 2. the native core (`_core.plan_assignment`) improves it with pairwise swaps that raise the
    number of pods -- incoming and resident -- predicted to meet their SLO under the
-   interference of their co-residents (the reference's `SLO > pred - intf` test), never
-   letting a GPU's predicted load exceed the initial plan's busiest GPU by more than
+   interference of their co-residents (the reference's `SLO > pred - intf` test), or keep
+   that number and lower the busier GPU's interference-adjusted load (alone work stretched
+   by the predicted slowdown `pred / (pred - intf)`: complementary pairs finish sooner),
+   never letting a GPU's adjusted load exceed the initial plan's busiest GPU by more than
    `planTolerance`.
 
 The plan is a hint: each pod still runs the full Filter/Score/Reserve cycle; Score ranks
@@ -57,14 +59,22 @@ class BurstPlanner:
         if hit is None or hit[0] != key:
             m = np.asarray([[intf.by_label[r].get(c, 0.0) for c in intf.columns] for r in intf.index], dtype=np.float64)
             self._mcache = hit = (key, (list(intf.index), list(intf.columns), np.nan_to_num(m)))
+            # a pod's interference lookup returns its row's dict object: row index by identity
+            self._row_of = {id(intf.by_label[r]): i for i, r in enumerate(intf.index)}
+            self._col_of = {c: j for j, c in enumerate(intf.columns)}
         return hit[1]
 
     def _ids(self, name: str, index: List[str], columns: List[str]) -> Tuple[int, int]:
-        model = self.plugin.args.model
-        lab = find_index_for_request(f"{name}_{model}".replace("-", "_"), index)
-        r = index.index(lab) if lab else -1
-        c = workload_column(name, dict.fromkeys(columns))
-        return r, (columns.index(c) if c is not None else -1)
+        """(interference row, column) of a pod: the row from the identity of the row dict its
+        (memoised) prediction lookup returned, the column by the recommender's substring
+        rule."""
+        _, intf = self.plugin._pod_predictions(name)
+        r = self._row_of.get(id(intf), -1) if intf else -1
+        if r < 0 and intf:
+            lab = find_index_for_request(f"{name}_{self.plugin.args.model}".replace("-", "_"), index)
+            r = index.index(lab) if lab else -1
+        c = self.plugin._workload_col(name, intf) if intf else workload_column(name, dict.fromkeys(columns))
+        return r, self._col_of.get(c, -1) if c is not None else -1
 
     # ---------------------------------------------------------------- plan
     def plan(self, pod: Obj, nodes: List[str]) -> Optional[Tuple[str, str]]:
@@ -142,7 +152,7 @@ class BurstPlanner:
             conf, _ = plugin._pod_predictions(O.name(p))
             items.append((plugin.pod_work(p, conf), p, req, conf))
         items.sort(key=lambda t: -t[0])
-        assign: List[Tuple[Any, Any, Any, int]] = []
+        assign: List[Tuple[Any, Any, Any, int, float]] = []
         for work, p, req, conf in items:
             best = None
             for d, st in enumerate(states):
@@ -157,29 +167,28 @@ class BurstPlanner:
             free_units[d] -= req.units
             free_hbm[d] -= req.hbm_gib
             load[gof[d]] += work
-            assign.append((p, req, conf, d))
+            assign.append((p, req, conf, d, work))
         if len(assign) < 2:
             return None
         n = len(assign)
         dev = np.array([a[3] for a in assign], dtype=np.int32)
         units = np.array([a[1].units for a in assign], dtype=np.int32)
         rows, cols, slo, pred, work = [], [], [], [], []
-        for p, req, conf, d in assign:
+        for p, req, conf, d, w in assign:
             r, c = self._ids(O.name(p), index, columns)
             rows.append(r)
             cols.append(c)
             slo.append(req.slo)
             pred.append(conf.get(plugin._col(req.units, states[d].device.units), -1.0) if conf else -1.0)
-            work.append(plugin.pod_work(p, conf))
-        max_load = max(load) * (1.0 + self.tolerance)
+            work.append(w)
         out = core.plan_assignment(
             dev, units, np.array(rows, dtype=np.int32), np.array(cols, dtype=np.int32),
             np.array(slo, dtype=np.float64), np.array(pred, dtype=np.float64), np.array(work, dtype=np.float64),
             np.array(gof, dtype=np.int32), np.array(base_load, dtype=np.float64),
             np.array(res_dev, dtype=np.int32), np.array(res_row, dtype=np.int32), np.array(res_col, dtype=np.int32),
-            np.array(res_slo, dtype=np.float64), np.array(res_pred, dtype=np.float64), M, float(max_load),
-            self.sweeps)
-        for (p, _, _, _), d in zip(assign, out[:n]):
+            np.array(res_slo, dtype=np.float64), np.array(res_pred, dtype=np.float64), M, 0.0,
+            self.sweeps, float(self.tolerance))
+        for (p, _, _, _, _), d in zip(assign, out[:n]):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
             plugin._pending_by_key[O.key(p)] = p
         self.planned_bursts += 1

@@ -376,15 +376,30 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                         (tv, int(time.monotonic()) if (tv and stale) else 0), sig)
                 if hit[0] != skey:
                     hit = None
-            choice = hit[1] if hit is not None else self._best_choice(state, pod, req, nn, scoring=True)
-            if plan is not None:
-                choice = self._apply_plan(state, req, nn, choice)
+            planned = self._planned_choice(state, req, nn, plan) if plan is not None else None
+            if planned is not None:         # the plan decides on its node: no scoring needed
+                choice = planned
+            else:
+                choice = hit[1] if hit is not None else self._best_choice(state, pod, req, nn, scoring=True)
+                if plan is not None:
+                    choice = self._apply_plan(state, req, nn, choice)
             if choice is None:
                 out.append(0)
                 continue
             choices[nn] = choice
             out.append(max(lo, min(hi, int(choice.score))))
         return out, None
+
+    def _planned_choice(self, state: CycleState, req: GpuRequest, node: str, plan: Any) -> Optional[Choice]:
+        """The plan's device on its node as a top-scored Choice, if it is still a candidate."""
+        pnode, puuid = plan
+        if node != pnode:
+            return None
+        for st, u0 in (state.read(_CANDS) or {}).get(node) or []:
+            if st.device.uuid == puuid:
+                return Choice(node, [(puuid, u0, req.units, req.hbm_gib, False)], float(C.MAX_NODE_SCORE),
+                              [st.device])
+        return None
 
     def _apply_plan(self, state: CycleState, req: GpuRequest, node: str,
                     choice: Optional[Choice]) -> Optional[Choice]:
@@ -394,13 +409,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         plan = state.read(_PLAN)
         if plan is None:
             return choice
-        pnode, puuid = plan
-        if node == pnode:
-            for st, u0 in (state.read(_CANDS) or {}).get(node) or []:
-                if st.device.uuid == puuid:
-                    return Choice(node, [(puuid, u0, req.units, req.hbm_gib, False)], float(C.MAX_NODE_SCORE),
-                                  [st.device])
-            return choice
+        if node == plan[0]:
+            return self._planned_choice(state, req, node, plan) or choice
         if choice is not None and choice.score > C.MAX_NODE_SCORE - 1:
             choice = dataclasses.replace(choice, score=float(C.MAX_NODE_SCORE - 1))
         return choice

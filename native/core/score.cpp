@@ -148,7 +148,7 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
                                      py::array_t<double, py::array::c_style | py::array::forcecast> res_slo,
                                      py::array_t<double, py::array::c_style | py::array::forcecast> res_pred,
                                      py::array_t<double, py::array::c_style | py::array::forcecast> M,
-                                     double max_load, int sweeps) {
+                                     double max_load, int sweeps, double tolerance) {
   const auto U = units.unchecked<1>();
   const auto R = row.unchecked<1>();
   const auto Cc = col.unchecked<1>();
@@ -187,29 +187,41 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
     std::vector<std::vector<int>> mem(D);
     for (py::ssize_t p = 0; p < P; ++p) mem[dev[p]].push_back((int)p);
     for (py::ssize_t r = 0; r < NR; ++r) mem[RD(r)].push_back(-1 - (int)r);
-    std::vector<double> load(n_gpu, 0.0);
-    for (int g = 0; g < n_gpu; ++g) load[g] = BL(g);
-    for (py::ssize_t p = 0; p < P; ++p) load[G(dev[p])] += Wk(p);
-    // number of SLO-satisfied members of device d
-    auto ok_dev = [&](int d) {
-      int ok = 0;
+    // number of SLO-satisfied members of device d, and its interference-adjusted work: an
+    // incoming pod's alone work stretched by its predicted slowdown pred / (pred - intf)
+    // (capped at 4x) -- co-located pods share the device, so pairing complementary
+    // workloads shortens the device's busy time, which is what paces a coupled epoch
+    auto eval_dev = [&](int d, int& ok, double& adj) {
+      ok = 0;
+      adj = 0.0;
       const auto& v = mem[d];
       for (int a : v) {
         const int ra = a >= 0 ? R(a) : RR(-1 - a);
         const double sa = a >= 0 ? S(a) : RS(-1 - a);
         const double pa = a >= 0 ? Pd(a) : RP(-1 - a);
-        if (sa <= 0) { ++ok; continue; }
         double intf = 0;
         for (int b : v)
           if (b != a) intf += m(ra, b >= 0 ? Cc(b) : RC(-1 - b));
-        ok += !(sa > pa - intf);
+        ok += sa <= 0 || !(sa > pa - intf);
+        if (a >= 0) adj += pa > 0 ? Wk(a) * pa / std::max(pa - intf, 0.25 * pa) : Wk(a);
       }
-      return ok;
     };
+    std::vector<int> okd(D, 0);
+    std::vector<double> adjd(D, 0.0), load(n_gpu, 0.0);
+    for (int g = 0; g < n_gpu; ++g) load[g] = BL(g);
+    for (py::ssize_t d = 0; d < D; ++d) {
+      eval_dev((int)d, okd[d], adjd[d]);
+      load[G(d)] += adjd[d];
+    }
+    double cap = max_load;
+    if (tolerance >= 0) cap = (1.0 + tolerance) * *std::max_element(load.begin(), load.end());
     auto swap_in = [&](int d, int from, int to) {
       for (int& x : mem[d])
         if (x == from) { x = to; return; }
     };
+    // first-improvement pairwise swaps of equal-size pods on different devices: accept a
+    // swap that meets more SLOs without pushing a GPU over the cap (unless it lowers an
+    // over-cap GPU), or meets as many and lowers the pair's busier GPU
     for (int sw = 0; sw < sweeps; ++sw) {
       bool improved = false;
       for (py::ssize_t i = 0; i < P; ++i) {
@@ -217,20 +229,25 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
           const int di = dev[i], dj = dev[j];
           if (di == dj || U(i) != U(j)) continue;
           const int gi = G(di), gj = G(dj);
-          double li = load[gi], lj = load[gj];
-          if (gi != gj) {
-            li += Wk(j) - Wk(i);
-            lj += Wk(i) - Wk(j);
-            // never push a GPU over the cap (unless it was already over and this lowers it)
-            if ((li > max_load && li > load[gi]) || (lj > max_load && lj > load[gj])) continue;
-          }
-          const int before = ok_dev(di) + ok_dev(dj);
           swap_in(di, (int)i, (int)j);
           swap_in(dj, (int)j, (int)i);
-          const int after = ok_dev(di) + ok_dev(dj);
-          if (after > before) {
+          int oki, okj;
+          double ai, aj;
+          eval_dev(di, oki, ai);
+          eval_dev(dj, okj, aj);
+          double li = load[gi] + ai - adjd[di], lj = load[gj] + aj - adjd[dj];
+          if (gi == gj) li = lj = load[gi] + ai - adjd[di] + aj - adjd[dj];
+          const int before = okd[di] + okd[dj], after = oki + okj;
+          const double mb = std::max(load[gi], load[gj]), ma = std::max(li, lj);
+          const bool over = (li > cap && li > load[gi] + 1e-12) || (lj > cap && lj > load[gj] + 1e-12);
+          const bool take = !over && (after > before || (after == before && ma < mb * (1.0 - 1e-9)));
+          if (take) {
             dev[i] = dj;
             dev[j] = di;
+            okd[di] = oki;
+            okd[dj] = okj;
+            adjd[di] = ai;
+            adjd[dj] = aj;
             load[gi] = li;
             load[gj] = lj;
             improved = true;
@@ -258,5 +275,5 @@ PYBIND11_MODULE(_core, m) {
   m.def("plan_assignment", &plan_assignment, py::arg("dev"), py::arg("units"), py::arg("row"), py::arg("col"),
         py::arg("slo"), py::arg("pred"), py::arg("work"), py::arg("gpu"), py::arg("base_load"), py::arg("res_dev"),
         py::arg("res_row"), py::arg("res_col"), py::arg("res_slo"), py::arg("res_pred"), py::arg("M"),
-        py::arg("max_load"), py::arg("sweeps") = 8);
+        py::arg("max_load"), py::arg("sweeps") = 8, py::arg("tolerance") = -1.0);
 }

@@ -70,6 +70,21 @@ def test_native_planner_respects_load_cap_and_units():
         _plan([0, 7], [2, 2], [0, 1], [0, 1], [1.0, 1.0], [2.0, 2.0], [1.0, 1.0], [0, 1], [0.0, 0.0], M, 9.0)
 
 
+def test_native_planner_lowers_interference_adjusted_load_when_slos_tie():
+    """No SLOs to win: the swap search still pairs complementary pods, because a GPU's load
+    is its pods' alone work stretched by the predicted slowdown pred / (pred - intf)."""
+    row = col = [0, 0, 1, 1]
+    slo, pred = [0.0] * 4, [100.0] * 4
+    # start: both memory pods on GPU 0 (each stretched 100/40 = 2.5x), compute pods on GPU 1
+    out = list(core.plan_assignment(np.array([0, 0, 1, 1], I32), np.array([2] * 4, I32), np.array(row, I32),
+                                    np.array(col, I32), np.array(slo, F64), np.array(pred, F64),
+                                    np.array([1.0] * 4, F64), np.array([0, 1], I32), np.array([0.0, 0.0], F64),
+                                    np.array([], I32), np.array([], I32), np.array([], I32), np.array([], F64),
+                                    np.array([], F64), np.array(M, F64), 0.0, 8, 0.0))
+    assert sorted(out[:2]) != [0, 0] and sorted(out) == [0, 0, 1, 1]
+    assert out[0] != out[1]                               # the memory pods now sit apart
+
+
 def test_native_planner_counts_residents():
     row = col = [0, 1]
     slo, pred = [90.0, 90.0], [100.0, 100.0]
