@@ -1,7 +1,7 @@
 """Torch-facing wrappers for the HIP load kernels (native/hip/loadgen.hip).
 
-`gemm(a, bt)` computes act(a @ bt.T + bias) in bf16 on MFMA; `triad(a, b, c, s)` streams
-HBM.  Shapes are validated on the host before launch (the kernels have no bounds checks
+`gemm(a, bt)` computes act(a @ bt.T + bias) in bf16 on MFMA, `gemm_fp8` the same with OCP
+e4m3fn operands on the block-scaled fp8 MFMA; `triad(a, b, c, s)` streams HBM.  Shapes are validated on the host before launch (the kernels have no bounds checks
 by design).  On a GPU box the native module is mandatory: there is no PyTorch fallback
 path here (tests compare against torch fp32 references instead).
 """
@@ -53,6 +53,40 @@ def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, 
         bptr = bias.data_ptr()
     _native.hip().gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
                                bt.stride(0), out.stride(0), relu, _stream_ptr(stream), cu_budget)
+    return out
+
+
+FP8 = torch.float8_e4m3fn          # OCP e4m3 (gfx950), not the MI300 "fnuz" encoding
+
+
+def gemm_fp8(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None,
+             bias: Optional[torch.Tensor] = None, relu: bool = False, stream: Optional[torch.cuda.Stream] = None,
+             cu_budget: int = 0) -> torch.Tensor:
+    """out[M,N] = act(a[M,K] @ bt[N,K]^T + bias[N]) -- e4m3fn operands, fp32 accumulate, bf16
+    out, on the block-scaled fp8 MFMA (unit scales).  M, N multiples of 64, K of 128."""
+    if a.dtype != FP8 or bt.dtype != FP8:
+        raise TypeError("gemm_fp8 expects float8_e4m3fn operands")
+    if not (a.is_cuda and bt.is_cuda):
+        raise ValueError("gemm_fp8 expects device tensors")
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"gemm_fp8 shape mismatch {tuple(a.shape)} x {tuple(bt.shape)}^T")
+    if a.stride(1) != 1 or bt.stride(1) != 1 or a.stride(0) % 16 or bt.stride(0) % 16:
+        raise ValueError("gemm_fp8 expects row-major operands with 16-byte aligned rows")
+    M, K = a.shape
+    N = bt.shape[0]
+    if M <= 0 or N <= 0 or K <= 0 or M % 64 or N % 64 or K % 128:
+        raise ValueError(f"gemm_fp8 shape ({M},{N},{K}) must be positive multiples of (64,64,128)")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise ValueError("bad output tensor")
+    bptr = 0
+    if bias is not None:
+        if bias.dtype != torch.float32 or bias.numel() != N or not bias.is_contiguous():
+            raise ValueError("bias must be a contiguous fp32 vector of length N")
+        bptr = bias.data_ptr()
+    _native.hip().gemm_fp8_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
+                              bt.stride(0), out.stride(0), relu, _stream_ptr(stream), cu_budget)
     return out
 
 

@@ -23,6 +23,8 @@ std::vector<uint32_t> get_stream_mask(uintptr_t s);
 std::vector<uint32_t> probe_xcd(uintptr_t stream, int n);
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
                   int ldc, bool relu, uintptr_t stream, int cu_budget);
+void gemm_fp8_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
+                 int ldc, bool relu, uintptr_t stream, int cu_budget);
 void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream);
 void set_triad_variant(int v);
 void set_gemm_tile(int t);

@@ -51,6 +51,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_bf16_nt", &gs::gemm_bf16_nt, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("bias"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("relu"),
         py::arg("stream"), py::arg("cu_budget") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_fp8_nt", &gs::gemm_fp8_nt, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("bias"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("relu"),
+        py::arg("stream"), py::arg("cu_budget") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("stream_triad", &gs::stream_triad, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("s"),
         py::arg("n_floats"), py::arg("blocks"), py::arg("stream"), py::call_guard<py::gil_scoped_release>());
   m.def("set_triad_variant", &gs::set_triad_variant, py::arg("variant"));

@@ -15,6 +15,8 @@
 //    Epilogue fuses bias + ReLU and stores packed bf16x4.  Lone large GEMMs use a separate
 //    256x256 "8-phase" kernel (gemm_bf16_nt_256_8ph: two staggered wave groups, one
 //    half-tile of glds per phase, counted vmcnt).
+//  * gemm_fp8_nt -- the same GEMM with OCP e4m3fn operands on the block-scaled
+//    v_mfma_scale_f32_16x16x128_f8f6f4 (unit scales): 2x the bf16 MFMA rate.
 //  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
 #include <cstdint>
 
@@ -212,6 +214,116 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   }
 
   // ---- epilogue (D = C^T layout): row m = lane&15, cols n..n+3 = (lane>>4)*4 + r ----
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + fk * 4;
+    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + col);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = m0 + wm * WTM + i * 16 + frow;
+      f32x4 v = acc[i][j] + bv;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+      *reinterpret_cast<bf16x4*>(C + (size_t)row * ldc + col) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// FP8 (OCP e4m3fn) GEMM: C[M,N] = act(A[M,K] . Bt[N,K]^T (+bias)), fp8 in / f32 accumulate /
+// bf16 out, on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4 with unit scales
+// (e8m0 127 = 2^0): twice the bf16 rate per clock (MI355X_MICROARCH.md "Matrix cores"),
+// where the non-scaled 16x16x32 fp8 form only matches bf16.  A K tile is 128 fp8 = 128 B per
+// row -- byte for byte the bf16 kernel's 64-deep tile -- so staging reuses stage_tile (the
+// fp8 rows are moved as 16-byte chunks through a bf16 view with half the K) and the same
+// XOR-swizzled, conflict-free LDS image.  One MFMA consumes a whole K tile: lane group
+// fk = lane>>4 supplies 32 k values, read as the two 16-B chunks 2fk and 2fk+1 of its row.
+// Which k a lane byte stands for does not matter as long as A and B agree (they are read
+// with the same map), so no k permutation is needed.  Epilogue as the bf16 kernel (D = C^T
+// layout, packed bf16x4 stores, fused bias + ReLU).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int kUnitScale = 0x7F7F7F7F;   // e8m0 1.0 in every byte (any OPSEL picks 127)
+
+__device__ __forceinline__ i32x8 lds_frag_fp8(const char* lds_tile, int row, int fk) {
+  const i32x4 lo = __builtin_bit_cast(i32x4, lds_frag<BK>(lds_tile, row, 2 * fk));
+  const i32x4 hi = __builtin_bit_cast(i32x4, lds_frag<BK>(lds_tile, row, 2 * fk + 1));
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS>
+__global__ void __launch_bounds__(WGM * WGN * 64, OCC)
+gemm_fp8_nt_kernel(const uint8_t* __restrict__ A8, const uint8_t* __restrict__ B8, __bf16* __restrict__ C,
+                   const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int KT8 = 128;                             // fp8 elements (bytes) per K tile
+  constexpr int A_BYTES = BM * KT8, B_BYTES = BN * KT8;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MI = WTM / 16, NJ = WTN / 16;
+  static_assert(A_BYTES / 16 % NT == 0 && B_BYTES / 16 % NT == 0, "stage split");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  // bf16 views of the fp8 rows for the 16-byte glds staging (K and ld halved)
+  const __bf16* A = reinterpret_cast<const __bf16*>(A8);
+  const __bf16* Bt = reinterpret_cast<const __bf16*>(B8);
+  const int lda2 = lda / 2, ldb2 = ldb / 2;
+
+  const int nwg = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b % kXcds;
+  const int q = nwg / kXcds, rem = nwg % kXcds;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (wgid % per_group) % gsize;
+  const int tn = (wgid % per_group) / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wm = wave / WGN, wn = wave % WGN;
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto tileA = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES); };
+  auto tileB = [&](int buf) { return smem + buf * (A_BYTES + B_BYTES) + A_BYTES; };
+  const int frow = lane & 15;
+  const int fk = lane >> 4;
+  auto stage = [&](int t, int buf) {
+    stage_tile<BM, NT, BK>(A, lda2, m0, t * BK, tileA(buf), wave, lane);
+    stage_tile<BN, NT, BK>(Bt, ldb2, n0, t * BK, tileB(buf), wave, lane);
+  };
+  auto compute = [&](const char* a_t, const char* b_t) {
+    i32x8 af[MI], bf[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[j] = lds_frag_fp8(b_t, wn * WTN + j * 16 + frow, fk);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[i] = lds_frag_fp8(a_t, wm * WTM + i * 16 + frow, fk);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[i][j], 0, 0, 0, kUnitScale,
+                                                                      0, kUnitScale);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const int nt = K / KT8;
+  stage(0, 0);
+  __syncthreads();
+  int buf = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) stage(t + 1, buf ^ 1);
+    compute(tileA(buf), tileB(buf));
+    __syncthreads();
+    buf ^= 1;
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = n0 + wn * WTN + j * 16 + fk * 4;
@@ -586,6 +698,49 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     }
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int BM, int BN, int WGM, int WGN, int OCC>
+static void launch_gemm_fp8(const uint8_t* A, const uint8_t* B, __bf16* Cp, const float* bp, int M, int N, int K,
+                            int lda, int ldb, int ldc, bool relu, hipStream_t s) {
+  const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
+  if (relu && bp)
+    hipLaunchKernelGGL((gemm_fp8_nt_kernel<BM, BN, WGM, WGN, OCC, true, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
+                       K, lda, ldb, ldc);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_fp8_nt_kernel<BM, BN, WGM, WGN, OCC, true, false>), grid, block, 0, s, A, B, Cp, bp, M,
+                       N, K, lda, ldb, ldc);
+  else if (bp)
+    hipLaunchKernelGGL((gemm_fp8_nt_kernel<BM, BN, WGM, WGN, OCC, false, true>), grid, block, 0, s, A, B, Cp, bp, M,
+                       N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((gemm_fp8_nt_kernel<BM, BN, WGM, WGN, OCC, false, false>), grid, block, 0, s, A, B, Cp, bp, M,
+                       N, K, lda, ldb, ldc);
+}
+
+void gemm_fp8_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
+                 int ldc, bool relu, uintptr_t stream, int cu_budget) {
+  if (M <= 0 || N <= 0 || K <= 0) throw std::runtime_error("gemm_fp8: empty shape");
+  if (M % 64 || N % 64 || K % 128) throw std::runtime_error("gemm_fp8: M,N must be multiples of 64 and K of 128");
+  if (lda < K || ldb < K || ldc < N || lda % 16 || ldb % 16) throw std::runtime_error("gemm_fp8: bad leading dims");
+  check_align(reinterpret_cast<void*>(a), "A");
+  check_align(reinterpret_cast<void*>(bt), "Bt");
+  if (ldc % 4 || reinterpret_cast<uintptr_t>(c) % 8) throw std::runtime_error("gemm_fp8: C rows must be 8-byte aligned");
+  if (bias) check_align(reinterpret_cast<void*>(bias), "bias");
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  auto A = reinterpret_cast<const uint8_t*>(a);
+  auto B = reinterpret_cast<const uint8_t*>(bt);
+  auto Cp = reinterpret_cast<__bf16*>(c);
+  auto bp = reinterpret_cast<const float*>(bias);
+  // same fill rule as the bf16 picker: 128x128 when it gives every CU of the budget a
+  // block (two for a lone kernel), else 64x64
+  const bool alone = cu_budget <= 0 || cu_budget >= kCus;
+  const int need = alone ? 2 * kCus : cu_budget;
+  if (M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= need)
+    launch_gemm_fp8<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
+  else
+    launch_gemm_fp8<64, 64, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
   HIP_CHECK(hipGetLastError());
 }
 

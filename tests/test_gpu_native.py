@@ -99,6 +99,38 @@ def test_gemm_layout_identity_asymmetric():
     assert torch.equal(out.float(), bt.float().T)
 
 
+@pytest.mark.parametrize("M,N,K,relu,bias", [(64, 64, 128, False, False), (128, 128, 256, True, True),
+                                             (384, 640, 384, False, True), (1024, 2048, 2048, True, False),
+                                             (4096, 4096, 1024, False, False)])
+def test_gemm_fp8_matches_fp32_reference(M, N, K, relu, bias):
+    """Block-scaled fp8 MFMA GEMM (unit scales) vs fp32 matmul of the same e4m3fn values
+    (both 64x64 and 128x128 tiles are hit by these shapes)."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).to(loadgen.FP8)
+    bt = torch.randn(N, K, device="cuda", generator=g).to(loadgen.FP8)
+    b = torch.randn(N, device="cuda", generator=g) if bias else None
+    out = loadgen.gemm_fp8(a, bt, bias=b, relu=relu)
+    ref = a.float() @ bt.float().T + (b if bias else 0)
+    if relu:
+        ref = torch.relu(ref)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 0.01 * ref.abs().max().item() + 1e-2, err
+
+
+def test_gemm_fp8_layout_identity_asymmetric():
+    """A = I (exact in e4m3) with an asymmetric integer B (0..15, exact in e4m3 and bf16)
+    pins the C layout and the k pairing of the A/B fragments: the result must be exact."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    for n in (128, 256, 640):
+        a = torch.eye(n, device="cuda").to(loadgen.FP8)
+        bt = (torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n) % 16).to(loadgen.FP8)
+        assert torch.equal(loadgen.gemm_fp8(a, bt).float(), bt.float().T), n
+    with pytest.raises(ValueError):
+        loadgen.gemm_fp8(torch.zeros(128, 64, device="cuda").to(loadgen.FP8),
+                         torch.zeros(128, 64, device="cuda").to(loadgen.FP8))
+
+
 def test_gemm_rejects_bad_shapes():
     from k8s_gpu_scheduler_amd.ops import loadgen
     a = torch.zeros(100, 64, device="cuda", dtype=torch.bfloat16)
