@@ -252,6 +252,12 @@ class ControlPlane:
                 gfx_activity=min(1.0, busy), vram_used_mb=float(per_gpu[g][3]) * 1024.0))
 
 
+# best rates measured on one MI355X: 8-phase bf16 GEMM at 8192^3 (profiles/r01_gemm_big.json)
+# and the non-temporal stream triad from HBM (profiles/r01_triad_pmc.txt)
+ACHIEVABLE_TFLOPS = 1434.0
+ACHIEVABLE_TBPS = 6.5
+
+
 class SimExecutor:
     """CPU stand-in for DeviceExecutor (tests / no-GPU runs).
 
@@ -268,6 +274,7 @@ class SimExecutor:
 
     def __init__(self, timed: bool = False, scale: float = 1.0) -> None:
         self.flops_done = 0.0
+        self.bytes_done = 0.0
         self.pending: List[Any] = []
         self.timed, self.scale = timed, scale
         self._dev_free = 0.0
@@ -304,6 +311,7 @@ class SimExecutor:
             if not self.timed:
                 r.ms = W.roofline_seconds(w, r.n_units / 8.0) * r.iters * 1e3
             self.flops_done += w.flops * r.iters
+            self.bytes_done += w.bytes * r.iters
         self.pending = runs
 
     def collect(self, runs) -> Dict[str, float]:
@@ -567,7 +575,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         ref["ev"] = torch.cuda.Event(enable_timing=True)
         ref["ev"].record(side)
-    flops0 = ex.flops_done
+    flops0, bytes0 = ex.flops_done, ex.bytes_done
     if rank == 0:
         if async_cp:
             cp.reset_stats()
@@ -584,14 +592,20 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         # simulated executor: wall time = modelled device time of each epoch (+ host time)
         elapsed = max(elapsed, 1e-9)
     busy_ms = _union_ms(intervals)
-    flops = torch.tensor([ex.flops_done - flops0, elapsed, busy_ms], dtype=torch.float64, device=dev)
+    # roofline floor of this rank's work: its GEMM FLOPs at the MFMA rate or its modelled HBM
+    # bytes at the HBM rate, whichever is longer (perfect overlap of the two)
+    fl_r, by_r = ex.flops_done - flops0, ex.bytes_done - bytes0
+    floor_peak = max(fl_r / (C.MI355X_BF16_DENSE_TFLOPS * 1e12), by_r / (C.MI355X_HBM_TBPS * 1e12))
+    floor_ach = max(fl_r / (ACHIEVABLE_TFLOPS * 1e12), by_r / (ACHIEVABLE_TBPS * 1e12))
+    flops = torch.tensor([fl_r, elapsed, busy_ms, by_r, floor_peak, floor_ach], dtype=torch.float64, device=dev)
     if world > 1:
-        summed = flops[[0, 2]].clone()
+        summed = flops[[0, 2, 3]].clone()
         dist.all_reduce(summed, op=dist.ReduceOp.SUM)
-        el = flops[1:2].clone()
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        flops = torch.stack([summed[0], el[0], summed[1]])
+        mx = flops[[1, 4, 5]].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)       # the busiest rank paces the step
+        flops = torch.stack([summed[0], mx[0], summed[1], summed[2], mx[1], mx[2]])
     flops_tot, elapsed, busy_tot_ms = float(flops[0]), float(flops[1]), float(flops[2])
+    bytes_tot, floor_peak, floor_ach = float(flops[3]), float(flops[4]), float(flops[5])
     result: Dict[str, Any] = {}
     if rank == 0:
         pods_per_s = totals["pods"] / elapsed
@@ -615,6 +629,14 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "cu_share_occupancy_pct": round(occ, 2),
             "mfma_util_pct": round(mfma, 2),
             "achieved_tflops": round(flops_tot / elapsed / 1e12, 1),
+            "achieved_hbm_tbps_per_gpu": round(bytes_tot / elapsed / n_gpus / 1e12, 2),
+            # speed of light: the step time if every GPU's FLOPs and modelled HBM bytes of the
+            # timed pods ran at the hardware peaks (2.5 PF bf16, 8 TB/s) / at the best rates
+            # measured on MI355X (1434 TF GEMM, 6.5 TB/s stream), fully overlapped
+            "roofline_floor_ms_per_step": {"peak": round(floor_peak / a.steps * 1e3, 3),
+                                           "achievable": round(floor_ach / a.steps * 1e3, 3)},
+            "sol_pct": {"peak": round(100.0 * floor_peak / elapsed, 1),
+                        "achievable": round(100.0 * floor_ach / elapsed, 1)},
             "slo_attainment_pct": round(100.0 * totals["slo_ok"] / max(totals["pods"], 1), 2),
             "sched_ms_per_pod": round(cp.sched_s / max(totals["pods"], 1) * 1e3, 4),
             "interference_mae": cp.interference_mae(),
