@@ -97,7 +97,7 @@ class ControlPlane:
     def __init__(self, n_gpus: int, pods_per_gpu: int, iters: int, seed: int, policy: str = "gpu",
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
-                 plan_tolerance: float = 0.05):
+                 plan_tolerance: float = 0.05, plan_objective: str = "slo"):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -111,7 +111,7 @@ class ControlPlane:
         self.predictions = predictions or measured_predictions() or analytic_predictions()
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
-                "plan_tolerance": plan_tolerance}
+                "plan_tolerance": plan_tolerance, "plan_objective": plan_objective}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
         # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
@@ -394,10 +394,14 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--sim-timed", action="store_true",
                     help="simulated executor sleeps out a modelled device time per epoch (multi-rank CPU rehearsal)")
     ap.add_argument("--sim-scale", type=float, default=1.0, help="modelled device-time multiplier (--sim-timed)")
-    ap.add_argument("--plan-bursts", type=int, default=0, choices=[0, 1],
-                    help="1: plan each epoch's burst of pods jointly (SLO-aware pairing under predicted "
-                         "interference, within --plan-tolerance of the balanced load).  Off by default: "
-                         "it trades ~2.5%% pods/s for SLO attainment (profiles/r01_plan_ab.txt)")
+    ap.add_argument("--plan-bursts", type=int, default=1, choices=[0, 1],
+                    help="1: plan each epoch's burst of pods jointly (pairings chosen by predicted "
+                         "interference: see --plan-objective).  On MI355X this lowers the slowest GPU's "
+                         "epoch time of an 8-GPU node by 6-7%% (tools/virtual_node_bench.py, "
+                         "profiles/r01_virtual_node_*.json)")
+    ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
+                    help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
+                         "'slo' = most predicted SLOs met first (within --plan-tolerance)")
     ap.add_argument("--plan-tolerance", type=float, default=0.05,
                     help="burst planner: max predicted load of any GPU over the balanced plan's busiest")
     ap.add_argument("--balance", type=float, default=1.0,
@@ -429,7 +433,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     n_gpus_planned = world if world > 1 else max(1, a.gpus if a.sim else 1)
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
-                     plan_tolerance=a.plan_tolerance)
+                     plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -623,7 +627,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                        "global_batch": P, "seq_len": a.iters, "parallelism": f"dp{n_gpus}",
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
                        "balance": a.balance, "plan_bursts": a.plan_bursts,
-                       "plan_tolerance": a.plan_tolerance,
+                       "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
                        "note": "global_batch = pods per scheduling epoch; seq_len = query batches per pod"},
             "gpu_util_pct": round(util, 2),
             "cu_share_occupancy_pct": round(occ, 2),

@@ -39,9 +39,12 @@ Obj = Dict[str, Any]
 
 
 class BurstPlanner:
-    def __init__(self, plugin: Any, tolerance: float = 0.05, sweeps: int = 8):
+    def __init__(self, plugin: Any, tolerance: float = 0.05, sweeps: int = 8, objective: str = "slo"):
+        if objective not in ("slo", "load"):
+            raise ValueError(f"plan objective must be 'slo' or 'load', not {objective!r}")
         self.plugin = plugin
         self.tolerance = tolerance
+        self.load_first = objective == "load"
         self.sweeps = sweeps
         self.plans: Dict[str, Tuple[str, str]] = {}      # pod key -> (node, device uuid)
         self.planned_bursts = 0
@@ -187,7 +190,7 @@ class BurstPlanner:
             np.array(gof, dtype=np.int32), np.array(base_load, dtype=np.float64),
             np.array(res_dev, dtype=np.int32), np.array(res_row, dtype=np.int32), np.array(res_col, dtype=np.int32),
             np.array(res_slo, dtype=np.float64), np.array(res_pred, dtype=np.float64), M, 0.0,
-            self.sweeps, float(self.tolerance))
+            self.sweeps, float(self.tolerance), int(self.load_first))
         for (p, _, _, _, _), d in zip(assign, out[:n]):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
             plugin._pending_by_key[O.key(p)] = p

@@ -96,6 +96,9 @@ class GPUArgs:
     # keep predicted SLOs under interference, within planTolerance of the balanced load
     plan_bursts: bool = False
     plan_tolerance: float = 0.05
+    # "slo": most predicted SLOs met first, then the lower busier GPU; "load": the lower
+    # interference-adjusted load of the busier GPU first, SLO count as the tie-break
+    plan_objective: str = "slo"
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
@@ -117,6 +120,7 @@ class GPUArgs:
         alias = {"weightSLO": "w_slo", "weightPack": "w_pack", "weightTelemetry": "w_telemetry",
                  "weightBalance": "w_balance", "lptWindowSeconds": "lpt_window_s",
                  "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
+                 "planObjective": "plan_objective",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle"}
@@ -152,7 +156,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self.planner = None
         if self.args.plan_bursts:
             from .planner import BurstPlanner
-            self.planner = BurstPlanner(self, self.args.plan_tolerance)
+            self.planner = BurstPlanner(self, self.args.plan_tolerance, objective=self.args.plan_objective)
         self._pred_version: Any = None
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)

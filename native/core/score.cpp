@@ -148,7 +148,7 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
                                      py::array_t<double, py::array::c_style | py::array::forcecast> res_slo,
                                      py::array_t<double, py::array::c_style | py::array::forcecast> res_pred,
                                      py::array_t<double, py::array::c_style | py::array::forcecast> M,
-                                     double max_load, int sweeps, double tolerance) {
+                                     double max_load, int sweeps, double tolerance, int load_first) {
   const auto U = units.unchecked<1>();
   const auto R = row.unchecked<1>();
   const auto Cc = col.unchecked<1>();
@@ -240,7 +240,10 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
           const int before = okd[di] + okd[dj], after = oki + okj;
           const double mb = std::max(load[gi], load[gj]), ma = std::max(li, lj);
           const bool over = (li > cap && li > load[gi] + 1e-12) || (lj > cap && lj > load[gj] + 1e-12);
-          const bool take = !over && (after > before || (after == before && ma < mb * (1.0 - 1e-9)));
+          // load_first: lower the pair's busier GPU first, SLO count as the tie-break
+          const bool take = load_first
+                                ? (ma < mb * (1.0 - 1e-9) || (ma <= mb * (1.0 + 1e-9) && after > before))
+                                : !over && (after > before || (after == before && ma < mb * (1.0 - 1e-9)));
           if (take) {
             dev[i] = dj;
             dev[j] = di;
@@ -275,5 +278,5 @@ PYBIND11_MODULE(_core, m) {
   m.def("plan_assignment", &plan_assignment, py::arg("dev"), py::arg("units"), py::arg("row"), py::arg("col"),
         py::arg("slo"), py::arg("pred"), py::arg("work"), py::arg("gpu"), py::arg("base_load"), py::arg("res_dev"),
         py::arg("res_row"), py::arg("res_col"), py::arg("res_slo"), py::arg("res_pred"), py::arg("M"),
-        py::arg("max_load"), py::arg("sweeps") = 8, py::arg("tolerance") = -1.0);
+        py::arg("max_load"), py::arg("sweeps") = 8, py::arg("tolerance") = -1.0, py::arg("load_first") = 0);
 }

@@ -155,7 +155,7 @@ def test_bench_timed_sim_four_ranks_balance_improves_throughput(tmp_path):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
                "--master-addr", "127.0.0.1", "--master-port", str(29621 + bal), os.path.join(ROOT, "bench.py"),
                "--sim-timed", "--sim-scale", "2", "--gpus", "4", "--steps", "16", "--warmup", "3",
-               "--balance", str(bal)]
+               "--balance", str(bal), "--plan-bursts", "0"]
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
         assert p.returncode == 0, p.stderr[-3000:]
         res[bal] = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])

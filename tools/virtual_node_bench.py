@@ -1,0 +1,120 @@
+"""Placement quality of an 8-GPU node, measured on ONE MI355X ("virtual node").
+
+The driver's 8-GPU bench couples the ranks through the per-epoch placement broadcast, so an
+epoch takes as long as its slowest GPU.  How long a GPU takes depends on WHICH four pods
+the scheduler put on it (their work and how well their GEMM / HBM phases overlap).  This
+tool runs the bench's control plane for an 8-GPU node (apiserver + scheduler + Poisson
+arrivals, `parallel.podbench.ControlPlane`) and executes each of the 8 GPUs' pod groups
+of every epoch on the one real GPU in turn (co-running, as on its own GPU), timing each
+group with HIP events.  Per epoch it reports the slowest group (the coupled 8-GPU epoch
+time), the mean group (the work-conserving bound) and the measured-vs-predicted SLO
+attainment, for placement policies side by side (interleaved per epoch, same arrivals):
+
+  * greedy (balance + LPT)
+  * planned (`planBursts`: joint SLO / interference-adjusted-load search; `planned_t0` with
+    no load tolerance, `planned_load` with the load-first objective)
+  * random
+
+    python tools/virtual_node_bench.py [--epochs 12] [--out gpurun_out/virtual_node.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from k8s_gpu_scheduler_amd.models import workloads as W  # noqa: E402
+from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun  # noqa: E402
+from k8s_gpu_scheduler_amd.parallel.podbench import (COST0, POD0, TELE, ControlPlane, _cost_rows,  # noqa: E402
+                                                     _pod_rows, _runs_for)
+
+N_GPUS = 8
+POLICIES = {
+    "greedy": dict(balance=1.0, plan_bursts=False),
+    "planned": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.05),
+    "planned_t0": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.0),
+    "planned_load": dict(balance=1.0, plan_bursts=True, plan_objective="load"),
+    "random": dict(policy="random", balance=0.0, plan_bursts=False),
+}
+
+
+def run_group(ex: DeviceExecutor, runs):
+    """Run one virtual GPU's pods co-located on the real GPU; returns wall ms."""
+    if not runs:
+        return 0.0
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    ex.launch_epoch(runs)
+    ex.join_current()
+    e.record()
+    e.synchronize()
+    for r in runs:
+        r.ms = r.start.elapsed_time(r.end)
+    return s.elapsed_time(e)
+
+
+def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray):
+    walls, per_gpu = [], np.zeros((N_GPUS, TELE))
+    ok = n = 0
+    for g in range(N_GPUS):
+        runs = _runs_for(arr, g)
+        walls.append(run_group(ex, runs))
+        for r in runs:
+            per_gpu[g, :4] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
+                               W.CATALOG[r.workload].hbm_gib)
+            ok += r.slo <= 0 or r.throughput >= r.slo
+            n += 1
+        per_gpu[g, COST0:POD0] = _cost_rows(runs).ravel()
+        per_gpu[g, POD0:] = _pod_rows(runs)
+    cp.update_telemetry(per_gpu, max(walls))
+    return walls, ok, n
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default="gpurun_out/virtual_node.json")
+    ap.add_argument("--policies", nargs="+", default=["greedy", "planned", "random"], choices=sorted(POLICIES))
+    a = ap.parse_args()
+    policies = {k: POLICIES[k] for k in a.policies}
+    cps = {k: ControlPlane(n_gpus=N_GPUS, pods_per_gpu=4, iters=20, seed=a.seed, **kw) for k, kw in policies.items()}
+    ex = DeviceExecutor(0, use_cu_masks=True)
+    ex.warm([PodRun(0, wl, u, 2, 20, masked=False) for wl in W.NAMES for u in (0, 2, 4, 6)])
+    stats = {k: {"max_ms": [], "mean_ms": [], "ok": 0, "n": 0} for k in policies}
+    for e in range(a.warmup + a.epochs):
+        for k, cp in cps.items():
+            cp.finish_live()
+            arr = cp.schedule_epoch()
+            walls, ok, n = epoch(cp, ex, arr)
+            if e >= a.warmup:
+                st = stats[k]
+                st["max_ms"].append(max(walls))
+                st["mean_ms"].append(statistics.mean(walls))
+                st["ok"] += ok
+                st["n"] += n
+        print(f"epoch {e}", {k: round(v["max_ms"][-1], 2) for k, v in stats.items() if v["max_ms"]}, flush=True)
+    out = {}
+    for k, st in stats.items():
+        mx, mn = statistics.mean(st["max_ms"]), statistics.mean(st["mean_ms"])
+        out[k] = {"epoch_ms_slowest_gpu": round(mx, 3), "epoch_ms_mean_gpu": round(mn, 3),
+                  "imbalance": round(mx / mn, 4), "pods_per_s_8gpu_coupled": round(4 * N_GPUS / mx * 1e3, 1),
+                  "slo_attainment_pct": round(100.0 * st["ok"] / max(st["n"], 1), 2), "pods": st["n"]}
+    print(json.dumps(out), flush=True)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    json.dump({"note": "each virtual GPU's 4 pods co-run on the one real MI355X in turn; coupled 8-GPU epoch = "
+                       "slowest group; policies interleaved per epoch, same seed", "epochs": a.epochs,
+               "results": out}, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
