@@ -61,12 +61,16 @@ def run_group(ex: DeviceExecutor, runs):
     return s.elapsed_time(e)
 
 
-def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray):
+GROUPS: list = []      # (policy, [workloads], wall ms) of every group, for --dump-groups
+
+
+def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
     walls, per_gpu = [], np.zeros((N_GPUS, TELE))
     ok = n = 0
     for g in range(N_GPUS):
         runs = _runs_for(arr, g)
         walls.append(run_group(ex, runs))
+        GROUPS.append((tag, [r.workload for r in runs], walls[-1]))
         for r in runs:
             per_gpu[g, :4] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
                                W.CATALOG[r.workload].hbm_gib)
@@ -84,6 +88,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/virtual_node.json")
+    ap.add_argument("--dump-groups", default="", help="write every group's workloads and wall ms (JSON)")
     ap.add_argument("--policies", nargs="+", default=["greedy", "planned", "random"], choices=sorted(POLICIES))
     a = ap.parse_args()
     policies = {k: POLICIES[k] for k in a.policies}
@@ -95,7 +100,7 @@ def main() -> None:
         for k, cp in cps.items():
             cp.finish_live()
             arr = cp.schedule_epoch()
-            walls, ok, n = epoch(cp, ex, arr)
+            walls, ok, n = epoch(cp, ex, arr, k)
             if e >= a.warmup:
                 st = stats[k]
                 st["max_ms"].append(max(walls))
@@ -110,6 +115,8 @@ def main() -> None:
                   "imbalance": round(mx / mn, 4), "pods_per_s_8gpu_coupled": round(4 * N_GPUS / mx * 1e3, 1),
                   "slo_attainment_pct": round(100.0 * st["ok"] / max(st["n"], 1), 2), "pods": st["n"]}
     print(json.dumps(out), flush=True)
+    if a.dump_groups:
+        json.dump(GROUPS, open(a.dump_groups, "w"))
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump({"note": "each virtual GPU's 4 pods co-run on the one real MI355X in turn; coupled 8-GPU epoch = "
                        "slowest group; policies interleaved per epoch, same seed", "epochs": a.epochs,
