@@ -85,6 +85,24 @@ def test_native_planner_lowers_interference_adjusted_load_when_slos_tie():
     assert out[0] != out[1]                               # the memory pods now sit apart
 
 
+def test_native_planner_load_first_objective():
+    """load_first: a swap that lowers the busier GPU's adjusted load is taken even when it
+    costs a predicted SLO; the SLO-first objective refuses it."""
+    row = col = [0, 0, 1, 1]
+    # memory pods (row 0) meet their SLO (90 of 100) only when apart (mutual interference 15);
+    # they sit apart on GPU 0/1, but GPU 0 also carries 6 of resident base load: putting both
+    # memory pods on GPU 1 (adjusted 2 x 4 x 100/85 = 9.4) lowers the busier GPU from 11.3
+    slo, pred = [90.0, 90.0, 0.0, 0.0], [100.0] * 4
+    args = (np.array([0, 1, 0, 1], I32), np.array([2] * 4, I32), np.array(row, I32), np.array(col, I32),
+            np.array(slo, F64), np.array(pred, F64), np.array([4.0, 4.0, 1.0, 1.0], F64), np.array([0, 1], I32),
+            np.array([6.0, 0.0], F64), np.array([], I32), np.array([], I32), np.array([], I32),
+            np.array([], F64), np.array([], F64), np.array([[15.0, 5.0], [5.0, 5.0]], F64), 0.0, 8, 0.0)
+    slo_first = list(core.plan_assignment(*args, 0))
+    load_first = list(core.plan_assignment(*args, 1))
+    assert slo_first == [0, 1, 0, 1]
+    assert load_first != slo_first and sorted(load_first) == [0, 0, 1, 1]
+
+
 def test_native_planner_counts_residents():
     row = col = [0, 1]
     slo, pred = [90.0, 90.0], [100.0, 100.0]
