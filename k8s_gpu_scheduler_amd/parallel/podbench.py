@@ -394,11 +394,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--sim-timed", action="store_true",
                     help="simulated executor sleeps out a modelled device time per epoch (multi-rank CPU rehearsal)")
     ap.add_argument("--sim-scale", type=float, default=1.0, help="modelled device-time multiplier (--sim-timed)")
-    ap.add_argument("--plan-bursts", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--plan-bursts", type=int, default=0, choices=[0, 1],
                     help="1: plan each epoch's burst of pods jointly (pairings chosen by predicted "
-                         "interference: see --plan-objective).  On MI355X this lowers the slowest GPU's "
-                         "epoch time of an 8-GPU node by 6-7%% (tools/virtual_node_bench.py, "
-                         "profiles/r01_virtual_node_*.json)")
+                         "interference: see --plan-objective).  On MI355X it lowers the slowest GPU's time "
+                         "of each epoch of an 8-GPU node by 6-7%% (what paces lock-step ranks), but through "
+                         "this bench's 2-deep launch-ahead pipeline greedy placement is 1.6%% faster "
+                         "(tools/virtual_node_bench.py, profiles/r01_virtual_node_s3b.json), so it is off")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
                     help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
                          "'slo' = most predicted SLOs met first (within --plan-tolerance)")

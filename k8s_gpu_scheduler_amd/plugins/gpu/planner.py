@@ -156,12 +156,18 @@ class BurstPlanner:
             items.append((plugin.pod_work(p, conf), p, req, conf))
         items.sort(key=lambda t: -t[0])
         assign: List[Tuple[Any, Any, Any, int, float]] = []
+        # equal loads are broken by a per-burst rotation of the device order: a fixed order
+        # would hand the same GPU the longest pod of every burst, and any bias in the
+        # predicted work would then pile up on that GPU across epochs (in a pipelined
+        # multi-GPU job the per-GPU totals, not one epoch's, pace the ranks)
+        rot = (self.planned_bursts * 5 + 1) % max(len(states), 1)
+        nst = len(states)
         for work, p, req, conf in items:
             best = None
             for d, st in enumerate(states):
                 if free_units[d] < req.units or free_hbm[d] + 1e-6 < req.hbm_gib:
                     continue
-                k2 = (load[gof[d]], d)
+                k2 = (load[gof[d]], (d - rot) % nst)
                 if best is None or k2 < best[0]:
                     best = (k2, d)
             if best is None:
