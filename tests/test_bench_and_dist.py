@@ -22,6 +22,11 @@ def test_bench_sim_single_process():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in r
+    # speed-of-light bookkeeping: the floor at the hardware peaks is below the floor at the
+    # measured-best rates, and both are positive for a run that did work
+    floor = r["roofline_floor_ms_per_step"]
+    assert 0 < floor["peak"] <= floor["achievable"]
+    assert r["sol_pct"]["peak"] <= r["sol_pct"]["achievable"] and r["achieved_hbm_tbps_per_gpu"] > 0
 
 
 def test_bench_random_policy_runs():
