@@ -16,9 +16,28 @@ from .. import _native
 BM, BN, BK = 64, 64, 64          # minimum granularity; the tile (128x128 / 64x128 / 64x64) is picked per shape
 
 
-def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> int:
-    s = stream if stream is not None else torch.cuda.current_stream()
+def _stream_ptr(stream: Optional[torch.cuda.Stream], device: Optional[torch.device] = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    if device is not None and s.device != device:
+        raise ValueError(f"stream is on {s.device}, operands on {device}")
     return int(s.cuda_stream)
+
+
+def _check_devices(name: str, *ts: Optional[torch.Tensor]) -> torch.device:
+    """Every operand (and output/bias when given) must be a device tensor on ONE GPU: a host
+    pointer handed to the kernel is a GPU memory fault (XNACK off), another GPU's pointer
+    a launch on the wrong device."""
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError(f"{name} expects device tensors (got a {t.device} tensor)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"{name}: operands on different devices ({dev} vs {t.device})")
+    return dev
 
 
 def check_gemm_shapes(M: int, N: int, K: int) -> None:
@@ -33,8 +52,7 @@ def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, 
     whole chip) -- steers the tile choice (native pick_gemm_tile)."""
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
         raise TypeError("gemm expects bf16 operands")
-    if not (a.is_cuda and bt.is_cuda):
-        raise ValueError("gemm expects device tensors")
+    _check_devices("gemm", a, bt, out, bias)
     if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
         raise ValueError(f"gemm shape mismatch {tuple(a.shape)} x {tuple(bt.shape)}^T")
     if a.stride(1) != 1 or bt.stride(1) != 1:
@@ -51,8 +69,9 @@ def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, 
         if bias.dtype != torch.float32 or bias.numel() != N or not bias.is_contiguous():
             raise ValueError("bias must be a contiguous fp32 vector of length N")
         bptr = bias.data_ptr()
-    _native.hip().gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
-                               bt.stride(0), out.stride(0), relu, _stream_ptr(stream), cu_budget)
+    with torch.cuda.device(a.device):
+        _native.hip().gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
+                                   bt.stride(0), out.stride(0), relu, _stream_ptr(stream, a.device), cu_budget)
     return out
 
 
@@ -66,8 +85,7 @@ def gemm_fp8(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = No
     out, on the block-scaled fp8 MFMA (unit scales).  M, N multiples of 64, K of 128."""
     if a.dtype != FP8 or bt.dtype != FP8:
         raise TypeError("gemm_fp8 expects float8_e4m3fn operands")
-    if not (a.is_cuda and bt.is_cuda):
-        raise ValueError("gemm_fp8 expects device tensors")
+    _check_devices("gemm_fp8", a, bt, out, bias)
     if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
         raise ValueError(f"gemm_fp8 shape mismatch {tuple(a.shape)} x {tuple(bt.shape)}^T")
     if a.stride(1) != 1 or bt.stride(1) != 1 or a.stride(0) % 16 or bt.stride(0) % 16:
@@ -85,22 +103,25 @@ def gemm_fp8(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = No
         if bias.dtype != torch.float32 or bias.numel() != N or not bias.is_contiguous():
             raise ValueError("bias must be a contiguous fp32 vector of length N")
         bptr = bias.data_ptr()
-    _native.hip().gemm_fp8_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
-                              bt.stride(0), out.stride(0), relu, _stream_ptr(stream), cu_budget)
+    with torch.cuda.device(a.device):
+        _native.hip().gemm_fp8_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
+                                  bt.stride(0), out.stride(0), relu, _stream_ptr(stream, a.device), cu_budget)
     return out
 
 
 def triad(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, s: float = 1.5, blocks: int = 0,
           stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
     """a = b + s*c (fp32, contiguous, numel % 4 == 0)."""
+    _check_devices("triad", a, b, c)
     for t in (a, b, c):
-        if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+        if t.dtype != torch.float32 or not t.is_contiguous():
             raise ValueError("triad expects contiguous fp32 device tensors")
     n = a.numel()
     if b.numel() != n or c.numel() != n or n % 4:
         raise ValueError("triad: sizes must match and be a multiple of 4")
-    _native.hip().stream_triad(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), n, int(blocks),
-                               _stream_ptr(stream))
+    with torch.cuda.device(a.device):
+        _native.hip().stream_triad(a.data_ptr(), b.data_ptr(), c.data_ptr(), float(s), n, int(blocks),
+                                   _stream_ptr(stream, a.device))
     return a
 
 

@@ -33,6 +33,7 @@ import collections
 import json
 import os
 import random
+import sys
 import time
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -252,9 +253,10 @@ class ControlPlane:
                 gfx_activity=min(1.0, busy), vram_used_mb=float(per_gpu[g][3]) * 1024.0))
 
 
-# best rates measured on one MI355X: 8-phase bf16 GEMM at 8192^3 (profiles/r01_gemm_big.json)
-# and the non-temporal stream triad from HBM (profiles/r01_triad_pmc.txt)
-ACHIEVABLE_TFLOPS = 1434.0
+# best rates measured on one MI355X by ANY implementation: hipBLASLt (torch.matmul) bf16 at
+# 8192^3, median 1647.5 TF/s (profiles/r01_gemm_big.json; our own 8-phase kernel: 1434) and
+# the non-temporal stream triad from HBM (profiles/r01_triad_pmc.txt)
+ACHIEVABLE_TFLOPS = 1648.0
 ACHIEVABLE_TBPS = 6.5
 
 
@@ -422,6 +424,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="epochs kept in flight per GPU before collecting (>= 1)")
     ap.add_argument("--gemm-policy", type=int, default=0, choices=[0, 1, 2],
                     help="GEMM tile policy (A/B knob): 0 default, 1 8-phase 256x256 also for co-running pods")
+    ap.add_argument("--launch", default="auto", choices=["auto", "spawn", "inline"],
+                    help="--gpus N > 1 outside torchrun: 'auto' spawns N rank processes on GPU hosts and "
+                         "simulates N GPUs in one process with --sim; 'spawn' always spawns (gloo ranks "
+                         "with --sim); 'inline' never spawns")
+    ap.add_argument("--smi-period-ms", type=float, default=5.0,
+                    help="amd-smi activity sampling period across warmup + timed region (0 = off)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     a.lookahead = max(1, a.lookahead)
@@ -429,9 +437,25 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1 and (
+            a.launch == "spawn" or (a.launch == "auto" and not a.sim)):
+        # One process per GPU without torchrun: spawn the ranks from this (GPU-untouched)
+        # process; never fall back to fewer GPUs than asked for.
+        from .launch import self_launch_script
+        bench = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                             "bench.py")
+        rc = self_launch_script(bench, list(sys.argv[1:] if argv is None else argv), a.gpus,
+                                require_gpus=not a.sim)
+        if rc:
+            raise SystemExit(rc)
+        return {"spawned_ranks": a.gpus}
+    if world > 1 and a.gpus not in (1, world):
+        raise SystemExit(f"--gpus {a.gpus} does not match WORLD_SIZE {world}")
+    if world == 1 and a.gpus > 1 and not a.sim:
+        raise SystemExit(f"--gpus {a.gpus} needs one process per GPU: use --launch spawn/auto or torchrun")
     # The control plane goes to its own process, started BEFORE anything touches the GPU
     # (torch.cuda.is_available() initialises HIP; a GPU-initialised process must not exec).
-    n_gpus_planned = world if world > 1 else max(1, a.gpus if a.sim else 1)
+    n_gpus_planned = world if world > 1 else max(1, a.gpus)
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
                      plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective)
@@ -449,7 +473,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     backend = a.backend or ("nccl" if use_gpu else "gloo")
     if world > 1 and not dist.is_initialized():
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
-    n_gpus = world if world > 1 else max(1, a.gpus if not use_gpu else 1)
+    if use_gpu and world > 1 and "GPUSCHED_FORCE_DEVICE" not in os.environ and torch.cuda.device_count() < world:
+        raise SystemExit(f"rank {rank}: WORLD_SIZE {world} but only {torch.cuda.device_count()} GPU(s) visible")
+    n_gpus = world if world > 1 else max(1, a.gpus)
     P = n_gpus * a.pods_per_gpu
 
     assert n_gpus == n_gpus_planned
@@ -637,7 +663,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "achieved_hbm_tbps_per_gpu": round(bytes_tot / elapsed / n_gpus / 1e12, 2),
             # speed of light: the step time if every GPU's FLOPs and modelled HBM bytes of the
             # timed pods ran at the hardware peaks (2.5 PF bf16, 8 TB/s) / at the best rates
-            # measured on MI355X (1434 TF GEMM, 6.5 TB/s stream), fully overlapped
+            # measured on MI355X (1648 TF hipBLASLt GEMM, 6.5 TB/s stream), fully overlapped
             "roofline_floor_ms_per_step": {"peak": round(floor_peak / a.steps * 1e3, 3),
                                            "achievable": round(floor_ach / a.steps * 1e3, 3)},
             "sol_pct": {"peak": round(100.0 * floor_peak / elapsed, 1),

@@ -9,7 +9,8 @@ convention (all-reduce busbw = algbw * 2(n-1)/n); on an 8xMI355X node one ring i
 by a single ~153 GB/s xGMI link per direction, and RCCL's multi-channel rings spread a
 k-GPU set over k-1 links per GPU.
 
-  torchrun --nproc-per-node 4 -m k8s_gpu_scheduler_amd.parallel.rccl_probe --sizes 1M,64M,512M
+  python -m k8s_gpu_scheduler_amd.parallel.rccl_probe --gpus 4 --sizes 1M,64M,512M
+  (or under torchrun --nproc-per-node 4; --gpus N outside torchrun spawns the N ranks)
 """
 from __future__ import annotations
 
@@ -75,8 +76,17 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="1M,16M,256M")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); outside torchrun the probe spawns them itself")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        from .launch import self_launch_module
+        return self_launch_module(__name__ if __name__ != "__main__" else "k8s_gpu_scheduler_amd.parallel.rccl_probe",
+                                  list(argv if argv is not None else __import__("sys").argv[1:]), a.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit(f"WORLD_SIZE {world} but only {torch.cuda.device_count()} GPU(s) visible")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if not dist.is_initialized():

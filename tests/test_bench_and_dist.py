@@ -79,3 +79,53 @@ def test_dead_control_plane_raises_instead_of_hanging():
     finally:
         cp._outstanding = 0
         cp.close()
+
+
+def _bench(args, timeout=300):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_bench_sim_gpus4_without_torchrun_reports_4():
+    """`python bench.py --sim --gpus 4` (no torchrun): N simulated GPUs, one JSON line."""
+    p = _bench(["--sim", "--gpus", "4", "--steps", "2", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 4 and r["config"]["parallelism"] == "dp4"
+
+
+@pytest.mark.slow
+def test_bench_self_launches_one_process_per_rank():
+    """`--launch spawn` without torchrun: the parent starts N rank processes itself (here
+    gloo ranks of the simulated executor) -- the path `bench.py --gpus N` takes on a GPU
+    host, where the parent never touches the GPU."""
+    p = _bench(["--sim", "--launch", "spawn", "--gpus", "2", "--steps", "2", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1                        # only rank 0 prints
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 8
+
+
+def test_bench_more_gpus_than_visible_fails_fast():
+    """No silent clamp: asking for 2 GPUs on a host with fewer fails with rc != 0."""
+    import time
+    t = time.time()
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], timeout=120)
+    assert p.returncode != 0
+    assert "GPU" in p.stderr and not [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert time.time() - t < 60
+
+
+def test_launcher_propagates_rank_failure():
+    from k8s_gpu_scheduler_amd.parallel.launch import spawn
+    code = "import os,sys,time; r=int(os.environ['RANK']); time.sleep(0.2*r); sys.exit(3 if r==1 else 0)"
+    assert spawn([sys.executable, "-c", code], 2, require_gpus=False) == 3
+    code = ("import os; assert os.environ['WORLD_SIZE']=='3' and os.environ['MASTER_ADDR']=='127.0.0.1'; "
+            "assert os.environ['RANK']==os.environ['LOCAL_RANK']")
+    assert spawn([sys.executable, "-c", code], 3, require_gpus=False) == 0
