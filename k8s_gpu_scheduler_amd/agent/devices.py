@@ -11,6 +11,7 @@ descriptor dicts as `plugins.gpu.devices.Device.to_json()`.
 from __future__ import annotations
 
 import re
+from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
 from ..api import constants as C
@@ -28,6 +29,69 @@ def parse_smi_list(text: str) -> List[str]:
             part = "MIG" in line or "Partition" in line
             out.append(("MIG-" if part else "GPU-") + m.group(0))
     return out
+
+
+# What an MI355X offers when nothing could be probed (synthetic nodes, tests): the four
+# compute modes, NPS1 with every one of them and NPS2 with the split modes.
+MI355X_PROFILES = [{"mode": "SPX", "partitions": 1, "memory_caps": ["NPS1"]},
+                   {"mode": "DPX", "partitions": 2, "memory_caps": ["NPS1", "NPS2"]},
+                   {"mode": "QPX", "partitions": 4, "memory_caps": ["NPS1", "NPS2"]},
+                   {"mode": "CPX", "partitions": 8, "memory_caps": ["NPS1", "NPS2"]}]
+
+
+@dataclass
+class PartitionCaps:
+    """Partition modes one GPU supports, from the read-only amd-smi probe
+    (`_smi.partition_info`: accelerator partition profiles + memory partition config)."""
+    current_compute: str = "SPX"
+    current_memory: str = "NPS1"
+    compute_modes: List[str] = field(default_factory=list)          # probed; empty = unknown
+    memory_by_compute: Dict[str, List[str]] = field(default_factory=dict)
+    memory_modes: List[str] = field(default_factory=list)
+    probed: bool = False
+
+    def check(self, compute: str, memory: Optional[str] = None) -> Optional[str]:
+        """None if (compute, memory) may be applied, else why not.  Nothing is assumed: a
+        GPU whose profiles could not be read accepts no change."""
+        if not self.probed or not self.compute_modes:
+            return "partition capabilities unknown (amd-smi profile query failed)"
+        if compute not in self.compute_modes:
+            return f"compute partition {compute} not supported (supported: {','.join(self.compute_modes)})"
+        if memory:
+            allowed = self.memory_by_compute.get(compute) or self.memory_modes
+            if allowed and memory not in allowed:
+                return f"memory partition {memory} not allowed with {compute} (allowed: {','.join(allowed)})"
+        return None
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"current_compute": self.current_compute, "current_memory": self.current_memory,
+                "compute_modes": self.compute_modes, "memory_by_compute": self.memory_by_compute,
+                "memory_modes": self.memory_modes, "probed": self.probed}
+
+    @classmethod
+    def from_json(cls, d: Dict[str, Any]) -> "PartitionCaps":
+        return cls(d.get("current_compute", "SPX"), d.get("current_memory", "NPS1"), list(d.get("compute_modes", [])),
+                   {k: list(v) for k, v in (d.get("memory_by_compute") or {}).items()},
+                   list(d.get("memory_modes", [])), bool(d.get("probed", False)))
+
+
+def partition_capabilities(info: Dict[str, Any]) -> PartitionCaps:
+    """PartitionCaps from one `partition_info` dict (amd-smi or synthetic)."""
+    profiles = [p for p in info.get("profiles") or [] if p.get("mode") in C.COMPUTE_PARTITIONS]
+    caps = PartitionCaps(current_compute=str(info.get("compute_partition") or info.get("current_profile") or "SPX"),
+                         current_memory=str(info.get("memory_partition") or "NPS1"))
+    seen = []
+    for p in profiles:
+        if p["mode"] not in seen:
+            seen.append(p["mode"])
+        caps.memory_by_compute.setdefault(p["mode"], [])
+        for m in p.get("memory_caps") or []:
+            if m not in caps.memory_by_compute[p["mode"]]:
+                caps.memory_by_compute[p["mode"]].append(m)
+    caps.compute_modes = sorted(seen, key=lambda m: C.COMPUTE_PARTITIONS[m])
+    caps.memory_modes = list(info.get("memory_caps") or sorted({m for v in caps.memory_by_compute.values() for m in v}))
+    caps.probed = bool(profiles)
+    return caps
 
 
 class DeviceSource:
@@ -48,16 +112,45 @@ class DeviceSource:
     def set_compute_partition(self, index: int, mode: str) -> str:
         return "unsupported"
 
+    def set_memory_partition(self, index: int, mode: str) -> str:
+        return "unsupported"
+
+    def partition_info(self, index: int) -> Dict[str, Any]:
+        """Read-only probe (see `partition_capabilities`); {} when unknown."""
+        return {}
+
 
 class StaticSource(DeviceSource):
     name = "static"
 
     def __init__(self, descriptors: List[Dict[str, Any]], topology: Optional[Dict[str, Any]] = None,
-                 samples: Optional[List[Dict[str, Any]]] = None):
+                 samples: Optional[List[Dict[str, Any]]] = None,
+                 profiles: Optional[List[Dict[str, Any]]] = None, memory_partition: str = "NPS1"):
         self.desc = list(descriptors)
         self.topo = topology
         self._samples = samples or []
         self.partition_calls: List[tuple] = []
+        self.profiles = MI355X_PROFILES if profiles is None else profiles
+        self.memory_partition = memory_partition
+        # scripted per-process usage: device index -> [{"pid", "vram_bytes", ...}] (tests)
+        self.procs: Dict[int, List[Dict[str, Any]]] = {}
+
+    def processes(self, index):
+        return [dict(p) for p in self.procs.get(index, [])]
+
+    def partition_info(self, index):
+        d = self.desc[index] if 0 <= index < len(self.desc) else {}
+        mode = C.PARTITIONS_TO_MODE.get(int(d.get("partitions", 1)), "SPX")
+        return {"compute_partition": mode, "memory_partition": self.memory_partition,
+                "memory_caps": sorted({m for p in self.profiles for m in p["memory_caps"]}),
+                "profiles": [dict(p) for p in self.profiles], "errors": {}}
+
+    def set_memory_partition(self, index, mode):
+        self.partition_calls.append((index, mode))
+        if mode not in C.MEMORY_PARTITIONS:
+            return "unknown mode"
+        self.memory_partition = mode
+        return ""
 
     def devices(self):
         return [dict(d) for d in self.desc]
@@ -152,6 +245,12 @@ class SmiSource(DeviceSource):
 
     def set_compute_partition(self, index, mode):
         return self.smi.set_compute_partition(index, mode)
+
+    def set_memory_partition(self, index, mode):
+        return self.smi.set_memory_partition(index, mode)
+
+    def partition_info(self, index):
+        return self.smi.partition_info(index)
 
 
 class HipSource(DeviceSource):

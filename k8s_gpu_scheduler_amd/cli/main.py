@@ -56,8 +56,10 @@ def _build_scheduler(args, client):
     from ..framework.config import default_gpu_config, load_config
     from ..framework.scheduler import Scheduler
     from ..plugins import full_registry
+    from ..telemetry.cache import TelemetryCache
     cfg = load_config(args.config) if args.config else default_gpu_config({})
     ep = _endpoints(args, client)
+    prom = getattr(args, "prometheus", "") or ep.prometheus
     for prof in cfg.profiles:
         gargs = prof.plugin_config.setdefault(C.PLUGIN_NAME, {})
         if ep.redis and not gargs.get("redis"):
@@ -65,7 +67,25 @@ def _build_scheduler(args, client):
             gargs.setdefault("redis_password", ep.redis_password)
         if ep.recommender and not gargs.get("recommender"):
             gargs["recommender"] = ep.recommender
-    return cfg, Scheduler(client, cfg, full_registry())
+        if prom and not gargs.get("prometheus"):
+            gargs["prometheus"] = prom
+        prom = prom or gargs.get("prometheus", "")
+    # one live-telemetry cache shared by every profile's GPU plugin, filled by the poller
+    tele = TelemetryCache(stale_s=getattr(args, "telemetry_stale", 10.0))
+    sched = Scheduler(client, cfg, full_registry(), extras={"telemetry": tele})
+    sched.telemetry_poller = _telemetry_poller(args, tele, prom)
+    return cfg, sched
+
+
+def _telemetry_poller(args, cache, prometheus: str):
+    """Background reader of the agents' GPU series (Prometheus instant queries, or direct
+    exporter scrapes with --telemetry-scrape); None when neither is configured."""
+    from ..telemetry.poller import TelemetryPoller, make_source
+    src = make_source(prometheus, getattr(args, "telemetry_scrape", ""))
+    if src is None:
+        logging.warning("no Prometheus / exporter endpoint: Score runs without live telemetry")
+        return None
+    return TelemetryPoller(cache, src, getattr(args, "telemetry_period", 2.0))
 
 
 def cmd_scheduler(args) -> int:
@@ -89,11 +109,15 @@ def cmd_scheduler(args) -> int:
         elector.start()
     else:
         sched.start()
+    if sched.telemetry_poller is not None:
+        sched.telemetry_poller.start()
     try:
         while not stop.is_set():
             stop.wait(1.0)
     except KeyboardInterrupt:
         pass
+    if sched.telemetry_poller is not None:
+        sched.telemetry_poller.stop()
     sched.stop()
     return 0
 
@@ -103,6 +127,8 @@ def cmd_extender(args) -> int:
     client = _client(args.kubeconfig, args.fake_apiserver)
     _, sched = _build_scheduler(args, client)
     sched.start_informers()
+    if sched.telemetry_poller is not None:
+        sched.telemetry_poller.start()
     srv = ExtenderServer(Extender(sched), "0.0.0.0", args.port).start()
     logging.info("extender listening on %s", srv.url)
     try:
@@ -174,6 +200,10 @@ def cmd_agent(args) -> int:
         return 1
     redis = Redis.connect(addr, args.redis_password)
     src = synthetic_node(args.synthetic, node=node) if args.synthetic else best_source()
+    if args.synthetic and args.synthetic_samples:
+        # scripted telemetry for a synthetic node: JSON list of per-device sample dicts
+        # ({"index": i, "gfx_activity": 95, "vram_used_mb": ...}, amd-smi units)
+        src._samples = json.loads(args.synthetic_samples)
     exp = GpuExporter(node, os.getenv("POD_NAME", "amd-gpu-exporter"), dcgm_compat=args.dcgm_compat)
     if args.metrics_port:
         exp.serve(args.metrics_port)
@@ -273,14 +303,24 @@ def build_parser() -> argparse.ArgumentParser:
         sp.add_argument("--recommender", default="")
         sp.add_argument("--no-discovery", action="store_true")
 
+    def telemetry(sp):
+        sp.add_argument("--prometheus", default="", help="Prometheus URL for the live GPU telemetry poller")
+        sp.add_argument("--telemetry-scrape", default="",
+                        help="comma-separated agent exporter /metrics URLs, scraped directly (no Prometheus)")
+        sp.add_argument("--telemetry-period", type=float, default=2.0, help="telemetry poll period (s)")
+        sp.add_argument("--telemetry-stale", type=float, default=10.0,
+                        help="samples older than this are ignored by Score (s)")
+
     s = sub.add_parser("scheduler")
     common(s)
+    telemetry(s)
     s.add_argument("--config", default="")
     s.add_argument("--metrics-port", type=int, default=10251,
                    help="Prometheus /metrics (pods scheduled, latency, per-extension-point means); 0 = off")
     s.set_defaults(fn=cmd_scheduler)
     s = sub.add_parser("extender")
     common(s)
+    telemetry(s)
     s.add_argument("--config", default="")
     s.add_argument("--port", type=int, default=8888)
     s.set_defaults(fn=cmd_extender)
@@ -308,6 +348,7 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--metrics-port", type=int, default=9400)
     s.add_argument("--dcgm-compat", action="store_true")
     s.add_argument("--synthetic", type=int, default=0, help="fake N GPUs (no hardware)")
+    s.add_argument("--synthetic-samples", default="", help="scripted telemetry of the synthetic GPUs (JSON list)")
     s.add_argument("--once", action="store_true")
     s.add_argument("--device-plugin", action="store_true",
                    help="also serve the kubelet device plugin (amd.com/gpu, gpu-cu, gpu-memory)")

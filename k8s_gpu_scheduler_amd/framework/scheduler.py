@@ -121,6 +121,7 @@ class Scheduler:
         self.cache = SchedulerCache()
         self.informers = informers or SharedInformerFactory(client)
         self.extras: Dict[str, Any] = dict(extras or {})
+        self.telemetry_poller: Any = None      # telemetry.poller.TelemetryPoller (CLI wiring)
         self.record_events = record_events
         self.handle = Handle(self)
         self.frameworks: Dict[str, Framework] = {}

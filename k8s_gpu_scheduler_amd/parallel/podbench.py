@@ -61,8 +61,10 @@ COST0 = 4
 POD0 = COST0 + 2 * len(W.NAMES)
 # busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods), then per pod of
 # this GPU's epoch: (workload id or -1, achieved iterations/s) -- the co-run observations the
-# online interference model learns from
-TELE = POD0 + 2 * MAX_PODS_GPU
+# online interference model learns from; last, amd-smi's view of the GPU over the epoch
+# (gfx activity 0..1, VRAM used GiB; -1 = no amd-smi sample)
+SMI0 = POD0 + 2 * MAX_PODS_GPU
+TELE = SMI0 + 2
 
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
@@ -237,20 +239,26 @@ class ControlPlane:
         """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib[, per-workload
         (sum of observed GPU-seconds per iteration, pods) x len(W.NAMES)])."""
         per_gpu = np.asarray(per_gpu, dtype=np.float64)
-        if per_gpu.shape[1] >= TELE:
+        smi = per_gpu.shape[1] >= TELE
+        if smi:
             cost = per_gpu[:, COST0:POD0].sum(axis=0).reshape(len(W.NAMES), 2)
             for wid, (tot, n) in enumerate(cost):
                 if n > 0:
                     self.workcost.observe(W.NAMES[wid], float(tot / n), int(n))
             if self.online is not None:
-                self._learn_interference(per_gpu[:, POD0:TELE])
+                self._learn_interference(per_gpu[:, POD0:SMI0])
         for st in self.ledger.devices(NODE):
             g = st.device.gpu
             if g >= len(per_gpu):
                 continue
-            busy = float(per_gpu[g][0]) / max(st.device.units * wall_ms, 1e-9)
-            self.telemetry.update(NODE, st.device.uuid, DeviceSample(
-                gfx_activity=min(1.0, busy), vram_used_mb=float(per_gpu[g][3]) * 1024.0))
+            if smi and per_gpu[g][SMI0] >= 0:
+                # what amd-smi measured on that GPU over the epoch (the deployed path's
+                # source: agent sampler -> exporter -> Prometheus poller -> this cache)
+                gfx, vram_mb = float(per_gpu[g][SMI0]), float(per_gpu[g][SMI0 + 1]) * 1024.0
+            else:           # no amd-smi (simulated executor): the executor's own busy accounting
+                gfx = float(per_gpu[g][0]) / max(st.device.units * wall_ms, 1e-9)
+                vram_mb = float(per_gpu[g][3]) * 1024.0
+            self.telemetry.update(NODE, st.device.uuid, DeviceSample(gfx_activity=min(1.0, gfx), vram_used_mb=vram_mb))
 
 
 # best rates measured on one MI355X by ANY implementation: hipBLASLt (torch.matmul) bf16 at
@@ -372,6 +380,22 @@ class _null:
         return False
 
 
+def _smi_report(rows: List[List[float]], period_ms: float) -> Optional[Dict[str, Any]]:
+    """Aggregate the ranks' amd-smi window summaries (None when no rank had amd-smi)."""
+    ok = [r for r in rows if r[0] >= 0 and r[5] > 0]
+    if not ok:
+        return None
+
+    def mean(i):
+        v = [r[i] for r in ok if r[i] >= 0]
+        return round(sum(v) / len(v), 2) if v else None
+    return {"gfx_activity_pct_mean": mean(0), "gfx_activity_pct_max": round(max(r[4] for r in ok), 2),
+            "umc_activity_pct_mean": mean(1), "power_w_mean": mean(2),
+            "vram_used_gib_max": round(max(r[3] for r in ok) / 1024.0, 2),
+            "samples_per_gpu": round(sum(r[5] for r in ok) / len(ok), 1), "gpus_sampled": len(ok),
+            "period_ms": period_ms}
+
+
 def _runs_for(arr: np.ndarray, gpu: int):
     from .executor import PodRun
     out = []
@@ -491,6 +515,13 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             _native.hip(required=True).set_gemm_policy(a.gemm_policy)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
+    smi_s = None
+    if use_gpu and a.smi_period_ms > 0:
+        from ..telemetry.smi_sampler import ActivitySampler
+        smi_s = ActivitySampler([dev_idx], a.smi_period_ms / 1e3)
+        if not smi_s.start():
+            print(f"[bench] rank {rank}: amd-smi sampler off ({smi_s.error})", file=sys.stderr, flush=True)
+            smi_s = None
     gpus_here = [rank] if world > 1 else list(range(n_gpus))
 
     # Control traffic (placements, telemetry) runs on a NON-blocking side stream: the
@@ -534,8 +565,13 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     intervals.append((ref["ev"].elapsed_time(r.start), ref["ev"].elapsed_time(r.end)))
         st = ex.collect(runs)
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
+        smi_vec = [-1.0, -1.0]
+        if smi_s is not None:
+            sm = smi_s.summary(rows=smi_s.poll())         # samples since the previous collect
+            if sm["gfx_activity_pct_mean"] is not None:
+                smi_vec = [sm["gfx_activity_pct_mean"] / 100.0, (sm["vram_used_mb_max"] or 0.0) / 1024.0]
         vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm] + _cost_rows(runs).ravel().tolist() + \
-            _pod_rows(runs)
+            _pod_rows(runs) + smi_vec
         if world > 1:
             with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
                 tele.copy_(torch.tensor(vec, dtype=torch.float64))
@@ -544,13 +580,14 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         elif not use_gpu and n_gpus > 1:
             # single-process simulation of several GPUs: split by gpu id
             per_gpu = np.zeros((n_gpus, TELE))
+            per_gpu[:, SMI0:] = -1.0
             for r in runs:
                 g = int(arr[r.pod_id][0])
                 per_gpu[g, :4] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
                                    W.CATALOG[r.workload].hbm_gib)
                 per_gpu[g, COST0:POD0] += _cost_rows([r]).ravel()
             for g in range(n_gpus):
-                per_gpu[g, POD0:] = _pod_rows([r for r in runs if int(arr[r.pod_id][0]) == g])
+                per_gpu[g, POD0:SMI0] = _pod_rows([r for r in runs if int(arr[r.pod_id][0]) == g])
         else:
             per_gpu = np.asarray(vec, dtype=np.float64)[None, :]
         if rank == 0:
@@ -603,6 +640,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         torch.cuda.synchronize()
     t_start = time.perf_counter()
+    wall0 = time.time()
     if use_gpu:
         ref["ev"] = torch.cuda.Event(enable_timing=True)
         ref["ev"].record(side)
@@ -619,6 +657,15 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    wall1 = time.time()
+    smi_sum: Dict[str, Any] = {}
+    if smi_s is not None:
+        smi_s.poll()
+        smi_sum = smi_s.summary(wall0, wall1)
+    # per rank: (gfx mean, umc mean, power mean, vram max MB, gfx max, samples); -1 = none
+    smi_t = torch.tensor([smi_sum.get(k) if smi_sum.get(k) is not None else -1.0 for k in
+                          ("gfx_activity_pct_mean", "umc_activity_pct_mean", "power_w_mean", "vram_used_mb_max",
+                           "gfx_activity_pct_max", "samples")], dtype=torch.float64, device=dev)
     if not use_gpu:
         # simulated executor: wall time = modelled device time of each epoch (+ host time)
         elapsed = max(elapsed, 1e-9)
@@ -635,6 +682,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         mx = flops[[1, 4, 5]].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)       # the busiest rank paces the step
         flops = torch.stack([summed[0], mx[0], summed[1], summed[2], mx[1], mx[2]])
+    smi_all = [smi_t.clone() for _ in range(world)]
+    if world > 1:
+        dist.all_gather(smi_all, smi_t)
+    smi_rows = [t.cpu().tolist() for t in smi_all]
     flops_tot, elapsed, busy_tot_ms = float(flops[0]), float(flops[1]), float(flops[2])
     bytes_tot, floor_peak, floor_ach = float(flops[3]), float(flops[4]), float(flops[5])
     result: Dict[str, Any] = {}
@@ -668,6 +719,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                                            "achievable": round(floor_ach / a.steps * 1e3, 3)},
             "sol_pct": {"peak": round(100.0 * floor_peak / elapsed, 1),
                         "achievable": round(100.0 * floor_ach / elapsed, 1)},
+            # what amd-smi itself reported over the timed region (C++ sampler thread,
+            # --smi-period-ms): mean over ranks of each GPU's mean gfx activity -- the
+            # externally observable counterpart of gpu_util_pct (HIP-event union)
+            "smi": _smi_report(smi_rows, a.smi_period_ms),
             "slo_attainment_pct": round(100.0 * totals["slo_ok"] / max(totals["pods"], 1), 2),
             "sched_ms_per_pod": round(cp.sched_s / max(totals["pods"], 1) * 1e3, 4),
             "interference_mae": cp.interference_mae(),
@@ -679,6 +734,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(result, f)
+    if smi_s is not None:
+        smi_s.stop()
     ex.close()
     if rank == 0 and async_cp:
         cp.close()

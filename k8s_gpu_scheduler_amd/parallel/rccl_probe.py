@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 from typing import Dict, List, Optional
 
@@ -83,7 +84,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         from .launch import self_launch_module
         return self_launch_module(__name__ if __name__ != "__main__" else "k8s_gpu_scheduler_amd.parallel.rccl_probe",
-                                  list(argv if argv is not None else __import__("sys").argv[1:]), a.gpus)
+                                  list(argv if argv is not None else sys.argv[1:]), a.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and torch.cuda.device_count() < world:
         raise SystemExit(f"WORLD_SIZE {world} but only {torch.cuda.device_count()} GPU(s) visible")

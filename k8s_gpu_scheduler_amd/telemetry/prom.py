@@ -23,7 +23,7 @@ import urllib.error
 import urllib.parse
 import urllib.request
 from concurrent.futures import ThreadPoolExecutor
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
 from ..api import constants as C
@@ -42,6 +42,10 @@ class Response:
     value: str = ""
     gpu_i_id: str = ""
     uuid: str = ""
+    # every label of the series and the sample's unix timestamp (the reference keeps only
+    # the five fields above; the scheduler's poller also needs `node`/`gpu` and the age)
+    labels: Dict[str, str] = field(default_factory=dict, compare=False, repr=False)
+    ts: float = field(default=0.0, compare=False, repr=False)
 
 
 def create_url(base_url: str, upath: str, params: Dict[str, str]) -> str:
@@ -79,7 +83,8 @@ def parse_response(body: Optional[bytes]) -> Optional[List[Response]]:
     for r in results:
         m = r["metric"]
         out.append(Response(metric_name=m["__name__"], exporter=m.get("pod", ""), value=str(r["value"][1]),
-                            gpu_i_id=m.get("GPU_I_ID", ""), uuid=m.get("UUID", "")))
+                            gpu_i_id=m.get("GPU_I_ID", ""), uuid=m.get("UUID", ""), labels=dict(m),
+                            ts=float(r["value"][0])))
     return out
 
 

@@ -11,7 +11,13 @@
 //  * MIG layouts via the NVIDIA MIG manager (gpu_plugins.go:402-413)
 //      -> amdsmi compute partition get/set (SPX/DPX/QPX/CPX) + memory partition get;
 //  * new: xGMI link matrix (type, hops, weight) + NUMA node for the topology Filter, and
-//    the per-process list (PID, VRAM, CU occupancy) for per-pod attribution.
+//    the per-process list (PID, VRAM, CU occupancy) for per-pod attribution;
+//  * new: read-only partition capability probe (accelerator partition profiles = the
+//    compute modes this GPU supports, and the NPS memory modes each allows) and NPS memory
+//    partition set -- the agent applies only what the probe lists;
+//  * new: amd-smi -> HIP enumeration map (hip_id / hsa_id / render node) and a light,
+//    fast activity sampler (gfx/umc activity, VRAM, power of selected GPUs) that the
+//    benchmark runs on a C++ thread across its timed region.
 #include <amd_smi/amdsmi.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -30,6 +36,34 @@
 namespace py = pybind11;
 
 namespace {
+
+struct Activity {                                   // light sample (benchmark sampler)
+  double ts = 0;
+  int index = 0;
+  double gfx = -1, umc = -1, vram_used_mb = -1, power_w = -1;
+};
+
+const char* const kNps[] = {"", "NPS1", "NPS2", "", "NPS4", "", "", "", "NPS8"};
+
+std::vector<std::string> nps_list(amdsmi_nps_caps_t c) {
+  std::vector<std::string> out;
+  if (c.nps_flags.nps1_cap) out.push_back("NPS1");
+  if (c.nps_flags.nps2_cap) out.push_back("NPS2");
+  if (c.nps_flags.nps4_cap) out.push_back("NPS4");
+  if (c.nps_flags.nps8_cap) out.push_back("NPS8");
+  return out;
+}
+
+const char* accel_name(amdsmi_accelerator_partition_type_t t) {
+  switch (t) {
+    case AMDSMI_ACCELERATOR_PARTITION_SPX: return "SPX";
+    case AMDSMI_ACCELERATOR_PARTITION_DPX: return "DPX";
+    case AMDSMI_ACCELERATOR_PARTITION_TPX: return "TPX";
+    case AMDSMI_ACCELERATOR_PARTITION_QPX: return "QPX";
+    case AMDSMI_ACCELERATOR_PARTITION_CPX: return "CPX";
+    default: return "";
+  }
+}
 
 struct Sample {
   double ts = 0;
@@ -237,6 +271,138 @@ class Smi {
     return out;
   }
 
+  // Read-only partition probe: current compute / memory mode, the accelerator partition
+  // profiles the driver offers (compute modes with their partition counts and allowed NPS
+  // modes) and the memory modes it reports as possible.  Fields that the driver or the
+  // caller's privileges do not provide are absent; "errors" says why.
+  py::dict partition_info(int idx) {
+    py::dict d;
+    py::dict errs;
+    if (idx < 0 || idx >= count()) {
+      errs["index"] = "bad index";
+      d["errors"] = errs;
+      return d;
+    }
+    auto h = gpus_[idx];
+    char part[64] = {0};
+    amdsmi_status_t st = amdsmi_get_gpu_compute_partition(h, part, sizeof(part));
+    if (st == AMDSMI_STATUS_SUCCESS) d["compute_partition"] = std::string(part);
+    else errs["compute_partition"] = status_str(st);
+    char mpart[64] = {0};
+    st = amdsmi_get_gpu_memory_partition(h, mpart, sizeof(mpart));
+    if (st == AMDSMI_STATUS_SUCCESS) d["memory_partition"] = std::string(mpart);
+    else errs["memory_partition"] = status_str(st);
+    amdsmi_memory_partition_config_t mc;
+    std::memset(&mc, 0, sizeof(mc));
+    st = amdsmi_get_gpu_memory_partition_config(h, &mc);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      d["memory_caps"] = nps_list(mc.partition_caps);
+      d["numa_ranges"] = mc.num_numa_ranges;
+    } else {
+      errs["memory_config"] = status_str(st);
+    }
+    auto* cfg = new amdsmi_accelerator_partition_profile_config_t();   // ~40 KB: keep it off the stack
+    st = amdsmi_get_gpu_accelerator_partition_profile_config(h, cfg);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      py::list profiles;
+      for (uint32_t k = 0; k < cfg->num_profiles && k < AMDSMI_MAX_ACCELERATOR_PROFILE; ++k) {
+        const auto& pr = cfg->profiles[k];
+        py::dict x;
+        x["mode"] = std::string(accel_name(pr.profile_type));
+        x["partitions"] = pr.num_partitions;
+        x["memory_caps"] = nps_list(pr.memory_caps);
+        x["profile_index"] = pr.profile_index;
+        profiles.append(x);
+      }
+      d["profiles"] = profiles;
+      d["default_profile_index"] = cfg->default_profile_index;
+    } else {
+      errs["profiles"] = status_str(st);
+    }
+    delete cfg;
+    amdsmi_accelerator_partition_profile_t cur;
+    std::memset(&cur, 0, sizeof(cur));
+    uint32_t ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {0};
+    st = amdsmi_get_gpu_accelerator_partition_profile(h, &cur, ids);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      d["current_profile"] = std::string(accel_name(cur.profile_type));
+      d["current_partitions"] = cur.num_partitions;
+      std::vector<uint32_t> v(ids, ids + std::min<uint32_t>(cur.num_partitions, AMDSMI_MAX_ACCELERATOR_PARTITIONS));
+      d["partition_ids"] = v;
+    } else {
+      errs["current_profile"] = status_str(st);
+    }
+    amdsmi_kfd_info_t kfd;
+    if (amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.current_partition_id != 0xFFFFFFFFu)
+      d["kfd_partition_id"] = kfd.current_partition_id;
+    d["errors"] = errs;
+    return d;
+  }
+
+  py::dict enumeration(int idx) {
+    py::dict d;
+    if (idx < 0 || idx >= count()) return d;
+    amdsmi_enumeration_info_t e;
+    std::memset(&e, 0, sizeof(e));
+    if (amdsmi_get_gpu_enumeration_info(gpus_[idx], &e) == AMDSMI_STATUS_SUCCESS) {
+      d["hip_id"] = e.hip_id;
+      d["hsa_id"] = e.hsa_id;
+      d["drm_render"] = e.drm_render;
+      d["drm_card"] = e.drm_card;
+      d["hip_uuid"] = std::string(e.hip_uuid);
+    }
+    amdsmi_bdf_t bdf;
+    if (amdsmi_get_gpu_device_bdf(gpus_[idx], &bdf) == AMDSMI_STATUS_SUCCESS) {
+      d["pci_domain"] = static_cast<uint64_t>(bdf.domain_number);
+      d["pci_bus"] = static_cast<unsigned>(bdf.bus_number);
+      d["pci_device"] = static_cast<unsigned>(bdf.device_number);
+    }
+    return d;
+  }
+
+  std::string set_memory_partition(int idx, const std::string& mode) {
+    if (idx < 0 || idx >= count()) return "bad index";
+    amdsmi_memory_partition_type_t t = AMDSMI_MEMORY_PARTITION_UNKNOWN;
+    for (int k = 1; k <= 8; ++k)
+      if (mode == kNps[k]) t = static_cast<amdsmi_memory_partition_type_t>(k);
+    if (t == AMDSMI_MEMORY_PARTITION_UNKNOWN) return "unknown mode";
+    amdsmi_status_t s = amdsmi_set_gpu_memory_partition(gpus_[idx], t);
+    return s == AMDSMI_STATUS_SUCCESS ? "" : status_str(s);
+  }
+
+  // ---- light activity sampler (benchmark): gfx/umc %, VRAM, power of selected GPUs ----
+  std::vector<Activity> activity(const std::vector<int>& idx) {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<Activity> out;
+    double ts = now_s();
+    for (int i : idx) {
+      if (i < 0 || i >= count()) continue;
+      Activity a;
+      a.ts = ts;
+      a.index = i;
+      amdsmi_engine_usage_t u;
+      if (amdsmi_get_gpu_activity(gpus_[i], &u) == AMDSMI_STATUS_SUCCESS) {
+        a.gfx = u.gfx_activity;
+        a.umc = u.umc_activity;
+      }
+      amdsmi_vram_usage_t v;
+      if (amdsmi_get_gpu_vram_usage(gpus_[i], &v) == AMDSMI_STATUS_SUCCESS) a.vram_used_mb = v.vram_used;
+      amdsmi_power_info_t p;
+      if (amdsmi_get_power_info(gpus_[i], &p) == AMDSMI_STATUS_SUCCESS)
+        a.power_w = (p.current_socket_power != UINT32_MAX) ? p.current_socket_power : (double)p.average_socket_power;
+      out.push_back(a);
+    }
+    return out;
+  }
+
+  void start_activity(double period_s, int capacity, std::vector<int> idx) {
+    act_sampler_.start([this, idx]() { return activity(idx); }, period_s, capacity);
+  }
+
+  void stop_activity() { act_sampler_.stop(); }
+
+  std::vector<std::vector<Activity>> drain_activity() { return act_sampler_.drain(); }
+
   std::string set_compute_partition(int idx, const std::string& mode) {
     if (idx < 0 || idx >= count()) return "bad index";
     amdsmi_compute_partition_type_t t = AMDSMI_COMPUTE_PARTITION_INVALID;
@@ -260,6 +426,7 @@ class Smi {
 
   void shutdown() {
     stop();
+    stop_activity();
     std::lock_guard<std::mutex> g(mu_);
     if (inited_) amdsmi_shut_down();
     inited_ = false;
@@ -272,7 +439,8 @@ class Smi {
   std::string err_;
   std::vector<amdsmi_processor_handle> gpus_;
   std::vector<Sample> prev_;
-  gs::PeriodicSampler<std::vector<Sample>> sampler_;   // last member: joined first on destruction
+  gs::PeriodicSampler<std::vector<Activity>> act_sampler_;
+  gs::PeriodicSampler<std::vector<Sample>> sampler_;   // last members: joined first on destruction
 };
 
 py::dict to_dict(const Sample& s) {
@@ -314,6 +482,20 @@ PYBIND11_MODULE(_smi, m) {
       .def("topology", &Smi::topology)
       .def("processes", &Smi::processes)
       .def("set_compute_partition", &Smi::set_compute_partition)
+      .def("set_memory_partition", &Smi::set_memory_partition)
+      .def("partition_info", &Smi::partition_info)
+      .def("enumeration", &Smi::enumeration)
+      .def("start_activity", &Smi::start_activity, py::arg("period_s") = 0.005, py::arg("capacity") = 200000,
+           py::arg("indices") = std::vector<int>{})
+      .def("stop_activity", &Smi::stop_activity, py::call_guard<py::gil_scoped_release>())
+      .def("drain_activity",
+           [](Smi& s) {
+             // flat rows (ts, index, gfx %, umc %, vram used MB, power W); -1 = not reported
+             std::vector<std::vector<double>> out;
+             for (auto& v : s.drain_activity())
+               for (auto& a : v) out.push_back({a.ts, (double)a.index, a.gfx, a.umc, a.vram_used_mb, a.power_w});
+             return out;
+           })
       .def("start", &Smi::start, py::arg("period_s") = 1.0, py::arg("capacity") = 600)
       .def("stop", &Smi::stop, py::call_guard<py::gil_scoped_release>())
       .def("drain",

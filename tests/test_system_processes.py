@@ -162,3 +162,55 @@ def test_agent_serves_device_plugin_to_kubelet_as_process(tmp_path):
                 p.kill()
         kubelet.stop(0)
         redis.stop()
+
+
+@pytest.mark.timeout(240)
+def test_live_telemetry_reaches_deployed_scheduler_as_processes():
+    """fake apiserver, node agent (scripted amd-smi samples: GPU 0 at 95 %, GPU 1 idle,
+    exported on /metrics) and scheduler (`--telemetry-scrape` poller) as three processes:
+    the busy GPU loses Score, so the pod lands on the idle one."""
+    procs = []
+    redis = FakeRedisServer(FakeRedisEngine(password=C.REDIS_PASSWORD)).start()
+    try:
+        fc = _spawn(["fake-cluster", "--port", str(_free_port()), "--nodes", "1", "--gpus", "2"])
+        procs.append(fc)
+        url = fc.stdout.readline().strip()
+        client = RestClient(RestConfig(url))
+        node = O.name(client.list("nodes")[0][0])
+        mport = _free_port()
+        samples = [{"index": 0, "gfx_activity": 95.0, "vram_used_mb": 2048.0, "vram_total_mb": 294912.0},
+                   {"index": 1, "gfx_activity": 0.0, "vram_used_mb": 16.0, "vram_total_mb": 294912.0}]
+        ag = _spawn(["agent", "--fake-apiserver", url, "--redis", redis.addr, "--node", node, "--synthetic", "2",
+                     "--synthetic-samples", json.dumps(samples), "--no-discovery", "--metrics-port", str(mport),
+                     "--poll", "0.3"])
+        procs.append(ag)
+        murl = f"http://127.0.0.1:{mport}/metrics"
+
+        def exported():
+            try:
+                return "amd_gpu_gfx_activity" in urllib.request.urlopen(murl, timeout=2).read().decode()
+            except Exception:
+                return False
+        assert _wait(exported, 90), "agent exporter not serving"
+        sc = _spawn(["scheduler", "--fake-apiserver", url, "--redis", redis.addr, "--no-discovery",
+                     "--config", os.path.join(ROOT, "deploy", "scheduler.yaml"), "--metrics-port", "0",
+                     "--telemetry-scrape", murl, "--telemetry-period", "0.3"])
+        procs.append(sc)
+        r = Redis.connect(redis.addr, C.REDIS_PASSWORD)
+        devs = _wait(lambda: json.loads(r.get_or("gpusched:devices:" + node) or "null"), 30)
+        assert devs, "agent did not publish descriptors"
+        by_gpu = {d["gpu"]: d["uuid"] for d in devs}
+        time.sleep(4.0)        # leader election + informer sync + a few telemetry polls
+        client.create("pods", O.make_pod("tele-0", gpu_cu=64, gpu_mem_gib=4))
+        pod = _wait(lambda: (lambda p: p if O.node_name_of(p) else None)(client.get("pods", "tele-0", "default")), 90)
+        assert pod, "pod not bound"
+        assert O.annotations(pod)[C.ANNOT_DEVICES] == by_gpu[1], (O.annotations(pod), by_gpu)
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        redis.stop()

@@ -33,7 +33,7 @@ import torch  # noqa: E402
 
 from k8s_gpu_scheduler_amd.models import workloads as W  # noqa: E402
 from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun  # noqa: E402
-from k8s_gpu_scheduler_amd.parallel.podbench import (COST0, POD0, TELE, ControlPlane, _cost_rows,  # noqa: E402
+from k8s_gpu_scheduler_amd.parallel.podbench import (COST0, POD0, SMI0, TELE, ControlPlane, _cost_rows,  # noqa: E402
                                                      _pod_rows, _runs_for)
 
 N_GPUS = 8
@@ -67,6 +67,7 @@ GROUPS: list = []      # (policy, [workloads], wall ms) of every group, for --du
 
 def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
     walls, per_gpu = [], np.zeros((N_GPUS, TELE))
+    per_gpu[:, SMI0:] = -1.0          # one real GPU stands in for eight: no per-GPU amd-smi view
     ok = n = 0
     for g in range(N_GPUS):
         runs = _runs_for(arr, g)
@@ -78,7 +79,7 @@ def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
             ok += r.slo <= 0 or r.throughput >= r.slo
             n += 1
         per_gpu[g, COST0:POD0] = _cost_rows(runs).ravel()
-        per_gpu[g, POD0:] = _pod_rows(runs)
+        per_gpu[g, POD0:SMI0] = _pod_rows(runs)
     cp.update_telemetry(per_gpu, max(walls))
     return walls, ok, n
 
