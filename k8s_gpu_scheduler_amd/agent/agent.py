@@ -12,19 +12,25 @@ The MI355X agent is one process that, every `poll_s`:
   * samples telemetry and feeds the Prometheus exporter (+ optional TelemetryCache);
   * appends per-pod usage history (`gpusched:hist:<pod>`) for the recommender's resize
     loop, attributing GPU processes to pods through their cgroup;
-  * reconciles compute partitioning: when the node label `amd.com/compute-partition`
-    asks for a different mode, taint the node (`amd.com/partitioning=NoSchedule`), apply
-    through amd-smi, republish, untaint -- asynchronous, never inside Score
-    (fixes SURVEY.md §2.9 #3).
+  * reconciles partitioning: when the node label `amd.com/compute-partition` (and/or
+    `amd.com/memory-partition`) asks for a different mode, check the mode against the
+    read-only amd-smi capability probe (published as the node annotation
+    `partition-caps`), check that the GPUs are idle (no process in amd-smi's process list,
+    no pod bound to the node) -- tainting `amd.com/partitioning=NoSchedule` meanwhile so
+    the node drains, and giving up after `drain_timeout_s` -- then apply through amd-smi
+    (memory mode first), republish, untaint.  Asynchronous, never inside Score (fixes
+    SURVEY.md §2.9 #2-#4); every outcome is recorded in the node annotation
+    `partition-state` and the Redis key `gpusched:partition:<node>`.
 The reference's 4-line stdin protocol is kept as `publish_from_stdin`.
 """
 from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 import time
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..api import constants as C
 from ..api import objects as O
@@ -32,7 +38,7 @@ from ..kube.client import KubeClient
 from ..kube.resources import Resources
 from ..store import schema
 from ..store.resp import Redis
-from .devices import DeviceSource
+from .devices import DeviceSource, PartitionCaps, partition_capabilities
 from .health import HealthMonitor
 
 log = logging.getLogger(__name__)
@@ -54,7 +60,8 @@ class NodeAgent:
     def __init__(self, node: str, redis: Redis, source: DeviceSource, client: Optional[KubeClient] = None,
                  poll_s: float = C.PROFILER_POLL_S, exporter: Any = None, telemetry: Any = None,
                  apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None,
-                 health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False):
+                 health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
+                 drain_timeout_s: float = 300.0):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -66,6 +73,9 @@ class NodeAgent:
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.partition_state = "idle"
+        self.drain_timeout_s = drain_timeout_s
+        self._drain_since: Optional[float] = None
+        self._caps_published: Optional[str] = None
         self.health = health or HealthMonitor()
         # Evict the pods of a device that turned unhealthy (their controllers recreate them
         # and the scheduler places them elsewhere -- the elastic-recovery path); off by
@@ -186,44 +196,167 @@ class NodeAgent:
 
     # ------------------------------------------------------------------ partitions
     def desired_partition(self) -> Optional[str]:
+        return self.desired_partitions()[0]
+
+    def desired_partitions(self) -> Tuple[Optional[str], Optional[str]]:
+        """(compute mode, memory mode) the node labels ask for (None = unset / unreadable)."""
         if self.client is None:
-            return None
+            return None, None
         try:
             node = self.client.get("nodes", self.node)
         except Exception:
-            return None
-        return O.labels(node).get(C.LABEL_COMPUTE_PARTITION)
+            return None, None
+        lab = O.labels(node)
+        c = (lab.get(C.LABEL_COMPUTE_PARTITION) or "").upper() or None
+        m = (lab.get(C.LABEL_MEMORY_PARTITION) or "").upper() or None
+        return c, m
 
     def current_partition(self) -> str:
         devs = self.source.devices()
         parts = max((d.get("partitions", 1) for d in devs), default=1)
         return C.PARTITIONS_TO_MODE.get(parts, "SPX")
 
+    def _gpu_indices(self) -> Dict[int, int]:
+        """physical GPU -> index of its first device (partition) in the source."""
+        out: Dict[int, int] = {}
+        for i, d in enumerate(self.source.devices()):
+            out.setdefault(int(d.get("gpu", i)), i)
+        return out
+
+    def partition_caps(self) -> Optional[PartitionCaps]:
+        """What every GPU of the node supports (intersection of the per-GPU probes)."""
+        caps: Optional[PartitionCaps] = None
+        for idx in self._gpu_indices().values():
+            c = partition_capabilities(self.source.partition_info(idx) or {})
+            if caps is None:
+                caps = c
+                continue
+            caps.probed = caps.probed and c.probed
+            caps.compute_modes = [m for m in caps.compute_modes if m in c.compute_modes]
+            for m in list(caps.memory_by_compute):
+                caps.memory_by_compute[m] = [x for x in caps.memory_by_compute[m] if x in c.memory_by_compute.get(m, [])]
+            caps.memory_modes = [m for m in caps.memory_modes if m in c.memory_modes]
+        return caps
+
+    def publish_caps(self, force: bool = False) -> None:
+        """Node annotation + Redis key with the probed capabilities (read by the controller)."""
+        caps = self.partition_caps()
+        if caps is None:
+            return
+        raw = json.dumps(caps.to_json(), sort_keys=True, separators=(",", ":"))
+        if raw == self._caps_published and not force:
+            return
+        self.redis.set(schema.partition_caps_key(self.node), raw)
+        if self.client is not None:
+            try:
+                self.client.patch("nodes", self.node, {"metadata": {"annotations": {C.ANNOT_PARTITION_CAPS: raw}}},
+                                  "merge")
+            except Exception as e:
+                log.warning("partition-caps annotation on %s failed: %s", self.node, e)
+                return
+        self._caps_published = raw
+
+    def busy_reasons(self) -> List[str]:
+        """Why the GPUs are not idle: processes in amd-smi's list (other than this agent)
+        and non-terminal GPU pods bound to the node.  Empty = safe to repartition."""
+        out = []
+        me = os.getpid()
+        for i, d in enumerate(self.source.devices()):
+            for p in self.source.processes(i):
+                if int(p.get("pid", 0)) != me:
+                    out.append(f"gpu{d.get('gpu', i)}: pid {p.get('pid')} ({p.get('name', '?')})")
+        if self.client is not None:
+            try:
+                pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+            except Exception as e:
+                return out + [f"cannot list pods on the node: {e}"]
+            for p in pods:
+                if not O.is_terminal(p) and (O.wants_gpu(p) or O.annotations(p).get(C.ANNOT_DEVICES)):
+                    out.append(f"pod {O.key(p)}")
+        return out
+
+    def _set_partition_state(self, state: str, **kw: Any) -> None:
+        doc = {"state": state, "ts": time.time(), **kw}
+        raw = json.dumps(doc, sort_keys=True, separators=(",", ":"))
+        self.partition_state = state
+        self.redis.set(schema.partition_key(self.node), raw)
+        if self.client is not None:
+            try:
+                self.client.patch("nodes", self.node, {"metadata": {"annotations": {C.ANNOT_PARTITION_STATE: raw}}},
+                                  "merge")
+            except Exception as e:
+                log.warning("partition-state annotation on %s failed: %s", self.node, e)
+
+    def _revert_request(self, cur_c: str, cur_m: str) -> None:
+        """Set the labels back to what the node runs, so a refused request is not retried."""
+        try:
+            self.client.patch("nodes", self.node, {"metadata": {"labels": {
+                C.LABEL_COMPUTE_PARTITION: cur_c, C.LABEL_MEMORY_PARTITION: cur_m}}}, "merge")
+        except Exception as e:
+            log.warning("reverting the partition labels of %s failed: %s", self.node, e)
+
     def reconcile_partitions(self) -> bool:
-        want = self.desired_partition()
-        if not want or want.upper() not in C.COMPUTE_PARTITIONS or not self.apply_partitions:
+        """One reconcile pass; True when a change was applied successfully."""
+        if not self.apply_partitions or self.client is None:
             return False
-        want = want.upper()
-        if want == self.current_partition():
+        want_c, want_m = self.desired_partitions()
+        if want_c is not None and want_c not in C.COMPUTE_PARTITIONS:
+            want_c = None
+        if want_m is not None and want_m not in C.MEMORY_PARTITIONS:
+            want_m = None
+        caps = self.partition_caps()
+        cur_c = self.current_partition()
+        cur_m = caps.current_memory if caps is not None else "NPS1"
+        if (want_c is None or want_c == cur_c) and (want_m is None or want_m == cur_m):
+            if self._drain_since is not None:       # request withdrawn while draining
+                self._drain_since = None
+                Resources(self.client, "default").untaint_node(self.node, C.TAINT_PARTITIONING)
+                self._set_partition_state("idle", mode=cur_c, memory=cur_m)
+            return False
+        target_c, target_m = want_c or cur_c, want_m or cur_m
+        why = caps.check(target_c, target_m) if caps is not None else "no GPU to partition"
+        if why:
+            log.warning("partition request %s/%s on %s refused: %s", target_c, target_m, self.node, why)
+            self._set_partition_state("refused", mode=target_c, memory=target_m, reason=why)
+            self._revert_request(cur_c, cur_m)
             return False
         res = Resources(self.client, "default")
-        self.partition_state = f"applying {want}"
-        res.taint_node(self.node, C.TAINT_PARTITIONING, want, "NoSchedule")
-        self.redis.set(schema.partition_key(self.node), json.dumps({"state": "applying", "mode": want}))
-        errs = []
-        gpus = sorted({d["gpu"] for d in self.source.devices()})
-        for g in gpus:
-            idx = next(i for i, d in enumerate(self.source.devices()) if d["gpu"] == g)
-            e = self.source.set_compute_partition(idx, want)
-            if e:
-                errs.append(f"gpu{g}: {e}")
+        busy = self.busy_reasons()
+        if busy:
+            now = time.monotonic()
+            if self._drain_since is None:
+                self._drain_since = now
+                res.taint_node(self.node, C.TAINT_PARTITIONING, target_c, "NoSchedule")   # drain: no new pods
+            if now - self._drain_since > self.drain_timeout_s:
+                self._drain_since = None
+                res.untaint_node(self.node, C.TAINT_PARTITIONING)
+                self._set_partition_state("refused", mode=target_c, memory=target_m,
+                                          reason="GPUs not idle: " + "; ".join(busy[:8]))
+                self._revert_request(cur_c, cur_m)
+            else:
+                self._set_partition_state("waiting-idle", mode=target_c, memory=target_m, busy=busy[:8])
+            return False
+        self._drain_since = None
+        res.taint_node(self.node, C.TAINT_PARTITIONING, target_c, "NoSchedule")
+        self._set_partition_state("applying", mode=target_c, memory=target_m)
+        errs: List[str] = []
+        for step, mode, cur, fn in (("memory", target_m, cur_m, self.source.set_memory_partition),
+                                    ("compute", target_c, cur_c, self.source.set_compute_partition)):
+            if mode == cur:
+                continue
+            for g in sorted(self._gpu_indices()):
+                idx = self._gpu_indices()[g]      # re-read: a change re-enumerates the devices
+                e = fn(idx, mode)
+                if e:
+                    errs.append(f"gpu{g} {step} {mode}: {e}")
+            if errs:
+                break                   # never apply the compute mode after a failed memory change
         self.publish(force=True)
+        self.publish_caps(force=True)
         res.untaint_node(self.node, C.TAINT_PARTITIONING)
-        self.redis.set(schema.partition_key(self.node), json.dumps(
-            {"state": "failed" if errs else "applied", "mode": want, "errors": errs}))
-        self.partition_state = "idle"
+        self._set_partition_state("failed" if errs else "applied", mode=target_c, memory=target_m, errors=errs)
         if errs:
-            log.warning("partitioning %s to %s: %s", self.node, want, errs)
+            log.warning("partitioning %s to %s/%s: %s", self.node, target_c, target_m, errs)
         return not errs
 
     # ------------------------------------------------------------------ loop
@@ -233,6 +366,10 @@ class NodeAgent:
         except Exception as e:
             log.warning("partition reconcile failed: %s", e)
         self.publish()
+        try:
+            self.publish_caps()
+        except Exception as e:
+            log.warning("publishing partition capabilities failed: %s", e)
         samples = self.sample()
         try:
             self.check_health(samples)

@@ -62,6 +62,17 @@ ANNOT_NODE_SCORE = ANNOT_PREFIX + "score"
 # node annotation kept by the agent: JSON {uuid: reason} of unhealthy devices ("{}" when
 # all are healthy) -- also the change trigger that makes schedulers re-read the inventory
 ANNOT_UNHEALTHY = ANNOT_PREFIX + "unhealthy-devices"
+# pod annotation "partition": the pod needs a hard-isolated compute partition (its own
+# XCDs / HBM share) rather than a CU-mask share of a GPU; its size is its amd.com/gpu-cu
+# request, or ANNOT_PARTITION_CUS as chosen by the partition controller from predictions
+ANNOT_ISOLATION = ANNOT_PREFIX + "isolation"
+ANNOT_PARTITION_CUS = ANNOT_PREFIX + "partition-cus"
+# node annotations kept by the agent: the probed partition capabilities (JSON
+# PartitionCaps) and the state of the last partition request (JSON {state, mode, ...})
+ANNOT_PARTITION_CAPS = ANNOT_PREFIX + "partition-caps"
+ANNOT_PARTITION_STATE = ANNOT_PREFIX + "partition-state"
+# per-pod HBM overuse verdicts of the agent (node annotation, JSON {pod: {used_gib, cap_gib}})
+ANNOT_HBM_OVERUSE = ANNOT_PREFIX + "hbm-overuse"
 
 ENV_SLO = "SLO"
 # batch pods: query batches the pod will run (the scheduler predicts its GPU time from it)

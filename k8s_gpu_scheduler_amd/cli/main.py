@@ -111,15 +111,34 @@ def cmd_scheduler(args) -> int:
         sched.start()
     if sched.telemetry_poller is not None:
         sched.telemetry_poller.start()
+    ctrls = _partition_controllers(sched)
     try:
         while not stop.is_set():
+            if ctrls and (not cfg.leader_election.leader_elect or sched._thread is not None):
+                for c in ctrls:         # only the leader (once its loop runs) re-partitions
+                    c.start()
             stop.wait(1.0)
     except KeyboardInterrupt:
         pass
+    for c in ctrls:
+        c.stop()
     if sched.telemetry_poller is not None:
         sched.telemetry_poller.stop()
     sched.stop()
     return 0
+
+
+def _partition_controllers(sched):
+    """The GPU plugin's partition controllers (plugins.gpu.partitioner), one per profile."""
+    out = []
+    for fw in sched.frameworks.values():
+        try:
+            p = fw.plugin(C.PLUGIN_NAME)
+        except Exception:
+            continue
+        if p is not None and getattr(p, "partitioner", None) is not None:
+            out.append(p.partitioner)
+    return out
 
 
 def cmd_extender(args) -> int:

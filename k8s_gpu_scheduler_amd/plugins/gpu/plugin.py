@@ -69,6 +69,19 @@ class GpuRequest:
     gpu_pod: bool = False
     burstable: bool = False
     implicit: bool = False  # SLO env only, no amd.com/* request: GPU preferred, not required
+    isolated: bool = False  # needs its own compute partition (ANNOT_ISOLATION = "partition")
+    part_cus: int = 0       # ... of this many CUs (0 = not sized yet)
+
+
+PARTITION_SIZES = tuple(C.MI355X_CUS // p for p in sorted(C.COMPUTE_PARTITIONS.values(), reverse=True))  # 32..256
+
+
+def partition_size(cus: int) -> int:
+    """Smallest MI355X compute-partition size (CPX 32 .. SPX 256 CUs) holding `cus`."""
+    for s in PARTITION_SIZES:
+        if cus <= s:
+            return s
+    return C.MI355X_CUS
 
 
 @dataclass
@@ -113,6 +126,10 @@ class GPUArgs:
     reconfigure_timeout_s: float = 60.0
     parity_shuffle: bool = True
     seed: Optional[int] = None
+    # partition controller (plugins.gpu.partitioner): "auto" re-partitions idle nodes for
+    # pending pods that ask for an isolated partition; "off" never requests a change
+    partitioning: str = "auto"
+    partition_period_s: float = 2.0
 
     @classmethod
     def from_dict(cls, d: Dict[str, Any]) -> "GPUArgs":
@@ -123,7 +140,8 @@ class GPUArgs:
                  "planObjective": "plan_objective",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
-                 "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle"}
+                 "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle",
+                 "partitionPeriodSeconds": "partition_period_s"}
         for k, v in (d or {}).items():
             k = alias.get(k, k)
             if hasattr(a, k):
@@ -173,8 +191,12 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if self.args.mode == "parity":
             from .parity import ParityLogic
             self.parity = ParityLogic(self)
+        self.partitioner = None
         if handle is not None:
             self._wire_informers()
+            if self.args.mode != "parity" and self.args.partitioning == "auto":
+                from .partitioner import PartitionController
+                self.partitioner = PartitionController(self, period_s=self.args.partition_period_s)
 
     # ------------------------------------------------------------------ wiring
     def _wire_informers(self) -> None:
@@ -240,6 +262,14 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         g, cu, mem = O.gpu_request(pod)
         slo = O.pod_slo(pod)
         r = GpuRequest(slo=slo, hbm_gib=mem, burstable=O.gpu_qos(pod) == "Burstable")
+        ann = O.annotations(pod)
+        if ann.get(C.ANNOT_ISOLATION) == "partition":
+            # one whole compute partition of the requested (or controller-chosen) size
+            size = cu if cu > 0 else int(float(ann.get(C.ANNOT_PARTITION_CUS) or 0))
+            r.isolated, r.gpu_pod, r.whole = True, True, 1
+            r.part_cus = partition_size(size) if size > 0 else 0
+            r.cu = r.part_cus
+            return r
         if cu > 0:
             r.cu = min(cu, C.MI355X_CUS)
             r.units = max(1, math.ceil(r.cu / CUS_PER_XCD))
@@ -283,12 +313,17 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return Status.unschedulable("node is being re-partitioned", self.NAME)
         if not self.ledger.has_node(node_info.name):
             self._on_node(node)
+        if req.isolated and not req.part_cus:
+            return Status.unschedulable("waiting for partition sizing", self.NAME)
         removed = getattr(node_info, "removed", None)
         if removed:                 # preemption what-if: victims' units/HBM released
             if self._fits_without(req, node_info.name, removed):
                 return None
             return Status.unschedulable("insufficient free GPU units/HBM even without lower-priority pods", self.NAME)
         choice = self._best_choice(state, pod, req, node_info.name, scoring=False)
+        if choice is None and req.isolated:
+            mode = C.PARTITIONS_TO_MODE.get(C.MI355X_CUS // req.part_cus, "?")
+            return Status.unschedulable(f"no free {mode} partition ({req.part_cus} CUs)", self.NAME)
         if choice is None and not req.implicit:
             return Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME)
         return None
@@ -299,6 +334,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if self.parity is not None:
             return [None] * len(node_infos)
         req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
+        if req.isolated:                # rare: the per-node path (with its partition messages)
+            return [self.filter(state, pod, ni) for ni in node_infos]
         out: List[Optional[Status]] = []
         memo = state.read(_CANDS)
         if memo is None:
@@ -772,7 +809,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
 
     def _whole_choice(self, req: GpuRequest, node: str, states: List[DeviceState]) -> Optional[Choice]:
         free = [st for st in states if st.device.healthy and not st.pods
-                and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)]
+                and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)
+                and (not req.isolated or st.device.cus == req.part_cus)]
         if len(free) < req.whole:
             return None
         per = req.hbm_gib / max(req.whole, 1)

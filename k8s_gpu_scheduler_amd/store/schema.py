@@ -37,6 +37,11 @@ def partition_key(node: str) -> str:
     return f"{PREFIX}partition:{node}"
 
 
+def partition_caps_key(node: str) -> str:
+    """JSON agent.devices.PartitionCaps: the modes the node's GPUs support (probed)."""
+    return f"{PREFIX}partcaps:{node}"
+
+
 def model_key(name: str) -> str:
     return f"{PREFIX}model:{name}"
 

@@ -1,0 +1,194 @@
+"""Scheduler-driven MI355X compute partitioning, end to end on a fake cluster.
+
+Reference: Score picks a MIG layout from the pod's predictions, relabels the node, restarts
+the profiler and polls Redis for the new UUIDs (pkg/plugins/gpu_plugin/gpu_plugins.go:357-453,
+478-496).  Here: pending isolated pods -> partition controller (idle nodes only) -> node
+label -> agent (capability probe, idleness check, taint, amd-smi apply, republish, untaint)
+-> scheduler re-reads the inventory -> the pods bind to partitions.
+"""
+import json
+import time
+
+from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+from k8s_gpu_scheduler_amd.agent.devices import StaticSource, partition_capabilities, synthetic_node
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+from k8s_gpu_scheduler_amd.kube.resources import Resources
+from k8s_gpu_scheduler_amd.plugins import full_registry
+from k8s_gpu_scheduler_amd.plugins.gpu.partitioner import size_from_predictions
+from k8s_gpu_scheduler_amd.store import schema
+from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+from k8s_gpu_scheduler_amd.store.resp import Redis
+
+ISO = {C.ANNOT_ISOLATION: "partition"}
+
+
+def rds():
+    return Redis(FakeRedisBackend(FakeRedisEngine()))
+
+
+def _cluster(nodes=("n1",)):
+    fc = FakeCluster()
+    r = rds()
+    agents = {}
+    for n in nodes:
+        fc.create("nodes", O.make_node(n, gpus=8))
+        ag = NodeAgent(n, r, synthetic_node(8, node=n), client=fc)
+        ag.step()                       # publish devices + partition capabilities
+        agents[n] = ag
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, record_events=False,
+                  extras={"redis": r})
+    s.start_informers()
+    plugin = s.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+    return fc, r, agents, s, plugin
+
+
+def _drain(s, fc, names, timeout=15.0):
+    t = time.time()
+    while time.time() - t < timeout:
+        s.schedule_pending(timeout_s=0.2)
+        if all(O.node_name_of(fc.get("pods", n, "default")) for n in names):
+            return True
+    return False
+
+
+def test_size_from_predictions_most_partitions_meeting_slo():
+    conf = {"1P_MI355X": 100.0, "2P_MI355X": 80.0, "4P_MI355X": 60.0, "8P_MI355X": 30.0}
+    assert size_from_predictions(conf, 50.0) == 64          # QPX: 60 >= 50, CPX 30 < 50
+    assert size_from_predictions(conf, 20.0) == 32          # CPX meets it
+    assert size_from_predictions(conf, 500.0) == 256        # nothing meets it: best predicted
+    assert size_from_predictions({}, 50.0) is None
+
+
+def test_agent_publishes_probed_capabilities():
+    fc, r, agents, s, plugin = _cluster()
+    caps = json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_CAPS])
+    assert caps["compute_modes"] == ["SPX", "DPX", "QPX", "CPX"] and caps["probed"]
+    assert json.loads(r.get(schema.partition_caps_key("n1"))) == caps
+
+
+def test_burst_of_eighth_gpu_pods_triggers_cpx_and_binds(monkeypatch):
+    fc, r, agents, s, plugin = _cluster()
+    taints = []
+    orig = Resources.taint_node
+
+    def spy(self, node, key, value="true", effect="NoSchedule"):
+        taints.append((node, key, value))
+        return orig(self, node, key, value, effect)
+    monkeypatch.setattr(Resources, "taint_node", spy)
+    names = [f"iso-{i}" for i in range(16)]
+    for n in names:
+        fc.create("pods", O.make_pod(n, gpu_cu=32, gpu_mem_gib=8, annotations_=ISO))
+    res = s.schedule_pending()
+    assert len(res) == 16 and not any(x.node for x in res)
+    assert "no free CPX partition" in res[0].status.message()
+    # the controller (never Score) asks for CPX on the idle node
+    dec = plugin.partitioner.step()
+    assert [(d.node, d.mode) for d in dec] == [("n1", "CPX")]
+    assert O.labels(fc.get("nodes", "n1"))[C.LABEL_COMPUTE_PARTITION] == "CPX"
+    assert plugin.partitioner.step() == []                  # already requested: no second request
+    # the agent: taint -> apply -> republish 64 UUIDs -> untaint
+    assert agents["n1"].reconcile_partitions()
+    assert taints == [("n1", C.TAINT_PARTITIONING, "CPX")]
+    assert not O.node_taints(fc.get("nodes", "n1"))
+    assert len(schema.read_uuids(r, "n1")) == 64
+    assert json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_STATE])["state"] == "applied"
+    # the scheduler re-reads the inventory on the node update; the pods bind to partitions
+    assert _drain(s, fc, names)
+    devs = {d.device.uuid: d.device for d in plugin.ledger.devices("n1")}
+    got = [O.annotations(fc.get("pods", n, "default"))[C.ANNOT_DEVICES] for n in names]
+    assert len(set(got)) == 16 and all(devs[u].cus == 32 and devs[u].partitions == 8 for u in got)
+
+
+def test_controller_never_picks_a_busy_node():
+    fc, r, agents, s, plugin = _cluster(("n1", "n2"))
+    fc.create("pods", O.make_pod("resident", gpu_cu=64, gpu_mem_gib=4,
+                                 node_selector={"kubernetes.io/hostname": "n1"}))
+    (res,) = s.schedule_pending()
+    assert res.node == "n1"
+    for i in range(8):
+        fc.create("pods", O.make_pod(f"iso-{i}", gpu_cu=64, annotations_=ISO))
+    s.schedule_pending()
+    dec = plugin.partitioner.step()
+    assert [(d.node, d.mode) for d in dec] == [("n2", "QPX")]
+    assert O.labels(fc.get("nodes", "n1"))[C.LABEL_COMPUTE_PARTITION] == "SPX"
+
+
+def test_slo_only_isolated_pod_is_sized_from_predictions():
+    from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, _Tab
+    fc, r, agents, s, plugin = _cluster()
+    cp = CachedPredictions()
+    cols = ["1P_MI355X", "2P_MI355X", "4P_MI355X", "8P_MI355X"]
+    cp._conf = _Tab(["onnx_resnet50_1024"], cols, [[400.0, 300.0, 200.0, 90.0]], "t")
+    cp._intf = _Tab(["onnx_resnet50_1024_MI355X"], ["onnx_resnet50_1024"], [[0.0]], "t")
+    plugin.predictions = cp
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-a", slo=150, annotations_=ISO))
+    s.schedule_pending()
+    dec = plugin.partitioner.step()
+    pod = fc.get("pods", "onnx-resnet50-1024-a", "default")
+    assert O.annotations(pod)[C.ANNOT_PARTITION_CUS] == "64"        # 4P meets 150, 8P does not
+    assert [d.mode for d in dec] == ["QPX"]
+    assert agents["n1"].reconcile_partitions()
+    assert _drain(s, fc, ["onnx-resnet50-1024-a"])
+    u = O.annotations(fc.get("pods", "onnx-resnet50-1024-a", "default"))[C.ANNOT_DEVICES]
+    assert {d.device.uuid: d.device.cus for d in plugin.ledger.devices("n1")}[u] == 64
+
+
+def test_agent_refuses_busy_gpu_then_gives_up():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=8))
+    src = synthetic_node(8, node="n1")
+    src.procs = {3: [{"pid": 4242, "name": "train.py", "vram_bytes": 2**30}]}
+    ag = NodeAgent("n1", rds(), src, client=fc, drain_timeout_s=3600)
+    ag.step()
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "CPX"}}}, "merge")
+    assert not ag.reconcile_partitions()
+    assert src.partition_calls == []                         # a busy GPU is never repartitioned
+    st = json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_STATE])
+    assert st["state"] == "waiting-idle" and "pid 4242" in st["busy"][0]
+    assert O.node_taints(fc.get("nodes", "n1"))[0]["key"] == C.TAINT_PARTITIONING    # draining
+    ag.drain_timeout_s = 0.0
+    time.sleep(0.01)
+    assert not ag.reconcile_partitions()
+    st = json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_STATE])
+    assert st["state"] == "refused" and not O.node_taints(fc.get("nodes", "n1"))
+    assert O.labels(fc.get("nodes", "n1"))[C.LABEL_COMPUTE_PARTITION] == "SPX"      # request reverted
+    assert src.partition_calls == []
+
+
+def test_agent_refuses_unsupported_mode_and_unprobed_gpu():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=2))
+    src = StaticSource(synthetic_node(2, node="n1").devices(), profiles=[
+        {"mode": "SPX", "partitions": 1, "memory_caps": ["NPS1"]},
+        {"mode": "CPX", "partitions": 8, "memory_caps": ["NPS1"]}])
+    ag = NodeAgent("n1", rds(), src, client=fc)
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "QPX"}}}, "merge")
+    assert not ag.reconcile_partitions() and src.partition_calls == []
+    st = json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_STATE])
+    assert st["state"] == "refused" and "not supported" in st["reason"]
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "CPX",
+                                                     C.LABEL_MEMORY_PARTITION: "NPS2"}}}, "merge")
+    assert not ag.reconcile_partitions() and src.partition_calls == []       # NPS2 not allowed with CPX
+    # no readable profiles (amd-smi without privileges): nothing is assumed, nothing applied
+    src.profiles = []
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "CPX"}}}, "merge")
+    assert not ag.reconcile_partitions() and src.partition_calls == []
+    assert "unknown" in json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_STATE])["reason"]
+
+
+def test_memory_partition_applied_before_compute():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=2))
+    src = synthetic_node(2, node="n1")
+    ag = NodeAgent("n1", rds(), src, client=fc)
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "DPX",
+                                                     C.LABEL_MEMORY_PARTITION: "NPS2"}}}, "merge")
+    assert ag.reconcile_partitions()
+    assert src.partition_calls[:2] == [(0, "NPS2"), (1, "NPS2")]
+    assert [m for _, m in src.partition_calls[2:]] == ["DPX", "DPX"]
+    caps = partition_capabilities(src.partition_info(0))
+    assert caps.current_memory == "NPS2" and caps.current_compute == "DPX"
