@@ -61,7 +61,7 @@ class NodeAgent:
                  poll_s: float = C.PROFILER_POLL_S, exporter: Any = None, telemetry: Any = None,
                  apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None,
                  health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
-                 drain_timeout_s: float = 300.0):
+                 drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -76,6 +76,11 @@ class NodeAgent:
         self.drain_timeout_s = drain_timeout_s
         self._drain_since: Optional[float] = None
         self._caps_published: Optional[str] = None
+        self._overuse_published: Optional[str] = None
+        self._overuse_flagged: set = set()
+        self.evict_hbm_overuse = evict_hbm_overuse
+        self.history_every = max(1, history_every)
+        self._steps = 0
         self.health = health or HealthMonitor()
         # Evict the pods of a device that turned unhealthy (their controllers recreate them
         # and the scheduler places them elsewhere -- the elastic-recovery path); off by
@@ -177,22 +182,107 @@ class NodeAgent:
                 except Exception as e:
                     log.warning("evicting %s failed: %s", O.key(p), e)
 
-    def record_history(self, uid_to_pod: Optional[Dict[str, str]] = None) -> int:
-        """Per-pod usage samples from the per-process list (VRAM, CU occupancy)."""
-        n = 0
-        uid_to_pod = uid_to_pod or {}
+    def _pods_on_node(self) -> Dict[str, Dict[str, Any]]:
+        """uid -> pod object of the non-terminal pods bound to this node ({} without apiserver)."""
+        if self.client is None:
+            return {}
+        try:
+            pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        except Exception as e:
+            log.debug("listing pods on %s failed: %s", self.node, e)
+            return {}
+        return {O.uid(p): p for p in pods if not O.is_terminal(p) and O.uid(p)}
+
+    def pod_usage(self, uid_to_pod: Optional[Dict[str, str]] = None) -> Dict[str, Dict[str, Any]]:
+        """Per-pod GPU usage from amd-smi's per-process list: processes are attributed to
+        pods through their cgroup (pod_resolver), VRAM summed over a pod's processes and
+        devices.  Keyed by "ns/name"; `uid_to_pod` overrides the apiserver lookup."""
+        pods = self._pods_on_node() if uid_to_pod is None else {}
+        out: Dict[str, Dict[str, Any]] = {}
         for i, d in enumerate(self.source.devices()):
             for p in self.source.processes(i):
                 uid = self.pod_resolver(int(p.get("pid", 0)))
-                pod = uid_to_pod.get(uid or "", uid)
-                if not pod:
+                if not uid:
                     continue
-                schema.append_history(self.redis, pod, {
-                    "ts": time.time(), "device": d["uuid"], "hbm_gib": p.get("vram_bytes", 0) / 2**30,
-                    "cu_busy": min(1.0, p.get("cu_occupancy", 0) / max(d.get("cus", C.MI355X_CUS), 1)),
-                    "cu": d.get("cus", C.MI355X_CUS)})
-                n += 1
+                obj = pods.get(uid)
+                key = (uid_to_pod or {}).get(uid) or (O.key(obj) if obj is not None else None)
+                if not key:
+                    continue
+                u = out.setdefault(key, {"pod": obj, "hbm_gib": 0.0, "cu_busy": 0.0, "devices": [], "pids": [],
+                                         "cus": d.get("cus", C.MI355X_CUS)})
+                u["hbm_gib"] += float(p.get("vram_bytes", 0)) / 2**30
+                u["cu_busy"] = max(u["cu_busy"], min(1.0, float(p.get("cu_occupancy", 0)) /
+                                                     max(d.get("cus", C.MI355X_CUS), 1)))
+                if d["uuid"] not in u["devices"]:
+                    u["devices"].append(d["uuid"])
+                u["pids"].append(int(p.get("pid", 0)))
+                if "throughput" in p:           # executors that know their pods' rate report it
+                    u["throughput"] = float(p["throughput"])
+        return out
+
+    def record_history(self, uid_to_pod: Optional[Dict[str, str]] = None,
+                       usage: Optional[Dict[str, Dict[str, Any]]] = None) -> int:
+        """Append one usage sample per running pod to its history in Redis -- keyed by the
+        pod's WORKLOAD (recommender.admission.workload_key), which is what the resize
+        admission reads; `uid_to_pod` (tests / no apiserver) keys by the given name."""
+        from ..recommender.admission import workload_key
+        usage = self.pod_usage(uid_to_pod) if usage is None else usage
+        n = 0
+        for key, u in usage.items():
+            pod = u.get("pod")
+            hist_key = workload_key(pod) if pod is not None else key
+            _, cu_req, _ = O.gpu_request(pod) if pod is not None else (0, 0, 0.0)
+            sample = {"ts": time.time(), "pod": key, "device": ",".join(u["devices"]), "hbm_gib": u["hbm_gib"],
+                      "cu_busy": u["cu_busy"], "cu": int(cu_req or u.get("cus", C.MI355X_CUS)), "source": "agent"}
+            if "throughput" in u:
+                sample["throughput"] = u["throughput"]
+            schema.append_history(self.redis, hist_key, sample)
+            n += 1
         return n
+
+    def check_hbm(self, usage: Optional[Dict[str, Dict[str, Any]]] = None, tolerance_gib: float = 0.25,
+                  evict: Optional[bool] = None) -> Dict[str, Dict[str, float]]:
+        """HBM share enforcement by detection (the driver does not cap a process's VRAM the
+        way MPS's CUDA_MPS_PINNED_DEVICE_MEM_LIMIT does, reference gpu_plugins.go:896-903):
+        a pod whose processes hold more VRAM than its cap -- its amd.com/gpu-memory request
+        (= the GPU_SCHED_HBM_LIMIT_GIB the scheduler gave it) -- is flagged in the node
+        annotation `hbm-overuse`, the exporter gauge `amd_gpu_pod_hbm_overuse` and a Warning
+        event, and with `evict_hbm_overuse` deleted (its controller recreates it)."""
+        usage = self.pod_usage() if usage is None else usage
+        evict = self.evict_hbm_overuse if evict is None else evict
+        over: Dict[str, Dict[str, float]] = {}
+        for key, u in usage.items():
+            pod = u.get("pod")
+            cap = O.gpu_request(pod)[2] if pod is not None else float(u.get("cap_gib", 0.0))
+            if self.exporter is not None:
+                self.exporter.observe_pod_hbm(key, u["hbm_gib"], cap)
+            if cap > 0 and u["hbm_gib"] > cap + tolerance_gib:
+                over[key] = {"used_gib": round(u["hbm_gib"], 3), "cap_gib": cap}
+        raw = json.dumps(over, sort_keys=True, separators=(",", ":"))
+        if raw != self._overuse_published and self.client is not None:
+            try:
+                self.client.patch("nodes", self.node, {"metadata": {"annotations": {C.ANNOT_HBM_OVERUSE: raw}}},
+                                  "merge")
+                self._overuse_published = raw
+            except Exception as e:
+                log.warning("hbm-overuse annotation on %s failed: %s", self.node, e)
+            for key in set(over) - self._overuse_flagged:
+                pod = usage[key].get("pod")
+                msg = f"HBM {over[key]['used_gib']:.2f} GiB exceeds the pod's {over[key]['cap_gib']:g} GiB share"
+                log.warning("%s: %s", key, msg)
+                if pod is not None:
+                    try:
+                        self.client.create_event(pod, "GPUMemoryOveruse", msg, "Warning")
+                    except Exception:
+                        pass
+                    if evict:
+                        try:
+                            self.client.delete("pods", O.name(pod), O.namespace(pod))
+                            self.evicted.append(key)
+                        except Exception as e:
+                            log.warning("evicting %s failed: %s", key, e)
+        self._overuse_flagged = set(over)
+        return over
 
     # ------------------------------------------------------------------ partitions
     def desired_partition(self) -> Optional[str]:
@@ -375,6 +465,15 @@ class NodeAgent:
             self.check_health(samples)
         except Exception as e:
             log.warning("health check failed: %s", e)
+        self._steps += 1
+        if self._steps % self.history_every == 0:
+            try:
+                usage = self.pod_usage()
+                if usage:
+                    self.record_history(usage=usage)
+                self.check_hbm(usage)
+            except Exception as e:
+                log.warning("per-pod usage / HBM check failed: %s", e)
 
     def run(self) -> None:
         while not self._stop.is_set():

@@ -226,7 +226,8 @@ def cmd_agent(args) -> int:
     exp = GpuExporter(node, os.getenv("POD_NAME", "amd-gpu-exporter"), dcgm_compat=args.dcgm_compat)
     if args.metrics_port:
         exp.serve(args.metrics_port)
-    agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy)
+    agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy,
+                      evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout)
     mgr = None
     if args.device_plugin:
         # kubelet device plugin for amd.com/gpu, amd.com/gpu-cu, amd.com/gpu-memory
@@ -374,6 +375,10 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--device-plugin-dir", default="/var/lib/kubelet/device-plugins")
     s.add_argument("--evict-unhealthy", action="store_true",
                    help="delete pods assigned to a GPU that turns unhealthy (controllers reschedule them)")
+    s.add_argument("--evict-hbm-overuse", action="store_true",
+                   help="delete pods whose processes hold more VRAM than their amd.com/gpu-memory share")
+    s.add_argument("--drain-timeout", type=float, default=300.0,
+                   help="seconds a partition request waits for the GPUs to go idle before it is refused")
     s.set_defaults(fn=cmd_agent)
     s = sub.add_parser("redisctl")
     s.add_argument("-l", "--list", action="store_true", help="List redis' data")

@@ -11,8 +11,11 @@ epoch:
      next epoch -- the backlog);
   3. the executor runs the placed pods (Guaranteed QoS: hard CU masks, so a pod's measured
      throughput belongs to its share) on the GPU -- or the roofline model with --sim;
-  4. each finished pod appends (share, throughput, HBM) to its workload's history (the
-     node agent's job in a cluster) and is deleted.
+  4. each finished pod is reported the way a node sees it -- a GPU process with its VRAM,
+     CU occupancy and (executor-known) throughput -- and the real node agent
+     (agent.NodeAgent.pod_usage / record_history: process -> pod attribution through the
+     apiserver, history keyed by workload) appends it to Redis, where the admission reads
+     it; then the pod is deleted.
 
 Reported per run: pods completed/s, mean CU request at admission, SLO attainment, backlog,
 GPU CU-share occupancy -- with and without the loop.
@@ -44,6 +47,37 @@ from ..store.resp import Redis
 from .podbench import SimExecutor, analytic_predictions, measured_predictions
 
 NODE = "mi355x-0"
+
+
+class ExecutorProcessSource:
+    """The executor's finished pods as the agent's device source would list them: one
+    "process" per pod on its device (pid -> pod uid through `uid_of`, like a cgroup)."""
+
+    def __init__(self, ledger: DeviceLedger, node: str):
+        self.ledger, self.node = ledger, node
+        self.procs: Dict[str, List[Dict[str, Any]]] = {}
+        self._uid: Dict[int, str] = {}
+        self._pid = 1000
+
+    def devices(self) -> List[Dict[str, Any]]:
+        return [d.device.to_json() for d in self.ledger.devices(self.node)]
+
+    def processes(self, index: int) -> List[Dict[str, Any]]:
+        devs = self.devices()
+        return list(self.procs.get(devs[index]["uuid"], [])) if 0 <= index < len(devs) else []
+
+    def report(self, uuid: str, pod_uid: str, vram_gib: float, cus: int, throughput: float) -> None:
+        self._pid += 1
+        self._uid[self._pid] = pod_uid
+        self.procs.setdefault(uuid, []).append({"pid": self._pid, "vram_bytes": int(vram_gib * 2**30),
+                                                "cu_occupancy": cus, "throughput": throughput})
+
+    def uid_of(self, pid: int) -> Optional[str]:
+        return self._uid.get(pid)
+
+    def clear(self) -> None:
+        self.procs.clear()
+        self._uid.clear()
 
 
 def _poisson(rng: random.Random, lam: float) -> int:
@@ -79,6 +113,9 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
     sched.keep_results = False
     sched.start_informers()
     sched.queue.initial_backoff_s = 0.0
+    from ..agent.agent import NodeAgent
+    procs = ExecutorProcessSource(ledger, NODE)
+    agent = NodeAgent(NODE, hist.redis, procs, client=fc, pod_resolver=procs.uid_of)    # type: ignore[arg-type]
     from .executor import PodRun
     if sim:
         ex: Any = SimExecutor()
@@ -104,6 +141,7 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
         results = sched.schedule_pending()
         runs: List[PodRun] = []
         placed: List[str] = []
+        devs_of: List[str] = []
         for r in results:
             if not r.node:
                 continue
@@ -117,6 +155,7 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
             stats["req_cu"].append(O.gpu_request(pod)[1])
             runs.append(PodRun(len(runs), workload_key(pod), u0, n, iters, O.pod_slo(pod), masked=True))
             placed.append(r.pod_key)
+            devs_of.append(pl[1][0])
         t0 = time.perf_counter()
         ex.launch_epoch(runs)
         if not sim:
@@ -124,10 +163,13 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
         st_ep = ex.collect(runs)
         wall_ms += (time.perf_counter() - t0) * 1e3 if not sim else max(st_ep["span_ms"], 0.0)
         stats["busy_unit_ms"] += st_ep["busy_unit_ms"]
+        procs.clear()
+        for r, key, uuid in zip(runs, placed, devs_of):
+            ns, name = key.split("/", 1)
+            procs.report(uuid, O.uid(fc.get("pods", name, ns)), W.CATALOG[r.workload].hbm_gib,
+                         r.n_units * CUS_PER_XCD, round(r.throughput, 3))
+        stats["history_samples"] = stats.get("history_samples", 0) + agent.record_history()   # agent -> Redis
         for r, key in zip(runs, placed):
-            w = W.CATALOG[r.workload]
-            hist.append(r.workload, {"cu": r.n_units * CUS_PER_XCD, "throughput": round(r.throughput, 3),
-                                     "hbm_gib": w.hbm_gib})
             stats["completed"] += 1
             stats["slo_ok"] += int(r.slo <= 0 or r.throughput >= r.slo)
             ns, name = key.split("/", 1)
@@ -144,7 +186,9 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
             "cu_share_occupancy_pct": round(100.0 * stats["busy_unit_ms"] / (8 * n_gpus * max(wall_ms, 1e-6)), 2),
             "final_backlog": stats["backlog"][-1] if stats["backlog"] else 0,
             "mean_backlog": round(float(np.mean(stats["backlog"])) if stats["backlog"] else 0.0, 2),
-            "admission": adm.stats if adm is not None else None}
+            "admission": adm.stats if adm is not None else None,
+            "history": {"source": "node agent (process list -> pod -> workload key)",
+                        "samples": stats.get("history_samples", 0)}}
 
 
 def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:

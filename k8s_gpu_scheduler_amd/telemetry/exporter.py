@@ -13,6 +13,9 @@ pkg/prom/fetch_prom_metrics/prom_metrics.go:63-70) and exports nothing of its ow
   amd_gpu_ecc_uncorrectable_total, amd_gpu_ecc_correctable_total (accumulated counts)
   amd_gpu_healthy                             (1/0, the agent's health verdict, agent/health.py)
 
+per pod (labels `pod`, `node`): amd_gpu_pod_hbm_used_gib / _cap_gib / amd_gpu_pod_hbm_overuse
+(the agent's per-process attribution against the pod's HBM share);
+
 optionally the same values under the DCGM names (`dcgm_compat=True`), and scheduler
 series: pods scheduled, scheduling latency histogram, SLO attainment, per-extension-point
 latency.
@@ -48,6 +51,13 @@ class GpuExporter:
                     for k in ("uncorrectable", "correctable")}
         self.healthy = Gauge("amd_gpu_healthy", "1 if the node agent considers the device healthy", lab,
                              registry=self.registry)
+        plab = ["pod", "node"]
+        self.pod_hbm = Gauge("amd_gpu_pod_hbm_used_gib", "VRAM held by a pod's processes (amd-smi process list)",
+                             plab, registry=self.registry)
+        self.pod_hbm_cap = Gauge("amd_gpu_pod_hbm_cap_gib", "the pod's HBM share (amd.com/gpu-memory request)",
+                                 plab, registry=self.registry)
+        self.pod_overuse = Gauge("amd_gpu_pod_hbm_overuse", "1 if the pod holds more VRAM than its HBM share",
+                                 plab, registry=self.registry)
 
     def observe_samples(self, samples: Iterable[Dict[str, float]], uuids: Dict[int, str]) -> None:
         for s in samples:
@@ -72,6 +82,11 @@ class GpuExporter:
             if self.dcgm:
                 for dm, am in C.DCGM_TO_AMD.items():
                     self.dcgm[dm].labels(*lv).set(vals[am])
+
+    def observe_pod_hbm(self, pod: str, used_gib: float, cap_gib: float, tolerance_gib: float = 0.25) -> None:
+        self.pod_hbm.labels(pod, self.node).set(used_gib)
+        self.pod_hbm_cap.labels(pod, self.node).set(cap_gib)
+        self.pod_overuse.labels(pod, self.node).set(1.0 if cap_gib > 0 and used_gib > cap_gib + tolerance_gib else 0.0)
 
     def observe_health(self, healthy: Dict[int, bool], uuids: Dict[int, str]) -> None:
         for idx, ok in healthy.items():

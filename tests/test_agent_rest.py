@@ -235,3 +235,58 @@ def test_profiled_launcher_records_history(tmp_path, monkeypatch):
     (h,) = hist.read("onnx_resnet50_1024")
     assert h["gpu_busy_ms"] == 2.5 and h["kernels"] == 80 and h["cu"] == 64 and h["hbm_gib"] == 8
     assert h["top"][0]["name"].startswith("gemm_bf16")
+
+
+def _bound_pod(fc, name, mem_gib, node="n1"):
+    pod = O.make_pod(name, gpu_cu=64, gpu_mem_gib=mem_gib, node_name=node, phase="Running")
+    fc.create("pods", pod)
+    return fc.get("pods", name, "default")
+
+
+def test_agent_flags_hbm_overuse_and_records_workload_history():
+    """Scripted amd-smi process list: pod A's process holds 6 GiB against a 4 GiB share
+    (flagged: node annotation, exporter gauge, event), pod B stays inside its share; both
+    get a history sample under their WORKLOAD key (what the resize admission reads)."""
+    from k8s_gpu_scheduler_amd.recommender.admission import RedisHistory, workload_key
+    from k8s_gpu_scheduler_amd.telemetry.exporter import GpuExporter
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=2))
+    a = _bound_pod(fc, "onnx-resnet50-1024-a", 4)
+    b = _bound_pod(fc, "tensorflow-mobilenet-1024-b", 8)
+    src = synthetic_node(2, node="n1")
+    src.procs = {0: [{"pid": 101, "vram_bytes": 6 * 2**30, "cu_occupancy": 64}],
+                 1: [{"pid": 202, "vram_bytes": 5 * 2**30, "cu_occupancy": 32}]}
+    pids = {101: O.uid(a), 202: O.uid(b)}
+    r = rds()
+    exp = GpuExporter("n1")
+    ag = NodeAgent("n1", r, src, client=fc, exporter=exp, pod_resolver=pids.get)
+    ag.step()
+    over = json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_HBM_OVERUSE])
+    assert list(over) == ["default/onnx-resnet50-1024-a"] and over["default/onnx-resnet50-1024-a"]["cap_gib"] == 4
+    txt = exp.render().decode()
+    assert 'amd_gpu_pod_hbm_overuse{node="n1",pod="default/onnx-resnet50-1024-a"} 1.0' in txt
+    assert 'amd_gpu_pod_hbm_overuse{node="n1",pod="default/tensorflow-mobilenet-1024-b"} 0.0' in txt
+    evs = [e for e in fc.list("events", "default")[0] if e.get("reason") == "GPUMemoryOveruse"]
+    assert len(evs) == 1
+    hist = RedisHistory(r)
+    ha = hist.read(workload_key(a))
+    assert ha and ha[-1]["hbm_gib"] == 6.0 and ha[-1]["cu"] == 64 and ha[-1]["source"] == "agent"
+    assert hist.read(workload_key(b))[-1]["hbm_gib"] == 5.0
+    ag.step()                                                    # same verdict: no second event
+    assert len([e for e in fc.list("events", "default")[0] if e.get("reason") == "GPUMemoryOveruse"]) == 1
+    src.procs[0][0]["vram_bytes"] = 3 * 2**30                    # back inside its share
+    ag.step()
+    assert json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_HBM_OVERUSE]) == {}
+
+
+def test_agent_evicts_hbm_overuse_when_asked():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=1))
+    a = _bound_pod(fc, "greedy", 2)
+    src = synthetic_node(1, node="n1")
+    src.procs = {0: [{"pid": 7, "vram_bytes": 40 * 2**30}]}
+    ag = NodeAgent("n1", rds(), src, client=fc, pod_resolver={7: O.uid(a)}.get, evict_hbm_overuse=True)
+    ag.step()
+    assert ag.evicted == ["default/greedy"]
+    with pytest.raises(NotFound):
+        fc.get("pods", "greedy", "default")

@@ -60,6 +60,8 @@ def test_resize_loop_clears_backlog_sim():
     assert on["created"] == off["created"]
     assert on["completed"] > off["completed"] and on["final_backlog"] < off["final_backlog"]
     assert on["mean_cu_request_placed"] < 128 and on["admission"]["resized"] > 0
+    # the history the admission resized from was written by the node agent's per-process path
+    assert on["history"]["samples"] == on["completed"]
 
 
 def test_dead_control_plane_raises_instead_of_hanging():

@@ -91,3 +91,51 @@ def test_activity_sampler_sees_gemm_load():
     assert busy["samples"] >= 50, busy
     assert busy["gfx_activity_pct_mean"] is not None and busy["gfx_activity_pct_mean"] > 50, (busy, idle)
     assert idle["gfx_activity_pct_mean"] is None or idle["gfx_activity_pct_mean"] < busy["gfx_activity_pct_mean"]
+
+
+def test_agent_flags_real_process_over_its_hbm_share():
+    """A real process allocates 6 GiB on GPU 0 while its pod's share is 4 GiB: the agent's
+    amd-smi process list attributes the VRAM to the pod and flags the overuse."""
+    import subprocess
+    import sys
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import SmiSource
+    from k8s_gpu_scheduler_amd.api import constants as C
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    try:
+        src = SmiSource()
+    except Exception as e:
+        pytest.skip(f"amd-smi unavailable: {e}")
+    code = ("import torch, time; x = torch.empty(6 * 2**30, dtype=torch.uint8, device='cuda:0'); x.fill_(1); "
+            "torch.cuda.synchronize(); print('ready', flush=True); time.sleep(90)")
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    try:
+        assert "ready" in child.stdout.readline()
+        fc = FakeCluster()
+        fc.create("nodes", O.make_node("box", gpus=1))
+        fc.create("pods", O.make_pod("hog", gpu_cu=64, gpu_mem_gib=4, node_name="box", phase="Running"))
+        uid = O.uid(fc.get("pods", "hog", "default"))
+        ag = NodeAgent("box", Redis(FakeRedisBackend(FakeRedisEngine())), src, client=fc,
+                       pod_resolver={child.pid: uid}.get)
+        usage = {}
+        t = time.time()
+        while time.time() - t < 15 and not usage:
+            usage = ag.pod_usage()
+            time.sleep(0.5)
+        procs = [p for i in range(len(src.devices())) for p in src.processes(i)]
+        os.makedirs(OUT, exist_ok=True)
+        with open(os.path.join(OUT, "hbm_overuse.json"), "w") as f:
+            json.dump({"child_pid": child.pid, "processes": procs,
+                       "usage": {k: {kk: vv for kk, vv in v.items() if kk != "pod"} for k, v in usage.items()}},
+                      f, indent=1, default=str)
+        if not usage:
+            pytest.skip(f"amd-smi process list does not show the child here: {procs}")
+        over = ag.check_hbm(usage)
+        assert "default/hog" in over and over["default/hog"]["used_gib"] >= 5.5, (over, usage)
+        assert json.loads(O.annotations(fc.get("nodes", "box"))[C.ANNOT_HBM_OVERUSE])["default/hog"]["cap_gib"] == 4
+    finally:
+        child.kill()
+        child.wait()
