@@ -507,8 +507,18 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         try:
             # Env into the pod's envFrom ConfigMaps BEFORE the bind (the kubelet reads them
             # at container creation -- fixes the reference's PostBind race).
-            if O.env_from_config_maps(pod):
-                res.append_to_existing_config_maps_in_pod(O.name(pod), env, True, pod=pod)
+            # Only into ConfigMaps no other live pod references: replicas sharing one
+            # ConfigMap (reference deploy/busybox: 4 replicas -> one `game-demo`) would
+            # overwrite each other's device (§2.9 #6); there the device identity is removed
+            # and delivered per pod (Binding annotations -> device-plugin Allocate env).
+            cms = O.env_from_config_maps(pod)
+            if cms:
+                shared = self._shared_config_maps(pod, cms)
+                for cm in cms:
+                    if cm in shared:
+                        self._strip_device_env(res, cm, env)
+                    else:
+                        res.update_config_map(cm, env, True)
         except Exception as e:
             return Status.error(f"PreBind: writing device assignment failed: {e}", self.NAME)
         # The per-pod assignment annotations ride on the Binding itself (the apiserver
@@ -518,6 +528,32 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         state.write(BIND_ANNOTATIONS, bind_ann)
         state.write("GPU/env", env)
         return None
+
+    def _shared_config_maps(self, pod: Obj, cms: List[str]) -> set:
+        """envFrom ConfigMaps of `pod` that another non-terminal pod (bound or pending) of the
+        namespace also references."""
+        ns, me = O.namespace(pod), O.key(pod)
+        try:
+            others = self.handle.informer_factory.pods().lister.list(namespace=ns)
+        except Exception:
+            others = self.handle.client.list("pods", ns)[0]
+        want = set(cms)
+        out = set()
+        for p in others:
+            if O.key(p) == me or O.is_terminal(p):
+                continue
+            out |= want & set(O.env_from_config_maps(p))
+            if out == want:
+                break
+        return out
+
+    @staticmethod
+    def _strip_device_env(res: Resources, cm: str, env: Dict[str, str]) -> None:
+        cur = res.get_config_map(cm)
+        data = (cur or {}).get("data") or {}
+        stale = [k for k in env if k in data]
+        if stale:       # JSON merge patch: null deletes the key
+            res.client.patch("configmaps", cm, {"data": {k: None for k in stale}}, "merge", res.namespace)
 
     def post_bind(self, state: CycleState, pod: Obj, node_name: str) -> None:
         if self.parity is not None:

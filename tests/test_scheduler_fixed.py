@@ -361,3 +361,25 @@ def test_default_placement_filters_ports_affinity_spread():
         z = O.labels(fc.get("nodes", r.node))["topology.kubernetes.io/zone"]
         per_zone[z] = per_zone.get(z, 0) + 1
     assert per_zone == {"z1": 2, "z2": 2}
+
+
+def test_replicas_sharing_a_config_map_keep_their_own_device():
+    """replicas referencing one envFrom ConfigMap would overwrite each
+    other's device env.  Fixed mode never writes device identity into a shared ConfigMap
+    (and removes a stale one); each replica's assignment lives in its own annotations (the
+    device plugin's Allocate env), while a pod with a private ConfigMap still gets the env."""
+    fc, s, ledger, tele = world()
+    fc.create("configmaps", O.make_config_map("game-demo", {C.ENV_ROCR_VISIBLE: "GPU-stale", "OTHER": "x"}))
+    fc.create("configmaps", O.make_config_map("private"))
+    for i in range(2):
+        fc.create("pods", O.make_pod(f"busybox-{i}", gpu_cu=64, gpu_mem_gib=4, config_maps=["game-demo"]))
+    fc.create("pods", O.make_pod("solo", gpu_cu=64, gpu_mem_gib=4, config_maps=["private"]))
+    res = s.schedule_pending()
+    assert all(r.status.ok for r in res)
+    shared = fc.get("configmaps", "game-demo", "default")["data"]
+    assert shared == {"OTHER": "x"}                 # no device identity, stale key removed
+    a0 = O.annotations(fc.get("pods", "busybox-0", "default"))
+    a1 = O.annotations(fc.get("pods", "busybox-1", "default"))
+    assert (a0[C.ANNOT_DEVICES], a0[C.ANNOT_DEVICE_INDICES]) != (a1[C.ANNOT_DEVICES], a1[C.ANNOT_DEVICE_INDICES])
+    priv = fc.get("configmaps", "private", "default")["data"]
+    assert priv[C.ENV_ROCR_VISIBLE] == O.annotations(fc.get("pods", "solo", "default"))[C.ANNOT_DEVICES]
