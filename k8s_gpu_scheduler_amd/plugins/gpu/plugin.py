@@ -851,19 +851,30 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return None
         per = req.hbm_gib / max(req.whole, 1)
         parts = states[0].device.partitions
-        if req.whole == 1 or parts > 1:
-            # single device (or partitions): least-fragmenting = GPU with most used devices
+        if req.whole == 1:
+            # single device: least-fragmenting = the GPU with the most used devices
             used_per_gpu: Dict[int, int] = {}
             for st in states:
                 if st.pods:
                     used_per_gpu[st.device.gpu] = used_per_gpu.get(st.device.gpu, 0) + 1
             free.sort(key=lambda s: (-used_per_gpu.get(s.device.gpu, 0), s.device.gpu, s.device.partition))
-            pick = free[:req.whole]
-            sc = 100.0 * (1.0 if req.whole == 1 else 0.8)
-            return Choice(node, [(s.device.uuid, 0, s.device.units, per, True) for s in pick], sc,
+            pick = free[:1]
+            return Choice(node, [(s.device.uuid, 0, s.device.units, per, True) for s in pick], 100.0,
                           [s.device for s in pick])
         topo = self.topologies.get(node) or Topology.fully_connected(max(s.device.gpu for s in states) + 1)
-        by_gpu = {st.device.gpu: st for st in free}
+        by_gpu: Dict[int, DeviceState] = {}
+        if parts > 1:
+            # Multi-device pod on a partitioned node: its devices go to DISTINCT physical
+            # GPUs forming an xGMI clique (select_gpu_set on the physical GPUs), and never to
+            # a GPU whose partitions already serve another multi-device pod -- all partitions
+            # of a GPU share its 7 xGMI links, so two such pods' collectives would contend
+            # (SURVEY.md §5.8 item 3).  Per GPU the lowest free partition is taken.
+            taken = self._multi_device_gpus(states)
+            for st in sorted(free, key=lambda s: (s.device.gpu, s.device.partition)):
+                if st.device.gpu not in taken:
+                    by_gpu.setdefault(st.device.gpu, st)
+        else:
+            by_gpu = {st.device.gpu: st for st in free}
         load: Dict[int, float] = {}
         if self.args.w_telemetry:
             for g, st in by_gpu.items():
@@ -877,6 +888,17 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         pick = [by_gpu[g] for g in gpus]
         return Choice(node, [(s.device.uuid, 0, s.device.units, per, True) for s in pick], 100.0 * quality,
                       [s.device for s in pick])
+
+    def _multi_device_gpus(self, states: List[DeviceState]) -> set:
+        """Physical GPUs hosting a device of a pod that holds more than one device."""
+        out = set()
+        for st in states:
+            for key in st.pods:
+                pl = self.ledger.placement(key)
+                if pl is not None and len(pl[1]) > 1:
+                    out.add(st.device.gpu)
+                    break
+        return out
 
 
 def register(registry: Any) -> None:

@@ -383,3 +383,36 @@ def test_replicas_sharing_a_config_map_keep_their_own_device():
     assert (a0[C.ANNOT_DEVICES], a0[C.ANNOT_DEVICE_INDICES]) != (a1[C.ANNOT_DEVICES], a1[C.ANNOT_DEVICE_INDICES])
     priv = fc.get("configmaps", "private", "default")["data"]
     assert priv[C.ENV_ROCR_VISIBLE] == O.annotations(fc.get("pods", "solo", "default"))[C.ANNOT_DEVICES]
+
+
+@pytest.mark.parametrize("mode,parts", [("CPX", 8), ("QPX", 4)])
+def test_multi_device_pods_on_partitions_spread_over_distinct_gpus(mode, parts):
+    """a multi-device pod on a partitioned node gets partitions of
+    DISTINCT physical GPUs forming an xGMI clique (same NUMA domain first), and two
+    multi-device pods never share a physical GPU (its partitions share its xGMI links);
+    single-device pods may still use any free partition."""
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("node-a", gpus=8, partition=mode))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, seed=0)
+    s.start_informers()
+    plugin = s.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+    gpu_of = {st.device.uuid: st.device.gpu for st in plugin.ledger.devices("node-a")}
+    assert len(gpu_of) == 8 * parts
+
+    def gpus(name):
+        ann = O.annotations(fc.get("pods", name, "default"))[C.ANNOT_DEVICES].split(",")
+        return [gpu_of[u] for u in ann]
+    fc.create("pods", O.make_pod("ring-a", gpus=4))
+    fc.create("pods", O.make_pod("ring-b", gpus=4))
+    r = s.schedule_pending()
+    assert all(x.status.ok for x in r), [x.status.message() for x in r]
+    ga, gb = gpus("ring-a"), gpus("ring-b")
+    assert len(set(ga)) == 4 and len(set(gb)) == 4 and not set(ga) & set(gb)
+    topo = plugin.topologies["node-a"]
+    assert len({topo.numa[g] for g in ga}) == 1 and len({topo.numa[g] for g in gb}) == 1
+    fc.create("pods", O.make_pod("ring-c", gpus=2))         # every GPU already carries a ring
+    (rc,) = s.schedule_pending()
+    assert not rc.node
+    fc.create("pods", O.make_pod("single", gpus=1))
+    (rs,) = s.schedule_pending()
+    assert rs.status.ok and rs.node == "node-a"
