@@ -226,8 +226,13 @@ def cmd_agent(args) -> int:
     exp = GpuExporter(node, os.getenv("POD_NAME", "amd-gpu-exporter"), dcgm_compat=args.dcgm_compat)
     if args.metrics_port:
         exp.serve(args.metrics_port)
+    # amd-smi reports HOST pids: attribute them through the host's /proc (the DaemonSet
+    # mounts it at /host/proc) unless told otherwise
+    from ..agent.agent import pod_of_pid
+    proc_root = args.proc_root or ("/host/proc" if os.path.isdir("/host/proc") else "/proc")
     agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy,
-                      evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout)
+                      evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout,
+                      pod_resolver=lambda pid: pod_of_pid(pid, proc_root))
     mgr = None
     if args.device_plugin:
         # kubelet device plugin for amd.com/gpu, amd.com/gpu-cu, amd.com/gpu-memory
@@ -377,6 +382,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="delete pods assigned to a GPU that turns unhealthy (controllers reschedule them)")
     s.add_argument("--evict-hbm-overuse", action="store_true",
                    help="delete pods whose processes hold more VRAM than their amd.com/gpu-memory share")
+    s.add_argument("--proc-root", default="", help="host /proc for pid -> pod attribution (default /host/proc)")
     s.add_argument("--drain-timeout", type=float, default=300.0,
                    help="seconds a partition request waits for the GPUs to go idle before it is refused")
     s.set_defaults(fn=cmd_agent)

@@ -111,15 +111,28 @@ def test_agent_flags_real_process_over_its_hbm_share():
         pytest.skip(f"amd-smi unavailable: {e}")
     code = ("import torch, time; x = torch.empty(6 * 2**30, dtype=torch.uint8, device='cuda:0'); x.fill_(1); "
             "torch.cuda.synchronize(); print('ready', flush=True); time.sleep(90)")
+    # amd-smi lists HOST pids (in a cluster the agent resolves them through the host's
+    # /proc); here the box's container has its own pid namespace, so the child's host pid
+    # is the one that appears in the process list when the child starts
+    def pids():
+        return {int(p["pid"]) for i in range(len(src.devices())) for p in src.processes(i)}
+    before = pids()
     child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
     try:
         assert "ready" in child.stdout.readline()
+        new = set()
+        t = time.time()
+        while time.time() - t < 15 and not new:
+            new = pids() - before
+            time.sleep(0.2)
         fc = FakeCluster()
         fc.create("nodes", O.make_node("box", gpus=1))
         fc.create("pods", O.make_pod("hog", gpu_cu=64, gpu_mem_gib=4, node_name="box", phase="Running"))
         uid = O.uid(fc.get("pods", "hog", "default"))
+        host_pids = {p: uid for p in new}
+        host_pids[child.pid] = uid
         ag = NodeAgent("box", Redis(FakeRedisBackend(FakeRedisEngine())), src, client=fc,
-                       pod_resolver={child.pid: uid}.get)
+                       pod_resolver=host_pids.get)
         usage = {}
         t = time.time()
         while time.time() - t < 15 and not usage:
@@ -128,7 +141,7 @@ def test_agent_flags_real_process_over_its_hbm_share():
         procs = [p for i in range(len(src.devices())) for p in src.processes(i)]
         os.makedirs(OUT, exist_ok=True)
         with open(os.path.join(OUT, "hbm_overuse.json"), "w") as f:
-            json.dump({"child_pid": child.pid, "processes": procs,
+            json.dump({"child_pid": child.pid, "new_host_pids": sorted(new), "processes": procs,
                        "usage": {k: {kk: vv for kk, vv in v.items() if kk != "pod"} for k, v in usage.items()}},
                       f, indent=1, default=str)
         if not usage:
