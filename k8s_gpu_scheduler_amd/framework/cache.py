@@ -13,6 +13,7 @@ import time
 from typing import Any, Dict, List, Optional
 
 from ..api import objects as O
+from .changes import ChangeFanout
 
 Obj = Dict[str, Any]
 
@@ -78,9 +79,17 @@ class NodeInfo:
 class Snapshot:
     """Immutable per-cycle view of all NodeInfos (ordered by name for determinism)."""
 
-    def __init__(self, infos: Dict[str, NodeInfo]):
+    def __init__(self, infos: Dict[str, NodeInfo], ordered: Optional[List[NodeInfo]] = None,
+                 index: Optional[Dict[str, int]] = None):
         self._infos = infos
-        self._list = [infos[k] for k in sorted(infos)]
+        self._list = ordered if ordered is not None else [infos[k] for k in sorted(infos)]
+        self._index = index
+
+    def index(self) -> Dict[str, int]:
+        """node name -> position in list() (shared between snapshots of one node set)."""
+        if self._index is None:
+            self._index = {ni.name: i for i, ni in enumerate(self._list)}
+        return self._index
 
     def get(self, node_name: str) -> Optional[NodeInfo]:
         return self._infos.get(node_name)
@@ -101,16 +110,36 @@ class SchedulerCache:
         self._snap_gen: Dict[str, int] = {}
         self._snap: Dict[str, NodeInfo] = {}
         self.assume_ttl_s = assume_ttl_s
+        # incremental snapshots: nodes touched since the last one, and whether the set of
+        # nodes changed (then the name-ordered list is rebuilt)
+        self._dirty: set = set()
+        self._members_changed = True
+        self._last: Optional[Snapshot] = None
+        self._index: Dict[str, int] = {}
+        self.changes = ChangeFanout()       # framework.changes logs of the scheduling cycle
+
+    def _touch(self, name: str) -> None:
+        self._dirty.add(name)
+        self.changes.touch(name)
+
+    def _membership(self) -> None:
+        self._members_changed = True
+        self.changes.touch_all()
 
     # ---------------------------------------------------------------- nodes
     def add_node(self, node: Obj) -> None:
         with self._lock:
-            ni = self._nodes.get(O.name(node))
+            name = O.name(node)
+            ni = self._nodes.get(name)
             if ni is None:
                 ni = NodeInfo(node)
-                self._nodes[O.name(node)] = ni
+                self._nodes[name] = ni
+                self._membership()
             else:
+                if ni.node is None:
+                    self._membership()
                 ni.set_node(node)
+            self._touch(name)
 
     update_node = add_node
 
@@ -119,6 +148,8 @@ class SchedulerCache:
             self._nodes.pop(O.name(node), None)
             self._snap.pop(O.name(node), None)
             self._snap_gen.pop(O.name(node), None)
+            self._membership()
+            self._touch(O.name(node))
 
     # ---------------------------------------------------------------- pods
     def _place(self, pod: Obj, node_name: str) -> None:
@@ -129,12 +160,14 @@ class SchedulerCache:
             self._nodes[node_name] = ni
         ni.add_pod(pod)
         self._pod_node[O.key(pod)] = node_name
+        self._touch(node_name)
 
     def _unplace(self, pod: Obj) -> None:
         k = O.key(pod)
         nn = self._pod_node.pop(k, None)
         if nn and nn in self._nodes:
             self._nodes[nn].remove_pod(pod)
+            self._touch(nn)
 
     def assume_pod(self, pod: Obj, node_name: str) -> None:
         with self._lock:
@@ -200,18 +233,48 @@ class SchedulerCache:
 
     # ---------------------------------------------------------------- snapshot
     def snapshot(self) -> Snapshot:
-        """Incremental: only NodeInfos whose generation moved are re-cloned."""
+        """Incremental: only NodeInfos touched since the last snapshot are re-cloned (and only
+        if their generation moved); an unchanged cluster returns the previous snapshot."""
         with self._lock:
-            for name, ni in self._nodes.items():
-                if ni.node is None:
-                    continue
-                if self._snap_gen.get(name) != ni.generation:
-                    self._snap[name] = ni.clone()
-                    self._snap_gen[name] = ni.generation
-            for name in list(self._snap):
-                if name not in self._nodes or self._nodes[name].node is None:
-                    self._snap.pop(name, None)
-            return Snapshot(dict(self._snap))
+            if self._last is not None and not self._dirty and not self._members_changed:
+                return self._last
+            infos = dict(self._snap)          # snapshots are immutable: copy on write
+            if self._members_changed or self._last is None:
+                for name, ni in self._nodes.items():
+                    if ni.node is None:
+                        continue
+                    if self._snap_gen.get(name) != ni.generation or name not in infos:
+                        infos[name] = ni.clone()
+                        self._snap_gen[name] = ni.generation
+                for name in list(infos):
+                    if name not in self._nodes or self._nodes[name].node is None:
+                        infos.pop(name, None)
+                        self._snap_gen.pop(name, None)
+                names = sorted(infos)
+                self._index = {n: i for i, n in enumerate(names)}
+                ordered = [infos[n] for n in names]
+            else:
+                ordered = list(self._last.list())
+                for name in self._dirty:
+                    ni = self._nodes.get(name)
+                    i = self._index.get(name)
+                    if ni is None or ni.node is None or i is None:
+                        continue
+                    if self._snap_gen.get(name) != ni.generation:
+                        c = ni.clone()
+                        infos[name] = c
+                        ordered[i] = c
+                        self._snap_gen[name] = ni.generation
+            self._snap = infos
+            self._dirty.clear()
+            self._members_changed = False
+            self._last = Snapshot(infos, ordered, self._index)
+            return self._last
+
+    def node_index(self) -> Dict[str, int]:
+        """Position of every node in the last snapshot's name-ordered list."""
+        with self._lock:
+            return self._index
 
     def node_names(self) -> List[str]:
         with self._lock:

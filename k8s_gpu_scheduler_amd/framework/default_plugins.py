@@ -6,6 +6,7 @@ resource fit, default binder) stay on.  These are the subset that matters for GP
 """
 from __future__ import annotations
 
+import json
 from typing import Any, Dict
 
 from ..api import constants as C
@@ -14,6 +15,15 @@ from .interface import BindPlugin, FilterPlugin, PreFilterPlugin, QueueSortPlugi
 from .runtime import Registry
 
 Obj = Dict[str, Any]
+
+
+def _canon(x: Any) -> str:
+    """Hashable canonical form of a pod-spec fragment (cycle-cache signatures)."""
+    return json.dumps(x, sort_keys=True, separators=(",", ":")) if x else ""
+
+
+# Every filter/score plugin below implements cache_signature(state, pod, phase): what its
+# per-node verdict depends on besides the node's own NodeInfo (framework.fastpath).
 
 
 class PrioritySort(QueueSortPlugin):
@@ -46,6 +56,9 @@ class NodeUnschedulable(FilterPlugin):
         if not O.node_ready(node):
             return Status.unschedulable("node(s) were not ready", self.NAME, True)
         return None
+
+    def cache_signature(self, state, pod, phase):
+        return O.tolerates(pod, {"key": "node.kubernetes.io/unschedulable", "effect": "NoSchedule"})
 
     def filter_nodes(self, state, pod, node_infos):
         tol = None
@@ -84,6 +97,9 @@ class NodeName(FilterPlugin):
             return Status.unschedulable("node(s) didn't match the requested node name", self.NAME, True)
         return None
 
+    def cache_signature(self, state, pod, phase):
+        return pod.get("spec", {}).get("nodeName") or ""
+
     def filter_nodes(self, state, pod, node_infos):
         want = pod.get("spec", {}).get("nodeName")
         if not want:
@@ -105,6 +121,9 @@ class TaintToleration(FilterPlugin):
                 return Status.unschedulable(f"node(s) had untolerated taint {{{t.get('key')}: {t.get('value', '')}}}",
                                             self.NAME, True)
         return None
+
+    def cache_signature(self, state, pod, phase):
+        return _canon(pod.get("spec", {}).get("tolerations"))
 
     def filter_nodes(self, state, pod, node_infos):
         # untainted nodes (the common case) need no per-node work
@@ -133,6 +152,10 @@ class NodeAffinity(FilterPlugin):
             if not ok:
                 return Status.unschedulable("node(s) didn't match Pod's node affinity/selector", self.NAME, True)
         return None
+
+    def cache_signature(self, state, pod, phase):
+        spec = pod.get("spec", {})
+        return (_canon(spec.get("nodeSelector")), _canon((spec.get("affinity") or {}).get("nodeAffinity")))
 
     def filter_nodes(self, state, pod, node_infos):
         spec = pod.get("spec", {})
@@ -169,6 +192,12 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
             if r in node_info.allocatable and node_info.free(r) < v - 1e-9:
                 return Status.unschedulable(f"Insufficient {r}", self.NAME)
         return None
+
+    def cache_signature(self, state, pod, phase):
+        req = state.read(_FIT_KEY)
+        if req is None:
+            req = O.pod_requests(pod)
+        return tuple(sorted((r, v) for r, v in req.items() if v > 0 and r not in self.ignored))
 
     def filter_nodes(self, state, pod, node_infos):
         req = state.read(_FIT_KEY)
@@ -228,6 +257,10 @@ class _ResourceScore(ScorePlugin):
             self._memo.clear()
         self._memo[node_name] = (key, v)
         return v, None
+
+    def cache_signature(self, state, pod, phase):
+        req = O.pod_requests(pod)
+        return tuple(req.get(r, 0.0) for r in self.RES)
 
     def score_nodes(self, state, pod, names):
         snap = self.handle.snapshot()

@@ -45,6 +45,10 @@ class NodePorts(PreFilterPlugin, FilterPlugin):
         state.write(self._KEY, ports)
         return None
 
+    def cache_signature(self, state, pod, phase):
+        # the verdict depends on the node's own pods only (framework.fastpath)
+        return tuple(sorted(state.read(self._KEY) or _host_ports(pod)))
+
     def filter(self, state, pod, node_info):
         wanted = state.read(self._KEY) or _host_ports(pod)
         if not wanted:

@@ -26,6 +26,8 @@ from ..api import objects as O
 from ..kube.client import KubeClient
 from ..kube.informer import SharedInformerFactory
 from .cache import SchedulerCache, Snapshot
+from .changes import ChangeLog
+from .fastpath import NodeResultCache
 from .config import SchedulerConfig
 from .interface import Code, CycleState, Status
 from .queue import QueuedPodInfo, SchedulingQueue
@@ -147,6 +149,21 @@ class Scheduler:
         self._started = False
         self._waiting: Dict[str, WaitingPod] = {}
         self._waiting_lock = threading.RLock()
+        # cross-cycle node-result cache (framework.fastpath): every source of node-local
+        # scheduling state reports changed nodes to one change log
+        self.changes = ChangeLog()
+        self.cache.changes.attach(self.changes)
+        self.fast_path = True
+        self._fast: Dict[str, NodeResultCache] = {}
+        for name, fw in self.frameworks.items():
+            for inst in fw._instances.values():
+                for attr in ("ledger", "telemetry"):
+                    fan = getattr(getattr(inst, attr, None), "changes", None)
+                    if fan is not None and hasattr(fan, "attach"):
+                        fan.attach(self.changes)
+            nc = NodeResultCache(fw, self.changes)
+            nc.fw_rng = self._rng
+            self._fast[name] = nc
 
     @staticmethod
     def _queue_less(fw: Framework):
@@ -224,15 +241,13 @@ class Scheduler:
         return max(self.MIN_FEASIBLE_NODES, n * pct // 100)
 
     def _select_host(self, scores: List[Any]) -> str:
-        best, cnt, sel = None, 0, ""
-        for ns in scores:
-            if best is None or ns.score > best:
-                best, cnt, sel = ns.score, 1, ns.name
-            elif ns.score == best:
-                cnt += 1
-                if self._rng.randrange(cnt) == 0:
-                    sel = ns.name
-        return sel
+        """Uniformly random among the nodes tied at the maximum (upstream selectHost's
+        reservoir sample has the same distribution); one draw, as the cycle cache's."""
+        if not scores:
+            return ""
+        best = max(ns.score for ns in scores)
+        ties = [ns.name for ns in scores if ns.score == best]
+        return ties[0] if len(ties) == 1 else ties[self._rng.randrange(len(ties))]
 
     def schedule_one(self, pi: QueuedPodInfo) -> ScheduleResult:
         t0 = time.perf_counter()
@@ -242,6 +257,8 @@ class Scheduler:
         if fw is None:
             res.status = Status.error("no profile for scheduler " + O.scheduler_name(pod))
             return res
+        fast = self._fast.get(O.scheduler_name(pod)) if self.fast_path else None
+        cursor = fast.cursor() if fast is not None else None     # before the snapshot
         self._snapshot = self.cache.snapshot()
         state = CycleState()
         nodes = self._snapshot.list()
@@ -249,6 +266,14 @@ class Scheduler:
         if not st.ok:
             return self._fail(pi, fw, state, res, st, t0)
         limit = self.num_feasible_nodes_to_find(len(nodes))
+        sampled = limit < len(nodes)
+        got = fast.schedule(state, pod, self._snapshot, self._next_start % len(nodes) if sampled else 0,
+                            limit if sampled else 0, cursor) if fast is not None and nodes else None
+        if got is not None:
+            host, processed, n_feasible, scores = got
+            self._next_start = (self._next_start + processed) % len(nodes)
+            res.evaluated, res.feasible, res.scores = processed, n_feasible, scores
+            return self._assume_and_bind(fw, state, pi, pod, host, res, t0)
         if limit < len(nodes):
             start = self._next_start % len(nodes)
             nodes = nodes[start:] + nodes[:start]
@@ -277,6 +302,10 @@ class Scheduler:
                 return self._fail(pi, fw, state, res, st, t0)
             res.scores = {s.name: s.score for s in scores}
             host = self._select_host(scores)
+        return self._assume_and_bind(fw, state, pi, pod, host, res, t0)
+
+    def _assume_and_bind(self, fw: Framework, state: CycleState, pi: QueuedPodInfo, pod: Obj, host: str,
+                         res: ScheduleResult, t0: float) -> ScheduleResult:
         # assume + reserve
         self.cache.assume_pod(pod, host)
         st = fw.run_reserve(state, pod, host)

@@ -225,6 +225,8 @@ class DeviceLedger:
         self.pod_index: Dict[str, Tuple[str, List[str]]] = {}     # pod key -> (node, uuids)
         self.generation = 0
         self.node_gen: Dict[str, int] = {}      # per-node change counter (Score memo key)
+        from ...framework.changes import ChangeFanout
+        self.changes = ChangeFanout()           # scheduling-cycle node-result caches
 
     def set_devices(self, node: str, devices: Iterable[Device]) -> None:
         with self._lock:
@@ -240,6 +242,7 @@ class DeviceLedger:
             self.nodes[node] = new
             self.generation += 1
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
+            self.changes.touch(node)
 
     def devices(self, node: str) -> List[DeviceState]:
         with self._lock:
@@ -276,6 +279,7 @@ class DeviceLedger:
             self.pod_index[pod_key] = (node, [a[0] for a in allocs])
             self.generation += 1
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
+            self.changes.touch(node)
             return True
 
     def release(self, pod_key: str) -> bool:
@@ -300,6 +304,7 @@ class DeviceLedger:
                 st.invalidate()
             self.generation += 1
             self.node_gen[node] = self.node_gen.get(node, 0) + 1
+            self.changes.touch(node)
             return True
 
     def invalidate_summaries(self) -> None:
@@ -308,6 +313,7 @@ class DeviceLedger:
             for states in self.nodes.values():
                 for st in states.values():
                     st.__dict__.pop("_slo", None)
+            self.changes.touch_all()
 
     def gpu_work(self, node: str) -> Dict[int, float]:
         """Predicted GPU time of the pods resident on each physical GPU of a node (its

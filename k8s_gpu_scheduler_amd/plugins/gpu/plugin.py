@@ -431,6 +431,28 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             out.append(max(lo, min(hi, int(choice.score))))
         return out, None
 
+    def cache_signature(self, state: CycleState, pod: Obj, phase: str) -> Any:
+        """Cycle-cache signature (framework.fastpath): everything a node's Filter verdict or
+        raw Score depends on besides that node's ledger entry, telemetry samples and
+        NodeInfo, which report their changes to the change log.  None = not cacheable:
+        parity mode (I/O in Score), the burst planner (couples nodes), random packing."""
+        if self.parity is not None or self.planner is not None:
+            return None
+        req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
+        rsig = (req.whole, req.units, req.cu, req.hbm_gib, req.isolated, req.part_cus, req.implicit, req.gpu_pod)
+        if phase != "score":
+            return rsig
+        if self.args.pack == "random":
+            return None
+        tele = self.telemetry
+        # samples age out after stale_s: a per-second token bounds how long a cached score
+        # can outlive its telemetry (the per-node memo uses the same granularity)
+        tok = int(time.monotonic()) if (self.args.w_telemetry and tele.stale_s and tele.updates) else 0
+        if req.whole:
+            return rsig, tok
+        sig = self._pod_ctx(state, pod, req)[4]
+        return None if sig is None else (rsig, sig, tok, self._pred_version)
+
     def _planned_choice(self, state: CycleState, req: GpuRequest, node: str, plan: Any) -> Optional[Choice]:
         """The plan's device on its node as a top-scored Choice, if it is still a candidate."""
         pnode, puuid = plan
@@ -455,6 +477,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if choice is not None and choice.score > C.MAX_NODE_SCORE - 1:
             choice = dataclasses.replace(choice, score=float(C.MAX_NODE_SCORE - 1))
         return choice
+
+    NORMALIZE = "minmax"        # what normalize_score does (the cycle cache re-does it natively)
 
     def score_extensions(self) -> ScoreExtensions:
         return self

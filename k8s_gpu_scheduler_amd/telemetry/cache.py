@@ -39,12 +39,15 @@ class TelemetryCache:
         self.stale_s = stale_s
         self.updates = 0
         self._node_ver: Dict[str, int] = {}
+        from ..framework.changes import ChangeFanout
+        self.changes = ChangeFanout()           # scheduling-cycle node-result caches
 
     def update(self, node: str, uuid: str, sample: DeviceSample) -> None:
         with self._lock:
             self._d.setdefault(node, {})[uuid] = sample
             self.updates += 1
             self._node_ver[node] = self._node_ver.get(node, 0) + 1
+        self.changes.touch(node)
 
     def node_version(self, node: str) -> int:
         """Bumped on every sample for the node (0 = never sampled): lets Score memoise

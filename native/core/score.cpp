@@ -268,6 +268,80 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
   return out;
 }
 
+// Host selection of one scheduling cycle over cached per-node results (framework.fastpath):
+// walk the nodes in rotated order from `start`, keep the first `limit` feasible ones (0 = all;
+// kube-scheduler's numFeasibleNodesToFind / nextStartNodeIndex), min-max normalise the
+// plugins that ask for it (Go integer arithmetic, reference gpu_plugins.go:816-841), sum
+// weight x score per node and return the positions (in feasible order) of every node tied
+// at the maximum -- the caller draws the winner among them with its own RNG.
+//   feasible[n]  1 = passes every filter, 0 = not
+//   raw[p, n]    plugin p's raw score of node n (only read for feasible nodes)
+//   norm[p]      1 = min-max normalise plugin p over the feasible set
+// Returns (processed, feasible node indices, totals, tie positions, bad plugin or -1): a
+// score outside [0, 100] after normalisation stops the cycle like the framework does.
+py::tuple select_nodes(py::array_t<int8_t, py::array::c_style | py::array::forcecast> feasible,
+                       py::array_t<int64_t, py::array::c_style | py::array::forcecast> raw,
+                       py::array_t<int8_t, py::array::c_style | py::array::forcecast> norm,
+                       py::array_t<int64_t, py::array::c_style | py::array::forcecast> weights, int64_t start,
+                       int64_t limit) {
+  const auto F = feasible.unchecked<1>();
+  const auto R = raw.unchecked<2>();
+  const auto Nm = norm.unchecked<1>();
+  const auto Wt = weights.unchecked<1>();
+  const py::ssize_t N = F.shape(0), P = R.shape(0);
+  if (R.shape(1) != N || Nm.shape(0) != P || Wt.shape(0) != P) throw std::runtime_error("select_nodes: shape mismatch");
+  std::vector<int32_t> feas;
+  std::vector<int64_t> tot;
+  std::vector<int32_t> ties;
+  int64_t processed = 0;
+  int bad = -1;
+  {
+    py::gil_scoped_release nogil;
+    const int64_t s0 = N ? ((start % N) + N) % N : 0;
+    feas.reserve(limit > 0 ? (size_t)limit : (size_t)N);
+    for (py::ssize_t i = 0; i < N; ++i) {
+      const int64_t n = (s0 + i) % N;
+      ++processed;
+      if (F(n)) {
+        feas.push_back((int32_t)n);
+        if (limit > 0 && (int64_t)feas.size() >= limit) break;
+      }
+    }
+    tot.assign(feas.size(), 0);
+    for (py::ssize_t p = 0; p < P && bad < 0; ++p) {
+      int64_t lo = 0, hi = 0;
+      if (Nm(p) && !feas.empty()) {
+        lo = hi = R(p, feas[0]);
+        for (int32_t n : feas) {
+          lo = std::min(lo, R(p, n));
+          hi = std::max(hi, R(p, n));
+        }
+      }
+      for (size_t k = 0; k < feas.size(); ++k) {
+        int64_t v = R(p, feas[k]);
+        if (Nm(p)) v = (hi == lo) ? 0 : ((v - lo) * 100) / (hi - lo);
+        if (v < 0 || v > 100) {
+          bad = (int)p;
+          break;
+        }
+        tot[k] += v * Wt(p);
+      }
+    }
+    if (bad < 0 && !feas.empty()) {
+      const int64_t best = *std::max_element(tot.begin(), tot.end());
+      for (size_t k = 0; k < tot.size(); ++k)
+        if (tot[k] == best) ties.push_back((int32_t)k);
+    }
+  }
+  py::array_t<int32_t> f_out(feas.size());
+  py::array_t<int64_t> t_out(tot.size());
+  py::array_t<int32_t> ties_out(ties.size());
+  std::copy(feas.begin(), feas.end(), f_out.mutable_data());
+  std::copy(tot.begin(), tot.end(), t_out.mutable_data());
+  std::copy(ties.begin(), ties.end(), ties_out.mutable_data());
+  return py::make_tuple(processed, f_out, t_out, ties_out, bad);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_core, m) {
@@ -279,4 +353,6 @@ PYBIND11_MODULE(_core, m) {
         py::arg("slo"), py::arg("pred"), py::arg("work"), py::arg("gpu"), py::arg("base_load"), py::arg("res_dev"),
         py::arg("res_row"), py::arg("res_col"), py::arg("res_slo"), py::arg("res_pred"), py::arg("M"),
         py::arg("max_load"), py::arg("sweeps") = 8, py::arg("tolerance") = -1.0, py::arg("load_first") = 0);
+  m.def("select_nodes", &select_nodes, py::arg("feasible"), py::arg("raw"), py::arg("norm"), py::arg("weights"),
+        py::arg("start"), py::arg("limit"));
 }

@@ -34,7 +34,11 @@ profiles:
 """
 
 
+FAST = True      # framework.fastpath cross-cycle node-result cache (--no-fast-path: off)
+
+
 def run(fc, sched, pods, batch=None):
+    sched.fast_path = FAST
     for p in pods:
         fc.create("pods", p)
     t = time.perf_counter()
@@ -110,10 +114,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pods", type=int, default=400)
     ap.add_argument("--out", default="")
+    ap.add_argument("--no-fast-path", action="store_true")
     a = ap.parse_args()
+    global FAST
+    FAST = not a.no_fast_path
     res = {"busybox_2nodes": busybox(a.pods), "fractional_4x8gpu": fractional(a.pods),
            "fractional_1000x8gpu_adaptive_sampling": fractional(a.pods, nodes=1000),
-           "reference_algorithm_parity_rpc": parity_rpc(min(a.pods, 40))}
+           "reference_algorithm_parity_rpc": parity_rpc(min(a.pods, 40)),
+           "fast_path": FAST}
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:
