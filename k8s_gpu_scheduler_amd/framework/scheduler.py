@@ -154,6 +154,7 @@ class Scheduler:
         self.changes = ChangeLog()
         self.cache.changes.attach(self.changes)
         self.fast_path = True
+        self.fast_min_nodes = 16      # below this the per-cycle signature work costs more than it saves
         self._fast: Dict[str, NodeResultCache] = {}
         for name, fw in self.frameworks.items():
             for inst in fw._instances.values():
@@ -257,7 +258,8 @@ class Scheduler:
         if fw is None:
             res.status = Status.error("no profile for scheduler " + O.scheduler_name(pod))
             return res
-        fast = self._fast.get(O.scheduler_name(pod)) if self.fast_path else None
+        fast = self._fast.get(O.scheduler_name(pod)) \
+            if self.fast_path and len(self.cache._nodes) >= self.fast_min_nodes else None
         cursor = fast.cursor() if fast is not None else None     # before the snapshot
         self._snapshot = self.cache.snapshot()
         state = CycleState()

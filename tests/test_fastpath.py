@@ -31,6 +31,7 @@ def _cluster(n_nodes, fast, seed=3, args=None, nodes_fn=None):
     s = Scheduler(fc, default_gpu_config(dict({"weightBalance": 1.0}, **(args or {}))), full_registry(),
                   bind_async=False, record_events=False, seed=seed, extras=extras)
     s.fast_path = fast
+    s.fast_min_nodes = 0
     s.start_informers()
     return fc, s, tele
 
