@@ -21,7 +21,7 @@ its SLO a minimum iterations/s -- the same semantics as the reference's SLO env
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 
 @dataclass(frozen=True)
@@ -105,6 +105,19 @@ def workload_for_pod(pod_name: str) -> Workload:
         if n in nm:
             return CATALOG[n]
     raise KeyError(pod_name)
+
+
+def roofline_split(pod_name: str, tflops: float = 1.0e3, tbps: float = 6.0) -> Optional[Tuple[float, float]]:
+    """(MFMA-bound s, HBM-bound s) of one iteration of the pod's workload alone on a whole
+    GPU (GEMMs at `tflops`, stream passes at `tbps`); None for a pod outside the catalog.
+    The GPU plugin's complementarity term reads this (extras "roofline")."""
+    try:
+        w = workload_for_pod(pod_name)
+    except KeyError:
+        return None
+    m = sum(o.flops for o in w.ops if o.kind == "gemm") / (tflops * 1e12)
+    h = sum(o.bytes for o in w.ops if o.kind != "gemm") / (tbps * 1e12)
+    return m, h
 
 
 # ---------------------------------------------------------------- analytic predictions

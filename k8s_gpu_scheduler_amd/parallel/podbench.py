@@ -100,7 +100,7 @@ class ControlPlane:
     def __init__(self, n_gpus: int, pods_per_gpu: int, iters: int, seed: int, policy: str = "gpu",
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
-                 plan_tolerance: float = 0.05, plan_objective: str = "slo"):
+                 plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -114,7 +114,7 @@ class ControlPlane:
         self.predictions = predictions or measured_predictions() or analytic_predictions()
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
-                "plan_tolerance": plan_tolerance, "plan_objective": plan_objective}
+                "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
         # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
@@ -125,7 +125,8 @@ class ControlPlane:
         self.sched = Scheduler(self.fc, cfg, full_registry(),
                                bind_async=False, record_events=False, seed=seed,
                                extras={"telemetry": self.telemetry, "ledger": self.ledger,
-                                       "predictions": self.predictions, "workcost": self.workcost})
+                                       "predictions": self.predictions, "workcost": self.workcost,
+                                       "roofline": W.roofline_split})
         self.sched.keep_results = False
         self.sched.start_informers()
         self.plugin = self.sched.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)

@@ -102,6 +102,10 @@ class GPUArgs:
     # least-predicted-load across a node's GPUs: each resident pod's predicted GPU time
     # (ITERATIONS / predicted whole-GPU throughput, or SLO / throughput for services)
     w_balance: float = 0.0
+    # roofline complementarity: prefer the GPU whose residents plus this pod split their
+    # predicted time most evenly between MFMA-bound and HBM-bound work (needs a roofline
+    # provider in the handle extras: name -> (mfma s, hbm s) per iteration)
+    w_complement: float = 0.0
     # queueSort (when GPU is the profile's queueSort plugin): pods arriving in the same
     # window are popped longest-predicted-work first (LPT), older windows first
     lpt_window_s: float = 1.0
@@ -135,7 +139,8 @@ class GPUArgs:
     def from_dict(cls, d: Dict[str, Any]) -> "GPUArgs":
         a = cls()
         alias = {"weightSLO": "w_slo", "weightPack": "w_pack", "weightTelemetry": "w_telemetry",
-                 "weightBalance": "w_balance", "lptWindowSeconds": "lpt_window_s",
+                 "weightBalance": "w_balance", "weightComplement": "w_complement",
+                 "lptWindowSeconds": "lpt_window_s",
                  "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
                  "planObjective": "plan_objective",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
@@ -164,6 +169,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self.redis = redis if redis is not None else extras.get("redis")
         self.predictions = predictions or extras.get("predictions")
         self.workcost = extras.get("workcost")      # telemetry.workcost.WorkCostModel (optional)
+        self.roofline = extras.get("roofline")      # name -> (mfma s, hbm s) per iteration, or None
+        self._mfma_frac: Dict[str, Optional[float]] = {}
         self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
         self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
         self._col_memo: Dict[str, Optional[str]] = {}
@@ -771,16 +778,40 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         a = self.args
         name = O.name(pod)
         conf, intf = state.read(_PRED) or self._pod_predictions(name)
-        work = self.pod_work(pod, conf) if a.w_balance else 0.0
+        work = self.pod_work(pod, conf) if (a.w_balance or a.w_complement) else 0.0
         sig = None
         if a.pack != "random":
             x_col = self._workload_col(name, intf) if intf else None
-            sig = (req.units, req.hbm_gib, req.slo, work, x_col,
+            sig = (req.units, req.hbm_gib, req.slo, work, x_col, self.mfma_fraction(name) if a.w_complement else None,
                    tuple(sorted(conf.items())) if conf else (),
                    () if x_col is not None or not intf else tuple(sorted(intf.items())))
         ctx = (name, conf, intf, work, sig)
         state.write(_SIG, ctx)
         return ctx
+
+    def mfma_fraction(self, name: str) -> Optional[float]:
+        """Share of a workload's alone time that is MFMA-bound (roofline provider), memoised."""
+        hit = self._mfma_frac.get(name, False)
+        if hit is False:
+            rf = self.roofline(name) if self.roofline is not None else None
+            hit = None if not rf or sum(rf) <= 0 else rf[0] / (rf[0] + rf[1])
+            if len(self._mfma_frac) > 65536:
+                self._mfma_frac.clear()
+            self._mfma_frac[name] = hit
+        return hit
+
+    def _gpu_roofline(self, node: str) -> Dict[int, Tuple[float, float]]:
+        """Per physical GPU: predicted MFMA-bound and HBM-bound seconds of its residents."""
+        out: Dict[int, Tuple[float, float]] = {}
+        for st in self.ledger.devices(node):
+            m, h = out.get(st.device.gpu, (0.0, 0.0))
+            for use in st.pods.values():
+                f = self.mfma_fraction(use.name)
+                if f is not None:
+                    m += use.work * f
+                    h += use.work * (1.0 - f)
+            out[st.device.gpu] = (m, h)
+        return out
 
     def _score_cands(self, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest, name: str,
                      conf: Dict[str, float], intf: Dict[str, float], work: float = 0.0) -> Optional[Choice]:
@@ -814,6 +845,10 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if a.w_balance:
             loads = self.ledger.gpu_work(node)
             top = max(loads.values(), default=0.0) + work
+        roof: Optional[Dict[int, Tuple[float, float]]] = None
+        xf = self.mfma_fraction(name) if a.w_complement else None
+        if xf is not None and work > 0:
+            roof = self._gpu_roofline(node)
         samples = self.telemetry.node(node) if a.w_telemetry else {}
         binpack = a.pack == "binpack"
         hbm_mb = req.hbm_gib * 1024
@@ -834,6 +869,13 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                 # busiest; equal loads (or no prediction) tie
                 num += a.w_balance * (100.0 * (1.0 - (loads.get(g, 0.0) + work) / top) if top > 0 else 100.0)
                 den += a.w_balance
+            if roof is not None:
+                # 100 when the GPU's MFMA-bound and HBM-bound predicted time are equal after
+                # placement (the most room for the two phases to overlap), 0 when one-sided
+                m, h = roof.get(g, (0.0, 0.0))
+                m, h = m + work * xf, h + work * (1.0 - xf)
+                num += a.w_complement * 100.0 * (min(m, h) / max(m, h) if max(m, h) > 0 else 1.0)
+                den += a.w_complement
             if samples:
                 smp = samples.get(st.device.uuid)
                 if smp is not None:

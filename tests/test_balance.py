@@ -240,3 +240,28 @@ def test_lpt_sort_key_follows_requeue_timestamp():
     assert p.less(a, b)
     a.timestamp = 30.0                       # a was requeued after b arrived
     assert p.less(b, a)
+
+
+def test_complement_term_prefers_the_gpu_with_the_other_roofline_class():
+    """weightComplement: a stream-bound pod joins the GPU running an MFMA-bound pod rather
+    than an idle GPU (balanced MFMA/HBM time after placement scores 100, one-sided 0), and
+    without the term the balance-free plugin packs by unit fill alone."""
+    def place(w_complement):
+        fc = FakeCluster()
+        fc.create("nodes", O.make_node("n0", gpus=2))
+        ledger = DeviceLedger()
+        split = {"gemmy": (1.0, 0.0), "streamy": (0.0, 1.0)}
+        extras = {"ledger": ledger, "telemetry": TelemetryCache(stale_s=0), "predictions": _Pred(),
+                  "roofline": lambda n: next((v for k, v in split.items() if k in n), None)}
+        s = Scheduler(fc, default_gpu_config({"w_complement": w_complement, "w_pack": 0.0, "w_slo": 0.0,
+                                              "w_balance": 1.0}, disable_defaults=True),
+                      full_registry(), bind_async=False, seed=0, extras=extras)
+        s.start_informers()
+        for name in ("big-gemmy-0", "big-streamy-0"):
+            fc.create("pods", _pod(name))
+            s.schedule_pending()
+        return {use.name: st.device.gpu for st in ledger.devices("n0") for use in st.pods.values()}
+    g = place(3.0)
+    assert g["big-gemmy-0"] == g["big-streamy-0"]
+    g = place(0.0)                      # balance alone spreads the two pods
+    assert g["big-gemmy-0"] != g["big-streamy-0"]

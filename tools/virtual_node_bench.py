@@ -43,6 +43,9 @@ POLICIES = {
     "planned_t0": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.0),
     "planned_load": dict(balance=1.0, plan_bursts=True, plan_objective="load"),
     "random": dict(policy="random", balance=0.0, plan_bursts=False),
+    # roofline complementarity term (GPU plugin weightComplement) on top of greedy
+    "greedy_comp": dict(balance=1.0, plan_bursts=False, complement=1.0),
+    "greedy_comp3": dict(balance=1.0, plan_bursts=False, complement=3.0),
 }
 
 
