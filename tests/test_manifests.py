@@ -3,6 +3,9 @@
 changes (ROCm device access, no NVIDIA runtime) and a loadable scheduler profile."""
 import glob
 import os
+import subprocess
+
+import pytest
 
 import yaml
 
@@ -105,3 +108,44 @@ def test_agent_daemonset_serves_the_device_plugin():
              for r in d["rules"]]
     pod_verbs = {v for r in rules if "pods" in r["resources"] for v in r["verbs"]}
     assert {"patch", "delete", "list"} <= pod_verbs
+
+
+def _replication_script():
+    import yaml
+    docs = list(yaml.safe_load_all(open(os.path.join(ROOT, "deploy/redis/redis-statefulset.yaml"))))
+    sts = next(d for d in docs if d and d.get("kind") == "StatefulSet")
+    init = sts["spec"]["template"]["spec"]["initContainers"][0]
+    return init["args"][0], {e["name"]: e["value"] for e in init["env"]}
+
+
+@pytest.mark.parametrize("host,sentinel,expect", [
+    ("redis-0", "", None),                                   # no sentinel: redis-0 is the master
+    ("redis-2", "", "redis-0.redis.redis.svc.cluster.local"),  # no sentinel: replicas follow redis-0
+    ("redis-0", "10.0.0.7", "10.0.0.7"),                     # sentinel failed over to another pod
+    ("redis-1", "10.0.0.9", None),                           # this pod IS the sentinel's master
+])
+def test_redis_replication_bootstrap(tmp_path, host, sentinel, expect):
+    """The init container's replicaof decision (reference deploy/redis/redis-statefulset.yaml:37-56),
+    run under sh with stub redis-cli / hostname."""
+    script, env = _replication_script()
+    conf, etc, bin_ = tmp_path / "conf", tmp_path / "etc", tmp_path / "bin"
+    for d in (conf, etc, bin_):
+        d.mkdir()
+    (conf / "redis.conf").write_text("appendonly yes\n")
+    ip = {"redis-0": "10.0.0.5", "redis-1": "10.0.0.9", "redis-2": "10.0.0.11"}[host]
+    (bin_ / "redis-cli").write_text(
+        "#!/bin/sh\ncase \"$*\" in *ping*) [ -n \"$SENT\" ] && echo PONG || exit 1;; "
+        "*get-master-addr-by-name*) echo \"$SENT\"; echo 6379;; esac\n")
+    (bin_ / "hostname").write_text(
+        f"#!/bin/sh\ncase \"$1\" in -f) echo {host}.redis.redis.svc.cluster.local;; -i) echo {ip};; *) echo {host};; esac\n")
+    for f in bin_.iterdir():
+        f.chmod(0o755)
+    script = script.replace("/conf/", f"{conf}/").replace("/etc/redis/", f"{etc}/")
+    e = dict(os.environ, PATH=f"{bin_}:{os.environ['PATH']}", HOSTNAME=host, SENT=sentinel, **env)
+    subprocess.run(["sh", "-ec", script], env=e, check=True, capture_output=True)
+    out = (etc / "redis.conf").read_text()
+    assert out.startswith("appendonly yes")
+    if expect is None:
+        assert "replicaof" not in out
+    else:
+        assert f"replicaof {expect} 6379" in out
