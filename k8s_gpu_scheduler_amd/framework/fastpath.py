@@ -53,17 +53,22 @@ def _plugin_sigs(plugins, skip, state, pod, phase) -> Optional[tuple]:
 
 
 def select_nodes_py(feasible: np.ndarray, raw: np.ndarray, norm: np.ndarray, weights: np.ndarray,
-                    start: int, limit: int) -> Tuple[int, np.ndarray, np.ndarray, np.ndarray, int]:
+                    start: int, limit: int) -> tuple:
     """Pure-Python twin of `_core.select_nodes` (no native build)."""
     n = len(feasible)
     order = [(start + i) % n for i in range(n)] if n else []
-    feas, processed = [], 0
+    feas, unknown, processed = [], [], 0
     for i in order:
         processed += 1
-        if feasible[i]:
+        if feasible[i] < 0:
+            unknown.append(i)
+        elif feasible[i]:
             feas.append(i)
-            if limit and len(feas) >= limit:
-                break
+        if limit and len(feas) + len(unknown) >= limit:
+            break
+    e = np.asarray([], np.int32)
+    if unknown:
+        return processed, e, np.asarray([], np.int64), e, -1, np.asarray(unknown, np.int32)
     tot = [0] * len(feas)
     for p in range(raw.shape[0]):
         vals = [int(raw[p, i]) for i in feas]
@@ -72,11 +77,11 @@ def select_nodes_py(feasible: np.ndarray, raw: np.ndarray, norm: np.ndarray, wei
             vals = [0 if hi == lo else ((v - lo) * 100) // (hi - lo) for v in vals]
         for k, v in enumerate(vals):
             if not (MIN_NODE_SCORE <= v <= MAX_NODE_SCORE):
-                return processed, np.asarray(feas), np.asarray(tot), np.asarray([], np.int32), p
+                return processed, np.asarray(feas), np.asarray(tot), e, p, e
             tot[k] += v * int(weights[p])
     best = max(tot) if tot else 0
     ties = [k for k, t in enumerate(tot) if t == best] if tot else []
-    return processed, np.asarray(feas, np.int32), np.asarray(tot, np.int64), np.asarray(ties, np.int32), -1
+    return processed, np.asarray(feas, np.int32), np.asarray(tot, np.int64), np.asarray(ties, np.int32), -1, e
 
 
 class _Entry:
@@ -84,7 +89,7 @@ class _Entry:
 
     def __init__(self, names: List[str], n_score: int, seq: int, epoch: int):
         self.names = names
-        self.feasible = np.zeros(len(names), np.int8)
+        self.feasible = np.full(len(names), -1, np.int8)       # -1 = not evaluated
         self.raw = np.zeros((n_score, len(names)), np.int64)
         self.seq = seq
         self.epoch = epoch
@@ -143,17 +148,14 @@ class NodeResultCache:
             self._entries[key] = ent
             while len(self._entries) > self.MAX_ENTRIES:
                 self._entries.popitem(last=False)
-            idx = list(range(len(nodes)))
-        else:
+        else:                                   # touched nodes: evaluate again when the scan needs them
             index = snapshot.index()
-            idx = sorted(index[n] for n in dirty if n in index)
+            for n in dirty:
+                i = index.get(n)
+                if i is not None:
+                    ent.feasible[i] = -1
         ent.seq, ent.epoch, ent.snap = seq, epoch, snapshot
-        self._score_ns = 0
-        if idx and not self._recompute(state, pod, ent, nodes, idx, score_plugins):
-            self._entries.pop(key, None)
-            return self._fallback()
-        self.stats["cycles"] += 1
-        self.stats["rescored"] += len(idx)
+        self._find_ns = 0
         norm = []
         for p in score_plugins:
             ext = p.score_extensions()
@@ -166,8 +168,19 @@ class NodeResultCache:
         norm = np.asarray(norm, np.int8)
         weights = np.asarray([fw.weights.get(p.name(), 1) for p in score_plugins], np.int64)
         t0 = time.perf_counter_ns()
-        processed, feas, tot, ties, bad = self._select(ent.feasible, ent.raw, norm, weights, start, limit)
-        fw.metrics.add("score", time.perf_counter_ns() - t0 + self._score_ns)
+        score_ns = 0
+        while True:
+            processed, feas, tot, ties, bad, unknown = self._select(ent.feasible, ent.raw, norm, weights, start, limit)
+            if len(unknown) == 0:
+                break
+            # evaluate exactly the nodes the sampled scan reached (in scan order), then rescan
+            if not self._recompute(state, pod, ent, nodes, unknown.tolist(), score_plugins):
+                self._entries.pop(key, None)
+                return self._fallback()
+            self.stats["rescored"] += len(unknown)
+            score_ns += self._score_ns
+        self.stats["cycles"] += 1
+        fw.metrics.add("score", time.perf_counter_ns() - t0 - self._find_ns + score_ns)
         if bad >= 0 or len(feas) == 0:
             self._entries.pop(key, None)
             return self._fallback()
@@ -179,6 +192,7 @@ class NodeResultCache:
 
     fw_rng: Any = None      # the scheduler's RNG (set by Scheduler): same draws as _select_host
     _score_ns = 0
+    _find_ns = 0
 
     def _fallback(self):
         self.stats["fallback"] += 1
@@ -190,7 +204,9 @@ class NodeResultCache:
         fw = self.fw
         self._score_ns = 0
         infos = [nodes[i] for i in idx]
+        t0 = time.perf_counter_ns()
         feasible, _ = fw.find_feasible(state, pod, infos, 0)
+        self._find_ns += time.perf_counter_ns() - t0
         ok = {ni.name for ni in feasible}
         fe = ent.feasible
         for i, ni in zip(idx, infos):

@@ -170,6 +170,15 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self.predictions = predictions or extras.get("predictions")
         self.workcost = extras.get("workcost")      # telemetry.workcost.WorkCostModel (optional)
         self.roofline = extras.get("roofline")      # name -> (mfma s, hbm s) per iteration, or None
+        # native node scoring: interned names / interference columns and per-node packs
+        self._name_ids: Dict[str, int] = {}
+        self._col_ids: Dict[str, int] = {}
+        self._packs: Dict[str, Tuple[Any, Dict[str, Any]]] = {}
+        self._xvec_memo: Any = None
+        self._core_mod: Any = False
+        self._weights_vec: Any = None
+        import numpy as _np
+        self._empty_vec = _np.zeros(0)
         self._mfma_frac: Dict[str, Optional[float]] = {}
         self.topologies: Dict[str, Topology] = dict(extras.get("topologies") or {})
         self._resident_memo: Dict[str, Tuple[Dict[str, float], Dict[str, float]]] = {}
@@ -789,6 +798,17 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         state.write(_SIG, ctx)
         return ctx
 
+    def _core(self) -> Any:
+        if self._core_mod is False:
+            try:
+                from ... import _native
+                self._core_mod = _native.core()
+            except Exception:
+                self._core_mod = None
+            if self._core_mod is not None and not hasattr(self._core_mod, "NodePack"):
+                self._core_mod = None           # an older build
+        return self._core_mod
+
     def mfma_fraction(self, name: str) -> Optional[float]:
         """Share of a workload's alone time that is MFMA-bound (roofline provider), memoised."""
         hit = self._mfma_frac.get(name, False)
@@ -813,22 +833,166 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             out[st.device.gpu] = (m, h)
         return out
 
+    # ------------------------------------------------------------------ native node scoring
+    native_score = True          # score a node's candidates in C++ (_core.score_node) when built
+    NATIVE_MIN_CANDS = 2
+
+    def _summary(self, st: DeviceState) -> DeviceSummary:
+        d = st.__dict__
+        ver = d.get("_ver", 0)
+        hit = d.get("_slo")
+        if hit is not None and hit[0] == ver:
+            return hit[1]
+        summ = self._device_summary(st)          # version-tagged like find_units' memo
+        d["_slo"] = (ver, summ)
+        return summ
+
+    def _intern(self, table: Dict[str, int], key: str) -> int:
+        i = table.get(key)
+        if i is None:
+            i = table[key] = len(table)
+        return i
+
+    def _node_pack(self, node: str, states: List[DeviceState]) -> Dict[str, Any]:
+        """Flat arrays of a node's device states for `_core.score_node`, rebuilt only when the
+        node's ledger entry (node_gen) or the prediction version changes."""
+        import numpy as np
+        key = (self.ledger.node_gen.get(node, 0), self._pred_version, self.args.w_complement)
+        hit = self._packs.get(node)
+        if hit is not None and hit[0] == key and len(hit[1]["uuid"]) == len(states):
+            return hit[1]
+        names, cols = self._name_ids, self._col_ids
+        t_off, t_name, t_slo, t_pred, t_base, rows = [0], [], [], [], [], []
+        k_off, k_name, k_col = [0], [], []
+        for st in states:
+            summ = self._summary(st)
+            for nm, slo, pred, base, row in summ.terms:
+                t_name.append(self._intern(names, nm))
+                t_slo.append(slo)
+                t_pred.append(pred)
+                t_base.append(base)
+                rows.append({self._intern(cols, c): v for c, v in row.items()})
+            t_off.append(len(t_name))
+            for nm, c in summ.cols:
+                k_name.append(self._intern(names, nm))
+                k_col.append(self._intern(cols, c))
+            k_off.append(len(k_name))
+        n_col = len(cols)
+        t_rows = np.zeros((len(rows), n_col), np.float64)
+        for t, r in enumerate(rows):
+            for c, v in r.items():
+                t_rows[t, c] = v
+        n_gpu = max((st.device.gpu for st in states), default=-1) + 1
+        tot, used = [0] * n_gpu, [0] * n_gpu
+        for st in states:
+            tot[st.device.gpu] += st.device.units
+            used[st.device.gpu] += st.device.units - st.free_units
+        loads = self.ledger.gpu_work(node)
+        roof = self._gpu_roofline(node) if self.args.w_complement else {}
+        pack = {"uuid": {st.device.uuid: i for i, st in enumerate(states)},
+                "t_off": np.asarray(t_off, np.int64), "t_name": np.asarray(t_name, np.int32),
+                "t_slo": np.asarray(t_slo, np.float64), "t_pred": np.asarray(t_pred, np.float64),
+                "t_base": np.asarray(t_base, np.float64), "t_rows": t_rows,
+                "k_off": np.asarray(k_off, np.int64), "k_name": np.asarray(k_name, np.int32),
+                "k_col": np.asarray(k_col, np.int32),
+                "dev_gpu": np.asarray([st.device.gpu for st in states], np.int32),
+                "gpu_tot": np.asarray(tot, np.int32), "gpu_used": np.asarray(used, np.int32),
+                "gpu_load": np.asarray([loads.get(g, 0.0) for g in range(n_gpu)], np.float64),
+                "roof_m": np.asarray([roof.get(g, (0.0, 0.0))[0] for g in range(n_gpu)], np.float64),
+                "roof_h": np.asarray([roof.get(g, (0.0, 0.0))[1] for g in range(n_gpu)], np.float64),
+                "max_load": max(loads.values(), default=0.0), "cands": {},
+                "no_tele": (np.zeros(len(states), np.int8), np.zeros(len(states)), np.zeros(len(states)))}
+        pack["native"] = self._core().NodePack(
+            pack["t_off"], pack["t_name"], pack["t_slo"], pack["t_pred"], pack["t_base"], pack["t_rows"],
+            pack["k_off"], pack["k_name"], pack["k_col"], pack["dev_gpu"], pack["gpu_tot"], pack["gpu_used"],
+            pack["gpu_load"], pack["roof_m"], pack["roof_h"])
+        if len(self._packs) > 65536:
+            self._packs.clear()
+        self._packs[node] = (key, pack)
+        return pack
+
+    def _x_vector(self, intf: Dict[str, float]):
+        """The incoming pod's interference row as a dense vector over interned column ids."""
+        import numpy as np
+        key = id(intf)
+        hit = self._xvec_memo
+        if hit is not None and hit[0] == key and hit[1] is intf and len(hit[2]) == len(self._col_ids):
+            return hit[2]
+        for c in intf:
+            self._intern(self._col_ids, c)
+        v = np.zeros(len(self._col_ids), np.float64)
+        for c, x in intf.items():
+            v[self._col_ids[c]] = x
+        self._xvec_memo = (key, intf, v)
+        return v
+
+    def _score_cands_native(self, core: Any, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest,
+                            name: str, conf: Dict[str, float], intf: Dict[str, float], work: float,
+                            states: List[DeviceState]) -> Optional[Choice]:
+        import numpy as np
+        a = self.args
+        pack = self._node_pack(node, states)
+        slo_on = bool(a.w_slo and req.slo > 0 and conf)
+        x_col_name = self._workload_col(name, intf) if slo_on else None
+        # candidate indices and the pod's prediction per candidate: memoised per candidate
+        # list object (itself memoised per node version x request) and prediction table
+        ck = (id(cands), id(conf) if slo_on else 0, req.units)
+        hit = pack["cands"].get(ck)
+        if hit is None or hit[0] is not cands:
+            uidx = pack["uuid"]
+            cand = np.asarray([uidx[st.device.uuid] for st, _ in cands], np.int32)
+            xp = np.asarray([conf.get(self._col(req.units, st.device.units), -1.0) for st, _ in cands]
+                            if slo_on else [-1.0] * len(cands), np.float64)
+            if len(pack["cands"]) > 64:
+                pack["cands"].clear()
+            hit = pack["cands"][ck] = (cands, cand, xp)
+        _, cand, xp = hit
+        x_vec = self._x_vector(intf) if slo_on else self._empty_vec
+        D = len(states)
+        samples = self.telemetry.node(node) if a.w_telemetry else {}
+        if not samples:
+            tele_ok, gfx, vfree = pack["no_tele"]
+        else:
+            tele_ok = np.zeros(D, np.int8)
+            gfx = np.zeros(D)
+            vfree = np.zeros(D)
+            for i, st in enumerate(states):
+                smp = samples.get(st.device.uuid)
+                if smp is not None:
+                    tele_ok[i] = 1
+                    gfx[i] = smp.gfx_activity
+                    vfree[i] = smp.vram_total_mb - smp.vram_used_mb
+        xf = self.mfma_fraction(name) if a.w_complement else None
+        flags = (1 if slo_on else 0) | (2 if a.pack == "binpack" else 0) | (4 if a.w_balance else 0) | \
+            (8 if xf is not None and work > 0 else 0)
+        top = pack["max_load"] + work if a.w_balance else 0.0
+        x_name = self._name_ids.get(name, -1)
+        x_col = self._intern(self._col_ids, x_col_name) if x_col_name is not None else -1
+        wt = self._weights_vec
+        if wt is None:
+            wt = self._weights_vec = np.asarray([a.w_slo, a.w_pack, a.w_balance, a.w_complement, a.w_telemetry],
+                                                np.float64)
+        best_i, best_sc = pack["native"].score(
+            cand, xp, tele_ok, gfx, vfree, x_vec, x_name, x_col, float(req.slo), int(req.units), float(work),
+            float(top), float(xf) if xf is not None else 0.0, float(req.hbm_gib * 1024), wt, flags)
+        if best_i < 0:
+            return None
+        st, u0 = cands[best_i]
+        return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], best_sc, [st.device])
+
     def _score_cands(self, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest, name: str,
                      conf: Dict[str, float], intf: Dict[str, float], work: float = 0.0) -> Optional[Choice]:
         a = self.args
         states = self.ledger.devices(node)
+        if self.native_score and a.pack != "random" and len(cands) >= self.NATIVE_MIN_CANDS:
+            core = self._core()
+            if core is not None:
+                return self._score_cands_native(core, node, cands, req, name, conf, intf, work, states)
         slo_scores: List[Optional[float]] = [None] * len(cands)
         if a.w_slo and req.slo > 0 and conf:
             x_col = self._workload_col(name, intf)
             for i, (st, _) in enumerate(cands):
-                d = st.__dict__
-                ver = d.get("_ver", 0)
-                hit = d.get("_slo")
-                if hit is not None and hit[0] == ver:
-                    summ = hit[1]
-                else:                           # version-tagged like find_units' memo
-                    summ = self._device_summary(st)
-                    d["_slo"] = (ver, summ)
+                summ = self._summary(st)
                 slo_scores[i] = fast_device_score(summ, name, x_col, req.slo,
                                                   conf.get(self._col(req.units, st.device.units), -1.0), intf)
         if a.pack == "random":

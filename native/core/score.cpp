@@ -268,17 +268,175 @@ py::array_t<int32_t> plan_assignment(py::array_t<int32_t, py::array::c_style | p
   return out;
 }
 
+// Fixed-mode GPU Score of one node (plugins/gpu/plugin.py GPUPlugin._score_cands): every
+// candidate device's blend of the SLO/interference objective (scoring.fast_device_score,
+// the reference's Logic terms, gpu_plugins.go:558-757, in float64), unit packing, the
+// least-predicted-load balance, roofline complementarity and live telemetry -- the same
+// terms in the same order of float operations, so the result is bit-identical to the
+// Python path.  The node's static part (its devices' resident terms, fill, loads) is a
+// NodePack built once per node version; names and interference columns are interned
+// integer ids, a resident's interference row a dense vector over column ids (missing = 0).
+//   t_off[d]..t_off[d+1]   SLO terms of device d: t_name, t_slo, t_pred, t_base, t_rows[t, :]
+//   k_off[d]..k_off[d+1]   (resident name id, column id) of the residents with a column
+//   dev_gpu[d]             physical GPU of device d
+//   gpu_tot/gpu_used[g]    unit fill per GPU; gpu_load[g] predicted resident work (balance);
+//   roof_m/roof_h[g]       residents' MFMA / HBM seconds (complementarity)
+struct NodePack {
+  // built once per node version (plugins/gpu/plugin.py _node_pack); see score() below
+  std::vector<int64_t> t_off, k_off;
+  std::vector<int32_t> t_name, k_name, k_col, dev_gpu, gpu_tot, gpu_used;
+  std::vector<double> t_slo, t_pred, t_base, t_rows, gpu_load, roof_m, roof_h;
+  int64_t n_col = 0;
+
+  template <typename T>
+  static std::vector<T> vec(const py::array_t<T, py::array::c_style | py::array::forcecast>& a) {
+    return std::vector<T>(a.data(), a.data() + a.size());
+  }
+
+  NodePack(py::array_t<int64_t, py::array::c_style | py::array::forcecast> t_off_,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> t_name_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> t_slo_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> t_pred_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> t_base_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> t_rows_,
+           py::array_t<int64_t, py::array::c_style | py::array::forcecast> k_off_,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> k_name_,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> k_col_,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> dev_gpu_,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> gpu_tot_,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> gpu_used_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> gpu_load_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> roof_m_,
+           py::array_t<double, py::array::c_style | py::array::forcecast> roof_h_)
+      : t_off(vec(t_off_)), k_off(vec(k_off_)), t_name(vec(t_name_)), k_name(vec(k_name_)), k_col(vec(k_col_)),
+        dev_gpu(vec(dev_gpu_)), gpu_tot(vec(gpu_tot_)), gpu_used(vec(gpu_used_)), t_slo(vec(t_slo_)),
+        t_pred(vec(t_pred_)), t_base(vec(t_base_)), t_rows(vec(t_rows_)), gpu_load(vec(gpu_load_)),
+        roof_m(vec(roof_m_)), roof_h(vec(roof_h_)) {
+    const size_t D = dev_gpu.size(), T = t_name.size(), K = k_name.size(), G = gpu_tot.size();
+    if (t_rows_.ndim() != 2 || (size_t)t_rows_.shape(0) != T) throw std::runtime_error("NodePack: t_rows shape");
+    n_col = t_rows_.shape(1);
+    if (t_off.size() != D + 1 || k_off.size() != D + 1 || (size_t)t_off[D] != T || (size_t)k_off[D] != K ||
+        t_slo.size() != T || t_pred.size() != T || t_base.size() != T || k_col.size() != K || gpu_used.size() != G ||
+        gpu_load.size() != G || roof_m.size() != G || roof_h.size() != G)
+      throw std::runtime_error("NodePack: array sizes mismatch");
+    for (int32_t g : dev_gpu)
+      if (g < 0 || (size_t)g >= G) throw std::runtime_error("NodePack: gpu id out of range");
+  }
+
+  // Returns (best candidate position or -1, its score); the first maximum wins.
+  //   cand[i], x_pred[i]   candidate device index and the incoming pod's prediction there
+  //   tele_ok/gfx/vram_free_mb[d]   fresh telemetry sample per device (tele_ok 0 = none)
+  //   wt = (w_slo, w_pack, w_balance, w_complement, w_telemetry)
+  //   flags: 1 slo term on, 2 binpack (else spread), 4 balance on, 8 complement on
+  py::tuple score(py::array_t<int32_t, py::array::c_style | py::array::forcecast> cand,
+                  py::array_t<double, py::array::c_style | py::array::forcecast> x_pred,
+                  py::array_t<int8_t, py::array::c_style | py::array::forcecast> tele_ok,
+                  py::array_t<double, py::array::c_style | py::array::forcecast> gfx,
+                  py::array_t<double, py::array::c_style | py::array::forcecast> vram_free_mb,
+                  py::array_t<double, py::array::c_style | py::array::forcecast> x_intf, int x_name, int x_col,
+                  double x_slo, int units, double work, double top, double xf, double hbm_mb,
+                  py::array_t<double, py::array::c_style | py::array::forcecast> wt, int flags) const {
+    const auto CA = cand.unchecked<1>();
+    const auto XP = x_pred.unchecked<1>();
+    const auto TK = tele_ok.unchecked<1>();
+    const auto GX = gfx.unchecked<1>();
+    const auto VF = vram_free_mb.unchecked<1>();
+    const auto XI = x_intf.unchecked<1>();
+    const auto W = wt.unchecked<1>();
+    const py::ssize_t D = (py::ssize_t)dev_gpu.size(), NC = CA.shape(0), XC = XI.shape(0);
+    if (XP.shape(0) != NC || W.shape(0) != 5 || TK.shape(0) != D || GX.shape(0) != D || VF.shape(0) != D)
+      throw std::runtime_error("NodePack.score: shape mismatch");
+    for (py::ssize_t i = 0; i < NC; ++i)
+      if (CA(i) < 0 || CA(i) >= D) throw std::runtime_error("NodePack.score: candidate out of range");
+    const double w_slo = W(0), w_pack = W(1), w_bal = W(2), w_comp = W(3), w_tel = W(4);
+    int best_i = -1;
+    double best_sc = 0.0;
+    for (py::ssize_t i = 0; i < NC; ++i) {
+      const int d = CA(i);
+      double num = 0.0, den = 0.0;
+      if (flags & 1) {
+        // scoring.fast_device_score, float64, same order of operations
+        double neg_sum = 0.0, pos_sum = 0.0;
+        int n_neg = 0, n_pos = 0;
+        auto add = [&](double slo, double pred, double it) {
+          const double dd = (slo - (pred - it)) / slo;
+          if (dd > 0) {
+            const double q = std::fabs(dd) + 1.0;
+            neg_sum += 1.0 / (1.0 + q * q);
+            ++n_neg;
+          } else {
+            pos_sum += 1.0 / (1.0 + std::fabs(dd));
+            ++n_pos;
+          }
+        };
+        for (int64_t t = t_off[d]; t < t_off[d + 1]; ++t) {
+          double it = t_base[t];
+          if (x_col >= 0 && t_name[t] != x_name) it += (x_col < n_col) ? t_rows[t * n_col + x_col] : 0.0;
+          add(t_slo[t], t_pred[t], it);
+        }
+        if (XP(i) != -1 && x_slo > 0) {
+          double it = 0.0;
+          for (int64_t k = k_off[d]; k < k_off[d + 1]; ++k)
+            if (k_name[k] != x_name) it += (k_col[k] >= 0 && k_col[k] < XC) ? XI(k_col[k]) : 0.0;
+          add(x_slo, XP(i), it);
+        }
+        double s = 0.0;
+        if (n_pos && n_neg) {
+          const double k = (double)n_neg / (double)(n_neg + n_pos);
+          s = 100.0 * ((1 - k) * pos_sum / n_pos) + 100.0 * (k * neg_sum / n_neg);
+        } else if (n_neg) {
+          s = 100.0 * neg_sum / n_neg;
+        } else if (n_pos) {
+          s = 100.0 * pos_sum / n_pos;
+        }
+        num += w_slo * s;
+        den += w_slo;
+      }
+      const int g = dev_gpu[d];
+      if (w_pack != 0.0) {
+        const double frac = (double)(gpu_used[g] + units) / (double)std::max(gpu_tot[g], 1);
+        num += w_pack * ((flags & 2) ? 100.0 * frac : 100.0 * (1.0 - frac));
+        den += w_pack;
+      }
+      if (flags & 4) {
+        num += w_bal * (top > 0 ? 100.0 * (1.0 - (gpu_load[g] + work) / top) : 100.0);
+        den += w_bal;
+      }
+      if (flags & 8) {
+        const double m = roof_m[g] + work * xf, h = roof_h[g] + work * (1.0 - xf);
+        const double mx = std::max(m, h);
+        num += w_comp * 100.0 * (mx > 0 ? std::min(m, h) / mx : 1.0);
+        den += w_comp;
+      }
+      if (TK(d)) {
+        const double hbm_ok = VF(d) >= hbm_mb ? 1.0 : 0.0;
+        num += w_tel * 100.0 * (1.0 - std::min(1.0, GX(d))) * hbm_ok;
+        den += w_tel;
+      }
+      const double sc = den > 0 ? num / den : 0.0;
+      if (best_i < 0 || sc > best_sc) {
+        best_i = (int)i;
+        best_sc = sc;
+      }
+    }
+    return py::make_tuple(best_i, best_sc);
+  }
+};
+
 // Host selection of one scheduling cycle over cached per-node results (framework.fastpath):
 // walk the nodes in rotated order from `start`, keep the first `limit` feasible ones (0 = all;
 // kube-scheduler's numFeasibleNodesToFind / nextStartNodeIndex), min-max normalise the
 // plugins that ask for it (Go integer arithmetic, reference gpu_plugins.go:816-841), sum
 // weight x score per node and return the positions (in feasible order) of every node tied
 // at the maximum -- the caller draws the winner among them with its own RNG.
-//   feasible[n]  1 = passes every filter, 0 = not
+//   feasible[n]  1 = passes every filter, 0 = not, -1 = not evaluated yet (lazy)
 //   raw[p, n]    plugin p's raw score of node n (only read for feasible nodes)
 //   norm[p]      1 = min-max normalise plugin p over the feasible set
-// Returns (processed, feasible node indices, totals, tie positions, bad plugin or -1): a
-// score outside [0, 100] after normalisation stops the cycle like the framework does.
+// Returns (processed, feasible node indices, totals, tie positions, bad plugin or -1,
+// unevaluated): a score outside [0, 100] after normalisation stops the cycle like the
+// framework does.  If the scan meets unevaluated nodes before it can close the sample, it
+// returns only them (every one the sample could still need: scanning on as if each were
+// feasible) -- the caller evaluates those and calls again.
 py::tuple select_nodes(py::array_t<int8_t, py::array::c_style | py::array::forcecast> feasible,
                        py::array_t<int64_t, py::array::c_style | py::array::forcecast> raw,
                        py::array_t<int8_t, py::array::c_style | py::array::forcecast> norm,
@@ -292,7 +450,7 @@ py::tuple select_nodes(py::array_t<int8_t, py::array::c_style | py::array::force
   if (R.shape(1) != N || Nm.shape(0) != P || Wt.shape(0) != P) throw std::runtime_error("select_nodes: shape mismatch");
   std::vector<int32_t> feas;
   std::vector<int64_t> tot;
-  std::vector<int32_t> ties;
+  std::vector<int32_t> ties, unknown;
   int64_t processed = 0;
   int bad = -1;
   {
@@ -302,11 +460,14 @@ py::tuple select_nodes(py::array_t<int8_t, py::array::c_style | py::array::force
     for (py::ssize_t i = 0; i < N; ++i) {
       const int64_t n = (s0 + i) % N;
       ++processed;
-      if (F(n)) {
+      if (F(n) < 0) {
+        unknown.push_back((int32_t)n);
+      } else if (F(n)) {
         feas.push_back((int32_t)n);
-        if (limit > 0 && (int64_t)feas.size() >= limit) break;
       }
+      if (limit > 0 && (int64_t)(feas.size() + unknown.size()) >= limit) break;
     }
+    if (!unknown.empty()) feas.clear();
     tot.assign(feas.size(), 0);
     for (py::ssize_t p = 0; p < P && bad < 0; ++p) {
       int64_t lo = 0, hi = 0;
@@ -336,10 +497,12 @@ py::tuple select_nodes(py::array_t<int8_t, py::array::c_style | py::array::force
   py::array_t<int32_t> f_out(feas.size());
   py::array_t<int64_t> t_out(tot.size());
   py::array_t<int32_t> ties_out(ties.size());
+  py::array_t<int32_t> u_out(unknown.size());
   std::copy(feas.begin(), feas.end(), f_out.mutable_data());
   std::copy(tot.begin(), tot.end(), t_out.mutable_data());
   std::copy(ties.begin(), ties.end(), ties_out.mutable_data());
-  return py::make_tuple(processed, f_out, t_out, ties_out, bad);
+  std::copy(unknown.begin(), unknown.end(), u_out.mutable_data());
+  return py::make_tuple(processed, f_out, t_out, ties_out, bad, u_out);
 }
 
 }  // namespace
@@ -353,6 +516,23 @@ PYBIND11_MODULE(_core, m) {
         py::arg("slo"), py::arg("pred"), py::arg("work"), py::arg("gpu"), py::arg("base_load"), py::arg("res_dev"),
         py::arg("res_row"), py::arg("res_col"), py::arg("res_slo"), py::arg("res_pred"), py::arg("M"),
         py::arg("max_load"), py::arg("sweeps") = 8, py::arg("tolerance") = -1.0, py::arg("load_first") = 0);
+  py::class_<NodePack>(m, "NodePack")
+      .def(py::init<py::array_t<int64_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int64_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>>())
+      .def("score", &NodePack::score);
   m.def("select_nodes", &select_nodes, py::arg("feasible"), py::arg("raw"), py::arg("norm"), py::arg("weights"),
         py::arg("start"), py::arg("limit"));
 }

@@ -79,6 +79,8 @@ def test_select_nodes_native_matches_python():
     for trial in range(200):
         n = int(rng.integers(1, 60))
         feas = (rng.random(n) < 0.6).astype(np.int8)
+        if trial % 3 == 0:
+            feas[rng.random(n) < 0.2] = -1      # not evaluated yet: returned for evaluation
         raw = rng.integers(0, 101, size=(3, n)).astype(np.int64)
         if trial % 5 == 0:
             raw[:, :] = 50                       # all tied
@@ -87,7 +89,10 @@ def test_select_nodes_native_matches_python():
         start, limit = int(rng.integers(0, n)), int(rng.integers(0, n + 1))
         a = core.select_nodes(feas, raw, norm, w, start, limit)
         b = select_nodes_py(feas, raw, norm, w, start, limit)
-        assert a[0] == b[0] and a[4] == b[4]
+        assert a[4] == b[4]
+        assert list(np.asarray(a[5])) == list(np.asarray(b[5]))
+        if len(a[5]) == 0:
+            assert a[0] == b[0]
         for x, y in zip(a[1:4], b[1:4]):
             assert list(np.asarray(x)) == list(np.asarray(y))
     # a score out of range is reported with the plugin index
