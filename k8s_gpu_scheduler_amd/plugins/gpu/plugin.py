@@ -174,6 +174,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self._name_ids: Dict[str, int] = {}
         self._col_ids: Dict[str, int] = {}
         self._packs: Dict[str, Tuple[Any, Dict[str, Any]]] = {}
+        self._pack_seen: Dict[str, Any] = {}
         self._xvec_memo: Any = None
         self._core_mod: Any = False
         self._weights_vec: Any = None
@@ -911,6 +912,18 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self._packs[node] = (key, pack)
         return pack
 
+    def _pack_ready(self, node: str) -> bool:
+        key = (self.ledger.node_gen.get(node, 0), self._pred_version, self.args.w_complement)
+        hit = self._packs.get(node)
+        if hit is not None and hit[0] == key:
+            return True
+        if self._pack_seen.get(node) == key:
+            return True
+        if len(self._pack_seen) > 65536:
+            self._pack_seen.clear()
+        self._pack_seen[node] = key
+        return False
+
     def _x_vector(self, intf: Dict[str, float]):
         """The incoming pod's interference row as a dense vector over interned column ids."""
         import numpy as np
@@ -986,7 +999,10 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         states = self.ledger.devices(node)
         if self.native_score and a.pack != "random" and len(cands) >= self.NATIVE_MIN_CANDS:
             core = self._core()
-            if core is not None:
+            # the node's pack is built on the SECOND score of one node version: a node that
+            # changes after every placement (a single busy node) stays on the Python path,
+            # where building the pack would cost more than it saves
+            if core is not None and self._pack_ready(node):
                 return self._score_cands_native(core, node, cands, req, name, conf, intf, work, states)
         slo_scores: List[Optional[float]] = [None] * len(cands)
         if a.w_slo and req.slo > 0 and conf:
