@@ -39,6 +39,7 @@ from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
 
 from ..api import constants as C
 from ..api import objects as O
+from ..utils.protodesc import field, map_entry
 
 log = logging.getLogger(__name__)
 Obj = Dict[str, Any]
@@ -48,22 +49,11 @@ KUBELET_SOCKET = "/var/lib/kubelet/device-plugins/kubelet.sock"
 RESOURCES = (C.RESOURCE_GPU, C.RESOURCE_GPU_CU, C.RESOURCE_GPU_MEM)
 ANNOT_ALLOCATED = C.ANNOT_PREFIX + "allocated"
 _F = descriptor_pb2.FieldDescriptorProto
-
-
-def _field(msg: Any, name: str, num: int, typ: int, label: int = _F.LABEL_OPTIONAL, type_name: str = "") -> None:
-    f = msg.field.add()
-    f.name, f.number, f.type, f.label = name, num, typ, label
-    if type_name:
-        f.type_name = type_name
+_field = field
 
 
 def _map_entry(msg: Any, name: str, num: int) -> None:
-    """map<string, string> field `name` = a repeated nested *Entry message."""
-    entry = msg.nested_type.add(name="".join(p.capitalize() for p in name.split("_")) + "Entry")
-    entry.options.map_entry = True
-    _field(entry, "key", 1, _F.TYPE_STRING)
-    _field(entry, "value", 2, _F.TYPE_STRING)
-    _field(msg, name, num, _F.TYPE_MESSAGE, _F.LABEL_REPEATED, f".v1beta1.{msg.name}.{entry.name}")
+    map_entry(msg, name, num, API_VERSION)
 
 
 def _build_pool() -> descriptor_pool.DescriptorPool:

@@ -24,14 +24,7 @@ from typing import Any, Callable, Dict
 import grpc
 from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
 
-_F = descriptor_pb2.FieldDescriptorProto
-
-
-def _field(msg: Any, name: str, num: int, typ: int, label: int = _F.LABEL_OPTIONAL, type_name: str = "") -> None:
-    f = msg.field.add()
-    f.name, f.number, f.type, f.label = name, num, typ, label
-    if type_name:
-        f.type_name = type_name
+from ..utils.protodesc import F as _F, field as _field
 
 
 def _build_pool() -> descriptor_pool.DescriptorPool:
