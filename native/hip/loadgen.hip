@@ -370,7 +370,7 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
   else wait_vmcnt<0>();
 }
 
-template <bool RELU, bool BIAS>
+template <bool RELU, bool BIAS, bool PEEL = false>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                      const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -459,7 +459,39 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   barrier();
   if (wr == 1) barrier();                          // group 1 runs one barrier behind
 
-  for (int t = 0; t < T; ++t) {
+  int t0 = 0;
+  if constexpr (PEEL) {
+    // Steady state (t <= T-3): every phase stages its half-tile and three half-tiles stay in
+    // flight, so the waits are the constant vmcnt(6) and nothing branches -- the generic
+    // loop below only runs the last two K-tiles, where the pipeline drains.
+    for (; t0 + 2 < T; ++t0) {
+      const char* cur = smem + (t0 & 1) * BUF;
+      read_b(cur + OB0, b0r);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(cur + OA0);
+      stage(t0 + 1, 2);
+      barrier();
+      mfma_quadrant(0, 0, b0r);
+      barrier();
+      read_b(cur + OB1, b1r);
+      stage(t0 + 1, 3);
+      wait_vmcnt<6>();
+      barrier();
+      mfma_quadrant(0, 1, b1r);
+      barrier();
+      read_a(cur + OA1);
+      stage(t0 + 2, 0);
+      barrier();
+      mfma_quadrant(1, 1, b1r);
+      barrier();
+      stage(t0 + 2, 1);
+      wait_vmcnt<6>();
+      barrier();
+      mfma_quadrant(1, 0, b0r);
+      barrier();
+    }
+  }
+  for (int t = t0; t < T; ++t) {
     const char* cur = smem + (t & 1) * BUF;
     const int p0 = 4 * t;
     // phase 1: (0,0)
@@ -597,6 +629,19 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
                        N, K, lda, ldb, ldc);
 }
 
+template <bool PEEL>
+static void launch_8ph(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
+                       int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
+  if (relu && bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+}
+
 // 0 = auto, 1 = 128x128 (4 waves, 2/CU), 2 = 64x128, 3 = 64x64,
 // 4 = 256x256 (8 waves of 128x64, 1/CU), 5 = 256x128 (8 waves of 64x64, 1/CU)
 static int g_gemm_tile = 0;
@@ -615,13 +660,15 @@ static int g_gemm_tile = 0;
 // the per-k-step reads on the catalog shapes, 4096^3 1105 vs 1047 TF; for 64x128 it is mixed
 // (profiles/r01_gemm_tiles_hoist.json), so that tile keeps per-k-step reads.  Tile 6 is the
 // non-hoisted 128x128 kept as the A/B reference.
-// 9 = 256x256 8-phase (gemm_bf16_nt_256_8ph; needs K >= 128).
-static const int kTileBM[10] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256};
-static const int kTileBN[10] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256};
+// 9 = 256x256 8-phase (gemm_bf16_nt_256_8ph; needs K >= 128); 10 = the same with the
+// steady-state K loop peeled (constant vmcnt, no per-phase stage conditions).
+static const int kTileBM[11] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256};
+static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256};
 
-// Study knob.  0 = default: the 8-phase 256x256 (tile 9) for lone GEMMs that still get one
-// block per CU (4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs 1211;
-// profiles/r01_gemm_big.json).  1 = also for co-running pods whose CU share it fills: +8 % on
+// Study knob.  0 = default: the 8-phase 256x256 with the peeled steady-state loop (tile 10)
+// for lone GEMMs that still get one block per CU (tile 9 4096^3 1306 vs 1109 TF for tile 4,
+// 8192^3 1434 vs 1211, profiles/r01_gemm_big.json; peeling the loop: +5-6 % over tile 9 on
+// every shape, profiles/r02_gemm_big_peeled.json).  1 = also for co-running pods whose CU share it fills: +8 % on
 // a GEMM-only 4-stream mix (855 vs 794 TF, profiles/r01_gemm_corun_8ph.json) but no gain in
 // the bench, where the pods' GEMMs share the chip with HBM-streaming phases (508 vs 510 pods/s,
 // interleaved A/B, profiles/r01_gemm_policy_ab.txt) -- so co-running pods keep the
@@ -634,7 +681,7 @@ void set_gemm_policy(int p) {
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 9) throw std::runtime_error("gemm tile must be 0..9");
+  if (t < 0 || t > 10) throw std::runtime_error("gemm tile must be 0..10");
   g_gemm_tile = t;
 }
 
@@ -651,8 +698,8 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const int budget = alone ? kCus : cu_budget;
   const int per_cu = alone ? 2 : 1;
   const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
-  if (alone && fits256) return g_gemm_policy == 2 ? 4 : 9;
-  if (!alone && fits256 && g_gemm_policy == 1) return 9;
+  if (alone && fits256) return g_gemm_policy == 2 ? 4 : 10;
+  if (!alone && fits256 && g_gemm_policy == 1) return 10;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
@@ -674,7 +721,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
   if (ldc % 4 || reinterpret_cast<uintptr_t>(c) % 8) throw std::runtime_error("gemm: C rows must be 8-byte aligned");
   if (bias) check_align(reinterpret_cast<void*>(bias), "bias");
   int t = pick_gemm_tile(M, N, cu_budget);
-  if (t == 9 && K < 128) t = 4;                  // the 8-phase prologue stages two K-tiles
+  if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
   switch (t) {
     case 1: launch_gemm<128, 128, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
@@ -684,16 +731,13 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 6: launch_gemm<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 7: launch_gemm<64, 128, 2, 2, 2, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 8: launch_gemm<256, 128, 4, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    case 9: {
+    case 9:
+    case 10: {
       const dim3 grid((M / 256) * (N / 256)), block(512);
-      if (relu && bp)
-        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
-      else if (relu)
-        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
-      else if (bp)
-        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+      if (t == 10)
+        launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
       else
-        hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+        launch_8ph<false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
       break;
     }
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;

@@ -56,8 +56,9 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-def test_gemm_256_8phase_numerics_and_race_screen():
-    """The 8-phase 256x256 kernel (tile 9): every K-tile count from the minimum (2) through odd
+@pytest.mark.parametrize("tile", [9, 10])
+def test_gemm_256_8phase_numerics_and_race_screen(tile):
+    """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled): every K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
     (guide §5 'A sync-structure edit makes a NEW template'), so every run is checked against
@@ -65,9 +66,9 @@ def test_gemm_256_8phase_numerics_and_race_screen():
     from k8s_gpu_scheduler_amd import _native
     from k8s_gpu_scheduler_amd.ops import loadgen
     h = _native.hip()
-    h.set_gemm_tile(9)
+    h.set_gemm_tile(tile)
     try:
-        for (M, N, K) in [(256, 256, 128), (256, 512, 192), (512, 256, 320), (768, 1024, 1024),
+        for (M, N, K) in [(256, 256, 128), (256, 512, 192), (512, 256, 320), (768, 1024, 1024), (512, 512, 384),
                           (2048, 2048, 4096), (4096, 4096, 640)]:
             g = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K)
             a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)

@@ -13,7 +13,7 @@ from k8s_gpu_scheduler_amd import _native  # noqa: E402
 from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
 
 SHAPES = [(4096, 4096, 4096), (8192, 8192, 8192), (8192, 8192, 2048), (4096, 8192, 4096), (2048, 4096, 8192)]
-ARMS = ["torch", 1, 4, 9]
+ARMS = ["torch"] + [int(x) for x in os.environ.get("GEMM_BIG_ARMS", "1,4,9,10").split(",")]
 
 
 def t_ms(fn, iters=20, warm=3):
