@@ -370,7 +370,7 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
   else wait_vmcnt<0>();
 }
 
-template <bool RELU, bool BIAS, bool PEEL = false>
+template <bool RELU, bool BIAS, bool PEEL = false, bool WIDE = false>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                      const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -524,6 +524,49 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   }
   if (wr == 0) barrier();                          // balance the barrier count
 
+  if constexpr (WIDE) {
+    // Wide epilogue: the whole 256x256 bf16 block tile is assembled in LDS (exactly the 128 KiB
+    // the K loop used; every wave is past its last LDS read and every LDS-DMA has retired --
+    // the drained pipeline's vmcnt(0) -- once the now-aligned wave groups meet at one more
+    // barrier), then each wave stores whole 512-B rows with 16-B stores: 16 coalesced
+    // stores per lane instead of 32 scattered 8-B ones (the scattered tail cost 7-20 % of
+    // the kernel at K = 8192 .. 2048).  Image: row r at r * 512 B, its 8-B slot s (4
+    // columns) at slot s ^ ((r & 15) << 1): the 16 rows a ds_write_b64 lane group covers
+    // land on 8 bank pairs (2-way), and a 16-B chunk c of row r stays whole at chunk
+    // c ^ (r & 15), so each ds_read_b128 lane group reads 16 distinct bank quads.
+    barrier();
+    char* img = smem;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = g * 128 + wc * 32 + j * 16 + fk * 4;
+        f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = h * 128 + wr * 64 + i * 16 + frow;
+            f32x4 v = acc[h][i][g][j] + bv;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+            const int slot = (col >> 2) ^ ((row & 15) << 1);
+            *reinterpret_cast<bf16x4*>(img + row * 512 + slot * 8) = o;
+          }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int id = k * 512 + (int)threadIdx.x;       // 32 chunks of 16 B per row
+      const int row = id >> 5, c = id & 31;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * 512 + ((c ^ (row & 15)) << 4));
+      *reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8) = v;
+    }
+    return;
+  }
+
   // epilogue (D = C^T layout, as in gemm_bf16_nt_kernel): lane holds 4 consecutive columns
 #pragma unroll
   for (int g = 0; g < 2; ++g)
@@ -629,17 +672,29 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
                        N, K, lda, ldb, ldc);
 }
 
+template <bool PEEL, bool WIDE>
+static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
+                         int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
+  if (relu && bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+}
+
+// tile 9 = the original 8-phase kernel; 10 = peeled steady-state loop + wide LDS-staged
+// epilogue (when C rows are 16-B aligned, else the 8-B epilogue)
 template <bool PEEL>
 static void launch_8ph(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                        int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
-  if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
-  else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
-  else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  const bool wide = PEEL && ldc % 8 == 0 && reinterpret_cast<uintptr_t>(Cp) % 16 == 0;
+  if (wide)
+    launch_8ph_v<PEEL, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    launch_8ph_v<PEEL, false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
 }
 
 // 0 = auto, 1 = 128x128 (4 waves, 2/CU), 2 = 64x128, 3 = 64x64,
