@@ -449,6 +449,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="epochs kept in flight per GPU before collecting (>= 1)")
     ap.add_argument("--gemm-policy", type=int, default=0, choices=[0, 1, 2],
                     help="GEMM tile policy (A/B knob): 0 default, 1 8-phase 256x256 also for co-running pods")
+    ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],
+                    help="GEMM epilogue (A/B knob): 1 LDS-staged 16-B row stores, 0 scattered 8-B stores")
     ap.add_argument("--launch", default="auto", choices=["auto", "spawn", "inline"],
                     help="--gpus N > 1 outside torchrun: 'auto' spawns N rank processes on GPU hosts and "
                          "simulates N GPUs in one process with --sim; 'spawn' always spawns (gloo ranks "
@@ -511,9 +513,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         from .executor import DeviceExecutor
         ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
         ex.use_graphs = bool(a.graphs)
+        from .. import _native
         if a.gemm_policy:
-            from .. import _native
             _native.hip(required=True).set_gemm_policy(a.gemm_policy)
+        _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
     smi_s = None

@@ -29,6 +29,7 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
 void set_triad_variant(int v);
 void set_gemm_tile(int t);
 void set_gemm_policy(int p);
+void set_wide_epilogue(int on);
 int pick_gemm_tile(int M, int N, int cu_budget);
 std::vector<int> peer_access_matrix();
 double peer_copy_gbps(int src, int dst, size_t bytes, int iters);

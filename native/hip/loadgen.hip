@@ -88,8 +88,36 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// Wide epilogue of a BM x BN block tile (all kernels below): the bf16 tile is assembled in the
+// (then idle) staging LDS and stored as whole rows with 16-B stores instead of each lane's
+// scattered 8-B pieces (the D = C^T layout gives a lane 4 consecutive columns of one row).
+// Image: row r at r * BN * 2 bytes; its 8-B slot s (4 columns) at slot s ^ ((r & MASK) << 1)
+// with MASK = min(15, BN / 8 - 1): a ds_write_b64 lane group (16 rows, one column) spreads
+// over 8 bank pairs (2-way), and the 16-B chunk c of row r stays whole at chunk c ^ (r & MASK)
+// for the ds_read_b128 pass.  Caller: every wave past its last LDS read, no LDS-DMA in flight.
+template <int BN>
+__device__ __forceinline__ void wide_put(char* img, int row, int col, bf16x4 o) {
+  constexpr int MASK = (BN / 8 - 1) < 15 ? (BN / 8 - 1) : 15;
+  const int slot = (col >> 2) ^ ((row & MASK) << 1);
+  *reinterpret_cast<bf16x4*>(img + row * (BN * 2) + slot * 8) = o;
+}
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__ C, int ldc, int m0, int n0) {
+  constexpr int MASK = (BN / 8 - 1) < 15 ? (BN / 8 - 1) : 15;
+  constexpr int CPR = BN / 8;                           // 16-B chunks per row
+  static_assert(BM * CPR % NT == 0, "wide epilogue split");
+#pragma unroll
+  for (int k = 0; k < BM * CPR / NT; ++k) {
+    const int id = k * NT + (int)threadIdx.x;
+    const int row = id / CPR, c = id % CPR;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * (BN * 2) + ((c ^ (row & MASK)) << 4));
+    *reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8) = v;
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int STAGES = 2, int KT = BK,
-          bool HOIST = false>
+          bool HOIST = false, bool WIDE = false>
 __global__ void __launch_bounds__(WGM * WGN * 64, OCC)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -211,6 +239,28 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
       if (t + STAGES - 1 < nt) stage(t + STAGES - 1, (t + STAGES - 1) % STAGES);
       compute(tileA(t % STAGES), tileB(t % STAGES));
     }
+  }
+
+  if constexpr (WIDE) {
+    static_assert(BM * BN * 2 <= STAGES * (A_BYTES + B_BYTES), "wide epilogue image exceeds the staging LDS");
+    __syncthreads();                          // every wave past its last fragment read
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = wn * WTN + j * 16 + fk * 4;
+      f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        f32x4 v = acc[i][j] + bv;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+        wide_put<BN>(smem, wm * WTM + i * 16 + frow, col, o);
+      }
+    }
+    __syncthreads();
+    wide_store<BM, BN, NT>(smem, C, ldc, m0, n0);
+    return;
   }
 
   // ---- epilogue (D = C^T layout): row m = lane&15, cols n..n+3 = (lane>>4)*4 + r ----
@@ -525,17 +575,13 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   if (wr == 0) barrier();                          // balance the barrier count
 
   if constexpr (WIDE) {
-    // Wide epilogue: the whole 256x256 bf16 block tile is assembled in LDS (exactly the 128 KiB
-    // the K loop used; every wave is past its last LDS read and every LDS-DMA has retired --
-    // the drained pipeline's vmcnt(0) -- once the now-aligned wave groups meet at one more
-    // barrier), then each wave stores whole 512-B rows with 16-B stores: 16 coalesced
-    // stores per lane instead of 32 scattered 8-B ones (the scattered tail cost 7-20 % of
-    // the kernel at K = 8192 .. 2048).  Image: row r at r * 512 B, its 8-B slot s (4
-    // columns) at slot s ^ ((r & 15) << 1): the 16 rows a ds_write_b64 lane group covers
-    // land on 8 bank pairs (2-way), and a 16-B chunk c of row r stays whole at chunk
-    // c ^ (r & 15), so each ds_read_b128 lane group reads 16 distinct bank quads.
+    // Wide epilogue (wide_put / wide_store): the whole 256x256 bf16 block tile is assembled in
+    // LDS (exactly the 128 KiB the K loop used; every wave is past its last LDS read and every
+    // LDS-DMA has retired -- the drained pipeline's vmcnt(0) -- once the now-aligned wave
+    // groups meet at one more barrier), then whole 512-B rows go out with 16-B stores: 16
+    // coalesced stores per lane instead of 32 scattered 8-B ones (the scattered tail cost
+    // 7-20 % of the kernel at K = 8192 .. 2048).
     barrier();
-    char* img = smem;
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -547,23 +593,15 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int row = h * 128 + wr * 64 + i * 16 + frow;
             f32x4 v = acc[h][i][g][j] + bv;
             bf16x4 o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
-            const int slot = (col >> 2) ^ ((row & 15) << 1);
-            *reinterpret_cast<bf16x4*>(img + row * 512 + slot * 8) = o;
+            wide_put<256>(smem, h * 128 + wr * 64 + i * 16 + frow, col, o);
           }
       }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int id = k * 512 + (int)threadIdx.x;       // 32 chunks of 16 B per row
-      const int row = id >> 5, c = id & 31;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * 512 + ((c ^ (row & 15)) << 4));
-      *reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8) = v;
-    }
+    wide_store<256, 256, 512>(smem, C, ldc, m0, n0);
     return;
   }
 
@@ -654,22 +692,41 @@ static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
 }
 
+template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES, int KT, bool HOIST, bool WIDE>
+static void launch_gemm_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
+                          int ldb, int ldc, bool relu, hipStream_t s) {
+  const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
+  if (relu && bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES, KT, HOIST, WIDE>), grid, block, 0, s,
+                       A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES, KT, HOIST, WIDE>), grid, block, 0,
+                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else if (bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES, KT, HOIST, WIDE>), grid, block, 0,
+                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES, KT, HOIST, WIDE>), grid, block, 0,
+                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+}
+
+// Wide (LDS-staged, 16-B row stores) epilogue whenever C rows are 16-B aligned; g_wide_epi = 0
+// keeps the scattered 8-B epilogue (A/B knob).
+static int g_wide_epi = 1;
+
+void set_wide_epilogue(int on) { g_wide_epi = on ? 1 : 0; }
+
+static bool wide_ok(const __bf16* Cp, int ldc) {
+  return g_wide_epi && ldc % 8 == 0 && reinterpret_cast<uintptr_t>(Cp) % 16 == 0;
+}
+
 template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES = 2, int KT = BK, bool HOIST = false>
 static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                         int ldb, int ldc, bool relu, hipStream_t s) {
-  const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
-  if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M, N,
-                       K, lda, ldb, ldc);
-  else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M, N,
-                       K, lda, ldb, ldc);
-  else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M, N,
-                       K, lda, ldb, ldc);
+  if (wide_ok(Cp, ldc))
+    launch_gemm_v<BM, BN, WGM, WGN, OCC, STAGES, KT, HOIST, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES, KT, HOIST>), grid, block, 0, s, A, B, Cp, bp, M,
-                       N, K, lda, ldb, ldc);
+    launch_gemm_v<BM, BN, WGM, WGN, OCC, STAGES, KT, HOIST, false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
 }
 
 template <bool PEEL, bool WIDE>
@@ -690,7 +747,7 @@ static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const flo
 template <bool PEEL>
 static void launch_8ph(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                        int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
-  const bool wide = PEEL && ldc % 8 == 0 && reinterpret_cast<uintptr_t>(Cp) % 16 == 0;
+  const bool wide = PEEL && wide_ok(Cp, ldc);
   if (wide)
     launch_8ph_v<PEEL, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
   else
