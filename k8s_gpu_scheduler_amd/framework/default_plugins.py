@@ -38,6 +38,10 @@ class PrioritySort(QueueSortPlugin):
             return pa > pb
         return a.timestamp < b.timestamp
 
+    def sort_key(self, pi) -> tuple:
+        """Total-order key of `less` (priority is immutable; a requeue re-pushes)."""
+        return -O.priority(pi.pod), pi.timestamp
+
 
 class NodeUnschedulable(FilterPlugin):
     NAME = "NodeUnschedulable"

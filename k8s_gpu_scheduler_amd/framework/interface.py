@@ -76,30 +76,26 @@ def as_status(s: Optional[Status]) -> Status:
 
 
 class CycleState:
-    """Per-scheduling-cycle key/value store shared by plugins (thread-safe)."""
+    """Per-scheduling-cycle key/value store shared by plugins.  Thread-safe without a
+    lock: every operation is ONE dict operation (get/set/pop/copy), atomic under the GIL
+    -- parallel Score workers (parity mode) read and write it concurrently."""
+
+    __slots__ = ("_d", "skip_filter_plugins", "skip_score_plugins", "read", "write")
 
     def __init__(self) -> None:
         self._d: Dict[str, Any] = {}
-        self._lock = threading.Lock()
         self.skip_filter_plugins: set = set()
         self.skip_score_plugins: set = set()
-
-    def write(self, k: str, v: Any) -> None:
-        with self._lock:
-            self._d[k] = v
-
-    def read(self, k: str, default: Any = None) -> Any:
-        with self._lock:
-            return self._d.get(k, default)
+        # bound dict methods: read(k[, default]) / write(k, v) are the hot accessors
+        self.read = self._d.get
+        self.write = self._d.__setitem__
 
     def delete(self, k: str) -> None:
-        with self._lock:
-            self._d.pop(k, None)
+        self._d.pop(k, None)
 
     def clone(self) -> "CycleState":
         c = CycleState()
-        with self._lock:
-            c._d = dict(self._d)
+        c._d.update(self._d)
         return c
 
 

@@ -103,10 +103,22 @@ class Framework:
         qs = self.points["queueSort"]
         return qs[0].less if qs else None
 
+    def queue_sort_key(self) -> Optional[Callable[[Any], Any]]:
+        """The queueSort plugin's `sort_key(pod_info)` when it offers one (a key whose `<`
+        is exactly its `less`); None = the queue compares with `less`."""
+        qs = self.points["queueSort"]
+        return getattr(qs[0], "sort_key", None) if qs else None
+
     # ---------------------------------------------------------------- filter
     def run_pre_filter(self, state: CycleState, pod: Obj) -> Status:
+        clock, add = time.perf_counter_ns, self.metrics.add
         for p in self.points["preFilter"]:
-            s = as_status(self._timed("preFilter", lambda p=p: p.pre_filter(state, pod)))
+            t0 = clock()
+            r = p.pre_filter(state, pod)
+            add("preFilter", clock() - t0)
+            if r is None:
+                continue
+            s = as_status(r)
             if s.code == Code.SKIP:
                 state.skip_filter_plugins.add(p.name())
                 continue
@@ -252,8 +264,14 @@ class Framework:
 
     # ---------------------------------------------------------------- reserve .. postBind
     def run_reserve(self, state: CycleState, pod: Obj, node: str) -> Status:
+        clock, add = time.perf_counter_ns, self.metrics.add
         for p in self.points["reserve"]:
-            s = as_status(self._timed("reserve", lambda p=p: p.reserve(state, pod, node)))
+            t0 = clock()
+            r = p.reserve(state, pod, node)
+            add("reserve", clock() - t0)
+            if r is None:
+                continue
+            s = as_status(r)
             if not s.ok:
                 s.plugin = s.plugin or p.name()
                 return s
@@ -286,8 +304,14 @@ class Framework:
         return (Status(Code.WAIT) if waiting else Status.success()), wait
 
     def run_pre_bind(self, state: CycleState, pod: Obj, node: str) -> Status:
+        clock, add = time.perf_counter_ns, self.metrics.add
         for p in self.points["preBind"]:
-            s = as_status(self._timed("preBind", lambda p=p: p.pre_bind(state, pod, node)))
+            t0 = clock()
+            r = p.pre_bind(state, pod, node)
+            add("preBind", clock() - t0)
+            if r is None:
+                continue
+            s = as_status(r)
             if not s.ok:
                 s.plugin = s.plugin or p.name()
                 return s

@@ -133,7 +133,7 @@ class Scheduler:
             self.frameworks[prof.scheduler_name] = Framework(prof, registry, self.handle, config.parallelism)
         first = next(iter(self.frameworks.values()))
         self.queue = SchedulingQueue(self._queue_less(first), config.pod_initial_backoff_s,
-                                     config.pod_max_backoff_s)
+                                     config.pod_max_backoff_s, sort_key=first.queue_sort_key())
         self.bind_async = bind_async
         self._bind_pool = ThreadPoolExecutor(bind_workers, thread_name_prefix="bind") if bind_async else None
         self._rng = random.Random(seed)

@@ -643,6 +643,10 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         ka, kb = self._sort_key(a), self._sort_key(b)
         return ka < kb
 
+    def sort_key(self, pi: Any) -> Tuple[int, int, float, float]:
+        """Total-order key of `less` (the scheduling queue keys its heap with it)."""
+        return self._sort_key(pi)
+
     def _sort_key(self, pi: Any) -> Tuple[int, int, float, float]:
         d = pi.__dict__
         hit = d.get("_gpu_sort")
