@@ -447,14 +447,21 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
-    ap.add_argument("--gemm-policy", type=int, default=0, choices=[0, 1, 2],
-                    help="GEMM tile policy (A/B knob): 0 default, 1 8-phase 256x256 also for co-running pods")
+    ap.add_argument("--gemm-policy", type=int, default=1, choices=[0, 1, 2],
+                    help="GEMM tile policy: 1 (default) 8-phase 256x256 also for co-running pods it fills, 0 128x128 for co-running pods")
     ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],
                     help="GEMM epilogue (A/B knob): 1 LDS-staged 16-B row stores, 0 scattered 8-B stores")
     ap.add_argument("--launch", default="auto", choices=["auto", "spawn", "inline"],
                     help="--gpus N > 1 outside torchrun: 'auto' spawns N rank processes on GPU hosts and "
                          "simulates N GPUs in one process with --sim; 'spawn' always spawns (gloo ranks "
                          "with --sim); 'inline' never spawns")
+    ap.add_argument("--gemm-share", type=int, default=1, choices=[0, 1],
+                    help="1: the GEMM tile picker sizes a pod's GEMMs for its CU share (co-running pods fill the "
+                         "rest); 0: for the whole chip")
+    ap.add_argument("--triad-blocks", type=int, default=0,
+                    help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
+    ap.add_argument("--triad-variant", type=int, default=6, choices=range(7),
+                    help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
                     help="amd-smi activity sampling period across warmup + timed region (0 = off)")
     ap.add_argument("--out", default="")
@@ -514,9 +521,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
         ex.use_graphs = bool(a.graphs)
         from .. import _native
-        if a.gemm_policy:
-            _native.hip(required=True).set_gemm_policy(a.gemm_policy)
+        _native.hip(required=True).set_gemm_policy(a.gemm_policy)
         _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
+        _native.hip(required=True).set_triad_variant(a.triad_variant)
+        ex.triad_blocks = a.triad_blocks
+        ex.gemm_share = bool(a.gemm_share)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
     smi_s = None

@@ -777,15 +777,16 @@ static int g_gemm_tile = 0;
 static const int kTileBM[11] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256};
 static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256};
 
-// Study knob.  0 = default: the 8-phase 256x256 with the peeled steady-state loop (tile 10)
-// for lone GEMMs that still get one block per CU (tile 9 4096^3 1306 vs 1109 TF for tile 4,
-// 8192^3 1434 vs 1211, profiles/r01_gemm_big.json; peeling the loop: +5-6 % over tile 9 on
-// every shape, profiles/r02_gemm_big_peeled.json).  1 = also for co-running pods whose CU share it fills: +8 % on
-// a GEMM-only 4-stream mix (855 vs 794 TF, profiles/r01_gemm_corun_8ph.json) but no gain in
-// the bench, where the pods' GEMMs share the chip with HBM-streaming phases (508 vs 510 pods/s,
-// interleaved A/B, profiles/r01_gemm_policy_ab.txt) -- so co-running pods keep the
-// 128x128 / 2-per-CU picker.  2 = tile 4 instead of tile 9 for lone GEMMs.
-static int g_gemm_policy = 0;
+// Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
+// peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
+// 1211, profiles/r01_gemm_big.json; peeling: +5-6 % over tile 9 on every shape,
+// profiles/r02_gemm_big_peeled.json).  1 = default: co-running pods whose CU share the 256x256
+// tile fills use it too -- +3.2 % pods/s in the bench once the wide epilogue and the peeled loop
+// landed and every pod stream got its own HW queue (interleaved A/B, profiles/r02_gemm_share_ab.txt;
+// in round 1, with the older kernels, it had been even: profiles/r01_gemm_policy_ab.txt).
+// 0 = co-running pods always take the 128x128 / 2-per-CU picker.  2 = tile 4 instead of tile
+// 10 for lone GEMMs.
+static int g_gemm_policy = 1;
 
 void set_gemm_policy(int p) {
   if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");

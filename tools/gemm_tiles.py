@@ -97,7 +97,7 @@ def main():
                 out["concurrent"].append({"tile": tile, "round": rnd, "tflops": round(flops / ms / 1e9, 1)})
                 print(out["concurrent"][-1], flush=True)
     h.set_gemm_tile(0)
-    h.set_gemm_policy(0)
+    h.set_gemm_policy(1)
     os.makedirs("gpurun_out", exist_ok=True)
     json.dump(out, open("gpurun_out/gemm_tiles.json", "w"), indent=1)
 
