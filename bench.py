@@ -9,12 +9,15 @@ RCCL.  Prints ONE JSON line on rank 0 (metric/config from BASELINE.json).
 import os
 import sys
 
-# HIP hardware queues per process (HIP's default is 4): the 4 pod streams, the control
-# stream, the null stream and RCCL's streams need their own queues -- pods whose streams
-# share a queue run back to back instead of side by side (interleaved A/B on MI355X:
-# 4 -> 8 queues = +2.9 % pods/s, profiles/r02_hwq_ab.txt).  Set before HIP initialises;
-# an explicit environment value wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP hardware queues per process (HIP's default, and the GPU box's environment, is 4): the 4
+# pod streams, the control stream, the null stream and RCCL's streams each need a queue of
+# their own -- pod streams that share a queue run back to back instead of side by side
+# (interleaved A/B on MI355X: 4 -> 8 queues = +2.9 % pods/s, profiles/r02_hwq_ab.txt; pod
+# start/end events: tools/concurrency_probe.py).  Raised (never lowered) before HIP
+# initialises; GPUSCHED_HW_QUEUES overrides the value.
+_q = int(os.environ.get("GPUSCHED_HW_QUEUES", "8"))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _q <= 32:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_q)
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
