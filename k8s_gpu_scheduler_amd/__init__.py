@@ -8,3 +8,9 @@ amd-smi telemetry/topology/partitions, CU-masked streams, MFMA/HBM load kernels)
 RCCL-over-xGMI distributed executor and probes.  See SURVEY.md / README.md.
 """
 __version__ = "0.1.0"
+
+# compiled control-plane modules (Cython, built by _native.build) when up to date with
+# their sources; pure Python otherwise or with GPUSCHED_PURE_PYTHON=1
+from ._native import cyaccel as _cyaccel  # noqa: E402
+
+_cyaccel.install()

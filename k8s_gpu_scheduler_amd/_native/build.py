@@ -90,6 +90,10 @@ def build(force: bool = False, asan: bool = False, only: Tuple[str, ...] = (), v
 
     with ThreadPoolExecutor(max(1, len(jobs))) as ex:
         built = list(ex.map(run, jobs))
+    if not kind and (not only or "cy" in only):
+        # the compiled control-plane modules (Cython; skipped when Cython is absent)
+        from . import cyaccel
+        built += cyaccel.build(force=force, verbose=verbose)
     return built
 
 
