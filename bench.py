@@ -13,9 +13,11 @@ import sys
 # pod streams, the control stream, the null stream and RCCL's streams each need a queue of
 # their own -- pod streams that share a queue run back to back instead of side by side
 # (interleaved A/B on MI355X: 4 -> 8 queues = +2.9 % pods/s, profiles/r02_hwq_ab.txt; pod
-# start/end events: tools/concurrency_probe.py).  Raised (never lowered) before HIP
-# initialises; GPUSCHED_HW_QUEUES overrides the value.
-_q = int(os.environ.get("GPUSCHED_HW_QUEUES", "8"))
+# start/end events: tools/concurrency_probe.py), and an RCCL stream sharing a pod's queue
+# would hold the per-epoch placement broadcast behind that pod's queued kernels.  HIP creates
+# a queue per stream only up to this limit, so headroom costs nothing while the process has
+# fewer streams.  Raised (never lowered) before HIP initialises; GPUSCHED_HW_QUEUES overrides.
+_q = int(os.environ.get("GPUSCHED_HW_QUEUES", "16"))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _q <= 32:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_q)
 
