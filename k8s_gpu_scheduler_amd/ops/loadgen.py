@@ -69,9 +69,19 @@ def gemm(a: torch.Tensor, bt: torch.Tensor, out: Optional[torch.Tensor] = None, 
         if bias.dtype != torch.float32 or bias.numel() != N or not bias.is_contiguous():
             raise ValueError("bias must be a contiguous fp32 vector of length N")
         bptr = bias.data_ptr()
+    h = _native.hip()
     with torch.cuda.device(a.device):
-        _native.hip().gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0),
-                                   bt.stride(0), out.stride(0), relu, _stream_ptr(stream, a.device), cu_budget)
+        sp = _stream_ptr(stream, a.device)
+        # split-K (lone GEMMs whose 256x256 tiles leave CUs idle): an fp32 partial workspace from
+        # the caching allocator, allocated on the launch stream so its reuse is ordered after
+        # the reduce kernel
+        wsf = h.splitk_workspace_floats(M, N, K, cu_budget)
+        ws = None
+        if wsf:
+            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(a.device)):
+                ws = torch.empty(wsf, dtype=torch.float32, device=a.device)
+        h.gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), bptr, M, N, K, a.stride(0), bt.stride(0),
+                       out.stride(0), relu, sp, cu_budget, ws.data_ptr() if ws is not None else 0, wsf)
     return out
 
 

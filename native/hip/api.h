@@ -22,7 +22,11 @@ void destroy_stream(uintptr_t s);
 std::vector<uint32_t> get_stream_mask(uintptr_t s);
 std::vector<uint32_t> probe_xcd(uintptr_t stream, int n);
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
-                  int ldc, bool relu, uintptr_t stream, int cu_budget);
+                  int ldc, bool relu, uintptr_t stream, int cu_budget, uintptr_t workspace = 0,
+                  size_t workspace_floats = 0);
+int pick_split_k(int M, int N, int K, int cu_budget);
+size_t splitk_workspace_floats(int M, int N, int K, int cu_budget);
+void set_split_k(int s);
 void gemm_fp8_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
                  int ldc, bool relu, uintptr_t stream, int cu_budget);
 void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream);

@@ -50,7 +50,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("probe_xcd", &gs::probe_xcd, py::arg("stream"), py::arg("n"));
   m.def("gemm_bf16_nt", &gs::gemm_bf16_nt, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("bias"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("relu"),
-        py::arg("stream"), py::arg("cu_budget") = 0, py::call_guard<py::gil_scoped_release>());
+        py::arg("stream"), py::arg("cu_budget") = 0, py::arg("workspace") = 0, py::arg("workspace_floats") = 0,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("pick_split_k", &gs::pick_split_k, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cu_budget") = 0);
+  m.def("splitk_workspace_floats", &gs::splitk_workspace_floats, py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("cu_budget") = 0);
+  m.def("set_split_k", &gs::set_split_k, py::arg("s"));
   m.def("gemm_fp8_nt", &gs::gemm_fp8_nt, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("bias"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("relu"),
         py::arg("stream"), py::arg("cu_budget") = 0, py::call_guard<py::gil_scoped_release>());

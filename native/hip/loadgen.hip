@@ -18,6 +18,7 @@
 //  * gemm_fp8_nt -- the same GEMM with OCP e4m3fn operands on the block-scaled
 //    v_mfma_scale_f32_16x16x128_f8f6f4 (unit scales): 2x the bf16 MFMA rate.
 //  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
+#include <algorithm>
 #include <cstdint>
 
 #include "api.h"
@@ -420,17 +421,30 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
   else wait_vmcnt<0>();
 }
 
-template <bool RELU, bool BIAS, bool PEEL = false, bool WIDE = false>
+// SPLIT (split-K for lone GEMMs with fewer 256x256 tiles than CUs, e.g. tall-K 2048x4096x8192):
+// the grid is tiles x S; block (s, tile) multiplies the K slice [s*K, (s+1)*K) (K = the slice
+// length here) and stores its fp32 partial tile to ws[s] (row-major, ld = N) instead of C;
+// splitk_reduce then sums the S partials, adds bias, applies the activation and writes bf16.
+template <bool RELU, bool BIAS, bool PEEL = false, bool WIDE = false, bool SPLIT = false>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
-                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc,
+                     float* __restrict__ ws = nullptr) {
   constexpr int HALF = 128 * 64 * 2;               // bytes of one half-tile image
   constexpr int BUF = 4 * HALF;                    // one K-tile: A0 A1 B0 B1
   constexpr int OA0 = 0, OA1 = HALF, OB0 = 2 * HALF, OB1 = 3 * HALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
-  const int nwg = gridDim.x;
-  const int b = blockIdx.x;
+  int nwg = gridDim.x;
+  int b = blockIdx.x;
+  int split = 0;
+  if constexpr (SPLIT) {
+    nwg = (M / 256) * (N / 256);                   // tiles; the S slices of one tile are nwg apart
+    split = b / nwg;
+    b -= split * nwg;
+    A += (size_t)split * K;
+    Bt += (size_t)split * K;
+  }
   const int xcd = b % kXcds;
   const int q = nwg / kXcds, rem = nwg % kXcds;
   const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
@@ -574,6 +588,25 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   }
   if (wr == 0) barrier();                          // balance the barrier count
 
+  if constexpr (SPLIT) {
+    // fp32 partial tile (D = C^T layout: 4 consecutive columns of one row per lane, 16-B stores)
+    float* P = ws + (size_t)split * M * N;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + g * 128 + wc * 32 + j * 16 + fk * 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = m0 + h * 128 + wr * 64 + i * 16 + frow;
+            *reinterpret_cast<f32x4*>(P + (size_t)row * N + col) = acc[h][i][g][j];
+          }
+      }
+    return;
+  }
+
   if constexpr (WIDE) {
     // Wide epilogue (wide_put / wide_store): the whole 256x256 bf16 block tile is assembled in
     // LDS (exactly the 128 KiB the K loop used; every wave is past its last LDS read and every
@@ -625,6 +658,26 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
           *reinterpret_cast<bf16x4*>(C + (size_t)row * ldc + col) = o;
         }
     }
+}
+
+// C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
+// bf16x4 out, grid-stride over M*N/4).
+template <bool RELU, bool BIAS>
+__global__ void __launch_bounds__(256) splitk_reduce(const float* __restrict__ ws, int S, int M, int N,
+                                                     const float* __restrict__ bias, __bf16* __restrict__ C,
+                                                     int ldc) {
+  const size_t mn = (size_t)M * N, n4 = mn / 4;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = q * 4;
+    f32x4 v = *reinterpret_cast<const f32x4*>(ws + e);
+    for (int sp = 1; sp < S; ++sp) v += *reinterpret_cast<const f32x4*>(ws + (size_t)sp * mn + e);
+    const int m = (int)(e / N), n = (int)(e % N);
+    if (BIAS) v += *reinterpret_cast<const f32x4*>(bias + n);
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+    *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+  }
 }
 
 __global__ void __launch_bounds__(256) stream_triad_kernel(float4* __restrict__ a, const float4* __restrict__ b,
@@ -787,6 +840,13 @@ static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 2
 // 0 = co-running pods always take the 128x128 / 2-per-CU picker.  2 = tile 4 instead of tile
 // 10 for lone GEMMs.
 static int g_gemm_policy = 1;
+// split-K for lone GEMMs whose 256x256 tiles leave CUs idle: -1 = auto (up to 8 slices), 0 = off,
+// 2..8 = at most that many slices.  Off by default: on the tall-K 2048x4096x8192 the split
+// kernel itself runs at ~1540 TF, but the fp32 partials + reduce pass (~144 MB of traffic) put
+// the whole GEMM at 1162 TF vs 1210 for the 128x128 tile and 1290 for hipBLASLt
+// (profiles/r02_gemm_big_splitk.json); a fused last-arriver fixup would need cross-XCD L2
+// coherence for the partials.
+static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
   if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");
@@ -818,8 +878,43 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   return 3;
 }
 
+// Split-K factor for a lone GEMM (cu_budget 0 / whole chip): the 8-phase 256x256 kernel with
+// S K-slices when its tiles leave CUs idle -- tiles x S <= CUs, every slice >= 1024 deep and a
+// multiple of 64 -- else 1.  Needs an fp32 workspace of S*M*N floats (splitk_workspace_floats).
+int pick_split_k(int M, int N, int K, int cu_budget) {
+  if (g_gemm_tile || g_split_k == 0) return 1;
+  if (!(cu_budget <= 0 || cu_budget >= kCus)) return 1;
+  if (M % 256 || N % 256) return 1;
+  const int tiles = (M / 256) * (N / 256);
+  if (tiles * 2 > kCus) return 1;
+  int S = std::min(g_split_k > 0 ? g_split_k : 8, kCus / tiles);
+  while (S > 1 && (K % (64 * S) != 0 || K / S < 1024)) --S;
+  return S;
+}
+
+size_t splitk_workspace_floats(int M, int N, int K, int cu_budget) {
+  const int S = pick_split_k(M, N, K, cu_budget);
+  return S > 1 ? (size_t)S * M * N : 0;
+}
+
+void set_split_k(int s) {
+  if (s < -1 || s > 8) throw std::runtime_error("split_k must be 0 (off) .. 8, or -1 (auto)");
+  g_split_k = s == 1 ? 0 : s;
+}
+
+template <bool RELU, bool BIAS>
+static void launch_splitk(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, float* ws, int S, int M,
+                          int N, int K, int lda, int ldb, int ldc, hipStream_t s) {
+  const dim3 grid((M / 256) * (N / 256) * S), block(512);
+  hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, true, false, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
+                     K / S, lda, ldb, ldc, ws);
+  const size_t n4 = (size_t)M * N / 4;
+  const int rblocks = (int)std::min<size_t>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL((splitk_reduce<RELU, BIAS>), dim3(rblocks), dim3(256), 0, s, ws, S, M, N, bp, Cp, ldc);
+}
+
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
-                  int ldc, bool relu, uintptr_t stream, int cu_budget) {
+                  int ldc, bool relu, uintptr_t stream, int cu_budget, uintptr_t workspace, size_t workspace_floats) {
   // Host-side shape checks: the kernel has no bounds checks by design.
   if (M <= 0 || N <= 0 || K <= 0) throw std::runtime_error("gemm: empty shape");
   if (M % 64 || N % 64 || K % BK) throw std::runtime_error("gemm: M,N must be multiples of 64 and K of 64");
@@ -833,6 +928,18 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
   auto bp = reinterpret_cast<const float*>(bias);
   if (ldc % 4 || reinterpret_cast<uintptr_t>(c) % 8) throw std::runtime_error("gemm: C rows must be 8-byte aligned");
   if (bias) check_align(reinterpret_cast<void*>(bias), "bias");
+  const int S = workspace ? pick_split_k(M, N, K, cu_budget) : 1;
+  if (S > 1) {
+    if (workspace_floats < (size_t)S * M * N) throw std::runtime_error("gemm: split-K workspace too small");
+    check_align(reinterpret_cast<void*>(workspace), "workspace");
+    auto ws = reinterpret_cast<float*>(workspace);
+    if (relu && bp) launch_splitk<true, true>(A, B, Cp, bp, ws, S, M, N, K, lda, ldb, ldc, s);
+    else if (relu) launch_splitk<true, false>(A, B, Cp, bp, ws, S, M, N, K, lda, ldb, ldc, s);
+    else if (bp) launch_splitk<false, true>(A, B, Cp, bp, ws, S, M, N, K, lda, ldb, ldc, s);
+    else launch_splitk<false, false>(A, B, Cp, bp, ws, S, M, N, K, lda, ldb, ldc, s);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   int t = pick_gemm_tile(M, N, cu_budget);
   if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)

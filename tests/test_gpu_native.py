@@ -90,6 +90,60 @@ def test_gemm_256_8phase_numerics_and_race_screen(tile):
         h.set_gemm_tile(0)
 
 
+@pytest.mark.parametrize("M,N,K,relu,bias", [(2048, 4096, 8192, True, True), (1024, 1024, 8192, False, False),
+                                             (512, 768, 4096, True, False), (256, 256, 2048, False, True)])
+def test_gemm_split_k_matches_fp32_reference(hip, M, N, K, relu, bias):
+    """Split-K (opt-in, set_split_k): lone GEMMs whose 256x256 tiles leave CUs idle run the 8-phase
+    kernel per K slice -> fp32 partials -> reduce + bias + ReLU; repeated runs screen for
+    ordering races."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    hip.set_split_k(-1)
+    try:
+        _split_k_case(hip, loadgen, M, N, K, relu, bias)
+    finally:
+        hip.set_split_k(0)
+
+
+def _split_k_case(hip, loadgen, M, N, K, relu, bias):
+    assert hip.pick_split_k(M, N, K) > 1
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g) if bias else None
+    ref = a.float() @ bt.float().T + (b if bias else 0)
+    if relu:
+        ref = torch.relu(ref)
+    tol = 0.01 * ref.abs().max().item() + 1e-2
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    for _ in range(4):
+        out.fill_(float("nan"))
+        loadgen.gemm(a, bt, out=out, bias=b, relu=relu)
+        assert (out.float() - ref).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("slice_", [0, 1])
+def test_gemm_split_k_layout_identity(hip, slice_):
+    """A = I placed in K slice 0 or 1 (zeros elsewhere) with an asymmetric B: pins the C layout
+    and each slice's K offset exactly."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    n, K = 256, 2048
+    hip.set_split_k(-1)
+    try:
+        _split_k_identity(hip, loadgen, n, K, slice_)
+    finally:
+        hip.set_split_k(0)
+
+
+def _split_k_identity(hip, loadgen, n, K, slice_):
+    assert hip.pick_split_k(n, n, K) == 2
+    a = torch.zeros(n, K, device="cuda", dtype=torch.bfloat16)
+    a[:, slice_ * 1024:slice_ * 1024 + n] = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    asym = (torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n) % 97).to(torch.bfloat16)
+    bt = torch.zeros(n, K, device="cuda", dtype=torch.bfloat16)
+    bt[:, slice_ * 1024:slice_ * 1024 + n] = asym
+    assert torch.equal(loadgen.gemm(a, bt).float(), asym.float().T)
+
+
 def test_gemm_layout_identity_asymmetric():
     """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
     from k8s_gpu_scheduler_amd.ops import loadgen

@@ -100,6 +100,8 @@ def main():
     res = {"shape": [M, N, K], "triad_floats": NF}
     # calibrate loop counts to ~15 ms alone on the full chip
     full_g, full_t = S(), S()
+    timed([(full_g.stream, lambda s: enqueue_gemm(s, 10))])            # warm-up (first launches)
+    timed([(full_t.stream, lambda s: enqueue_triad(s, 4))])
     tg = timed([(full_g.stream, lambda s: enqueue_gemm(s, 10))])[0] / 10
     tt = timed([(full_t.stream, lambda s: enqueue_triad(s, 4))])[0] / 4
     ng, nt = max(4, int(15 / tg)), max(2, int(15 / tt))
@@ -108,8 +110,14 @@ def main():
     res["full_share"] = case("full_share", full_g, full_t, ng, nt)
     res["prio_gemm_high"] = case("prio_gemm_high", S(priority=-1), S(), ng, nt)
     res["prio_triad_high"] = case("prio_triad_high", S(), S(priority=-1), ng, nt)
-    for gu, tu in (((0, 6), (6, 8)), ((0, 4), (4, 8)), ((0, 7), (7, 8))):
+    for gu, tu in (((0, 6), (6, 8)), ((0, 4), (4, 8)), ((0, 3), (3, 8)), ((0, 2), (2, 8))):
         res[f"masked_g{gu}_t{tu}"] = case(f"masked g{gu} t{tu}", S(gu), S(tu), ng, nt, gbudget=(gu[1] - gu[0]) * 32)
+    for tu in ((3, 8), (2, 8), (4, 8)):     # only the stream kernel confined; GEMM may use every CU
+        res[f"triad_only_masked_t{tu}"] = case(f"triad-only masked t{tu}", S(), S(tu), ng, nt)
+    if os.environ.get("PROBE_SHORT"):
+        os.makedirs("gpurun_out", exist_ok=True)
+        json.dump(res, open("gpurun_out/contention.json", "w"), indent=1)
+        return
     # triad launch shape under full sharing
     sweep = {}
     for v, nb in ((6, 0), (3, 256), (3, 512), (3, 1024), (4, 256), (4, 512), (2, 2048)):

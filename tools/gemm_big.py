@@ -1,4 +1,5 @@
-"""Large lone GEMMs (a whole-GPU pod): the 256x256 8-phase kernel (tile 9) against the
+"""Large lone GEMMs (a whole-GPU pod): the default picker (arm 0: 8-phase 256x256, or split-K
+when its tiles leave CUs idle), the 256x256 8-phase kernel (tile 9/10) against the
 256x256 2-stage (4), the 128x128 (1) and hipBLASLt (torch), interleaved rounds in one
 process on uniform [-1, 1) operands.  Writes gpurun_out/gemm_big.json."""
 import json
@@ -13,7 +14,7 @@ from k8s_gpu_scheduler_amd import _native  # noqa: E402
 from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
 
 SHAPES = [(4096, 4096, 4096), (8192, 8192, 8192), (8192, 8192, 2048), (4096, 8192, 4096), (2048, 4096, 8192)]
-ARMS = ["torch"] + [int(x) for x in os.environ.get("GEMM_BIG_ARMS", "1,4,9,10").split(",")]
+ARMS = ["torch"] + [int(x) for x in os.environ.get("GEMM_BIG_ARMS", "0,1,10").split(",")]
 
 
 def t_ms(fn, iters=20, warm=3):
