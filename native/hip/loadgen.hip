@@ -849,7 +849,7 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");
+  if (p < 0 || p > 4) throw std::runtime_error("gemm policy must be 0..4");
   g_gemm_policy = p;
 }
 
@@ -872,7 +872,12 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const int per_cu = alone ? 2 : 1;
   const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
   if (alone && fits256) return g_gemm_policy == 2 ? 4 : 10;
-  if (!alone && fits256 && g_gemm_policy == 1) return 10;
+  if (!alone && fits256 && g_gemm_policy >= 1) return 10;
+  // study policies: 3 / 4 = co-running pods also take the 8-phase 256x256 when its tiles fill
+  // half / a quarter of their CU share (fewer, more efficient blocks; other pods fill the rest)
+  if (!alone && g_gemm_policy >= 3 && M % 256 == 0 && N % 256 == 0 &&
+      (M / 256) * (N / 256) * (g_gemm_policy == 3 ? 2 : 4) >= budget)
+    return 10;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
