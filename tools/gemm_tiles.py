@@ -88,7 +88,7 @@ def main():
         for st in streams:
             torch.cuda.current_stream().wait_stream(st)
     for rnd in range(3):
-        for tile in ("torch", "budget64", "budget64_8ph", 0) + TILES:
+        for tile in ("torch", "budget64", "budget64_8ph", 0) + (() if os.environ.get("GEMM_TILES_CONCURRENT_ONLY") else TILES):
             budget["b"] = {"torch": -1, "budget64": 64, "budget64_8ph": 64}.get(tile, 0)
             h.set_gemm_tile(tile if isinstance(tile, int) else 0)
             h.set_gemm_policy(1 if tile == "budget64_8ph" else 0)
