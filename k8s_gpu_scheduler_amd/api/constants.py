@@ -52,6 +52,8 @@ LABEL_MIG_CONFIG = "nvidia.com/mig.config"          # parity mode only
 TAINT_PARTITIONING = "amd.com/partitioning"
 
 ANNOT_PREFIX = "gpu-scheduler.amd.com/"
+# upstream kube-scheduler NodePreferAvoidPods annotation (JSON AvoidPods)
+ANNOT_PREFER_AVOID_PODS = "scheduler.alpha.kubernetes.io/preferAvoidPods"
 ANNOT_DEVICES = ANNOT_PREFIX + "devices"            # comma separated device UUIDs
 ANNOT_DEVICE_INDICES = ANNOT_PREFIX + "device-indices"
 ANNOT_CU_MASK = ANNOT_PREFIX + "cu-mask"

@@ -26,9 +26,15 @@ DEFAULT_PLUGINS: Dict[str, List[Dict[str, Any]]] = {
                {"name": "NodeAffinity"}, {"name": "NodePorts"}, {"name": "NodeResourcesFit"},
                {"name": "InterPodAffinity"}, {"name": "PodTopologySpread"}],
     "postFilter": [{"name": "DefaultPreemption"}],
-    "preScore": [],
-    "score": [{"name": "NodeResourcesBalancedAllocation", "weight": 1},
-              {"name": "NodeResourcesLeastAllocated", "weight": 1}],
+    # upstream v1.21 defaults (pkg/scheduler/algorithmprovider/registry.go); NodeAffinity,
+    # ImageLocality and NodePreferAvoidPods also PreScore here, only to skip themselves
+    # when they cannot change the ranking
+    "preScore": [{"name": "InterPodAffinity"}, {"name": "PodTopologySpread"}, {"name": "TaintToleration"},
+                 {"name": "NodeAffinity"}, {"name": "ImageLocality"}, {"name": "NodePreferAvoidPods"}],
+    "score": [{"name": "NodeResourcesBalancedAllocation", "weight": 1}, {"name": "ImageLocality", "weight": 1},
+              {"name": "InterPodAffinity", "weight": 1}, {"name": "NodeResourcesLeastAllocated", "weight": 1},
+              {"name": "NodeAffinity", "weight": 1}, {"name": "NodePreferAvoidPods", "weight": 10000},
+              {"name": "PodTopologySpread", "weight": 2}, {"name": "TaintToleration", "weight": 1}],
     "reserve": [],
     "permit": [],
     "preBind": [],
@@ -189,8 +195,10 @@ def default_gpu_config(gpu_args: Optional[Dict[str, Any]] = None, disable_defaul
     fixed-mode plugin implements (filter/reserve/preBind/postBind); `queue_sort` also makes
     GPU the queueSort plugin (longest predicted work first within an arrival window)."""
     score: Dict[str, Any] = {"enabled": [{"name": C.PLUGIN_NAME, "weight": C.DEFAULT_SCORE_WEIGHT}]}
+    pre_score: Dict[str, Any] = {"enabled": [{"name": C.PLUGIN_NAME}]}
     if disable_defaults:
         score["disabled"] = [{"name": "*"}]
+        pre_score["disabled"] = [{"name": "*"}]      # their Score halves are off too
     doc = {
         "apiVersion": "kubescheduler.config.k8s.io/v1beta1",
         "kind": "KubeSchedulerConfiguration",
@@ -201,7 +209,7 @@ def default_gpu_config(gpu_args: Optional[Dict[str, Any]] = None, disable_defaul
                 **({"queueSort": {"enabled": [{"name": C.PLUGIN_NAME}]}} if queue_sort else {}),
                 "preFilter": {"enabled": [{"name": C.PLUGIN_NAME}]},
                 "filter": {"enabled": [{"name": C.PLUGIN_NAME}]},
-                "preScore": {"enabled": [{"name": C.PLUGIN_NAME}]},
+                "preScore": pre_score,
                 "score": score,
                 "reserve": {"enabled": [{"name": C.PLUGIN_NAME}]},
                 "preBind": {"enabled": [{"name": C.PLUGIN_NAME}]},

@@ -11,6 +11,7 @@ from typing import Any, Dict
 
 from ..api import constants as C
 from ..api import objects as O
+from .score_plugins import NodeAffinityScore, TaintTolerationScore, node_selector_term_matches
 from .interface import BindPlugin, FilterPlugin, PreFilterPlugin, QueueSortPlugin, ScorePlugin, Status
 from .runtime import Registry
 
@@ -111,11 +112,13 @@ class NodeName(FilterPlugin):
         return [None if ni.name == want else self.filter(state, pod, ni) for ni in node_infos]
 
 
-class TaintToleration(FilterPlugin):
+class TaintToleration(FilterPlugin, TaintTolerationScore):
+    """Filter: NoSchedule / NoExecute taints must be tolerated.  Score (score_plugins): fewer
+    intolerable PreferNoSchedule taints rank higher."""
     NAME = "TaintToleration"
 
     def __init__(self, args=None, handle=None):
-        pass
+        self._tt_init(handle)
 
     def filter(self, state, pod, node_info):
         for t in O.node_taints(node_info.node):
@@ -134,11 +137,13 @@ class TaintToleration(FilterPlugin):
         return [self.filter(state, pod, ni) if O.node_taints(ni.node) else None for ni in node_infos]
 
 
-class NodeAffinity(FilterPlugin):
+class NodeAffinity(FilterPlugin, NodeAffinityScore):
+    """Filter: nodeSelector and required node-selector terms (matchExpressions incl. Gt/Lt,
+    matchFields on metadata.name; terms ORed).  Score (score_plugins): preferred terms."""
     NAME = "NodeAffinity"
 
     def __init__(self, args=None, handle=None):
-        pass
+        self._na_init(handle)
 
     def filter(self, state, pod, node_info):
         sel = pod.get("spec", {}).get("nodeSelector") or {}
@@ -149,12 +154,8 @@ class NodeAffinity(FilterPlugin):
         aff = (pod.get("spec", {}).get("affinity") or {}).get("nodeAffinity") or {}
         req = aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
         terms = req.get("nodeSelectorTerms") or []
-        if terms:
-            from ..kube.patch import match_label_selector
-            ok = any(match_label_selector(lab, {"matchExpressions": t.get("matchExpressions") or []})
-                     for t in terms)
-            if not ok:
-                return Status.unschedulable("node(s) didn't match Pod's node affinity/selector", self.NAME, True)
+        if terms and not any(node_selector_term_matches(node_info.node, t) for t in terms):
+            return Status.unschedulable("node(s) didn't match Pod's node affinity/selector", self.NAME, True)
         return None
 
     def cache_signature(self, state, pod, phase):
@@ -339,9 +340,10 @@ def default_registry() -> Registry:
     from .placement_plugins import InterPodAffinity, NodePorts, PodTopologySpread
     from .coscheduling import Coscheduling
     from .preemption import DefaultPreemption
+    from .score_plugins import ImageLocality, NodePreferAvoidPods
     r = Registry()
     for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
                 NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption,
-                NodePorts, InterPodAffinity, PodTopologySpread, Coscheduling):
+                NodePorts, InterPodAffinity, PodTopologySpread, Coscheduling, ImageLocality, NodePreferAvoidPods):
         r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
     return r

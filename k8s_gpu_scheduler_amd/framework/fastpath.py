@@ -126,11 +126,12 @@ class NodeResultCache:
         if not nodes:
             return None
         fsig = _plugin_sigs(fw.points["filter"], state.skip_filter_plugins, state, pod, "filter")
-        if fsig is None or _plugin_sigs(fw.points["preScore"], (), state, pod, "preScore") is None:
+        if fsig is None:
             return self._fallback()
         seq, epoch = cursor
         st = fw.run_pre_score(state, pod, [])
-        if not st.ok:
+        # a PreScore plugin that skipped itself contributes nothing to this cycle's scores
+        if not st.ok or _plugin_sigs(fw.points["preScore"], state.skip_score_plugins, state, pod, "preScore") is None:
             return self._fallback()
         score_plugins = [p for p in fw.points["score"] if p.name() not in state.skip_score_plugins]
         ssig = _plugin_sigs(score_plugins, (), state, pod, "score")

@@ -17,6 +17,7 @@ from typing import Any, Dict, List, Optional, Tuple
 from ..api import objects as O
 from ..kube.patch import match_label_selector
 from .interface import FilterPlugin, PreFilterPlugin, Status
+from .score_plugins import InterPodAffinityScore, PodTopologySpreadScore, _has_affinity
 
 Obj = Dict[str, Any]
 
@@ -71,7 +72,7 @@ def _term_matches(term: Obj, pod: Obj, other: Obj) -> bool:
     return O.namespace(other) in nss and match_label_selector(O.labels(other), term.get("labelSelector") or {})
 
 
-class InterPodAffinity(PreFilterPlugin, FilterPlugin):
+class InterPodAffinity(PreFilterPlugin, FilterPlugin, InterPodAffinityScore):
     """Required pod affinity / anti-affinity (requiredDuringSchedulingIgnoredDuringExecution),
     including existing pods' anti-affinity against the incoming pod (symmetry).  PreFilter
     turns every term into the set of topology domains it allows or forbids, once per cycle;
@@ -83,6 +84,7 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin):
     def __init__(self, args=None, handle=None):
         self.handle = handle
         self._anti: Dict[str, Obj] = {}         # assigned pods with required anti-affinity
+        self._with_aff: Dict[str, Obj] = {}     # assigned pods with any pod (anti-)affinity (Score)
         if handle is not None:
             try:
                 inf = handle.informer_factory.pods()
@@ -91,13 +93,19 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin):
                 pass
 
     def _on_pod(self, pod: Obj) -> None:
-        if O.node_name_of(pod) and not O.is_terminal(pod) and self._terms(pod, "podAntiAffinity"):
+        live = bool(O.node_name_of(pod)) and not O.is_terminal(pod)
+        if live and self._terms(pod, "podAntiAffinity"):
             self._anti[O.key(pod)] = pod
         else:
             self._anti.pop(O.key(pod), None)
+        if live and _has_affinity(pod):
+            self._with_aff[O.key(pod)] = pod
+        else:
+            self._with_aff.pop(O.key(pod), None)
 
     def _on_delete(self, pod: Obj) -> None:
         self._anti.pop(O.key(pod), None)
+        self._with_aff.pop(O.key(pod), None)
 
     @staticmethod
     def _terms(pod: Obj, kind: str) -> List[Obj]:
@@ -153,10 +161,11 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin):
         return None
 
 
-class PodTopologySpread(PreFilterPlugin, FilterPlugin):
+class PodTopologySpread(PreFilterPlugin, FilterPlugin, PodTopologySpreadScore):
     """topologySpreadConstraints with whenUnsatisfiable: DoNotSchedule -- placing the pod in
     this node's domain must keep (count in domain + 1) - (min over domains) <= maxSkew.
-    Domain counts are built once per cycle in PreFilter."""
+    Domain counts are built once per cycle in PreFilter.  ScheduleAnyway constraints are
+    scored (score_plugins.PodTopologySpreadScore)."""
     NAME = "PodTopologySpread"
     _KEY = "PodTopologySpread/counts"
 
