@@ -458,6 +458,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--gemm-share", type=int, default=1, choices=[0, 1],
                     help="1: the GEMM tile picker sizes a pod's GEMMs for its CU share (co-running pods fill the "
                          "rest); 0: for the whole chip")
+    ap.add_argument("--unit-rotate", type=int, default=0, choices=[0, 1],
+                    help="study knob: rotate each epoch's CU-slice slots on the executor (the scheduler's "
+                         "first-fit gives the longest pod of every epoch the same slot)")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
     ap.add_argument("--triad-variant", type=int, default=6, choices=range(7),
@@ -624,6 +627,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             runs: List[Any] = []
             for g in gpus_here:
                 runs += _runs_for(arr, g)
+            if a.unit_rotate:
+                shift = 2 * (state.setdefault("epochs", 0) % (UNITS_PER_GPU // 2))
+                for r in runs:
+                    if UNITS_PER_GPU % max(r.n_units, 1) == 0 and shift % max(r.n_units, 1) == 0:
+                        r.first_unit = (r.first_unit + shift) % UNITS_PER_GPU
+            state["epochs"] = state.get("epochs", 0) + 1
             t1 = time.perf_counter()
             if rank == 0 and async_cp:
                 cp.request_schedule()          # the control-plane process works in parallel
