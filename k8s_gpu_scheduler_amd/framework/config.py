@@ -21,10 +21,12 @@ from ..api import constants as C
 DEFAULT_PLUGINS: Dict[str, List[Dict[str, Any]]] = {
     "queueSort": [{"name": "PrioritySort"}],
     "preFilter": [{"name": "NodeResourcesFit"}, {"name": "NodePorts"}, {"name": "InterPodAffinity"},
-                  {"name": "PodTopologySpread"}],
+                  {"name": "PodTopologySpread"}, {"name": "VolumeBinding"}, {"name": "VolumeRestrictions"},
+                  {"name": "VolumeZone"}, {"name": "NodeVolumeLimits"}],
     "filter": [{"name": "NodeUnschedulable"}, {"name": "NodeName"}, {"name": "TaintToleration"},
                {"name": "NodeAffinity"}, {"name": "NodePorts"}, {"name": "NodeResourcesFit"},
-               {"name": "InterPodAffinity"}, {"name": "PodTopologySpread"}],
+               {"name": "VolumeRestrictions"}, {"name": "NodeVolumeLimits"}, {"name": "VolumeBinding"},
+               {"name": "VolumeZone"}, {"name": "InterPodAffinity"}, {"name": "PodTopologySpread"}],
     "postFilter": [{"name": "DefaultPreemption"}],
     # upstream v1.21 defaults (pkg/scheduler/algorithmprovider/registry.go); NodeAffinity,
     # ImageLocality and NodePreferAvoidPods also PreScore here, only to skip themselves
@@ -35,9 +37,9 @@ DEFAULT_PLUGINS: Dict[str, List[Dict[str, Any]]] = {
               {"name": "InterPodAffinity", "weight": 1}, {"name": "NodeResourcesLeastAllocated", "weight": 1},
               {"name": "NodeAffinity", "weight": 1}, {"name": "NodePreferAvoidPods", "weight": 10000},
               {"name": "PodTopologySpread", "weight": 2}, {"name": "TaintToleration", "weight": 1}],
-    "reserve": [],
+    "reserve": [{"name": "VolumeBinding"}],
     "permit": [],
-    "preBind": [],
+    "preBind": [{"name": "VolumeBinding"}],
     "bind": [{"name": "DefaultBinder"}],
     "postBind": [],
 }

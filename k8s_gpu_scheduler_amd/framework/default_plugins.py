@@ -341,9 +341,11 @@ def default_registry() -> Registry:
     from .coscheduling import Coscheduling
     from .preemption import DefaultPreemption
     from .score_plugins import ImageLocality, NodePreferAvoidPods
+    from .volume_plugins import NodeVolumeLimits, VolumeBinding, VolumeRestrictions, VolumeZone
     r = Registry()
     for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
                 NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption,
-                NodePorts, InterPodAffinity, PodTopologySpread, Coscheduling, ImageLocality, NodePreferAvoidPods):
+                NodePorts, InterPodAffinity, PodTopologySpread, Coscheduling, ImageLocality, NodePreferAvoidPods,
+                VolumeBinding, VolumeRestrictions, VolumeZone, NodeVolumeLimits):
         r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
     return r

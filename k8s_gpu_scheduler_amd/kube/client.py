@@ -22,9 +22,15 @@ from .patch import apply_json_patch, apply_merge_patch, match_field_selector, ma
 Obj = Dict[str, Any]
 
 NAMESPACED = {"pods": True, "configmaps": True, "events": True, "leases": True,
-              "nodes": False, "namespaces": False}
+              "nodes": False, "namespaces": False,
+              # storage (kube-scheduler's volume plugins: framework.volume_plugins)
+              "persistentvolumeclaims": True, "persistentvolumes": False, "storageclasses": False,
+              "csinodes": False}
 KIND_OF = {"pods": "Pod", "configmaps": "ConfigMap", "events": "Event", "leases": "Lease",
-           "nodes": "Node", "namespaces": "Namespace"}
+           "nodes": "Node", "namespaces": "Namespace", "persistentvolumeclaims": "PersistentVolumeClaim",
+           "persistentvolumes": "PersistentVolume", "storageclasses": "StorageClass", "csinodes": "CSINode"}
+API_VERSION_OF = {"leases": "coordination.k8s.io/v1", "storageclasses": "storage.k8s.io/v1",
+                  "csinodes": "storage.k8s.io/v1"}
 
 
 class ApiError(Exception):
@@ -232,7 +238,7 @@ class FakeCluster(KubeClient):
             md.setdefault("uid", f"uid-{resource}-{md['name']}-{next(self._rv)}")
             md.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
             obj.setdefault("kind", KIND_OF[resource])
-            obj.setdefault("apiVersion", "coordination.k8s.io/v1" if resource == "leases" else "v1")
+            obj.setdefault("apiVersion", API_VERSION_OF.get(resource, "v1"))
             if resource == "pods":
                 obj.setdefault("status", {}).setdefault("phase", "Pending")
             self._bump(obj)

@@ -267,6 +267,18 @@ class SharedInformerFactory:
     def config_maps(self) -> Informer:
         return self.informer("configmaps")
 
+    def persistent_volume_claims(self) -> Informer:
+        return self.informer("persistentvolumeclaims")
+
+    def persistent_volumes(self) -> Informer:
+        return self.informer("persistentvolumes")
+
+    def storage_classes(self) -> Informer:
+        return self.informer("storageclasses")
+
+    def csi_nodes(self) -> Informer:
+        return self.informer("csinodes")
+
     def start(self) -> None:
         for inf in list(self._informers.values()):
             if not inf._synced.is_set() and inf._thread is None and inf._cancel is None:

@@ -29,8 +29,10 @@ Obj = Dict[str, Any]
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
 GROUP_PATH = {"pods": "/api/v1", "nodes": "/api/v1", "configmaps": "/api/v1", "events": "/api/v1",
-              "namespaces": "/api/v1", "leases": "/apis/coordination.k8s.io/v1"}
-CLUSTER_SCOPED = {"nodes", "namespaces"}
+              "namespaces": "/api/v1", "leases": "/apis/coordination.k8s.io/v1",
+              "persistentvolumeclaims": "/api/v1", "persistentvolumes": "/api/v1",
+              "storageclasses": "/apis/storage.k8s.io/v1", "csinodes": "/apis/storage.k8s.io/v1"}
+CLUSTER_SCOPED = {"nodes", "namespaces", "persistentvolumes", "storageclasses", "csinodes"}
 PATCH_CT = {"json": "application/json-patch+json", "merge": "application/merge-patch+json",
             "strategic": "application/strategic-merge-patch+json"}
 
@@ -161,8 +163,8 @@ class RestClient(KubeClient):
         if field_selector:
             q["fieldSelector"] = field_selector
         doc = self._json("GET", self._path(resource, namespace), query=q)
-        kind = {"pods": "Pod", "nodes": "Node", "configmaps": "ConfigMap", "events": "Event",
-                "leases": "Lease", "namespaces": "Namespace"}[resource]
+        from .client import KIND_OF
+        kind = KIND_OF[resource]
         items = doc.get("items") or []
         for it in items:
             it.setdefault("kind", kind)
