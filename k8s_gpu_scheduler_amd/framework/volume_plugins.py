@@ -169,6 +169,8 @@ class VolumeBinding(PreFilterPlugin, FilterPlugin, ReservePlugin, PreBindPlugin)
 
     # ------------------------------------------------------------------ PreFilter / Filter
     def pre_filter(self, state, pod):
+        if not (pod.get("spec") or {}).get("volumes"):
+            return Status.skip()
         names = pod_claim_names(pod)
         if not names:
             return Status.skip()
@@ -249,7 +251,10 @@ class VolumeBinding(PreFilterPlugin, FilterPlugin, ReservePlugin, PreBindPlugin)
 
     # ------------------------------------------------------------------ Reserve / PreBind
     def reserve(self, state, pod, node_name):
-        dec = (state.read(self._DEC) or {}).get(node_name)
+        decs = state.read(self._DEC)
+        if not decs:
+            return None
+        dec = decs.get(node_name)
         if not dec:
             return None
         with self._lock:
@@ -269,7 +274,10 @@ class VolumeBinding(PreFilterPlugin, FilterPlugin, ReservePlugin, PreBindPlugin)
                 self._assumed.pop(pv, None)
 
     def pre_bind(self, state, pod, node_name):
-        dec = (state.read(self._DEC) or {}).get(node_name)
+        decs = state.read(self._DEC)
+        if not decs:
+            return None
+        dec = decs.get(node_name)
         if not dec:
             return None
         client = self.handle.client
@@ -333,6 +341,7 @@ class VolumeRestrictions(PreFilterPlugin, FilterPlugin):
     def __init__(self, args=None, handle=None):
         self.handle = handle
         self._rwop: Dict[str, Set[str]] = {}        # ReadWriteOncePod claim key -> pods using it
+        self._uses: Dict[str, List[str]] = {}       # pod key -> its ReadWriteOncePod claim keys
         self._claims_inf = None
         if handle is not None:
             try:
@@ -351,19 +360,29 @@ class VolumeRestrictions(PreFilterPlugin, FilterPlugin):
         return out
 
     def _on_pod(self, pod: Obj) -> None:
+        vols = (pod.get("spec") or {}).get("volumes")
+        if not vols and not self._uses:
+            return                                  # the common case: no claims anywhere
         self._on_pod_delete(pod)
-        if O.node_name_of(pod) and not O.is_terminal(pod) and pod_claim_names(pod):
-            for c in self._rwop_claims(pod):
-                self._rwop.setdefault(c, set()).add(O.key(pod))
+        if vols and O.node_name_of(pod) and not O.is_terminal(pod):
+            claims = self._rwop_claims(pod)
+            if claims:
+                self._uses[O.key(pod)] = claims
+                for c in claims:
+                    self._rwop.setdefault(c, set()).add(O.key(pod))
 
     def _on_pod_delete(self, pod: Obj) -> None:
         k = O.key(pod)
-        for c in [c for c, users in self._rwop.items() if k in users]:
-            self._rwop[c].discard(k)
-            if not self._rwop[c]:
-                del self._rwop[c]
+        for c in self._uses.pop(k, ()):
+            users = self._rwop.get(c)
+            if users is not None:
+                users.discard(k)
+                if not users:
+                    del self._rwop[c]
 
     def pre_filter(self, state, pod):
+        if not (pod.get("spec") or {}).get("volumes"):
+            return Status.skip()
         disks = _inline_disks(pod)
         claims = self._rwop_claims(pod) if pod_claim_names(pod) else []
         if not disks and not claims:
@@ -405,6 +424,8 @@ class VolumeZone(PreFilterPlugin, FilterPlugin):
                 pass
 
     def pre_filter(self, state, pod):
+        if not (pod.get("spec") or {}).get("volumes"):
+            return Status.skip()
         names = pod_claim_names(pod)
         if not names:
             return Status.skip()
