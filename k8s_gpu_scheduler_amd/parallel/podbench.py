@@ -408,6 +408,22 @@ def _runs_for(arr: np.ndarray, gpu: int):
     return out
 
 
+def _prewarm(dev: torch.device, ms: float) -> None:
+    """Back-to-back 4096^3 MFMA GEMMs for about `ms` (untimed setup), so the firmware's
+    moving-average activity counter that the amd-smi sampler reads starts the timed region
+    from a busy GPU rather than from the idle process start-up (see --prewarm-ms)."""
+    from ..ops import loadgen
+    a = torch.rand(4096, 4096, device=dev).to(torch.bfloat16)
+    bt = torch.rand(4096, 4096, device=dev).to(torch.bfloat16)
+    c = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(16):
+            loadgen.gemm(a, bt, out=c)
+        torch.cuda.synchronize(dev)
+    del a, bt, c
+
+
 def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap = argparse.ArgumentParser(description="MI355X pod-arrival scheduling benchmark")
     ap.add_argument("--gpus", type=int, default=1)
@@ -461,6 +477,14 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--unit-rotate", type=int, default=0, choices=[0, 1],
                     help="study knob: rotate each epoch's CU-slice slots on the executor (the scheduler's "
                          "first-fit gives the longest pod of every epoch the same slot)")
+    ap.add_argument("--slot-balance", type=int, default=0, choices=[0, 1],
+                    help="study knob: the executor maps each epoch's pods (longest predicted first) onto the "
+                         "CU-slice slots with the least predicted backlog (per-workload EMA of measured pod time)")
+    ap.add_argument("--prewarm-ms", type=float, default=300.0,
+                    help="untimed device warm-up before the warm-up epochs: this long of back-to-back MFMA "
+                         "GEMMs.  It does not change pods/s (interleaved A/B, profiles/r02_prewarm_ab.txt) but "
+                         "amd-smi's gfx_activity is a moving average: after the idle process start-up it reads "
+                         "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
     ap.add_argument("--triad-variant", type=int, default=6, choices=range(7),
@@ -564,11 +588,16 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         from .executor import PodRun
         ex.warm([PodRun(0, wl, u, 2, a.iters, masked=a.qos == "guaranteed") for wl in W.NAMES for u in (0, 2, 4, 6)])
 
+    if use_gpu and a.prewarm_ms > 0:
+        _prewarm(dev, a.prewarm_ms)
+
     totals = {"pods": 0.0, "busy_unit_ms": 0.0, "slo_ok": 0.0}
     state: Dict[str, Any] = {"next": cp.schedule_epoch() if rank == 0 else None}
 
     host = {"launch": 0.0, "schedule": 0.0, "wait": 0.0, "comm": 0.0}
     intervals: List[Tuple[float, float]] = []
+    trace: Optional[List[Any]] = [] if (os.environ.get("GPUSCHED_BENCH_TRACE") and rank == 0) else None
+    t_start = time.perf_counter()
     ref: Dict[str, Any] = {"ev": None}
 
     def collect(runs: List[Any], arr: np.ndarray, timed: bool) -> None:
@@ -579,7 +608,17 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             if ref["ev"] is not None:
                 for r in runs:
                     intervals.append((ref["ev"].elapsed_time(r.start), ref["ev"].elapsed_time(r.end)))
+                    if trace is not None:   # GPUSCHED_BENCH_TRACE: per-pod timeline of the timed region
+                        trace.append((state.get("collected", 0), r.first_unit, r.workload, intervals[-1][0],
+                                      intervals[-1][1], (time.perf_counter() - t_start) * 1e3))
+        if timed:
+            state["collected"] = state.get("collected", 0) + 1
         st = ex.collect(runs)
+        if a.slot_balance:
+            est = state.setdefault("est_ms", {})
+            for r in runs:
+                if r.ms > 0:
+                    est[r.workload] = 0.7 * est.get(r.workload, r.ms) + 0.3 * r.ms
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
         smi_vec = [-1.0, -1.0]
         if smi_s is not None:
@@ -627,6 +666,18 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             runs: List[Any] = []
             for g in gpus_here:
                 runs += _runs_for(arr, g)
+            if a.slot_balance and runs and all(r.n_units == 2 for r in runs):
+                now = time.perf_counter() * 1e3
+                bl = state.setdefault("backlog", [0.0] * (UNITS_PER_GPU // 2))
+                dt = now - state.get("bl_t", now)
+                state["bl_t"] = now
+                bl[:] = [max(0.0, b - dt) for b in bl]
+                est = state.setdefault("est_ms", {})
+                order = sorted(runs, key=lambda r: -est.get(r.workload, 5.0))
+                for r in order:
+                    k = min(range(len(bl)), key=lambda i: bl[i])
+                    r.first_unit = 2 * k
+                    bl[k] += est.get(r.workload, 5.0)
             if a.unit_rotate:
                 shift = 2 * (state.setdefault("epochs", 0) % (UNITS_PER_GPU // 2))
                 for r in runs:
@@ -753,6 +804,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "simulated": not use_gpu,
         }
         print(json.dumps(result), flush=True)
+        if trace is not None:
+            with open(os.environ["GPUSCHED_BENCH_TRACE"], "w") as f:
+                json.dump({"ms_total": elapsed * 1e3, "pods": trace}, f)
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(result, f)

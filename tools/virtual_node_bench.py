@@ -135,7 +135,10 @@ def main() -> None:
         out[k] = {"epoch_ms_slowest_gpu": round(mx, 3), "epoch_ms_mean_gpu": round(mn, 3),
                   "imbalance": round(mx / mn, 4), "pods_per_s_8gpu_coupled": round(4 * N_GPUS / mx * 1e3, 1),
                   "slo_attainment_pct": round(100.0 * st["ok"] / max(st["n"], 1), 2), "pods": st["n"],
-                  "epoch_ms_pipelined_l2": round(pipelined_ms(np.array(st["walls"]), 2), 3)}
+                  "epoch_ms_pipelined_l2": round(pipelined_ms(np.array(st["walls"]), 2), 3),
+                  "epoch_ms_pipelined_l3": round(pipelined_ms(np.array(st["walls"]), 3), 3),
+                  "epoch_ms_pipelined_l4": round(pipelined_ms(np.array(st["walls"]), 4), 3),
+                  "walls_ms": [[round(x, 3) for x in w] for w in st["walls"]]}
     print(json.dumps(out), flush=True)
     if a.dump_groups:
         json.dump(GROUPS, open(a.dump_groups, "w"))
