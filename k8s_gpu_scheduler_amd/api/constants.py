@@ -43,6 +43,7 @@ RESOURCE_GPU_MEM = "amd.com/gpu-memory"   # fractional: HBM in GiB
 RESOURCE_CPU = "cpu"
 RESOURCE_MEMORY = "memory"
 RESOURCE_PODS = "pods"
+RESOURCE_EPHEMERAL_STORAGE = "ephemeral-storage"
 
 LABEL_GPU_PRODUCT = "amd.com/gpu.product-name"
 LABEL_GPU_COUNT = "amd.com/gpu.count"

@@ -288,6 +288,53 @@ def pod_requests(pod: Obj) -> Dict[str, float]:
     return _pod_requests(pod)
 
 
+# kube-scheduler's scoring view of a container without a cpu / memory request
+# (upstream schedutil.DefaultMilliCPURequest / DefaultMemoryRequest)
+DEFAULT_MILLI_CPU_REQUEST = 100
+DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
+_NZ_CACHE: Dict[str, Tuple[int, int]] = {}
+
+
+def pod_nonzero_requests(pod: Obj) -> Tuple[int, int]:
+    """(milli-CPU, memory bytes) the resource Score plugins charge for a pod: each container's
+    request, with an unset cpu / memory request counted as 100m / 200 MiB (an explicit 0
+    stays 0), init containers as a max, plus the pod overhead (upstream
+    calculatePodResourceRequest + GetNonzeroRequests).  Memoised per pod UID."""
+    u = pod.get("metadata", {}).get("uid")
+    if u:
+        hit = _NZ_CACHE.get(u)
+        if hit is not None:
+            return hit
+    spec = pod.get("spec") or {}
+
+    def one(c: Obj) -> Tuple[int, int]:
+        res = c.get("resources") or {}
+        reqs = dict(res.get("limits") or {})       # the apiserver defaults requests from limits
+        reqs.update(res.get("requests") or {})
+        cpu = int(round(parse_quantity(reqs["cpu"]) * 1000)) if "cpu" in reqs else DEFAULT_MILLI_CPU_REQUEST
+        mem = int(parse_quantity(reqs["memory"])) if "memory" in reqs else DEFAULT_MEMORY_REQUEST
+        return cpu, mem
+
+    cpu = mem = 0
+    for c in spec.get("containers") or []:
+        a, b = one(c)
+        cpu, mem = cpu + a, mem + b
+    for c in spec.get("initContainers") or []:
+        a, b = one(c)
+        cpu, mem = max(cpu, a), max(mem, b)
+    ov = spec.get("overhead") or {}
+    if "cpu" in ov:
+        cpu += int(round(parse_quantity(ov["cpu"]) * 1000))
+    if "memory" in ov:
+        mem += int(parse_quantity(ov["memory"]))
+    out = (cpu, mem)
+    if u:
+        if len(_NZ_CACHE) > 200000:
+            _NZ_CACHE.clear()
+        _NZ_CACHE[u] = out
+    return out
+
+
 def _pod_requests(pod: Obj) -> Dict[str, float]:
     tot: Dict[str, float] = {}
     for c in containers(pod):

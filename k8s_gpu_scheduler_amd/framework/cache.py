@@ -19,7 +19,7 @@ Obj = Dict[str, Any]
 
 
 class NodeInfo:
-    __slots__ = ("node", "pods", "requested", "allocatable", "generation", "_name")
+    __slots__ = ("node", "pods", "requested", "allocatable", "generation", "_name", "non_zero")
 
     def __init__(self, node: Optional[Obj] = None):
         self.node: Optional[Obj] = None
@@ -28,6 +28,7 @@ class NodeInfo:
         self.allocatable: Dict[str, float] = {}
         self.generation = 0
         self._name = ""
+        self.non_zero = [0, 0]      # milli-CPU, memory bytes with scoring defaults (O.pod_nonzero_requests)
         if node is not None:
             self.set_node(node)
 
@@ -49,6 +50,8 @@ class NodeInfo:
         for r, v in O.pod_requests(pod).items():
             self.requested[r] = self.requested.get(r, 0.0) + v
         self.requested["pods"] = self.requested.get("pods", 0.0) + 1
+        nz = O.pod_nonzero_requests(pod)
+        self.non_zero = [self.non_zero[0] + nz[0], self.non_zero[1] + nz[1]]
         self.generation += 1
 
     def remove_pod(self, pod: Obj) -> bool:
@@ -59,6 +62,8 @@ class NodeInfo:
         for r, v in O.pod_requests(old).items():
             self.requested[r] = self.requested.get(r, 0.0) - v
         self.requested["pods"] = self.requested.get("pods", 0.0) - 1
+        nz = O.pod_nonzero_requests(old)
+        self.non_zero = [self.non_zero[0] - nz[0], self.non_zero[1] - nz[1]]
         self.generation += 1
         return True
 
@@ -72,6 +77,7 @@ class NodeInfo:
         n.pods = dict(self.pods)
         n.requested = dict(self.requested)
         n.allocatable = dict(self.allocatable)
+        n.non_zero = list(self.non_zero)
         n.generation = self.generation
         return n
 

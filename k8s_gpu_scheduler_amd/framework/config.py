@@ -22,10 +22,12 @@ DEFAULT_PLUGINS: Dict[str, List[Dict[str, Any]]] = {
     "queueSort": [{"name": "PrioritySort"}],
     "preFilter": [{"name": "NodeResourcesFit"}, {"name": "NodePorts"}, {"name": "InterPodAffinity"},
                   {"name": "PodTopologySpread"}, {"name": "VolumeBinding"}, {"name": "VolumeRestrictions"},
-                  {"name": "VolumeZone"}, {"name": "NodeVolumeLimits"}],
+                  {"name": "VolumeZone"}, {"name": "EBSLimits"}, {"name": "GCEPDLimits"},
+                  {"name": "NodeVolumeLimits"}, {"name": "AzureDiskLimits"}],
     "filter": [{"name": "NodeUnschedulable"}, {"name": "NodeName"}, {"name": "TaintToleration"},
                {"name": "NodeAffinity"}, {"name": "NodePorts"}, {"name": "NodeResourcesFit"},
-               {"name": "VolumeRestrictions"}, {"name": "NodeVolumeLimits"}, {"name": "VolumeBinding"},
+               {"name": "VolumeRestrictions"}, {"name": "EBSLimits"}, {"name": "GCEPDLimits"},
+               {"name": "NodeVolumeLimits"}, {"name": "AzureDiskLimits"}, {"name": "VolumeBinding"},
                {"name": "VolumeZone"}, {"name": "InterPodAffinity"}, {"name": "PodTopologySpread"}],
     "postFilter": [{"name": "DefaultPreemption"}],
     # upstream v1.21 defaults (pkg/scheduler/algorithmprovider/registry.go); NodeAffinity,

@@ -1,12 +1,18 @@
-"""In-tree default plugins the reference profile keeps enabled.
+"""In-tree plugins of kube-scheduler v1.21 (the reference's scheduler binary, reference
+cmd/scheduler/main.go:15-28, go.mod k8s.io/kubernetes v1.21.0).
 
 The reference's profile only *adds* GPU at score/postBind (reference
-deploy/scheduler.yaml:16-23), so upstream defaults (queue sort, node filters,
-resource fit, default binder) stay on.  These are the subset that matters for GPU pods.
+deploy/scheduler.yaml:16-23), so the upstream defaults stay on; `default_registry` holds
+every in-tree plugin of that release so a KubeSchedulerConfiguration written for it (e.g.
+NodeResourcesMostAllocated or RequestedToCapacityRatio for bin-packing) loads unchanged.
+This module has the node filters, resource fit and the resource-allocation scorers; the rest
+live in placement_plugins, score_plugins, volume_plugins, spread_plugins, preemption and
+coscheduling.
 """
 from __future__ import annotations
 
 import json
+import math
 from typing import Any, Dict
 
 from ..api import constants as C
@@ -176,8 +182,15 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
     NAME = "NodeResourcesFit"
 
     def __init__(self, args=None, handle=None):
-        self.ignored = set((args or {}).get("ignoredResources", []))
+        args = args or {}
+        self.ignored = set(args.get("ignoredResources", []))
+        # ignoredResourceGroups: every extended resource of these prefixes ("example.com" of
+        # "example.com/foo") is left to other plugins
+        self.ignored_groups = set(args.get("ignoredResourceGroups", []))
         self._memo: Dict[str, tuple] = {}      # node -> (generation, node object, request sig, status)
+
+    def _ignored(self, r: str) -> bool:
+        return r in self.ignored or (bool(self.ignored_groups) and "/" in r and r.split("/", 1)[0] in self.ignored_groups)
 
     def pre_filter(self, state, pod):
         state.write(_FIT_KEY, O.pod_requests(pod))
@@ -190,7 +203,7 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
         if node_info.free(C.RESOURCE_PODS) < 1 and C.RESOURCE_PODS in node_info.allocatable:
             return Status.unschedulable("Too many pods", self.NAME)
         for r, v in req.items():
-            if v <= 0 or r in self.ignored:
+            if v <= 0 or self._ignored(r):
                 continue
             if r not in node_info.allocatable and r.startswith(("amd.com/", "nvidia.com/")):
                 return Status.unschedulable(f"Insufficient {r}", self.NAME)
@@ -202,14 +215,14 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
         req = state.read(_FIT_KEY)
         if req is None:
             req = O.pod_requests(pod)
-        return tuple(sorted((r, v) for r, v in req.items() if v > 0 and r not in self.ignored))
+        return tuple(sorted((r, v) for r, v in req.items() if v > 0 and not self._ignored(r)))
 
     def filter_nodes(self, state, pod, node_infos):
         req = state.read(_FIT_KEY)
         if req is None:
             req = O.pod_requests(pod)
         want = [(r, v - 1e-9, r.startswith(("amd.com/", "nvidia.com/"))) for r, v in req.items()
-                if v > 0 and r not in self.ignored]
+                if v > 0 and not self._ignored(r)]
         sig = tuple(want)
         pods_key = C.RESOURCE_PODS
         memo = self._memo
@@ -243,34 +256,62 @@ class NodeResourcesFit(PreFilterPlugin, FilterPlugin):
 
 
 class _ResourceScore(ScorePlugin):
-    RES = (C.RESOURCE_CPU, C.RESOURCE_MEMORY)
+    """Shared body of the resource-allocation Score plugins (upstream noderesources
+    resource_allocation.go, v1.21): per configured resource an (allocatable, requested) pair --
+    cpu and memory charge every pod's non-zero request (O.pod_nonzero_requests: an unset
+    request counts as 100m / 200 MiB), other resources their plain requests, an extended
+    resource the node lacks (0, 0) -- in integer units (milli-CPU, bytes), then the plugin's
+    scorer.  `resources` args: [{name, weight}] (default cpu 1, memory 1)."""
+    DEFAULT_RES = ((C.RESOURCE_CPU, 1), (C.RESOURCE_MEMORY, 1))
 
     def __init__(self, args=None, handle=None):
         self.handle = handle
         self._memo = {}
+        res = (args or {}).get("resources")
+        self.res = tuple((r["name"], int(r.get("weight") or 1)) for r in res) if res else self.DEFAULT_RES
+        if any(w <= 0 for _, w in self.res):
+            raise ValueError(f"{self.NAME}: resource weights must be positive")
+        self._other = tuple(r for r, _ in self.res if r not in (C.RESOURCE_CPU, C.RESOURCE_MEMORY))
+
+    def _request_sig(self, pod) -> tuple:
+        nz = O.pod_nonzero_requests(pod)
+        if not self._other:
+            return nz
+        req = O.pod_requests(pod)
+        return nz + tuple(req.get(r, 0.0) for r in self._other)
+
+    def _pairs(self, ni, rq: tuple):
+        """[(allocatable, requested)] per configured resource, node + incoming pod."""
+        out = []
+        if ni is None or ni.node is None:
+            return [(0, 0)] * len(self.res)
+        alloc = ni.allocatable
+        k = 2
+        for r, _ in self.res:
+            if r == C.RESOURCE_CPU:
+                out.append((int(round(alloc.get(r, 0.0) * 1000)), ni.non_zero[0] + rq[0]))
+            elif r == C.RESOURCE_MEMORY:
+                out.append((int(alloc.get(r, 0.0)), ni.non_zero[1] + rq[1]))
+            else:
+                v = rq[k]
+                k += 1
+                if r in alloc or r == C.RESOURCE_EPHEMERAL_STORAGE:
+                    out.append((int(alloc.get(r, 0.0)), int(ni.requested.get(r, 0.0) + v)))
+                else:
+                    out.append((0, 0))
+        return out
 
     def score(self, state, pod, node_name):
-        # a node's score only changes with its NodeInfo generation and the request
-        ni = self.handle.snapshot().get(node_name)
-        req = O.pod_requests(pod)
-        key = (ni.generation if ni else -1, id(ni.node) if ni else 0) + tuple(req.get(r, 0.0) for r in self.RES)
-        hit = self._memo.get(node_name)
-        if hit is not None and hit[0] == key:
-            return hit[1], None
-        v = self._score(self._fractions(pod, node_name, ni, req))
-        if len(self._memo) > 100000:
-            self._memo.clear()
-        self._memo[node_name] = (key, v)
-        return v, None
+        v, _ = self.score_nodes(state, pod, [node_name])
+        return v[0], None
 
     def cache_signature(self, state, pod, phase):
-        req = O.pod_requests(pod)
-        return tuple(req.get(r, 0.0) for r in self.RES)
+        return self._request_sig(pod)
 
     def score_nodes(self, state, pod, names):
+        # a node's score only changes with its NodeInfo generation and the request
         snap = self.handle.snapshot()
-        req = O.pod_requests(pod)
-        rq = tuple(req.get(r, 0.0) for r in self.RES)
+        rq = self._request_sig(pod)
         memo = self._memo
         if len(memo) > 100000:
             memo.clear()
@@ -282,43 +323,121 @@ class _ResourceScore(ScorePlugin):
             if hit is not None and hit[0] == key:
                 out.append(hit[1])
                 continue
-            v = self._score(self._fractions(pod, nn, ni, req))
+            v = self._score(self._pairs(ni, rq))
             memo[nn] = (key, v)
             out.append(v)
         return out, None
 
-    def _fractions(self, pod, node_name, ni=None, req=None):
-        if ni is None:
-            ni = self.handle.snapshot().get(node_name)
-        if req is None:
-            req = O.pod_requests(pod)
-        fr = []
-        for r in self.RES:
-            alloc = ni.allocatable.get(r, 0.0) if ni else 0.0
-            if alloc <= 0:
-                continue
-            fr.append(min(1.0, (ni.requested.get(r, 0.0) + req.get(r, 0.0)) / alloc))
-        return fr
+    def _weighted(self, pairs, per) -> int:
+        tot = wsum = 0
+        for (cap, req), (_, w) in zip(pairs, self.res):
+            tot += per(req, cap) * w
+            wsum += w
+        return tot // wsum if wsum else 0
+
+
+def _least_requested(req: int, cap: int) -> int:
+    if cap == 0 or req > cap:
+        return 0
+    return (cap - req) * C.MAX_NODE_SCORE // cap
+
+
+def _most_requested(req: int, cap: int) -> int:
+    if cap == 0 or req > cap:
+        return 0
+    return req * C.MAX_NODE_SCORE // cap
 
 
 class NodeResourcesLeastAllocated(_ResourceScore):
+    """(capacity - requested) / capacity per resource, weighted mean: spreads load."""
     NAME = "NodeResourcesLeastAllocated"
 
-    def _score(self, fr):
-        if not fr:
-            return 0
-        return int(sum((1 - f) * C.MAX_NODE_SCORE for f in fr) / len(fr))
+    def _score(self, pairs):
+        return self._weighted(pairs, _least_requested)
+
+
+class NodeResourcesMostAllocated(_ResourceScore):
+    """requested / capacity per resource, weighted mean: bin-packs (upstream v1.21
+    most_allocated.go)."""
+    NAME = "NodeResourcesMostAllocated"
+
+    def _score(self, pairs):
+        return self._weighted(pairs, _most_requested)
 
 
 class NodeResourcesBalancedAllocation(_ResourceScore):
+    """100 x (1 - |cpu fraction - memory fraction|) (upstream v1.21 balanced_allocation.go;
+    fractions of a zero capacity count as 1 and are capped at 1)."""
     NAME = "NodeResourcesBalancedAllocation"
 
-    def _score(self, fr):
-        if len(fr) < 2:
-            return C.MAX_NODE_SCORE
-        mean = sum(fr) / len(fr)
-        var = sum((f - mean) ** 2 for f in fr) / len(fr)
-        return int((1 - var ** 0.5) * C.MAX_NODE_SCORE)
+    def __init__(self, args=None, handle=None):
+        super().__init__(None, handle)          # always cpu + memory
+
+    def _score(self, pairs):
+        fr = [1.0 if cap == 0 else min(1.0, req / cap) for cap, req in pairs]
+        return int((1 - abs(fr[0] - fr[1])) * C.MAX_NODE_SCORE)
+
+
+class RequestedToCapacityRatio(_ResourceScore):
+    """A broken-linear function of each resource's utilisation (args `shape`:
+    [{utilization 0..100, score 0..10}], strictly increasing utilisation), weighted over the
+    resources whose score is positive, rounded (upstream v1.21 requested_to_capacity_ratio.go)."""
+    NAME = "RequestedToCapacityRatio"
+    MAX_UTILIZATION = 100
+    MAX_CUSTOM_SCORE = 10
+
+    def __init__(self, args=None, handle=None):
+        super().__init__(args, handle)
+        shape = (args or {}).get("shape") or []
+        if not shape:
+            raise ValueError("RequestedToCapacityRatio: shape must not be empty")
+        pts = []
+        for p in shape:
+            u, sc = int(p.get("utilization", 0)), int(p.get("score", 0))
+            if not 0 <= u <= self.MAX_UTILIZATION:
+                raise ValueError(f"RequestedToCapacityRatio: utilization {u} outside 0..100")
+            if not 0 <= sc <= self.MAX_CUSTOM_SCORE:
+                raise ValueError(f"RequestedToCapacityRatio: score {sc} outside 0..10")
+            if pts and u <= pts[-1][0]:
+                raise ValueError("RequestedToCapacityRatio: utilization values must be strictly increasing")
+            pts.append((u, sc * (C.MAX_NODE_SCORE // self.MAX_CUSTOM_SCORE)))
+        self.shape = tuple(pts)
+
+    def _raw(self, p: int) -> int:
+        s = self.shape
+        for i, (u, sc) in enumerate(s):
+            if p <= u:
+                if i == 0:
+                    return s[0][1]
+                u0, s0 = s[i - 1]
+                return s0 + _go_div((sc - s0) * (p - u0), u - u0)
+        return s[-1][1]
+
+    def _resource(self, req: int, cap: int) -> int:
+        m = self.MAX_UTILIZATION
+        if cap == 0 or req > cap:
+            return self._raw(m)
+        return self._raw(m - (cap - req) * m // cap)
+
+    def _score(self, pairs):
+        tot = wsum = 0
+        for (cap, req), (_, w) in zip(pairs, self.res):
+            v = self._resource(req, cap)
+            if v > 0:
+                tot += v * w
+                wsum += w
+        return int(round_half_away(tot / wsum)) if wsum else 0
+
+
+def _go_div(a: int, b: int) -> int:
+    """Go's integer division (truncates toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def round_half_away(x: float) -> float:
+    """Go's math.Round (half away from zero)."""
+    return math.floor(x + 0.5) if x >= 0 else -math.floor(-x + 0.5)
 
 
 class DefaultBinder(BindPlugin):
@@ -341,11 +460,15 @@ def default_registry() -> Registry:
     from .coscheduling import Coscheduling
     from .preemption import DefaultPreemption
     from .score_plugins import ImageLocality, NodePreferAvoidPods
-    from .volume_plugins import NodeVolumeLimits, VolumeBinding, VolumeRestrictions, VolumeZone
+    from .spread_plugins import NodeLabel, SelectorSpread, ServiceAffinity
+    from .volume_plugins import (AzureDiskLimits, CinderLimits, EBSLimits, GCEPDLimits, NodeVolumeLimits, VolumeBinding,
+                                 VolumeRestrictions, VolumeZone)
     r = Registry()
     for cls in (PrioritySort, NodeUnschedulable, NodeName, TaintToleration, NodeAffinity, NodeResourcesFit,
-                NodeResourcesLeastAllocated, NodeResourcesBalancedAllocation, DefaultBinder, DefaultPreemption,
+                NodeResourcesLeastAllocated, NodeResourcesMostAllocated, NodeResourcesBalancedAllocation,
+                RequestedToCapacityRatio, DefaultBinder, DefaultPreemption,
                 NodePorts, InterPodAffinity, PodTopologySpread, Coscheduling, ImageLocality, NodePreferAvoidPods,
-                VolumeBinding, VolumeRestrictions, VolumeZone, NodeVolumeLimits):
+                VolumeBinding, VolumeRestrictions, VolumeZone, NodeVolumeLimits,
+                EBSLimits, GCEPDLimits, AzureDiskLimits, CinderLimits, SelectorSpread, ServiceAffinity, NodeLabel):
         r.register(cls.NAME, lambda args, handle, cls=cls: cls(args, handle))
     return r

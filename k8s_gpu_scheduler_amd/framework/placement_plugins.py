@@ -165,22 +165,61 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PodTopologySpreadScore):
     """topologySpreadConstraints with whenUnsatisfiable: DoNotSchedule -- placing the pod in
     this node's domain must keep (count in domain + 1) - (min over domains) <= maxSkew.
     Domain counts are built once per cycle in PreFilter.  ScheduleAnyway constraints are
-    scored (score_plugins.PodTopologySpreadScore)."""
+    scored (score_plugins.PodTopologySpreadScore).  Pods without constraints get the
+    default constraints (args defaultingType System | List, defaultConstraints) over the
+    selectors of their Services and controller (spread_plugins.default_selector)."""
     NAME = "PodTopologySpread"
     _KEY = "PodTopologySpread/counts"
 
+    # upstream v1.21 system defaults (defaultingType: System), applied to pods without
+    # constraints that a Service / ReplicationController / ReplicaSet / StatefulSet selects
+    SYSTEM_DEFAULT_CONSTRAINTS = (
+        {"maxSkew": 3, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "ScheduleAnyway"},
+        {"maxSkew": 5, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "ScheduleAnyway"})
+
     def __init__(self, args=None, handle=None):
+        from .spread_plugins import Owners
+        args = args or {}
         self.handle = handle
+        dt = args.get("defaultingType", "System")
+        given = list(args.get("defaultConstraints") or [])
+        if dt == "System":
+            if given:
+                raise ValueError("PodTopologySpread: defaultConstraints need defaultingType: List")
+            self.default_constraints = list(self.SYSTEM_DEFAULT_CONSTRAINTS)
+        elif dt == "List":
+            if any(c.get("labelSelector") for c in given):
+                raise ValueError("PodTopologySpread: defaultConstraints must not set labelSelector")
+            self.default_constraints = given
+        else:
+            raise ValueError(f"PodTopologySpread: unknown defaultingType {dt!r}")
+        self._owners = Owners(handle) if self.default_constraints else None
+
+    def spread_constraints(self, pod, mode: str):
+        """([(topologyKey, maxSkew, [label selectors])], explicit) of the pod's constraints with
+        whenUnsatisfiable == mode -- or, when the pod declares none, the default constraints
+        with the selectors of its Services / controller (none when nothing selects it)."""
+        spec_cons = (pod.get("spec") or {}).get("topologySpreadConstraints") or []
+        if spec_cons:
+            return [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)), [c.get("labelSelector") or {}])
+                    for c in spec_cons if c.get("whenUnsatisfiable", "DoNotSchedule") == mode], True
+        defs = [c for c in self.default_constraints if c.get("whenUnsatisfiable", "DoNotSchedule") == mode]
+        if not defs or self._owners is None:
+            return [], False
+        from .spread_plugins import default_selector
+        sels = default_selector(pod, self._owners)
+        if not sels:
+            return [], False
+        return [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)), sels) for c in defs], False
 
     def pre_filter(self, state, pod):
-        cons = [c for c in (pod.get("spec") or {}).get("topologySpreadConstraints") or []
-                if c.get("whenUnsatisfiable", "DoNotSchedule") == "DoNotSchedule"]
+        cons, _ = self.spread_constraints(pod, "DoNotSchedule")
         if not cons:
             return Status.skip()
         snap = self.handle.snapshot()
         out = []
-        for c in cons:
-            key = c.get("topologyKey", "")
+        ns = O.namespace(pod)
+        for key, max_skew, sels in cons:
             counts: Dict[str, int] = {}
             for ni in snap.list():
                 d = _domain(ni.node, key)
@@ -188,8 +227,8 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PodTopologySpreadScore):
                     continue
                 counts[d] = counts.get(d, 0) + sum(
                     1 for o in ni.pods.values()
-                    if O.namespace(o) == O.namespace(pod) and match_label_selector(O.labels(o), c.get("labelSelector") or {}))
-            out.append((key, int(c.get("maxSkew", 1)), counts, min(counts.values()) if counts else 0))
+                    if O.namespace(o) == ns and all(match_label_selector(O.labels(o), sl) for sl in sels))
+            out.append((key, max_skew, counts, min(counts.values()) if counts else 0))
         state.write(self._KEY, out)
         return None
 

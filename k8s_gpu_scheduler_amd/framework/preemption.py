@@ -38,6 +38,7 @@ class WhatIfNodeInfo(NodeInfo):
         w = cls()
         w.node, w._name = ni.node, ni._name
         w.pods, w.requested, w.allocatable = dict(ni.pods), dict(ni.requested), dict(ni.allocatable)
+        w.non_zero = list(ni.non_zero)
         w.generation = ni.generation
         w.removed = set()
         for v in victims:

@@ -311,29 +311,30 @@ class PodTopologySpreadScore(PreScorePlugin, ScorePlugin):
     _pts_norm = _SpreadNormalize()
 
     def pre_score(self, state, pod, nodes):
-        cons = [c for c in (pod.get("spec") or {}).get("topologySpreadConstraints") or []
-                if c.get("whenUnsatisfiable") == "ScheduleAnyway"]
+        cons, require_all = self.spread_constraints(pod, "ScheduleAnyway")
         if not cons:
             return Status.skip()
         snap = self.handle.snapshot()
         infos = snap.list()
         cand = nodes if nodes else infos
-        ignored = {ni.name for ni in cand if any(c.get("topologyKey", "") not in O.labels(ni.node) for c in cons)}
+        # explicit constraints: nodes lacking a topology key are ignored (score 0); the
+        # defaulted ones (Service / controller spreading) just skip the missing keys
+        ignored = {ni.name for ni in cand if any(key not in O.labels(ni.node) for key, _, _ in cons)} \
+            if require_all else set()
         out = []
-        for c in cons:
-            key = c.get("topologyKey", "")
-            sel = c.get("labelSelector") or {}
-            domains = {O.labels(ni.node)[key] for ni in cand if ni.name not in ignored}
+        ns = O.namespace(pod)
+        for key, max_skew, sels in cons:
+            domains = {O.labels(ni.node)[key] for ni in cand if ni.name not in ignored and key in O.labels(ni.node)}
             counts: Dict[str, int] = {}
             for ni in infos:
                 d = O.labels(ni.node).get(key)
                 if d is None or d not in domains:
                     continue
                 counts[d] = counts.get(d, 0) + sum(1 for o in ni.pods.values()
-                                                   if O.namespace(o) == O.namespace(pod)
-                                                   and match_label_selector(O.labels(o), sel))
+                                                   if O.namespace(o) == ns
+                                                   and all(match_label_selector(O.labels(o), sl) for sl in sels))
             weight = math.log(len(domains) + 2)
-            out.append((key, int(c.get("maxSkew", 1)), counts, weight))
+            out.append((key, max_skew, counts, weight))
         state.write(self._PTS_KEY, (out, ignored))
         return None
 

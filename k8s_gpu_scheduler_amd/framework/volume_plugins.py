@@ -24,6 +24,15 @@ limits hold.  Same semantics here, on the framework's extension points:
                      values joined by "__") must contain the node's label value.
   NodeVolumeLimits   CSI volumes on the node (distinct driver + volume handle, incl. the
                      pod's) may not exceed the node's CSINode allocatable count per driver.
+  EBSLimits, GCEPDLimits, AzureDiskLimits, CinderLimits
+                     the in-tree attach limits: distinct AWS EBS / GCE PD / Azure disk /
+                     Cinder volumes (in-line or through a bound claim's PV, plus unbound
+                     claims whose class provisions that type) may not exceed the node's
+                     `attachable-volumes-*` allocatable, else the upstream default (EBS 39,
+                     25 on Nitro instance types; GCE PD 16; Azure 16; Cinder 256;
+                     KUBE_MAX_PD_VOLS overrides).  A plugin migrated to CSI on the node
+                     (CSINode storage.alpha.kubernetes.io/migrated-plugins) is left to
+                     NodeVolumeLimits.
 
 Each plugin returns Skip at PreFilter for pods without volumes of its kind, so ordinary pods
 (and the cross-cycle node-result cache) are unaffected.  `kube.pv_controller` is the PV
@@ -31,6 +40,8 @@ controller half for the fake cluster (bind + a provisioner).
 """
 from __future__ import annotations
 
+import os
+import re
 import threading
 import time
 from typing import Any, Dict, List, Optional, Set, Tuple
@@ -506,3 +517,127 @@ class NodeVolumeLimits(PreFilterPlugin, FilterPlugin):
             if drv in limits and len(vols) > limits[drv]:
                 return Status.unschedulable("node(s) exceed max volume count", self.NAME)
         return None
+
+
+# ---------------------------------------------------------------------------- in-tree volume limits
+_EBS_NITRO = re.compile(r"^[cmr]5.*|t3|z1d")
+_MIGRATED_ANNOT = "storage.alpha.kubernetes.io/migrated-plugins"
+
+
+class _InTreeLimits(PreFilterPlugin, FilterPlugin):
+    """Base of the non-CSI attach-limit filters (upstream nodevolumelimits/non_csi.go)."""
+    VOLUME = ""            # pod volume source / PV spec key
+    ID = ""                # field naming the volume inside that source
+    PROVISIONER = ""       # in-tree provisioner of dynamically provisioned volumes
+    ALLOCATABLE = ""       # node allocatable key
+    PLUGIN = ""            # in-tree plugin name (CSI migration annotation)
+    DEFAULT_MAX = 0
+
+    def __init__(self, args=None, handle=None):
+        self.vb = VolumeZone(None, handle).vb
+        self._csinodes = None
+        self._key = f"{self.NAME}/volumes"
+        if handle is not None:
+            try:
+                self._csinodes = handle.informer_factory.csi_nodes()
+            except AttributeError:
+                pass
+
+    def _ids(self, pod: Obj, with_unbound: bool) -> Set[str]:
+        out: Set[str] = set()
+        ns = O.namespace(pod)
+        for v in (pod.get("spec") or {}).get("volumes") or []:
+            src = v.get(self.VOLUME)
+            if src:
+                out.add(str(src.get(self.ID, "")))
+                continue
+            claim = (v.get("persistentVolumeClaim") or {}).get("claimName")
+            if not claim:
+                continue
+            pvc = self.vb._pvc(ns, claim)
+            if pvc is None:
+                continue
+            vol = (pvc.get("spec") or {}).get("volumeName")
+            if vol:
+                src = ((self.vb._pv(vol) or {}).get("spec") or {}).get(self.VOLUME)
+                if src:
+                    out.add(str(src.get(self.ID, "")))
+            elif with_unbound:
+                sc = self.vb._class(_claim_class(pvc))
+                if sc is not None and sc.get("provisioner") == self.PROVISIONER:
+                    out.add(f"{ns}/{claim}-unbound")        # one new volume, identity unknown yet
+        return out
+
+    def _max(self, node: Obj) -> int:
+        env = os.environ.get("KUBE_MAX_PD_VOLS", "")
+        if env.isdigit() and int(env) > 0:
+            return int(env)
+        alloc = ((node.get("status") or {}).get("allocatable") or {}).get(self.ALLOCATABLE)
+        if alloc is not None:
+            return int(O.parse_quantity(alloc))
+        return self._default_max(node)
+
+    def _default_max(self, node: Obj) -> int:
+        return self.DEFAULT_MAX
+
+    def _migrated(self, node_name: str) -> bool:
+        csinode = self._csinodes.lister.get(node_name) if self._csinodes is not None else None
+        if csinode is None:
+            return False
+        return self.PLUGIN in O.annotations(csinode).get(_MIGRATED_ANNOT, "").split(",")
+
+    def pre_filter(self, state, pod):
+        if not (pod.get("spec") or {}).get("volumes"):
+            return Status.skip()
+        ids = self._ids(pod, True)
+        if not ids:
+            return Status.skip()
+        state.write(self._key, ids)
+        return None
+
+    def filter(self, state, pod, node_info):
+        new = state.read(self._key)
+        if not new or self._migrated(node_info.name):
+            return None
+        attached: Set[str] = set()
+        for other in node_info.pods.values():
+            if (other.get("spec") or {}).get("volumes"):
+                attached |= self._ids(other, False)
+        extra = len(new - attached)
+        if extra and len(attached) + extra > self._max(node_info.node):
+            return Status.unschedulable("node(s) exceed max volume count", self.NAME)
+        return None
+
+
+class EBSLimits(_InTreeLimits):
+    NAME = "EBSLimits"
+    VOLUME, ID = "awsElasticBlockStore", "volumeID"
+    PROVISIONER, ALLOCATABLE, PLUGIN = "kubernetes.io/aws-ebs", "attachable-volumes-aws-ebs", "kubernetes.io/aws-ebs"
+    DEFAULT_MAX = 39
+
+    def _default_max(self, node: Obj) -> int:
+        lab = O.labels(node)
+        itype = lab.get("node.kubernetes.io/instance-type") or lab.get("beta.kubernetes.io/instance-type") or ""
+        return 25 if itype and _EBS_NITRO.match(itype) else 39
+
+
+class GCEPDLimits(_InTreeLimits):
+    NAME = "GCEPDLimits"
+    VOLUME, ID = "gcePersistentDisk", "pdName"
+    PROVISIONER, ALLOCATABLE, PLUGIN = "kubernetes.io/gce-pd", "attachable-volumes-gce-pd", "kubernetes.io/gce-pd"
+    DEFAULT_MAX = 16
+
+
+class AzureDiskLimits(_InTreeLimits):
+    NAME = "AzureDiskLimits"
+    VOLUME, ID = "azureDisk", "diskName"
+    PROVISIONER, ALLOCATABLE, PLUGIN = ("kubernetes.io/azure-disk", "attachable-volumes-azure-disk",
+                                        "kubernetes.io/azure-disk")
+    DEFAULT_MAX = 16
+
+
+class CinderLimits(_InTreeLimits):
+    NAME = "CinderLimits"
+    VOLUME, ID = "cinder", "volumeID"
+    PROVISIONER, ALLOCATABLE, PLUGIN = "kubernetes.io/cinder", "attachable-volumes-cinder", "kubernetes.io/cinder"
+    DEFAULT_MAX = 256

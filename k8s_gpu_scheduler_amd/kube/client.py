@@ -25,12 +25,16 @@ NAMESPACED = {"pods": True, "configmaps": True, "events": True, "leases": True,
               "nodes": False, "namespaces": False,
               # storage (kube-scheduler's volume plugins: framework.volume_plugins)
               "persistentvolumeclaims": True, "persistentvolumes": False, "storageclasses": False,
-              "csinodes": False}
+              "csinodes": False,
+              # workload owners (SelectorSpread, ServiceAffinity, PodTopologySpread system defaults)
+              "services": True, "replicationcontrollers": True, "replicasets": True, "statefulsets": True}
 KIND_OF = {"pods": "Pod", "configmaps": "ConfigMap", "events": "Event", "leases": "Lease",
            "nodes": "Node", "namespaces": "Namespace", "persistentvolumeclaims": "PersistentVolumeClaim",
-           "persistentvolumes": "PersistentVolume", "storageclasses": "StorageClass", "csinodes": "CSINode"}
+           "persistentvolumes": "PersistentVolume", "storageclasses": "StorageClass", "csinodes": "CSINode",
+           "services": "Service", "replicationcontrollers": "ReplicationController", "replicasets": "ReplicaSet",
+           "statefulsets": "StatefulSet"}
 API_VERSION_OF = {"leases": "coordination.k8s.io/v1", "storageclasses": "storage.k8s.io/v1",
-                  "csinodes": "storage.k8s.io/v1"}
+                  "csinodes": "storage.k8s.io/v1", "replicasets": "apps/v1", "statefulsets": "apps/v1"}
 
 
 class ApiError(Exception):

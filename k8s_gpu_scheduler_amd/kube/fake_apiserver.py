@@ -18,10 +18,10 @@ from urllib.parse import parse_qs, urlsplit
 from .client import ApiError, FakeCluster
 
 _CORE = re.compile(r"^/api/v1(?:/namespaces/(?P<ns>[^/]+))?/(?P<res>pods|nodes|configmaps|events|namespaces|"
-                   r"persistentvolumeclaims|persistentvolumes)"
+                   r"persistentvolumeclaims|persistentvolumes|services|replicationcontrollers)"
                    r"(?:/(?P<name>[^/]+))?(?:/(?P<sub>binding|status))?$")
-_COORD = re.compile(r"^/apis/(?:coordination\.k8s\.io|storage\.k8s\.io)/v1(?:/namespaces/(?P<ns>[^/]+))?/"
-                    r"(?P<res>leases|storageclasses|csinodes)(?:/(?P<name>[^/]+))?$")
+_COORD = re.compile(r"^/apis/(?:coordination\.k8s\.io|storage\.k8s\.io|apps)/v1(?:/namespaces/(?P<ns>[^/]+))?/"
+                    r"(?P<res>leases|storageclasses|csinodes|replicasets|statefulsets)(?:/(?P<name>[^/]+))?$")
 _PT = {"application/json-patch+json": "json", "application/merge-patch+json": "merge",
        "application/strategic-merge-patch+json": "strategic"}
 

@@ -279,6 +279,18 @@ class SharedInformerFactory:
     def csi_nodes(self) -> Informer:
         return self.informer("csinodes")
 
+    def services(self) -> Informer:
+        return self.informer("services")
+
+    def replication_controllers(self) -> Informer:
+        return self.informer("replicationcontrollers")
+
+    def replica_sets(self) -> Informer:
+        return self.informer("replicasets")
+
+    def stateful_sets(self) -> Informer:
+        return self.informer("statefulsets")
+
     def start(self) -> None:
         for inf in list(self._informers.values()):
             if not inf._synced.is_set() and inf._thread is None and inf._cancel is None:

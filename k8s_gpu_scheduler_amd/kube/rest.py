@@ -31,7 +31,9 @@ SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 GROUP_PATH = {"pods": "/api/v1", "nodes": "/api/v1", "configmaps": "/api/v1", "events": "/api/v1",
               "namespaces": "/api/v1", "leases": "/apis/coordination.k8s.io/v1",
               "persistentvolumeclaims": "/api/v1", "persistentvolumes": "/api/v1",
-              "storageclasses": "/apis/storage.k8s.io/v1", "csinodes": "/apis/storage.k8s.io/v1"}
+              "storageclasses": "/apis/storage.k8s.io/v1", "csinodes": "/apis/storage.k8s.io/v1",
+              "services": "/api/v1", "replicationcontrollers": "/api/v1", "replicasets": "/apis/apps/v1",
+              "statefulsets": "/apis/apps/v1"}
 CLUSTER_SCOPED = {"nodes", "namespaces", "persistentvolumes", "storageclasses", "csinodes"}
 PATCH_CT = {"json": "application/json-patch+json", "merge": "application/merge-patch+json",
             "strategic": "application/strategic-merge-patch+json"}
