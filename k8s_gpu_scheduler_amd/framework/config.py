@@ -80,6 +80,25 @@ class LeaderElection:
 
 
 @dataclass
+class ExtenderConfig:
+    """One `extenders[]` entry (kube-scheduler's HTTP scheduler extenders, called by this
+    scheduler -- framework.extender_client)."""
+    url_prefix: str
+    filter_verb: str = ""
+    prioritize_verb: str = ""
+    bind_verb: str = ""
+    preempt_verb: str = ""
+    weight: int = 1
+    enable_https: bool = False
+    tls_insecure: bool = False
+    tls_ca_file: str = ""
+    http_timeout_s: float = 30.0
+    node_cache_capable: bool = False
+    managed_resources: List[Dict[str, Any]] = field(default_factory=list)
+    ignorable: bool = False
+
+
+@dataclass
 class SchedulerConfig:
     profiles: List[Profile] = field(default_factory=list)
     leader_election: LeaderElection = field(default_factory=LeaderElection)
@@ -87,6 +106,7 @@ class SchedulerConfig:
     percentage_of_nodes_to_score: int = 0
     pod_initial_backoff_s: float = 1.0
     pod_max_backoff_s: float = 10.0
+    extenders: List[ExtenderConfig] = field(default_factory=list)
 
     def profile(self, scheduler_name: str) -> Optional[Profile]:
         for p in self.profiles:
@@ -132,6 +152,8 @@ def parse_config(doc: Dict[str, Any]) -> SchedulerConfig:
     def dur(v: Any, d: float) -> float:
         if v is None:
             return d
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            return float(v) / 1e9              # a bare metav1.Duration number is nanoseconds
         s = str(v)
         if s.endswith("ms"):
             return float(s[:-2]) / 1000
@@ -169,6 +191,29 @@ def parse_config(doc: Dict[str, Any]) -> SchedulerConfig:
         for pc in p.get("pluginConfig") or []:
             prof.plugin_config[pc["name"]] = dict(pc.get("args") or {})
         cfg.profiles.append(prof)
+    ignored_ext: List[str] = []
+    for e in doc.get("extenders") or []:
+        if not e.get("urlPrefix"):
+            raise ValueError("extenders[].urlPrefix is required")
+        w = int(e.get("weight", 1) if e.get("weight") is not None else 1)
+        if e.get("prioritizeVerb") and w <= 0:
+            raise ValueError("extenders[].weight must be positive with a prioritizeVerb")
+        tls = e.get("tlsConfig") or {}
+        managed = list(e.get("managedResources") or [])
+        ignored_ext += [m["name"] for m in managed if m.get("ignoredByScheduler")]
+        cfg.extenders.append(ExtenderConfig(
+            url_prefix=e["urlPrefix"], filter_verb=e.get("filterVerb", ""), prioritize_verb=e.get("prioritizeVerb", ""),
+            bind_verb=e.get("bindVerb", ""), preempt_verb=e.get("preemptVerb", ""), weight=w,
+            enable_https=bool(e.get("enableHTTPS", False)), tls_insecure=bool(tls.get("insecure", False)),
+            tls_ca_file=tls.get("caFile", ""), http_timeout_s=dur(e.get("httpTimeout"), 30.0),
+            node_cache_capable=bool(e.get("nodeCacheCapable", False)), managed_resources=managed,
+            ignorable=bool(e.get("ignorable", False))))
+    if sum(1 for x in cfg.extenders if x.bind_verb) > 1:
+        raise ValueError("only one extender can implement bind")
+    if ignored_ext:         # resources an extender manages are not NodeResourcesFit's to check
+        for prof in cfg.profiles:
+            fit = prof.plugin_config.setdefault("NodeResourcesFit", {})
+            fit["ignoredResources"] = sorted(set(fit.get("ignoredResources") or []) | set(ignored_ext))
     return cfg
 
 

@@ -22,6 +22,7 @@ from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
+from ..api import constants as C
 from ..api import objects as O
 from ..kube.client import KubeClient
 from ..kube.informer import SharedInformerFactory
@@ -153,7 +154,10 @@ class Scheduler:
         # scheduling state reports changed nodes to one change log
         self.changes = ChangeLog()
         self.cache.changes.attach(self.changes)
-        self.fast_path = True
+        # HTTP extenders this scheduler calls (config `extenders:`, framework.extender_client)
+        from .extender_client import HTTPExtender
+        self.extenders = [HTTPExtender(c) for c in getattr(config, "extenders", None) or []]
+        self.fast_path = not self.extenders     # the node-result cache cannot see extender verdicts
         self.fast_min_nodes = 16      # below this the per-cycle signature work costs more than it saves
         self._fast: Dict[str, NodeResultCache] = {}
         for name, fw in self.frameworks.items():
@@ -284,6 +288,10 @@ class Scheduler:
         if nodes:
             self._next_start = (self._next_start + processed) % len(nodes)
         res.evaluated = processed
+        if feasible and self.extenders:
+            feasible, st = self._extender_filter(pod, feasible, failed)
+            if st is not None:
+                return self._fail(pi, fw, state, res, st, t0)
         res.feasible = len(feasible)
         if not feasible:
             nominated, pst = fw.run_post_filter(state, pod, failed)
@@ -302,9 +310,49 @@ class Scheduler:
             scores, st = fw.run_score(state, pod, feasible)
             if not st.ok:
                 return self._fail(pi, fw, state, res, st, t0)
+            if self.extenders:
+                self._extender_prioritize(pod, feasible, scores)
             res.scores = {s.name: s.score for s in scores}
             host = self._select_host(scores)
         return self._assume_and_bind(fw, state, pi, pod, host, res, t0)
+
+    # ---------------------------------------------------------------- extenders
+    def _extender_filter(self, pod: Obj, feasible: List[Any], failed: Dict[str, Status]):
+        """Each interested extender narrows the feasible set in turn; (nodes, error status)."""
+        from .extender_client import ExtenderError
+        for ext in self.extenders:
+            if not feasible:
+                break
+            if not ext.is_interested(pod):
+                continue
+            try:
+                feasible, bad, unresolvable = ext.filter(pod, feasible)
+            except ExtenderError as e:
+                if ext.is_ignorable:
+                    log.warning("skipping ignorable extender: %s", e)
+                    continue
+                return feasible, Status.error(str(e))
+            for name, why in bad.items():
+                failed[name] = Status.unschedulable(why or "rejected by extender", ext.name)
+            for name, why in unresolvable.items():
+                failed[name] = Status.unschedulable(why or "rejected by extender", ext.name, True)
+        return feasible, None
+
+    def _extender_prioritize(self, pod: Obj, feasible: List[Any], scores: List[Any]) -> None:
+        from .extender_client import ExtenderError, MAX_EXTENDER_PRIORITY
+        extra: Dict[str, int] = {}
+        for ext in self.extenders:
+            if not ext.cfg.prioritize_verb or not ext.is_interested(pod):
+                continue
+            try:
+                got = ext.prioritize(pod, feasible)
+            except ExtenderError as e:     # upstream ignores prioritize errors
+                log.warning("extender prioritize failed: %s", e)
+                continue
+            for host, v in got.items():
+                extra[host] = extra.get(host, 0) + v * ext.cfg.weight * (C.MAX_NODE_SCORE // MAX_EXTENDER_PRIORITY)
+        for ns in scores:
+            ns.score += extra.get(ns.name, 0)
 
     def _assume_and_bind(self, fw: Framework, state: CycleState, pi: QueuedPodInfo, pod: Obj, host: str,
                          res: ScheduleResult, t0: float) -> ScheduleResult:
@@ -390,7 +438,15 @@ class Scheduler:
         try:
             st = fw.run_pre_bind(state, pod, host)
             if st.ok:
-                st = fw.run_bind(state, pod, host)
+                binder = next((e for e in self.extenders if e.is_binder and e.is_interested(pod)), None)
+                if binder is not None:
+                    from .extender_client import ExtenderError
+                    try:
+                        binder.bind(pod, host)
+                    except ExtenderError as e:
+                        st = Status.error(str(e))
+                else:
+                    st = fw.run_bind(state, pod, host)
             if not st.ok:
                 fw.run_unreserve(state, pod, host)
                 self.cache.forget_pod(pod)
