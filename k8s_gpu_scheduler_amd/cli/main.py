@@ -30,10 +30,19 @@ from typing import List, Optional
 from ..api import constants as C
 
 
-def _client(kubeconfig: str = "", fake_url: str = ""):
+def _client(kubeconfig: str = "", fake_url: str = "", master: str = ""):
+    """REST client: a fake apiserver URL as is; else the kubeconfig / in-cluster config, with
+    `master` (kube-scheduler's --master) replacing its server address."""
     from ..kube.rest import RestClient, RestConfig
     if fake_url:
         return RestClient(RestConfig(fake_url))
+    if master:
+        try:
+            base = RestClient.auto(kubeconfig).cfg
+        except Exception:
+            return RestClient(RestConfig(master))
+        base.host = master
+        return RestClient(base)
     return RestClient.auto(kubeconfig)
 
 
@@ -90,14 +99,22 @@ def _telemetry_poller(args, cache, prometheus: str):
 
 def cmd_scheduler(args) -> int:
     from ..kube.leader import LeaderElector
-    client = _client(args.kubeconfig, args.fake_apiserver)
+    client = _client(args.kubeconfig, args.fake_apiserver, getattr(args, "master", ""))
     cfg, sched = _build_scheduler(args, client)
+    # kube-scheduler's command-line overrides of the config file
+    if getattr(args, "leader_elect", None) is not None:
+        cfg.leader_election.leader_elect = args.leader_elect
+    if getattr(args, "leader_elect_resource_name", ""):
+        cfg.leader_election.resource_name = args.leader_elect_resource_name
+    if getattr(args, "leader_elect_resource_namespace", ""):
+        cfg.leader_election.resource_namespace = args.leader_elect_resource_namespace
+    http = None
     if args.metrics_port:
-        from ..telemetry.exporter import GpuExporter, attach_scheduler_metrics
+        from ..telemetry.exporter import GpuExporter, SchedulerHTTP, attach_scheduler_metrics
         exp = GpuExporter(os.getenv("NODE_NAME", socket.gethostname()), exporter_pod=os.getenv("POD_NAME", ""))
         attach_scheduler_metrics(exp, sched)
-        exp.serve(args.metrics_port)
-        logging.info("scheduler metrics on :%d/metrics", args.metrics_port)
+        http = SchedulerHTTP(exp, sched, args.metrics_port, getattr(args, "bind_address", "0.0.0.0")).start()
+        logging.info("scheduler /metrics /healthz /livez /readyz on :%d", http.port)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: stop.set())
     if cfg.leader_election.leader_elect:
@@ -125,6 +142,8 @@ def cmd_scheduler(args) -> int:
     if sched.telemetry_poller is not None:
         sched.telemetry_poller.stop()
     sched.stop()
+    if http is not None:
+        http.stop()
     return 0
 
 
@@ -340,8 +359,15 @@ def build_parser() -> argparse.ArgumentParser:
     common(s)
     telemetry(s)
     s.add_argument("--config", default="")
-    s.add_argument("--metrics-port", type=int, default=10251,
-                   help="Prometheus /metrics (pods scheduled, latency, per-extension-point means); 0 = off")
+    s.add_argument("--metrics-port", "--port", type=int, default=10251,
+                   help="HTTP port of /metrics (pods scheduled, latency, per-extension-point means) and "
+                        "/healthz /livez /readyz; 0 = off")
+    s.add_argument("--bind-address", default="0.0.0.0")
+    s.add_argument("--master", default="", help="apiserver URL (overrides the kubeconfig's server)")
+    s.add_argument("--leader-elect", default=None, type=lambda v: str(v).lower() in ("1", "true", "yes"),
+                   help="override the config's leaderElection.leaderElect (true/false)")
+    s.add_argument("--leader-elect-resource-name", default="")
+    s.add_argument("--leader-elect-resource-namespace", default="")
     s.set_defaults(fn=cmd_scheduler)
     s = sub.add_parser("extender")
     common(s)

@@ -137,3 +137,55 @@ def attach_scheduler_metrics(exporter: "GpuExporter", sched, period_s: float = 5
             exporter.observe_scheduler(ext=ext)
     threading.Thread(target=loop, daemon=True, name="sched-metrics").start()
     return stop.set
+
+
+class SchedulerHTTP:
+    """The scheduler's HTTP endpoint (kube-scheduler serves the same paths): /metrics (the
+    exporter's registry), /healthz and /livez (200 while the process serves; 500 once the
+    scheduling loop that was started has died), /readyz (200 once the informer caches have
+    synced and, under leader election, this replica leads or stands by -- 503 before)."""
+
+    def __init__(self, exporter: "GpuExporter", sched, port: int, addr: str = "0.0.0.0"):
+        import threading
+        from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+        outer = self
+        self.exporter, self.sched = exporter, sched
+
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                path = self.path.split("?", 1)[0].rstrip("/")
+                if path == "/metrics":
+                    code, ctype, body = 200, "text/plain; version=0.0.4", outer.exporter.render()
+                elif path in ("/healthz", "/livez", "/readyz"):
+                    ok = outer.ready() if path == "/readyz" else outer.alive()
+                    code, ctype, body = (200 if ok else (503 if path == "/readyz" else 500)), "text/plain", \
+                        (b"ok" if ok else b"not ok")
+                else:
+                    code, ctype, body = 404, "text/plain", b"not found"
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+        self.server = ThreadingHTTPServer((addr, port), H)
+        self.port = self.server.server_address[1]
+        self._thread = threading.Thread(target=self.server.serve_forever, daemon=True, name="sched-http")
+
+    def alive(self) -> bool:
+        t = getattr(self.sched, "_thread", None)
+        stopped = getattr(self.sched, "_stop", None)
+        return t is None or t.is_alive() or (stopped is not None and stopped.is_set())
+
+    def ready(self) -> bool:
+        return bool(getattr(self.sched, "_started", False)) and self.alive()
+
+    def start(self) -> "SchedulerHTTP":
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self.server.shutdown()
+        self.server.server_close()

@@ -110,3 +110,42 @@ def test_scheduler_metrics_exporter():
     assert 'gpusched_pods_scheduled_total{result="unschedulable"} 1.0' in txt
     assert "gpusched_scheduling_latency_seconds_count 3.0" in txt
     assert 'gpusched_extension_point_mean_us{point="score"}' in txt
+
+
+def test_scheduler_http_endpoint_health_and_metrics():
+    """kube-scheduler's serving paths: /metrics, /healthz, /livez, /readyz (ready once the
+    informer caches synced; liveness fails when the started scheduling loop died)."""
+    import urllib.error
+    import urllib.request
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+    from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.plugins import full_registry
+    from k8s_gpu_scheduler_amd.telemetry.exporter import GpuExporter, SchedulerHTTP, attach_scheduler_metrics
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n", gpus=1))
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False)
+    exp = GpuExporter("n")
+    stop = attach_scheduler_metrics(exp, s, period_s=0.05)
+    http = SchedulerHTTP(exp, s, 0, "127.0.0.1").start()
+
+    def get(path):
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{http.port}{path}", timeout=5) as r:
+                return r.status, r.read().decode()
+        except urllib.error.HTTPError as e:
+            return e.code, ""
+    try:
+        assert get("/healthz") == (200, "ok") and get("/livez")[0] == 200
+        assert get("/readyz")[0] == 503                     # informers not synced yet
+        s.start_informers()
+        assert get("/readyz") == (200, "ok")
+        fc.create("pods", O.make_pod("p0", gpu_cu=64))
+        s.schedule_pending()
+        code, body = get("/metrics")
+        assert code == 200 and 'gpusched_pods_scheduled_total{result="scheduled"} 1.0' in body
+        assert get("/nope")[0] == 404
+    finally:
+        stop()
+        http.stop()
