@@ -10,7 +10,6 @@ CycleState, Reserve/Unreserve, Permit, PreBind/Bind/PostBind.
 from __future__ import annotations
 
 import enum
-import threading
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
 

@@ -20,7 +20,7 @@ default constraints (score_plugins.PodTopologySpreadScore).
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Dict, List, Optional
 
 from ..api import objects as O
 from ..kube.patch import match_label_selector

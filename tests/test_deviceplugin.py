@@ -4,7 +4,6 @@ steers whole-GPU allocations to the scheduler's choice and returns each containe
 assignment the scheduler recorded on its pod."""
 import os
 import tempfile
-import threading
 from concurrent import futures
 
 import grpc
