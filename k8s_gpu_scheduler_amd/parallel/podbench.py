@@ -471,6 +471,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="--gpus N > 1 outside torchrun: 'auto' spawns N rank processes on GPU hosts and "
                          "simulates N GPUs in one process with --sim; 'spawn' always spawns (gloo ranks "
                          "with --sim); 'inline' never spawns")
+    ap.add_argument("--xcd-blocks", type=int, default=1, choices=[0, 1],
+                    help="GEMM tile order: each XCD takes a near-square block of output tiles (1) or a "
+                         "tall GROUP_M strip (0)")
     ap.add_argument("--gemm-share", type=int, default=1, choices=[0, 1],
                     help="1: the GEMM tile picker sizes a pod's GEMMs for its CU share (co-running pods fill the "
                          "rest); 0: for the whole chip")
@@ -550,6 +553,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         from .. import _native
         _native.hip(required=True).set_gemm_policy(a.gemm_policy)
         _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
+        _native.hip(required=True).set_xcd_blocks(a.xcd_blocks)
         _native.hip(required=True).set_triad_variant(a.triad_variant)
         ex.triad_blocks = a.triad_blocks
         ex.gemm_share = bool(a.gemm_share)

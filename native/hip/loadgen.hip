@@ -33,6 +33,40 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 
+// Block index -> output tile.  Workgroup b runs on XCD b % 8 (round-robin dispatch), so the
+// XCD-aware bijective remap first makes each XCD's workgroups one contiguous range of wgid.
+// xmap = 0: GROUP_M-row grouped order over the whole grid (an XCD's range is a tall 8-row
+// strip of tiles).  xmap = px > 0: the tile grid is cut into px x (8 / px) equal rectangles,
+// XCD x walks rectangle x (4-row grouped order inside), so the A row-strips and B column-strips
+// one XCD's L2 has to fetch are those of a near-square block: on the co-run catalog shapes
+// 18-33 % fewer strips per XCD than the tall strip (pick_xcd_map; the host only passes px when
+// both dimensions divide and the grid is a multiple of 8).
+__device__ __forceinline__ void tile_coords(int b, int nwg, int tiles_m, int tiles_n, int xmap, int& tm, int& tn) {
+  const int xcd = b % kXcds;
+  const int q = nwg / kXcds, rem = nwg % kXcds;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
+  if (xmap > 0) {
+    const int py = kXcds / xmap;
+    const int bm = tiles_m / xmap, bn = tiles_n / py;
+    const int per = bm * bn;
+    const int x = wgid / per, l = wgid - x * per;
+    constexpr int GM = 4;
+    const int per_group = GM * bn;
+    const int g = l / per_group;
+    const int gsize = min(bm - g * GM, GM);
+    const int r = l - g * per_group;
+    tm = (x / py) * bm + g * GM + r % gsize;
+    tn = (x % py) * bn + r / gsize;
+    return;
+  }
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  tm = first_m + (wgid % per_group) % gsize;
+  tn = (wgid % per_group) / gsize;
+}
+
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
@@ -121,7 +155,7 @@ template <int BM, int BN, int WGM, int WGN, int OCC, bool RELU, bool BIAS, int S
           bool HOIST = false, bool WIDE = false>
 __global__ void __launch_bounds__(WGM * WGN * 64, OCC)
 gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
-                    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+                    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
   constexpr int NT = WGM * WGN * 64;
   static_assert(KT == 32 || KT == 64, "K tile");
   constexpr int A_BYTES = BM * KT * 2, B_BYTES = BN * KT * 2;
@@ -132,19 +166,9 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   constexpr int LOADS = (BM + BN) * KT * 2 / 16 / NT;    // glds per thread per K-tile
   __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
 
-  // ---- XCD-aware bijective remap, then grouped (GROUP_M) tile order ----------------
-  const int nwg = gridDim.x;
-  const int b = blockIdx.x;
-  const int xcd = b % kXcds;
-  const int q = nwg / kXcds, rem = nwg % kXcds;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
-  const int tiles_m = M / BM, tiles_n = N / BN;
-  const int per_group = GROUP_M * tiles_n;
-  const int group = wgid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (wgid % per_group) % gsize;
-  const int tn = (wgid % per_group) / gsize;
+  // ---- XCD-aware tile order (tile_coords) -------------------------------------------
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, M / BM, N / BN, xmap, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -428,7 +452,7 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 template <bool RELU, bool BIAS, bool PEEL = false, bool WIDE = false, bool SPLIT = false>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
-                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc,
+                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap,
                      float* __restrict__ ws = nullptr) {
   constexpr int HALF = 128 * 64 * 2;               // bytes of one half-tile image
   constexpr int BUF = 4 * HALF;                    // one K-tile: A0 A1 B0 B1
@@ -445,16 +469,9 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     A += (size_t)split * K;
     Bt += (size_t)split * K;
   }
-  const int xcd = b % kXcds;
-  const int q = nwg / kXcds, rem = nwg % kXcds;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
-  const int tiles_m = M / 256, tiles_n = N / 256;
-  const int per_group = GROUP_M * tiles_n;
-  const int group = wgid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int m0 = (first_m + (wgid % per_group) % gsize) * 256;
-  const int n0 = ((wgid % per_group) / gsize) * 256;
+  int tm, tn;
+  tile_coords(b, nwg, M / 256, N / 256, xmap, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x & (kWave - 1);
@@ -749,18 +766,39 @@ template <int BM, int BN, int WGM, int WGN, int OCC, int STAGES, int KT, bool HO
 static void launch_gemm_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                           int ldb, int ldc, bool relu, hipStream_t s) {
   const dim3 grid((M / BM) * (N / BN)), block(WGM * WGN * 64);
+  const int xmap = pick_xcd_map(M / BM, N / BN);
   if (relu && bp)
     hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, true, STAGES, KT, HOIST, WIDE>), grid, block, 0, s,
-                       A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+                       A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (relu)
     hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, true, false, STAGES, KT, HOIST, WIDE>), grid, block, 0,
-                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (bp)
     hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, true, STAGES, KT, HOIST, WIDE>), grid, block, 0,
-                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else
     hipLaunchKernelGGL((gemm_bf16_nt_kernel<BM, BN, WGM, WGN, OCC, false, false, STAGES, KT, HOIST, WIDE>), grid, block, 0,
-                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+                       s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+}
+
+// XCD-block tile order (tile_coords): 1 = on (px chosen per grid), 0 = the GROUP_M order over
+// the whole grid (A/B knob).
+static int g_xcd_blocks = 1;
+
+void set_xcd_blocks(int on) { g_xcd_blocks = on ? 1 : 0; }
+
+// px (XCD-block rows, 8 / px columns) minimising the strips one XCD fetches, A rows + B
+// columns of its block, among the splits that divide the grid; 0 = none (legacy order).
+int pick_xcd_map(int tiles_m, int tiles_n) {
+  if (!g_xcd_blocks || (tiles_m * tiles_n) % kXcds) return 0;
+  int best = 0, best_cost = 1 << 30;
+  for (int px = 1; px <= kXcds; px *= 2) {
+    const int py = kXcds / px;
+    if (tiles_m % px || tiles_n % py) continue;
+    const int cost = tiles_m / px + tiles_n / py;
+    if (cost < best_cost) best = px, best_cost = cost;
+  }
+  return best;
 }
 
 // Wide (LDS-staged, 16-B row stores) epilogue whenever C rows are 16-B aligned; g_wide_epi = 0
@@ -785,14 +823,15 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
 template <bool PEEL, bool WIDE>
 static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                          int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
+  const int xmap = pick_xcd_map(M / 256, N / 256);
   if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
 }
 
 // tile 9 = the original 8-phase kernel; 10 = peeled steady-state loop + wide LDS-staged
@@ -912,7 +951,7 @@ static void launch_splitk(const __bf16* A, const __bf16* B, __bf16* Cp, const fl
                           int N, int K, int lda, int ldb, int ldc, hipStream_t s) {
   const dim3 grid((M / 256) * (N / 256) * S), block(512);
   hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, true, false, true>), grid, block, 0, s, A, B, Cp, bp, M, N,
-                     K / S, lda, ldb, ldc, ws);
+                     K / S, lda, ldb, ldc, 0, ws);
   const size_t n4 = (size_t)M * N / 4;
   const int rblocks = (int)std::min<size_t>((n4 + 255) / 256, 8192);
   hipLaunchKernelGGL((splitk_reduce<RELU, BIAS>), dim3(rblocks), dim3(256), 0, s, ws, S, M, N, bp, Cp, ldc);

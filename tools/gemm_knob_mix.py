@@ -1,6 +1,8 @@
-"""Wide vs scattered GEMM epilogue on the catalog GEMM shapes: each shape alone (auto tile,
-whole chip) and the bench's co-run setting (4 streams, every pod's GEMMs with a 64-CU
-budget), interleaved rounds in one process, uniform [-1, 1) operands, bias + ReLU."""
+"""A/B of a 0/1 GEMM launch knob of the native module (default set_wide_epilogue; argv[1] names
+another, e.g. set_xcd_blocks) on the catalog GEMM shapes: each shape alone (auto tile, whole
+chip) and the bench's co-run setting (4 streams, every pod's GEMMs with a 64-CU budget),
+interleaved rounds in one process, uniform [-1, 1) operands, bias + ReLU.  Lone big shapes
+(4096^3, 8192^3, 8192x8192x2048) are included with argv[2] = "big"."""
 import json
 import os
 import sys
@@ -16,9 +18,12 @@ from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
 
 def main():
     h = _native.hip(required=True)
+    knob = sys.argv[1] if len(sys.argv) > 1 else "set_wide_epilogue"
+    setk = getattr(h, knob)
     shapes = sorted({(o.M, o.N, o.K) for w in W.CATALOG.values() for o in w.ops if o.kind == "gemm"})
+    big = [(4096, 4096, 4096), (8192, 8192, 8192), (8192, 8192, 2048)] if "big" in sys.argv[2:] else []
     bufs = {}
-    for (M, N, K) in shapes:
+    for (M, N, K) in shapes + big:
         bufs[(M, N, K)] = ((torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16),
                            (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16),
                            torch.randn(N, device="cuda"), torch.empty(M, N, device="cuda", dtype=torch.bfloat16))
@@ -58,15 +63,16 @@ def main():
     res = {"lone": {}, "mix": {0: [], 1: []}}
     for rnd in range(3):
         for w in (0, 1):
-            h.set_wide_epilogue(w)
+            setk(w)
             res["mix"][w].append(round(mix(), 1))
-            for shape in shapes:
+            for shape in shapes + big:
                 res["lone"].setdefault(str(shape), {0: [], 1: []})[w].append(round(lone(shape), 1))
-    h.set_wide_epilogue(1)
+    setk(1)
     summ = {"mix_tflops": {str(w): sorted(v)[1] for w, v in res["mix"].items()},
             "lone_tflops_median": {k: {str(w): sorted(v)[1] for w, v in d.items()} for k, d in res["lone"].items()}}
     os.makedirs("gpurun_out", exist_ok=True)
-    json.dump({"raw": res, "summary": summ}, open("gpurun_out/wide_epi_mix.json", "w"), indent=1)
+    json.dump({"knob": knob, "raw": res, "summary": summ},
+              open(f"gpurun_out/{knob.replace('set_', '')}_mix.json", "w"), indent=1)
     print(json.dumps(summ))
 
 

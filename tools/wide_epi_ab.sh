@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 timeout -k 10 200 python -u -m pytest tests/test_gpu_native.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "gemm" > gpurun_out/gemm_test.log 2>&1 || exit $?
 tail -1 gpurun_out/gemm_test.log
-timeout -k 10 300 python -u tools/wide_epi_mix.py > gpurun_out/wide_epi_mix.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/gemm_knob_mix.py > gpurun_out/wide_epi_mix.log 2>&1 || exit $?
 cat gpurun_out/wide_epi_mix.log
 for i in 1 2 3; do
   for w in 0 1; do
