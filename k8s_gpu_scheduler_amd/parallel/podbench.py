@@ -490,6 +490,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
+    ap.add_argument("--triad-aux", type=int, default=2, choices=(0, 1, 2, 3, 16, 17, 18, 19),
+                    help="cache-policy bits of --triad-variant 5 (buffer instructions): sc0 1, nt 2, sc1 16")
     ap.add_argument("--triad-variant", type=int, default=6, choices=range(7),
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
@@ -555,6 +557,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
         _native.hip(required=True).set_xcd_blocks(a.xcd_blocks)
         _native.hip(required=True).set_triad_variant(a.triad_variant)
+        _native.hip(required=True).set_triad_aux(a.triad_aux)
         ex.triad_blocks = a.triad_blocks
         ex.gemm_share = bool(a.gemm_share)
     else:

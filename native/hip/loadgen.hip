@@ -748,6 +748,49 @@ __global__ void __launch_bounds__(256) stream_triad_u(float4* __restrict__ a_, c
   }
 }
 
+// Buffer-instruction variant with an explicit cache policy (AUX = the gfx950 CPol bits of the
+// raw buffer builtins: 1 = sc0, 2 = nt, 16 = sc1): the study of how the co-running streams'
+// lines share the XCD L2 and the MALL with the GEMMs' operand strips (variant 5 + aux).
+// Buffer byte offsets are 32-bit: arrays up to 4 GiB (checked on the host).
+template <int U, int AUX>
+__global__ void __launch_bounds__(256) stream_triad_buf(float4* __restrict__ a_, const float4* __restrict__ b_,
+                                                        const float4* __restrict__ c_, float s, size_t n4) {
+  const unsigned bytes = (unsigned)(n4 * 16);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(a_, 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)b_, 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)c_, 0, bytes, 0x00020000);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const size_t tile = (size_t)blockDim.x * U;
+  const size_t step = (size_t)gridDim.x * tile;
+  for (size_t base = (size_t)blockIdx.x * tile + threadIdx.x; base < n4; base += step) {
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const size_t i = base + (size_t)k * blockDim.x;
+      if (i < n4) {
+        x[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)(i * 16), 0, AUX));
+        y[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (unsigned)(i * 16), 0, AUX));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const size_t i = base + (size_t)k * blockDim.x;
+      if (i < n4) {
+        const f32x4 r = x[k] + s * y[k];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), ra, (unsigned)(i * 16), 0, AUX);
+      }
+    }
+  }
+}
+
+static int g_triad_aux = 2;
+
+void set_triad_aux(int aux) {
+  if (aux != 0 && aux != 1 && aux != 2 && aux != 3 && aux != 16 && aux != 17 && aux != 18 && aux != 19)
+    throw std::runtime_error("triad aux must be a combination of sc0 (1), nt (2), sc1 (16)");
+  g_triad_aux = aux;
+}
+
 // 6 = auto: working set (3 arrays) <= 96 MiB -> cached 2x-unrolled loads (the stream
 // stays in the 256 MiB Infinity Cache across iterations: 7.1 TB/s measured), larger ->
 // non-temporal 4x (6.5 TB/s vs 6.1 for torch.add) -- profiles/r01_kernel_bench.json.
@@ -1071,6 +1114,16 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
     case 2: hipLaunchKernelGGL((stream_triad_u<4, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 3: hipLaunchKernelGGL((stream_triad_u<4, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 4: hipLaunchKernelGGL((stream_triad_u<8, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 5: {
+      if (n_floats * 4 > 0xFFFFFFFFull) throw std::runtime_error("triad variant 5: arrays above 4 GiB");
+#define GS_TRIAD_BUF(X) case X: hipLaunchKernelGGL((stream_triad_buf<4, X>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+      switch (g_triad_aux) {
+        GS_TRIAD_BUF(0) GS_TRIAD_BUF(1) GS_TRIAD_BUF(2) GS_TRIAD_BUF(3)
+        GS_TRIAD_BUF(16) GS_TRIAD_BUF(17) GS_TRIAD_BUF(18) GS_TRIAD_BUF(19)
+      }
+#undef GS_TRIAD_BUF
+      break;
+    }
     default: hipLaunchKernelGGL((stream_triad_u<2, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
   }
   HIP_CHECK(hipGetLastError());

@@ -205,6 +205,28 @@ def test_triad_matches_reference():
     torch.testing.assert_close(a, b + 2.5 * c)
 
 
+def test_triad_variants_and_cache_policies_match_reference():
+    """Every stream-kernel variant, incl. the buffer-instruction one under each cache policy,
+    on a length that leaves a partial unrolled trip (fp32 reference b + s*c)."""
+    from k8s_gpu_scheduler_amd import _native
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    h = _native.hip(required=True)
+    n = (1 << 20) + 4 * 123
+    b, c = torch.rand(n, device="cuda"), torch.rand(n, device="cuda")
+    ref = b + 1.5 * c
+    try:
+        for v in range(7):
+            h.set_triad_variant(v)
+            for aux in ((2, 0, 18, 19) if v == 5 else (2,)):
+                h.set_triad_aux(aux)
+                a = torch.full_like(b, -1.0)
+                loadgen.triad(a, b, c, 1.5)
+                torch.testing.assert_close(a, ref, msg=f"variant {v} aux {aux}")
+    finally:
+        h.set_triad_variant(6)
+        h.set_triad_aux(2)
+
+
 def test_cu_mask_slices_map_to_all_xccs():
     """A 2-word mask = 64 CUs = 8 CUs on each of the 8 XCCs (measured mapping)."""
     from k8s_gpu_scheduler_amd.ops.cumask import probe_xcd_map
