@@ -36,8 +36,8 @@ constexpr int GROUP_M = 8;
 // Block index -> output tile.  Workgroup b runs on XCD b % 8 (round-robin dispatch), so the
 // XCD-aware bijective remap first makes each XCD's workgroups one contiguous range of wgid.
 // xmap = 0: GROUP_M-row grouped order over the whole grid (an XCD's range is a tall 8-row
-// strip of tiles).  xmap = px > 0: the tile grid is cut into px x (8 / px) equal rectangles,
-// XCD x walks rectangle x (4-row grouped order inside), so the A row-strips and B column-strips
+// strip of tiles).  xmap = px | (gm << 8): the tile grid is cut into px x (8 / px) equal
+// rectangles, XCD x walks rectangle x (gm-row grouped order inside), so the A row-strips and B column-strips
 // one XCD's L2 has to fetch are those of a near-square block: on the co-run catalog shapes
 // 18-33 % fewer strips per XCD than the tall strip (pick_xcd_map; the host only passes px when
 // both dimensions divide and the grid is a multiple of 8).
@@ -46,11 +46,11 @@ __device__ __forceinline__ void tile_coords(int b, int nwg, int tiles_m, int til
   const int q = nwg / kXcds, rem = nwg % kXcds;
   const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
   if (xmap > 0) {
-    const int py = kXcds / xmap;
-    const int bm = tiles_m / xmap, bn = tiles_n / py;
+    const int px = xmap & 0xFF, GM = xmap >> 8;     // bands, rows per group inside the block
+    const int py = kXcds / px;
+    const int bm = tiles_m / px, bn = tiles_n / py;
     const int per = bm * bn;
     const int x = wgid / per, l = wgid - x * per;
-    constexpr int GM = 4;
     const int per_group = GM * bn;
     const int g = l / per_group;
     const int gsize = min(bm - g * GM, GM);
@@ -827,8 +827,14 @@ static void launch_gemm_v(const __bf16* A, const __bf16* B, __bf16* Cp, const fl
 // XCD-block tile order (tile_coords): 1 = on (px chosen per grid), 0 = the GROUP_M order over
 // the whole grid (A/B knob).
 static int g_xcd_blocks = 1;
+static int g_xcd_group = 4;         // tile rows per group inside an XCD block
 
 void set_xcd_blocks(int on) { g_xcd_blocks = on ? 1 : 0; }
+
+void set_xcd_group(int rows) {
+  if (rows < 1 || rows > 64) throw std::runtime_error("xcd group rows must be 1..64");
+  g_xcd_group = rows;
+}
 
 // px (XCD-block rows, 8 / px columns) minimising the strips one XCD fetches, A rows + B
 // columns of its block, among the splits that divide the grid; 0 = none (legacy order).
@@ -841,7 +847,7 @@ int pick_xcd_map(int tiles_m, int tiles_n) {
     const int cost = tiles_m / px + tiles_n / py;
     if (cost < best_cost) best = px, best_cost = cost;
   }
-  return best;
+  return best ? best | (g_xcd_group << 8) : 0;
 }
 
 // Wide (LDS-staged, 16-B row stores) epilogue whenever C rows are 16-B aligned; g_wide_epi = 0

@@ -6,11 +6,11 @@ def _tile_coords(b, nwg, tiles_m, tiles_n, xmap, xcds=8):
     q, rem = divmod(nwg, xcds)
     wgid = (xcd * (q + 1) if xcd < rem else rem * (q + 1) + (xcd - rem) * q) + b // xcds
     if xmap > 0:
-        py = xcds // xmap
-        bm, bn = tiles_m // xmap, tiles_n // py
+        px, gm = xmap & 0xFF, xmap >> 8
+        py = xcds // px
+        bm, bn = tiles_m // px, tiles_n // py
         per = bm * bn
         x, l = divmod(wgid, per)
-        gm = 4
         g, r = divmod(l, gm * bn)
         gsize = min(bm - g * gm, gm)
         return (x // py) * bm + g * gm + r % gsize, (x % py) * bn + r // gsize, x
@@ -38,6 +38,7 @@ def test_gemm_xcd_block_tile_map_is_a_bijection():
             tm_, tn_ = M // bt, N // bt
             nwg = tm_ * tn_
             xmap = h.pick_xcd_map(tm_, tn_)
+            assert xmap == 0 or xmap >> 8 == 4
             seen, strips_new, strips_old = set(), {}, {}
             for b in range(nwg):
                 m, n, x = _tile_coords(b, nwg, tm_, tn_, xmap)
