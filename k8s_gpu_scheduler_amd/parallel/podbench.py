@@ -475,6 +475,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="GEMM tile order: each XCD takes a near-square block of output tiles (1) or a "
                          "tall GROUP_M strip (0)")
     ap.add_argument("--xcd-group", type=int, default=4, help="tile rows per group inside an XCD block")
+    ap.add_argument("--c-nt", type=int, default=0, choices=[0, 1], help="study: non-temporal GEMM output stores")
     ap.add_argument("--gemm-share", type=int, default=1, choices=[0, 1],
                     help="1: the GEMM tile picker sizes a pod's GEMMs for its CU share (co-running pods fill the "
                          "rest); 0: for the whole chip")
@@ -558,6 +559,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
         _native.hip(required=True).set_xcd_blocks(a.xcd_blocks)
         _native.hip(required=True).set_xcd_group(a.xcd_group)
+        _native.hip(required=True).set_c_nontemporal(a.c_nt)
         _native.hip(required=True).set_triad_variant(a.triad_variant)
         _native.hip(required=True).set_triad_aux(a.triad_aux)
         ex.triad_blocks = a.triad_blocks

@@ -45,8 +45,8 @@ __device__ __forceinline__ void tile_coords(int b, int nwg, int tiles_m, int til
   const int xcd = b % kXcds;
   const int q = nwg / kXcds, rem = nwg % kXcds;
   const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / kXcds;
-  if (xmap > 0) {
-    const int px = xmap & 0xFF, GM = xmap >> 8;     // bands, rows per group inside the block
+  if (xmap & 0xFF) {
+    const int px = xmap & 0xFF, GM = (xmap >> 8) & 0xFF;     // bands, rows per group inside the block
     const int py = kXcds / px;
     const int bm = tiles_m / px, bn = tiles_n / py;
     const int per = bm * bn;
@@ -138,7 +138,8 @@ __device__ __forceinline__ void wide_put(char* img, int row, int col, bf16x4 o) 
 }
 
 template <int BM, int BN, int NT>
-__device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__ C, int ldc, int m0, int n0) {
+__device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__ C, int ldc, int m0, int n0,
+                                           bool nt = false) {
   constexpr int MASK = (BN / 8 - 1) < 15 ? (BN / 8 - 1) : 15;
   constexpr int CPR = BN / 8;                           // 16-B chunks per row
   static_assert(BM * CPR % NT == 0, "wide epilogue split");
@@ -147,7 +148,11 @@ __device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__
     const int id = k * NT + (int)threadIdx.x;
     const int row = id / CPR, c = id % CPR;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * (BN * 2) + ((c ^ (row & MASK)) << 4));
-    *reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8) = v;
+    bf16x8* dst = reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8);
+    if (nt)                                             // xmap bit 16: streaming C stores (study)
+      __builtin_nontemporal_store(v, dst);
+    else
+      *dst = v;
   }
 }
 
@@ -284,7 +289,7 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
       }
     }
     __syncthreads();
-    wide_store<BM, BN, NT>(smem, C, ldc, m0, n0);
+    wide_store<BM, BN, NT>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
     return;
   }
 
@@ -651,7 +656,7 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
           }
       }
     __syncthreads();
-    wide_store<256, 256, 512>(smem, C, ldc, m0, n0);
+    wide_store<256, 256, 512>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
     return;
   }
 
@@ -828,6 +833,9 @@ static void launch_gemm_v(const __bf16* A, const __bf16* B, __bf16* Cp, const fl
 // the whole grid (A/B knob).
 static int g_xcd_blocks = 1;
 static int g_xcd_group = 4;         // tile rows per group inside an XCD block
+static int g_c_nt = 0;              // study: non-temporal C stores in the wide epilogue
+
+void set_c_nontemporal(int on) { g_c_nt = on ? 1 : 0; }
 
 void set_xcd_blocks(int on) { g_xcd_blocks = on ? 1 : 0; }
 
@@ -839,7 +847,8 @@ void set_xcd_group(int rows) {
 // px (XCD-block rows, 8 / px columns) minimising the strips one XCD fetches, A rows + B
 // columns of its block, among the splits that divide the grid; 0 = none (legacy order).
 int pick_xcd_map(int tiles_m, int tiles_n) {
-  if (!g_xcd_blocks || (tiles_m * tiles_n) % kXcds) return 0;
+  const int flags = g_c_nt << 16;
+  if (!g_xcd_blocks || (tiles_m * tiles_n) % kXcds) return flags;
   int best = 0, best_cost = 1 << 30;
   for (int px = 1; px <= kXcds; px *= 2) {
     const int py = kXcds / px;
@@ -847,7 +856,7 @@ int pick_xcd_map(int tiles_m, int tiles_n) {
     const int cost = tiles_m / px + tiles_n / py;
     if (cost < best_cost) best = px, best_cost = cost;
   }
-  return best ? best | (g_xcd_group << 8) : 0;
+  return (best ? best | (g_xcd_group << 8) : 0) | flags;
 }
 
 // Wide (LDS-staged, 16-B row stores) epilogue whenever C rows are 16-B aligned; g_wide_epi = 0

@@ -5,8 +5,8 @@ def _tile_coords(b, nwg, tiles_m, tiles_n, xmap, xcds=8):
     xcd = b % xcds
     q, rem = divmod(nwg, xcds)
     wgid = (xcd * (q + 1) if xcd < rem else rem * (q + 1) + (xcd - rem) * q) + b // xcds
-    if xmap > 0:
-        px, gm = xmap & 0xFF, xmap >> 8
+    if xmap & 0xFF:
+        px, gm = xmap & 0xFF, (xmap >> 8) & 0xFF
         py = xcds // px
         bm, bn = tiles_m // px, tiles_n // py
         per = bm * bn
