@@ -96,6 +96,26 @@ __device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld,
   }
 }
 
+// ---- XCD confinement (study) -------------------------------------------------------------
+// A pod's kernel may be confined to a set of XCDs (8-bit mask): workgroups dispatched to other
+// XCDs exit at once (round-robin dispatch puts block b on XCD b % 8 -- xcd_probe_kernel checks
+// it on the box), the rest share the work, so the pod's GEMM operand strips live in only its
+// own XCDs' L2s -- a software QPX partition.
+__device__ __forceinline__ int xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xF; }
+
+__global__ void xcd_probe_kernel(int* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = xcc_id();
+}
+
+// confined block -> (participant index, participants), -1 when this block sits out
+__device__ __forceinline__ int xcd_part(int xmask, int& nparts) {
+  const int slot = blockIdx.x % kXcds;
+  const int nx = __popc(xmask);
+  nparts = (gridDim.x / kXcds) * nx;
+  if (!((xmask >> slot) & 1)) return -1;
+  return (blockIdx.x / kXcds) * nx + __popc(xmask & ((1 << slot) - 1));
+}
+
 template <int KT = BK>
 __device__ __forceinline__ bf16x8 lds_frag(const char* lds_tile, int row, int kchunk) {
   const int phys = kchunk ^ ((row >> 1) & (KT / 8 - 1));
@@ -475,7 +495,23 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     Bt += (size_t)split * K;
   }
   int tm, tn;
-  tile_coords(b, nwg, M / 256, N / 256, xmap, tm, tn);
+  const int xmask = (xmap >> 24) & 0xFF;
+  if (xmask) {
+    // confined: allowed XCD r (rank among the mask) takes row band r of the tile grid (host:
+    // tiles_m % popcount(mask) == 0, grid = 8 x band tiles), GROUP_M-grouped inside
+    const int slot = b % kXcds;
+    if (!((xmask >> slot) & 1)) return;
+    const int nx = __popc(xmask), rank = __popc(xmask & ((1 << slot) - 1));
+    const int tiles_n = N / 256, band = (M / 256) / nx;
+    const int l = b / kXcds;
+    if (l >= band * tiles_n) return;
+    const int per_group = 4 * tiles_n;
+    const int g = l / per_group, gsize = min(band - g * 4, 4), r = l - g * per_group;
+    tm = rank * band + g * 4 + r % gsize;
+    tn = r / gsize;
+  } else {
+    tile_coords(b, nwg, M / 256, N / 256, xmap, tm, tn);
+  }
   const int m0 = tm * 256, n0 = tn * 256;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -788,7 +824,48 @@ __global__ void __launch_bounds__(256) stream_triad_buf(float4* __restrict__ a_,
   }
 }
 
+template <int U>
+__global__ void __launch_bounds__(256) stream_triad_xcd(float4* __restrict__ a_, const float4* __restrict__ b_,
+                                                        const float4* __restrict__ c_, float s, size_t n4, int xmask) {
+  int nparts;
+  const int part = xcd_part(xmask, nparts);
+  if (part < 0) return;
+  auto a = reinterpret_cast<f32x4*>(a_);
+  auto b = reinterpret_cast<const f32x4*>(b_);
+  auto c = reinterpret_cast<const f32x4*>(c_);
+  const size_t tile = (size_t)blockDim.x * U;
+  const size_t step = (size_t)nparts * tile;
+  for (size_t base = (size_t)part * tile + threadIdx.x; base < n4; base += step) {
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const size_t i = base + (size_t)k * blockDim.x;
+      if (i < n4) {
+        x[k] = __builtin_nontemporal_load(b + i);
+        y[k] = __builtin_nontemporal_load(c + i);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const size_t i = base + (size_t)k * blockDim.x;
+      if (i < n4) __builtin_nontemporal_store(x[k] + s * y[k], a + i);
+    }
+  }
+}
+
 static int g_triad_aux = 2;
+static int g_xcd_mask = 0;          // study: confine GEMMs / stream kernels to these XCDs (0 = all)
+
+void set_xcd_mask(int mask) {
+  if (mask < 0 || mask > 0xFF) throw std::runtime_error("xcd mask must be 8 bits");
+  g_xcd_mask = mask == 0xFF ? 0 : mask;
+}
+
+void xcd_probe(uintptr_t out, int blocks, uintptr_t stream) {
+  hipLaunchKernelGGL(xcd_probe_kernel, dim3(blocks), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<int*>(out));
+  HIP_CHECK(hipGetLastError());
+}
 
 void set_triad_aux(int aux) {
   if (aux != 0 && aux != 1 && aux != 2 && aux != 3 && aux != 16 && aux != 17 && aux != 18 && aux != 19)
@@ -881,7 +958,13 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
 template <bool PEEL, bool WIDE>
 static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                          int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
-  const int xmap = pick_xcd_map(M / 256, N / 256);
+  int xmap = pick_xcd_map(M / 256, N / 256);
+  if (g_xcd_mask) {
+    const int nx = __builtin_popcount(g_xcd_mask);
+    if ((M / 256) % nx) throw std::runtime_error("xcd-confined GEMM: tile rows must divide by the XCD count");
+    xmap = (xmap & 0x10000) | (g_xcd_mask << 24);
+    grid = dim3(kXcds * ((M / 256) / nx) * (N / 256));
+  }
   if (relu && bp)
     hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (relu)
@@ -1121,6 +1204,12 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
   auto B = reinterpret_cast<const float4*>(b);
   auto Cc = reinterpret_cast<const float4*>(c);
   const size_t n4 = n_floats / 4;
+  if (g_xcd_mask) {
+    blocks = (blocks + kXcds - 1) / kXcds * kXcds;
+    hipLaunchKernelGGL((stream_triad_xcd<4>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4, g_xcd_mask);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   int variant = g_triad_variant;
   if (variant == 6) variant = (n_floats * 12 <= (size_t)96 << 20) ? 1 : 3;
   switch (variant) {
