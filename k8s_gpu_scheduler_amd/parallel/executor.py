@@ -76,6 +76,11 @@ class DeviceExecutor:
     split_by_pod = False         # phase_split per pod (dominant class), not per op
     split_masks = True
     split_shared = False         # one stream pair for every slot (same-class pods serialise)
+    #   xcd_confine  -- study: a Burstable pod's kernels run only on the XCDs of its unit slot
+    #                   (units [u, u+n) -> XCDs [u, u+n), a software QPX partition: blocks on
+    #                   other XCDs exit at once), GEMMs on the 8-phase tile, so each pod's
+    #                   operand strips live in its own XCDs' L2s (tools/xcd_confine_probe.py)
+    xcd_confine = False
 
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
         self.device = device
@@ -180,19 +185,30 @@ class DeviceExecutor:
         r.end.record(prev)
 
     def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:
-        for _ in range(r.iters):
-            for o, t in bufs.ops:
-                if o.kind == "gemm":
-                    a, bt, bias, c = t
-                    loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
-                else:
-                    x, y, z = t
-                    loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
+        h = None
+        if self.xcd_confine and not r.masked:
+            from .. import _native
+            h = _native.hip(required=True)
+            h.set_xcd_mask(((1 << r.n_units) - 1) << r.first_unit)
+            h.set_gemm_tile(10)
+        try:
+            for _ in range(r.iters):
+                for o, t in bufs.ops:
+                    if o.kind == "gemm":
+                        a, bt, bias, c = t
+                        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+                    else:
+                        x, y, z = t
+                        loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
+        finally:
+            if h is not None:
+                h.set_xcd_mask(0)
+                h.set_gemm_tile(0)
 
     def _graph_for(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> "torch.cuda.CUDAGraph":
         """One HIP graph per (workload, unit slot, QoS, iters): captured on the pod's own
         stream, so replaying it there keeps the stream's CU mask and its ordering."""
-        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks)
+        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks, self.xcd_confine)
         g = self._graphs.get(k)
         if g is None:
             torch.cuda.synchronize(self.device)

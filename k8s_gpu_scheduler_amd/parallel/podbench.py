@@ -475,6 +475,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="GEMM tile order: each XCD takes a near-square block of output tiles (1) or a "
                          "tall GROUP_M strip (0)")
     ap.add_argument("--xcd-group", type=int, default=4, help="tile rows per group inside an XCD block")
+    ap.add_argument("--xcd-confine", type=int, default=0, choices=[0, 1],
+                    help="study: each Burstable pod's kernels confined to the XCDs of its unit slot")
     ap.add_argument("--c-nt", type=int, default=0, choices=[0, 1], help="study: non-temporal GEMM output stores")
     ap.add_argument("--gemm-share", type=int, default=1, choices=[0, 1],
                     help="1: the GEMM tile picker sizes a pod's GEMMs for its CU share (co-running pods fill the "
@@ -564,6 +566,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_triad_aux(a.triad_aux)
         ex.triad_blocks = a.triad_blocks
         ex.gemm_share = bool(a.gemm_share)
+        ex.xcd_confine = bool(a.xcd_confine)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
     smi_s = None
