@@ -11,13 +11,20 @@
 //    waves; 64x64 or 128x64 per wave) picked per shape; both operands staged global->LDS with 16-byte
 //    global_load_lds (no VGPR round trip) into a double-buffered, XOR-swizzled LDS image
 //    (bank-conflict-free ds_read_b128 fragment reads); stage of tile t+1 is issued before
-//    the MFMAs of tile t; XCD-aware bijective block remap + grouped tile order for L2 reuse.
+//    the MFMAs of tile t; XCD-aware bijective block remap + XCD-block tile order for L2 reuse.
 //    Epilogue fuses bias + ReLU and stores packed bf16x4.  Lone large GEMMs use a separate
 //    256x256 "8-phase" kernel (gemm_bf16_nt_256_8ph: two staggered wave groups, one
 //    half-tile of glds per phase, counted vmcnt).
 //  * gemm_fp8_nt -- the same GEMM with OCP e4m3fn operands on the block-scaled
 //    v_mfma_scale_f32_16x16x128_f8f6f4 (unit scales): 2x the bf16 MFMA rate.
 //  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
+//
+// Launch settings (set_gemm_policy, set_gemm_tile, set_split_k, set_wide_epilogue,
+// set_xcd_blocks, set_xcd_group, set_c_nontemporal, set_xcd_mask, set_triad_variant,
+// set_triad_aux) are process-wide values read on the launching host thread when a kernel is
+// enqueued (a captured HIP graph keeps the values of its capture).  One host thread per rank
+// launches every pod kernel (parallel.executor), so they are plain statics; the defaults are
+// the measured winners, the rest are A/B knobs whose results are recorded in profiles/.
 #include <algorithm>
 #include <cstdint>
 
