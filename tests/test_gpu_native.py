@@ -503,3 +503,40 @@ def test_agent_exports_real_telemetry_to_prometheus():
         assert f"{m}{{" in text, m
     assert f'UUID="{uuids[0]}"' in text
     assert any(l.startswith("amd_gpu_healthy{") and l.endswith(" 1.0") for l in text.splitlines())
+
+
+def test_xcd_dispatch_and_confined_kernels_bit_exact():
+    """Block b runs on XCD b % 8 (HW_REG_XCC_ID), which the XCD-block tile order and the
+    XCD-confinement study rely on; confined 8-phase GEMM and stream kernels are bit-exact vs
+    their unconfined launches; the XCD-block order vs the GROUP_M order too."""
+    from k8s_gpu_scheduler_amd import _native
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    h = _native.hip(required=True)
+    ids = torch.full((4096,), -1, dtype=torch.int32, device="cuda")
+    h.xcd_probe(ids.data_ptr(), 4096, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert bool((ids.cpu() == torch.arange(4096) % 8).all())
+    M, N, K = 2048, 1536, 1024
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    bt = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    y, z = torch.rand(1 << 20, device="cuda"), torch.rand(1 << 20, device="cuda")
+    try:
+        h.set_gemm_tile(10)
+        ref = loadgen.gemm(a, bt, bias=bias, relu=True)
+        tref = torch.empty_like(y)
+        loadgen.triad(tref, y, z, 1.5)
+        torch.testing.assert_close(ref.float(), torch.relu(a.float() @ bt.float().T + bias), atol=0.1, rtol=0.02)
+        h.set_xcd_blocks(0)
+        assert torch.equal(loadgen.gemm(a, bt, bias=bias, relu=True), ref)
+        h.set_xcd_blocks(1)
+        for m in (0x03, 0x30, 0x0F):
+            h.set_xcd_mask(m)
+            x = torch.empty_like(y)
+            loadgen.triad(x, y, z, 1.5)
+            assert torch.equal(loadgen.gemm(a, bt, bias=bias, relu=True), ref), hex(m)
+            assert torch.equal(x, tref), hex(m)
+    finally:
+        h.set_xcd_mask(0)
+        h.set_xcd_blocks(1)
+        h.set_gemm_tile(0)
