@@ -40,8 +40,10 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 
-// Block index -> output tile.  Workgroup b runs on XCD b % 8 (round-robin dispatch), so the
-// XCD-aware bijective remap first makes each XCD's workgroups one contiguous range of wgid.
+// Block index -> output tile.  Workgroups b and b + 8 run on the same XCD (round-robin dispatch;
+// which XCD takes block 0 rotates with earlier dispatches -- tests/test_gpu_native.py reads
+// HW_REG_XCC_ID), so the XCD-aware bijective remap first makes each XCD's workgroups one
+// contiguous range of wgid.
 // xmap = 0: GROUP_M-row grouped order over the whole grid (an XCD's range is a tall 8-row
 // strip of tiles).  xmap = px | (gm << 8): the tile grid is cut into px x (8 / px) equal
 // rectangles, XCD x walks rectangle x (gm-row grouped order inside), so the A row-strips and B column-strips
@@ -104,10 +106,12 @@ __device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld,
 }
 
 // ---- XCD confinement (study) -------------------------------------------------------------
-// A pod's kernel may be confined to a set of XCDs (8-bit mask): workgroups dispatched to other
-// XCDs exit at once (round-robin dispatch puts block b on XCD b % 8 -- xcd_probe_kernel checks
-// it on the box), the rest share the work, so the pod's GEMM operand strips live in only its
-// own XCDs' L2s -- a software QPX partition.
+// A pod's kernel may be confined to a set of XCDs (8-bit mask over the block residues b % 8):
+// workgroups of other residues exit at once, the rest share the work, so the pod's GEMM operand
+// strips live in only its own XCDs' L2s -- a software QPX partition.  Residue r runs on XCD
+// (r + rot) % 8 for a rotation that depends on earlier dispatches, so concurrently launched
+// pods' masks are disjoint only in residue space (a study; measured and rejected,
+// profiles/r02_xcd_confine_rejected.json).
 __device__ __forceinline__ int xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xF; }
 
 __global__ void xcd_probe_kernel(int* out) {

@@ -2,7 +2,8 @@
 kernels confined to its own 2 XCDs, so its GEMM operand strips live in 2 L2s instead of 8 --
 beat full sharing?
 
-  1. dispatch check: block b runs on XCD b % 8 (xcd_probe_kernel reads HW_REG_XCC_ID);
+  1. dispatch check: block b runs on XCD b % 8 (xcd_probe_kernel reads HW_REG_XCC_ID; in a
+     fresh process -- later launches rotate which XCD takes block 0);
   2. numerics: confined 8-phase GEMM and stream kernel vs the unconfined results (bit-exact);
   3. stream-kernel HBM rate confined to 1 / 2 / 4 / 8 XCDs, and 4 confined streams at once;
   4. the bench's 4-pod pattern: 2 GEMM pods + 2 stream pods on 4 streams, full sharing
