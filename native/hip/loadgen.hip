@@ -729,6 +729,206 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x256 "one wave per SIMD" GEMM (tiles 11 / 12, study against the 8-phase kernel): 4 waves
+// as 2 x 2, each owning a 128x128 output block = 8 x 8 MFMA 16x16 tiles (256 fp32 accumulators,
+// AGPR-resident).  PMC of hipBLASLt's MT256x256x64 kernel at 8192^3 (4 waves, 128x128 wave
+// tiles; profiles/r02_gemm_clock_8192.json) shows what the bigger wave tile buys: 34 % fewer
+// LDS instructions per FLOP than the 8-phase kernel's 128x64 wave tiles and 4.7 % vs 29 %
+// of wave cycles waiting, 88 % vs 79 % MFMA-busy per SIMD at the same clock.
+// K-tile KT = 32 (16 KiB per operand), S LDS stages (128 KiB for S = 4).  Iteration t:
+//   MFMAs of rows 0-3 of tile t (fragments already in registers)
+//   lgkmcnt(0); counted vmcnt (tile t+1 landed: tiles t+2 .. t+S-1 may stay in flight); barrier
+//   glds of tile t+S into tile t's buffer (every wave finished reading it before the barrier)
+//   ds_reads of tile t+1's fragments into the other register slot
+//   MFMAs of rows 4-7 of tile t (hide the fragment-read and barrier latency)
+// so a K-tile's glds have S-1 iterations (~(S-1) x 64 MFMAs) to land, and every LDS-DMA write is
+// read only after the issuing waves' vmcnt + a barrier the reader passed (RAW), into a buffer no
+// wave reads any more (WAR).  The wide epilogue assembles the block tile in the 128 KiB.
+// PROBE (timing-only study arms, wrong results): 1 = no barrier in the steady-state loop,
+// 2 = no barrier and no vmcnt wait there either.
+template <bool RELU, bool BIAS, int S, int PROBE = 0>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_bf16_nt_256_4w(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
+                    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
+  constexpr int KT = 32;
+  constexpr int OPB = 256 * KT * 2;                // bytes of one operand's K-tile image
+  constexpr int BUF = 2 * OPB;                     // A then B
+  constexpr int G = 2 * 256 * KT * 2 / 16 / 256;   // glds per thread per K-tile (8)
+  static_assert(S >= 2 && S * BUF <= 128 * 1024, "stages");
+  __shared__ __attribute__((aligned(16))) char smem[128 * 1024];
+
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, M / 256, N / 256, xmap, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int frow = lane & 15, fk = lane >> 4;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ra[2][8], rb[2][8];
+
+  const int T = K / KT;
+  // LDS-DMA through buffer_load ... lds: the per-lane byte offset (row, swizzled chunk: the
+  // stage_tile image) is one VGPR fixed for the whole K loop -- row-group and K-tile offsets go
+  // in the scalar soffset -- so the 16 loads of a K-tile hold no 64-bit address registers (the
+  // global_load_lds form spilled at 256 accumulators + 2 fragment slots).
+  constexpr int CH = KT / 8, RPI = 256 / CH;       // 16-B chunks per row, rows per load
+  const int tid = threadIdx.x, r = tid / CH;
+  const unsigned voff_a = (unsigned)(r * lda * 2 + (((tid % CH) ^ ((r >> 1) % CH)) * 16));
+  const unsigned voff_b = (unsigned)(r * ldb * 2 + (((tid % CH) ^ ((r >> 1) % CH)) * 16));
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bt + (size_t)n0 * ldb), 0, 256 * ldb * 2, 0x00020000);
+  auto stage = [&](int u) {
+    char* buf = smem + (u % S) * BUF;
+#pragma unroll
+    for (int i = 0; i < 256 * KT * 2 / 16 / 256; ++i) {
+      char* dst = buf + (i * 256 + wave * 64) * 16;            // wave-uniform base
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)dst, 16, voff_a, i * RPI * lda * 2 + u * KT * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(dst + OPB), 16, voff_b, i * RPI * ldb * 2 + u * KT * 2, 0, 0);
+    }
+  };
+  auto read = [&](int u, bf16x8 (&a)[8], bf16x8 (&b)[8]) {
+    const char* buf = smem + (u % S) * BUF;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = lds_frag<KT>(buf + OPB, wc * 128 + j * 16 + frow, fk);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = lds_frag<KT>(buf, wr * 128 + i * 16 + frow, fk);
+  };
+  auto mfma_rows = [&](int i0, const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
+#pragma unroll
+    for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        // AGPR-pinned, tied accumulator: with the builtin the compiler's AGPR-form MFMAs here
+        // renamed every accumulator through v_accvgpr_read/write copies (~4 per MFMA)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b[j]), "v"(a[i]));
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma1 = [&](int i, int j, const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b[j]), "v"(a[i]));
+  };
+  // Steady-state halves with the memory work spread between MFMAs: one wave per SIMD has no
+  // partner wave to issue MFMAs while it stalls on a load issue, so each group of 4 MFMAs is
+  // followed by one LDS-DMA load and two fragment reads (sched_barrier pins the order).
+  // First half: rows 0-3, column-major so the fragments read last (b[7]) are needed last.
+  auto half1 = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mfma1(i, j, a, b);
+  };
+  auto half2 = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[8], int us, int ur, bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
+    char* sbuf = smem + (us % S) * BUF;
+    const char* rbuf = smem + (ur % S) * BUF;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int i = 4; i < 8; ++i) mfma1(i, q, a, b);
+      const int c = q & 3;
+      char* dst = sbuf + (q >= 4 ? OPB : 0) + (c * 256 + wave * 64) * 16;
+      if (q < 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)dst, 16, voff_a, c * RPI * lda * 2 + us * KT * 2, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)dst, 16, voff_b, c * RPI * ldb * 2 + us * KT * 2, 0, 0);
+      // next tile's fragments: a[0..3] and b[0..3] in the first four groups (half1 needs them first)
+      na[q] = lds_frag<KT>(rbuf, wr * 128 + q * 16 + frow, fk);
+      nb[q] = lds_frag<KT>(rbuf + OPB, wc * 128 + q * 16 + frow, fk);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // vmcnt at iteration t: tiles t+2 .. min(T-1, t+S-1) may stay in flight
+  auto wait_tile = [&](int t) {
+    const int n = max(0, min(T - 1, t + S - 1) - (t + 1));
+    if (n >= 2) wait_vmcnt<2 * G>();
+    else if (n == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+  };
+  // lgkmcnt(0) (vmcnt / expcnt fields at their no-wait maxima)
+  auto wait_lds = [] { __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4)); };
+
+#pragma unroll
+  for (int u = 0; u < S; ++u)
+    if (u < T) stage(u);
+  // tile 0 landed: tiles 1 .. min(T, S) - 1 may stay in flight
+  {
+    const int n = min(T, S) - 1;
+    if (n >= 3) wait_vmcnt<3 * G>();
+    else if (n == 2) wait_vmcnt<2 * G>();
+    else if (n == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+  }
+  barrier();
+  read(0, ra[0], rb[0]);
+
+  // two K-tiles per trip so the register slots are compile-time
+  int t = 0;
+  {
+    // steady state: every iteration restages and tiles t+2 .. t+S-1 stay in flight
+    for (; t + S + 1 < T; t += 2) {
+      half1(ra[0], rb[0]);
+      wait_lds();
+      if (PROBE < 2) wait_vmcnt<(S - 2) * G>();
+      if (PROBE < 1) barrier();
+      half2(ra[0], rb[0], t + S, t + 1, ra[1], rb[1]);
+
+      half1(ra[1], rb[1]);
+      wait_lds();
+      if (PROBE < 2) wait_vmcnt<(S - 2) * G>();
+      if (PROBE < 1) barrier();
+      half2(ra[1], rb[1], t + 1 + S, t + 2, ra[0], rb[0]);
+    }
+  }
+  for (; t < T; t += 2) {
+    mfma_rows(0, ra[0], rb[0]);
+    wait_lds();
+    wait_tile(t);
+    barrier();
+    if (t + S < T) stage(t + S);
+    if (t + 1 < T) read(t + 1, ra[1], rb[1]);
+    mfma_rows(4, ra[0], rb[0]);
+    if (t + 1 >= T) break;
+    mfma_rows(0, ra[1], rb[1]);
+    wait_lds();
+    wait_tile(t + 1);
+    barrier();
+    if (t + 1 + S < T) stage(t + 1 + S);
+    if (t + 2 < T) read(t + 2, ra[0], rb[0]);
+    mfma_rows(4, ra[1], rb[1]);
+  }
+  // every wave past its last LDS read and every LDS-DMA retired (the last wait was vmcnt(0));
+  // the s_nops cover the MFMA-result -> VALU-read latency the hazard pass cannot see in asm
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  barrier();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = wc * 128 + j * 16 + fk * 4;
+    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 v = acc[i][j] + bv;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+      wide_put<256>(smem, wr * 128 + i * 16 + frow, col, o);
+    }
+  }
+  __syncthreads();
+  wide_store<256, 256, 256>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
+}
+
 // C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
 // bf16x4 out, grid-stride over M*N/4).
 template <bool RELU, bool BIAS>
@@ -1018,8 +1218,10 @@ static int g_gemm_tile = 0;
 // non-hoisted 128x128 kept as the A/B reference.
 // 9 = 256x256 8-phase (gemm_bf16_nt_256_8ph; needs K >= 128); 10 = the same with the
 // steady-state K loop peeled (constant vmcnt, no per-phase stage conditions).
-static const int kTileBM[11] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256};
-static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256};
+// 11 / 12 = 256x256 with 4 waves of 128x128 (gemm_bf16_nt_256_4w), K-tile 32, 4 / 3 LDS stages
+// (wide epilogue only: falls back to tile 10 when C rows are not 16-B aligned).
+static const int kTileBM[15] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 256, 256, 256, 256};
+static const int kTileBN[15] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 256, 256, 256, 256};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -1045,7 +1247,7 @@ void set_gemm_policy(int p) {
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 10) throw std::runtime_error("gemm tile must be 0..10");
+  if (t < 0 || t > 14) throw std::runtime_error("gemm tile must be 0..14");
   g_gemm_tile = t;
 }
 
@@ -1098,6 +1300,23 @@ void set_split_k(int s) {
   g_split_k = s == 1 ? 0 : s;
 }
 
+template <int S, int PROBE = 0>
+static void launch_4w(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
+                      int ldb, int ldc, bool relu, hipStream_t s) {
+  const dim3 grid((M / 256) * (N / 256)), block(256);
+  const int xmap = pick_xcd_map(M / 256, N / 256);
+  if (PROBE)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, false, S, PROBE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+  else if (relu && bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<true, true, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<true, false, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+  else if (bp)
+    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, true, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+  else
+    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, false, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+}
+
 template <bool RELU, bool BIAS>
 static void launch_splitk(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, float* ws, int S, int M,
                           int N, int K, int lda, int ldb, int ldc, hipStream_t s) {
@@ -1137,6 +1356,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     return;
   }
   int t = pick_gemm_tile(M, N, cu_budget);
+  if (t >= 11 && !wide_ok(Cp, ldc)) t = 10;
   if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
   switch (t) {
@@ -1156,6 +1376,10 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
         launch_8ph<false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
       break;
     }
+    case 11: launch_4w<4>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 12: launch_4w<3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 13: launch_4w<4, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;   // timing probes
+    case 14: launch_4w<4, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
   HIP_CHECK(hipGetLastError());

@@ -56,9 +56,10 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-@pytest.mark.parametrize("tile", [9, 10])
+@pytest.mark.parametrize("tile", [9, 10, 11, 12])
 def test_gemm_256_8phase_numerics_and_race_screen(tile):
-    """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled): every K-tile count from the minimum (2) through odd
+    """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled) and the
+    4-wave 256x256 kernel (tiles 11 / 12: 4 / 3 LDS stages): every K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
     (guide §5 'A sync-structure edit makes a NEW template'), so every run is checked against
@@ -68,8 +69,8 @@ def test_gemm_256_8phase_numerics_and_race_screen(tile):
     h = _native.hip()
     h.set_gemm_tile(tile)
     try:
-        for (M, N, K) in [(256, 256, 128), (256, 512, 192), (512, 256, 320), (768, 1024, 1024), (512, 512, 384),
-                          (2048, 2048, 4096), (4096, 4096, 640)]:
+        for (M, N, K) in [(256, 256, 64), (256, 256, 128), (256, 512, 192), (512, 256, 320), (768, 1024, 1024),
+                          (512, 512, 384), (2048, 2048, 4096), (4096, 4096, 640), (1024, 512, 1088)]:
             g = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K)
             a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
             bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
