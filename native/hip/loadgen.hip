@@ -929,6 +929,154 @@ gemm_bf16_nt_256_4w(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   wide_store<256, 256, 256>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
 }
 
+// Register-staged variant (tile 15): the LDS-DMA piece costs its wave 60-185 issue cycles among
+// MFMAs (MI355X_MICROARCH.md, LDS-DMA issue cost), which one wave per SIMD cannot hide, so here
+// every K-tile goes global -> VGPRs (buffer_load_dwordx4, issued two K-tiles ahead: two register
+// buffers of 8 x 16 B) -> LDS (ds_write_b128 into the swizzled image lds_frag reads), hipBLASLt's
+// "prefetch global read 2" shape.  Iteration t (LDS buffer t % 2 holds tile t, its fragments are
+// in register slot t & 1):
+//   rows 0-3 MFMAs, with the ds_writes of tile t+1 (registers R[(t+1) & 1]) into buffer (t+1) % 2
+//     (free: tile t-1's fragment reads retired before the previous barrier)
+//   lgkmcnt(0) (tile t+1 written, tile t's reads done); barrier
+//   rows 4-7 MFMAs, with tile t+1's fragment reads and the global loads of tile t+3 into R[(t+1) & 1]
+// vmcnt(8) before the ds_writes of tile t+1 leaves only tile t+2's 8 loads in flight.
+template <bool RELU, bool BIAS>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_bf16_nt_256_4wr(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
+                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
+  constexpr int KT = 32;
+  constexpr int OPB = 256 * KT * 2;                // bytes of one operand's K-tile image
+  constexpr int BUF = 2 * OPB;                     // A then B
+  __shared__ __attribute__((aligned(16))) char smem[128 * 1024];
+
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, M / 256, N / 256, xmap, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int frow = lane & 15, fk = lane >> 4;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ra[2][8], rb[2][8];
+  f32x4 rg[2][8];                                  // staged K-tiles: [buffer][A chunks 0-3, B chunks 0-3]
+
+  const int T = K / KT;
+  // thread -> (row tid / 4 + 64 c, logical 16-B chunk tid % 4) of every K-tile, c = 0..3
+  const int tid = threadIdx.x, r = tid >> 2, kc = tid & 3;
+  const unsigned voff_a = (unsigned)(r * lda * 2 + kc * 16);
+  const unsigned voff_b = (unsigned)(r * ldb * 2 + kc * 16);
+  const int wofs = r * (KT * 2) + ((kc ^ ((r >> 1) & 3)) << 4);   // swizzled LDS byte offset
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bt + (size_t)n0 * ldb), 0, 256 * ldb * 2, 0x00020000);
+  auto gload = [&](int u, int q, f32x4 (&g)[8]) {  // q: A chunks 0-3, B chunks 4-7
+    const int c = q & 3;
+    if (q < 4)
+      g[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, voff_a, c * 64 * lda * 2 + u * KT * 2, 0));
+    else
+      g[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsb, voff_b, c * 64 * ldb * 2 + u * KT * 2, 0));
+  };
+  auto lwrite = [&](int u, int q, const f32x4 (&g)[8]) {
+    char* buf = smem + (u & 1) * BUF + (q < 4 ? 0 : OPB);
+    *reinterpret_cast<f32x4*>(buf + (q & 3) * 64 * (KT * 2) + wofs) = g[q];
+  };
+  auto frag_a = [&](int u, int i) { return lds_frag<KT>(smem + (u & 1) * BUF, wr * 128 + i * 16 + frow, fk); };
+  auto frag_b = [&](int u, int j) { return lds_frag<KT>(smem + (u & 1) * BUF + OPB, wc * 128 + j * 16 + frow, fk); };
+  auto mfma1 = [&](int i, int j, const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b[j]), "v"(a[i]));
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto wait_lds = [] { __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4)); };
+  // one K-tile step; W / L / R = ds_write tile t+1 / global-load tile t+3 / read tile t+1 frags
+  auto step = [&](int t, bf16x8 (&a)[8], bf16x8 (&b)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], f32x4 (&gw)[8],
+                  bool W, bool L, bool R, bool more) {
+    if (more) wait_vmcnt<8>(); else wait_vmcnt<0>();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mfma1(i, q, a, b);
+      if (W) lwrite(t + 1, q, gw);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_lds();
+    barrier();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int i = 4; i < 8; ++i) mfma1(i, q, a, b);
+      if (L) gload(t + 3, q, gw);
+      if (R) {
+        na[q] = frag_a(t + 1, q);
+        nb[q] = frag_b(t + 1, q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // prologue: tiles 0, 1 -> registers; tile 0 -> LDS; tile 2 -> registers; tile 0 fragments
+#pragma unroll
+  for (int q = 0; q < 8; ++q) gload(0, q, rg[0]);
+  if (T > 1) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gload(1, q, rg[1]);
+    wait_vmcnt<8>();
+  } else {
+    wait_vmcnt<0>();
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) lwrite(0, q, rg[0]);
+  if (T > 2) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gload(2, q, rg[0]);
+  }
+  wait_lds();
+  barrier();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    ra[0][q] = frag_a(0, q);
+    rb[0][q] = frag_b(0, q);
+  }
+
+  int t = 0;
+  for (; t + 4 < T; t += 2) {                      // steady state: every step writes, loads and reads
+    step(t, ra[0], rb[0], ra[1], rb[1], rg[1], true, true, true, true);
+    step(t + 1, ra[1], rb[1], ra[0], rb[0], rg[0], true, true, true, true);
+  }
+  for (; t < T; t += 2) {
+    step(t, ra[0], rb[0], ra[1], rb[1], rg[1], t + 1 < T, t + 3 < T, t + 1 < T, t + 2 < T);
+    if (t + 1 >= T) break;
+    step(t + 1, ra[1], rb[1], ra[0], rb[0], rg[0], t + 2 < T, t + 4 < T, t + 2 < T, t + 3 < T);
+  }
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  barrier();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = wc * 128 + j * 16 + fk * 4;
+    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 v = acc[i][j] + bv;
+      bf16x4 o;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) o[rr] = (__bf16)(RELU ? (v[rr] > 0.f ? v[rr] : 0.f) : v[rr]);
+      wide_put<256>(smem, wr * 128 + i * 16 + frow, col, o);
+    }
+  }
+  __syncthreads();
+  wide_store<256, 256, 256>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
+}
+
 // C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
 // bf16x4 out, grid-stride over M*N/4).
 template <bool RELU, bool BIAS>
@@ -1220,8 +1368,8 @@ static int g_gemm_tile = 0;
 // steady-state K loop peeled (constant vmcnt, no per-phase stage conditions).
 // 11 / 12 = 256x256 with 4 waves of 128x128 (gemm_bf16_nt_256_4w), K-tile 32, 4 / 3 LDS stages
 // (wide epilogue only: falls back to tile 10 when C rows are not 16-B aligned).
-static const int kTileBM[15] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 256, 256, 256, 256};
-static const int kTileBN[15] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 256, 256, 256, 256};
+static const int kTileBM[16] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 256, 256, 256, 256, 256};
+static const int kTileBN[16] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 256, 256, 256, 256, 256};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -1247,7 +1395,7 @@ void set_gemm_policy(int p) {
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 14) throw std::runtime_error("gemm tile must be 0..14");
+  if (t < 0 || t > 15) throw std::runtime_error("gemm tile must be 0..15");
   g_gemm_tile = t;
 }
 
@@ -1305,7 +1453,16 @@ static void launch_4w(const __bf16* A, const __bf16* B, __bf16* Cp, const float*
                       int ldb, int ldc, bool relu, hipStream_t s) {
   const dim3 grid((M / 256) * (N / 256)), block(256);
   const int xmap = pick_xcd_map(M / 256, N / 256);
-  if (PROBE)
+  if constexpr (S == 0) {
+    if (relu && bp)
+      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    else if (relu)
+      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    else if (bp)
+      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    else
+      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+  } else if (PROBE)
     hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, false, S, PROBE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (relu && bp)
     hipLaunchKernelGGL((gemm_bf16_nt_256_4w<true, true, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
@@ -1380,6 +1537,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 12: launch_4w<3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 13: launch_4w<4, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;   // timing probes
     case 14: launch_4w<4, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 15: launch_4w<0>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;     // register-staged
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
   HIP_CHECK(hipGetLastError());

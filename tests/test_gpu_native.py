@@ -56,10 +56,10 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-@pytest.mark.parametrize("tile", [9, 10, 11, 12])
+@pytest.mark.parametrize("tile", [9, 10, 11, 12, 15])
 def test_gemm_256_8phase_numerics_and_race_screen(tile):
     """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled) and the
-    4-wave 256x256 kernel (tiles 11 / 12: 4 / 3 LDS stages): every K-tile count from the minimum (2) through odd
+    4-wave 256x256 kernel (tiles 11 / 12: 4 / 3 LDS stages; 15: register-staged): every K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
     (guide §5 'A sync-structure edit makes a NEW template'), so every run is checked against
