@@ -100,7 +100,8 @@ class ControlPlane:
     def __init__(self, n_gpus: int, pods_per_gpu: int, iters: int, seed: int, policy: str = "gpu",
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
-                 plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0):
+                 plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0,
+                 online_scale: bool = False):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -144,7 +145,8 @@ class ControlPlane:
                 prior = np.array([[tab.by_label[r][c] for c in cols] for r in rows], dtype=np.float64)
                 # refit about every 4 epochs (each refit re-summarises the scheduler's devices)
                 self.online = OnlineInterference(W.NAMES, W.NAMES, prior,
-                                                 refit_every=max(32, 4 * n_gpus * pods_per_gpu))
+                                                 refit_every=max(32, 4 * n_gpus * pods_per_gpu),
+                                                 scale=online_scale)
                 self._online_rows = rows
         self.epoch = 0
         self.live: List[Tuple[str, str]] = []
@@ -443,6 +445,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "of each epoch of an 8-GPU node by 6-7%% (what paces lock-step ranks), but through "
                          "this bench's 2-deep launch-ahead pipeline greedy placement is 1.6%% faster "
                          "(tools/virtual_node_bench.py, profiles/r01_virtual_node_s3b.json), so it is off")
+    ap.add_argument("--online-scale", type=int, default=0,
+                    help="online interference learning: shrink rows toward the prior SCALED by a learned "
+                         "global / per-row factor (recommender.online) instead of the prior itself")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
                     help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
                          "'slo' = most predicted SLOs met first (within --plan-tolerance)")
@@ -528,7 +533,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     n_gpus_planned = world if world > 1 else max(1, a.gpus)
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
-                     plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective)
+                     plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective,
+                     online_scale=bool(a.online_scale))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -793,6 +799,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
                        "balance": a.balance, "plan_bursts": a.plan_bursts,
                        "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
+                       "online_scale": a.online_scale,
                        "note": "global_batch = pods per scheduling epoch; seq_len = query batches per pod"},
             "gpu_util_pct": round(util, 2),
             "cu_share_occupancy_pct": round(occ, 2),

@@ -209,7 +209,8 @@ class RecommenderService:
             base = self.intf.file_version or self.intf.version
             if self._online is None or self._online_base != base:
                 self._online = OnlineInterference(t.table.index, t.table.columns, t.completed(),
-                                                  refit_every=max(1, int(os.getenv("ONLINE_REFIT_EVERY", "32"))))
+                                                  refit_every=max(1, int(os.getenv("ONLINE_REFIT_EVERY", "32"))),
+                                                  scale=os.getenv("ONLINE_PRIOR_SCALE", "0") == "1")
                 self._online_base = base
             on = self._online
             cols = list(t.table.columns)

@@ -282,12 +282,14 @@ def test_online_interference_learns_additive_model():
     true = rng.uniform(0, 100, (w, w))
     prior = true + rng.normal(0, 40, (w, w))
     prior[0, 0] = np.nan                                  # unmeasured entry: filled, not fatal
-    m = OnlineInterference([f"w{i}" for i in range(w)], [f"w{i}" for i in range(w)], prior, lam=2.0, refit_every=16)
+    m = OnlineInterference([f"w{i}" for i in range(w)], [f"w{i}" for i in range(w)], prior, lam=2.0, refit_every=16,
+                           scale=True)
     assert np.isfinite(m.matrix).all()
     # few observations: row stays near the prior
     m.observe(1, [2, 3, 4], float(true[1, [2, 3, 4]].sum()))
     m.refit()
-    assert abs(m.matrix[1, 5] - m.prior[1, 5]) < 1e-9   # column never seen -> prior kept
+    # column never seen -> the prior entry, scaled by the row's learned prior scale
+    assert abs(m.matrix[1, 5] - m.prior[1, 5] * m.row_scale[1]) < 1e-9
     for _ in range(3000):
         a = int(rng.integers(w))
         others = [int(x) for x in rng.integers(0, w, 3)]
@@ -296,6 +298,34 @@ def test_online_interference_learns_additive_model():
     assert np.abs(m.matrix - true).max() < 5.0
     e = m.mae()
     assert e["n"] == 3001 and e["online"] < 0.5 * e["prior"]
+    plain = OnlineInterference([f"w{i}" for i in range(w)], [f"w{i}" for i in range(w)], prior, scale=False)
+    plain.observe(1, [2, 3, 4], float(true[1, [2, 3, 4]].sum()))
+    plain.refit()
+    assert abs(plain.matrix[1, 5] - plain.prior[1, 5]) < 1e-9     # scale=False: prior kept
+
+
+def test_online_interference_learns_a_systematic_prior_bias_fast():
+    """A pairwise table that under-predicts 4-way co-run loss by a common factor: the prior
+    scale (global, then per row) is learned from every row's observations, so 100 observations
+    over 18 rows (~5 per row) already beat the plain ridge-to-prior by a wide margin."""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.recommender.online import OnlineInterference
+    rng = np.random.default_rng(0)
+    w = 18
+    prior = rng.uniform(50, 500, (w, w))
+    true = prior * 1.6 + rng.normal(0, 20, (w, w))
+    maes = {}
+    for scale in (False, True):
+        r = np.random.default_rng(1)
+        m = OnlineInterference([str(i) for i in range(w)], [str(i) for i in range(w)], prior, scale=scale)
+        for _ in range(100):
+            a = int(r.integers(w))
+            others = [int(x) for x in r.integers(0, w, 3)]
+            m.observe(a, others, float(true[a, others].sum() + r.normal(0, 50)))
+        maes[scale] = m.mae()["online"]
+        if scale:
+            assert 1.4 < m.global_scale < 1.8
+    assert maes[True] < 0.6 * maes[False]
 
 
 def test_plugin_forgets_memoised_predictions_on_new_table():
