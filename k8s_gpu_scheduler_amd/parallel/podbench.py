@@ -445,7 +445,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "of each epoch of an 8-GPU node by 6-7%% (what paces lock-step ranks), but through "
                          "this bench's 2-deep launch-ahead pipeline greedy placement is 1.6%% faster "
                          "(tools/virtual_node_bench.py, profiles/r01_virtual_node_s3b.json), so it is off")
-    ap.add_argument("--online-scale", type=int, default=0,
+    ap.add_argument("--online-scale", type=int, default=1,
                     help="online interference learning: shrink rows toward the prior SCALED by a learned "
                          "global / per-row factor (recommender.online) instead of the prior itself")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
