@@ -505,6 +505,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
                     help="amd-smi activity sampling period across warmup + timed region (0 = off)")
+    ap.add_argument("--dist-single", type=int, default=0, choices=[0, 1],
+                    help="check knob: a 1-rank process group takes the multi-rank collective path "
+                         "(placement broadcast, telemetry all-gather, result all-reduce, barriers) so a "
+                         "1-GPU box runs the RCCL code of the scaling run")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     a.lookahead = max(1, a.lookahead)
@@ -512,6 +516,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # collectives run when there are several ranks, or a 1-rank group with --dist-single
+    dist_on = world > 1 or bool(a.dist_single)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1 and (
             a.launch == "spawn" or (a.launch == "auto" and not a.sim)):
         # One process per GPU without torchrun: spawn the ranks from this (GPU-untouched)
@@ -526,6 +532,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         return {"spawned_ranks": a.gpus}
     if world > 1 and a.gpus not in (1, world):
         raise SystemExit(f"--gpus {a.gpus} does not match WORLD_SIZE {world}")
+    if a.dist_single and world == 1 and a.gpus > 1:
+        raise SystemExit("--dist-single is a 1-rank check (--gpus 1)")
     if world == 1 and a.gpus > 1 and not a.sim:
         raise SystemExit(f"--gpus {a.gpus} needs one process per GPU: use --launch spawn/auto or torchrun")
     # The control plane goes to its own process, started BEFORE anything touches the GPU
@@ -547,8 +555,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx) if use_gpu else torch.device("cpu")
     backend = a.backend or ("nccl" if use_gpu else "gloo")
-    if world > 1 and not dist.is_initialized():
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+    if dist_on and not dist.is_initialized():
+        kw: Dict[str, Any] = {}
+        if world == 1:                      # --dist-single outside a launcher: private rendezvous
+            from .launch import free_port
+            kw = dict(init_method=f"tcp://127.0.0.1:{free_port()}", world_size=1, rank=0)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None, **kw)
     if use_gpu and world > 1 and "GPUSCHED_FORCE_DEVICE" not in os.environ and torch.cuda.device_count() < world:
         raise SystemExit(f"rank {rank}: WORLD_SIZE {world} but only {torch.cuda.device_count()} GPU(s) visible")
     n_gpus = world if world > 1 else max(1, a.gpus)
@@ -589,13 +601,13 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     # default stream would implicitly wait for every queued pod kernel and serialise the
     # host with the GPU (measured: 11.7 ms/epoch vs ~3 ms of host work).
     side = torch.cuda.Stream(device=dev) if use_gpu else None
-    cdev = dev if (world > 1 and backend == "nccl") else torch.device("cpu")
+    cdev = dev if (dist_on and backend == "nccl") else torch.device("cpu")
     assign = torch.zeros((P, FIELDS), dtype=torch.int32, device=cdev)
     tele = torch.zeros((TELE,), dtype=torch.float64, device=cdev)
     tele_all = [torch.zeros_like(tele) for _ in range(world)]
 
     def bcast(arr: Optional[np.ndarray]) -> np.ndarray:
-        if world == 1:
+        if not dist_on:
             return arr
         with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
             if rank == 0:
@@ -647,7 +659,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                 smi_vec = [sm["gfx_activity_pct_mean"] / 100.0, (sm["vram_used_mb_max"] or 0.0) / 1024.0]
         vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm] + _cost_rows(runs).ravel().tolist() + \
             _pod_rows(runs) + smi_vec
-        if world > 1:
+        if dist_on:
             with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
                 tele.copy_(torch.tensor(vec, dtype=torch.float64))
                 dist.all_gather(tele_all, tele)
@@ -728,7 +740,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             collect(*pending.popleft(), timed)
 
     run_epochs(a.warmup, False)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     if use_gpu:
         torch.cuda.synchronize()
@@ -745,7 +757,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             cp.sched_s = 0.0
             cp.unscheduled = 0
     run_epochs(a.steps, True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     if use_gpu:
         torch.cuda.synchronize()
@@ -769,14 +781,14 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     floor_peak = max(fl_r / (C.MI355X_BF16_DENSE_TFLOPS * 1e12), by_r / (C.MI355X_HBM_TBPS * 1e12))
     floor_ach = max(fl_r / (ACHIEVABLE_TFLOPS * 1e12), by_r / (ACHIEVABLE_TBPS * 1e12))
     flops = torch.tensor([fl_r, elapsed, busy_ms, by_r, floor_peak, floor_ach], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         summed = flops[[0, 2, 3]].clone()
         dist.all_reduce(summed, op=dist.ReduceOp.SUM)
         mx = flops[[1, 4, 5]].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)       # the busiest rank paces the step
         flops = torch.stack([summed[0], mx[0], summed[1], summed[2], mx[1], mx[2]])
     smi_all = [smi_t.clone() for _ in range(world)]
-    if world > 1:
+    if dist_on:
         dist.all_gather(smi_all, smi_t)
     smi_rows = [t.cpu().tolist() for t in smi_all]
     flops_tot, elapsed, busy_tot_ms = float(flops[0]), float(flops[1]), float(flops[2])
@@ -836,7 +848,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ex.close()
     if rank == 0 and async_cp:
         cp.close()
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     return result

@@ -134,3 +134,30 @@ def test_launcher_propagates_rank_failure():
     code = ("import os; assert os.environ['WORLD_SIZE']=='3' and os.environ['MASTER_ADDR']=='127.0.0.1'; "
             "assert os.environ['RANK']==os.environ['LOCAL_RANK']")
     assert spawn([sys.executable, "-c", code], 3, require_gpus=False) == 0
+
+
+def test_bench_dist_single_takes_the_collective_path():
+    """--dist-single: a 1-rank process group runs the multi-rank collective code (broadcast,
+    all-gather, all-reduce, barriers) -- on a 1-GPU box that is the RCCL path of the scaling run."""
+    from k8s_gpu_scheduler_amd.parallel.podbench import main
+    import torch.distributed as dist
+    r = main(["--sim", "--dist-single", "1", "--steps", "3", "--warmup", "1", "--control-plane", "inline"])
+    assert r["n_gpus"] == 1 and r["value"] > 0 and r["unscheduled"] == 0
+    assert not dist.is_initialized() and "WORLD_SIZE" not in os.environ
+    with pytest.raises(SystemExit):
+        main(["--sim", "--dist-single", "1", "--gpus", "2", "--steps", "1", "--warmup", "0"])
+
+
+@pytest.mark.gpu
+def test_bench_rccl_collective_path_on_gpu(tmp_path):
+    """The scaling run's collective code over RCCL on one MI355X: bench.py --dist-single runs a
+    1-rank nccl group (placement broadcast on the side stream, telemetry all-gather, result
+    all-reduce / all-gather, barriers, destroy) through the real HIP executor."""
+    out = tmp_path / "b.json"
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dist-single", "1", "--steps", "5",
+                        "--warmup", "2", "--out", str(out)], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = json.loads(out.read_text())
+    assert r["n_gpus"] == 1 and r["simulated"] is False and r["value"] > 0 and r["unscheduled"] == 0
