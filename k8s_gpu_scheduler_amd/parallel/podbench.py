@@ -509,8 +509,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="a 1-rank process group takes the multi-rank collective path (placement broadcast, "
                          "telemetry all-gather, result all-reduce, barriers): 1 always, 0 never, -1 (default) "
                          "on a GPU -- N=1 then runs the same code as the N-GPU scaling run, and it measured "
-                         "faster (587 vs 567 pods/s at 20 steps, 4/4 interleaved pairs, GPU util 99.7 vs "
-                         "95.7 %%; profiles/r02_rccl_single_rank/)")
+                         "faster in the driver's 20-step window (593 vs 569 pods/s, 6/6 interleaved pairs, GPU "
+                         "util 99.5 vs 95.6 %%; a tie over 60 steps; profiles/r02_rccl_single_rank/)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     a.lookahead = max(1, a.lookahead)
