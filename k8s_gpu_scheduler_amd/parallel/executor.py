@@ -68,19 +68,6 @@ class DeviceExecutor:
     #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
     #                   HIP graph on the pod's stream (captured once per workload/slot)
     use_graphs = False
-    #   phase_split  -- k > 0: a Burstable pod's HBM-bound ops (stream triads) run on a stream
-    #                   masked to CU units [0, k) and its MFMA-bound ops (GEMMs) on one masked
-    #                   to [k, units), ordered by events; co-running pods then never compete
-    #                   for one CU's issue slots across roofline classes
-    phase_split = 0
-    split_by_pod = False         # phase_split per pod (dominant class), not per op
-    split_masks = True
-    split_shared = False         # one stream pair for every slot (same-class pods serialise)
-    #   xcd_confine  -- study: a Burstable pod's kernels run only on the XCDs of its unit slot
-    #                   (units [u, u+n) -> XCDs [u, u+n), a software QPX partition: blocks on
-    #                   other XCDs exit at once), GEMMs on the 8-phase tile, so each pod's
-    #                   operand strips live in its own XCDs' L2s (tools/xcd_confine_probe.py)
-    xcd_confine = False
 
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
         self.device = device
@@ -129,86 +116,20 @@ class DeviceExecutor:
     def _budget(self, r: PodRun) -> int:
         return r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
 
-    def _split_streams(self, r: PodRun):
-        """(hbm stream, mfma stream) of a pod slot in phase-split mode."""
-        k = self.phase_split
-        key = ("split", -1 if self.split_shared else r.first_unit, r.n_units, k, self.split_masks)
-        pair = self._streams.get(key)
-        if pair is None:
-            from ..ops.cumask import MaskedStream
-            if self.split_masks:
-                pair = _StreamPair(MaskedStream(cu_slice_mask(0, k), self.device),
-                                   MaskedStream(cu_slice_mask(k, self.units - k), self.device))
-            else:                   # study control: the same two-stream ordering, no masks
-                pair = _StreamPair(_PlainStream(self.device), _PlainStream(self.device))
-            self._streams[key] = pair
-        return pair.hbm.stream, pair.mfma.stream
-
-    def _enqueue_split(self, r: PodRun, bufs: "_Buffers", budget: int, deps: List[torch.cuda.Event]) -> None:
-        """Phase-split enqueue: each op on the stream of its roofline class; a switch of
-        class records an event on the previous stream that the next one waits for."""
-        sh, sm = self._split_streams(r)
-        seq = [(o, t) for _ in range(r.iters) for o, t in bufs.ops]
-        if self.split_by_pod:
-            # the whole pod on the stream of its dominant class (no switches)
-            w = CATALOG[r.workload]
-            t_mfma = sum(o.flops for o in w.ops if o.kind == "gemm") / 1.0e15
-            t_hbm = sum(o.bytes for o in w.ops if o.kind != "gemm") / 5.5e12
-            s = sh if t_hbm > t_mfma else sm
-            for ev in deps:
-                s.wait_event(ev)
-            r.start.record(s)
-            self._enqueue_ops(r, bufs, s, (self.units - self.phase_split) * CUS_PER_UNIT if s is sm
-                              else self.phase_split * CUS_PER_UNIT)
-            r.end.record(s)
-            return
-        for s in (sh, sm):
-            for ev in deps:
-                s.wait_event(ev)
-        first = sh if seq and seq[0][0].kind != "gemm" else sm
-        r.start.record(first)
-        prev = first
-        for o, t in seq:
-            s = sm if o.kind == "gemm" else sh
-            if s is not prev:
-                ev = torch.cuda.Event()
-                ev.record(prev)
-                s.wait_event(ev)
-                prev = s
-            if o.kind == "gemm":
-                a, bt, bias, c = t
-                loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=s,
-                             cu_budget=(self.units - self.phase_split) * CUS_PER_UNIT)
-            else:
-                x, y, z = t
-                loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=s)
-        r.end.record(prev)
-
     def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:
-        h = None
-        if self.xcd_confine and not r.masked:
-            from .. import _native
-            h = _native.hip(required=True)
-            h.set_xcd_mask(((1 << r.n_units) - 1) << r.first_unit)
-            h.set_gemm_tile(10)
-        try:
-            for _ in range(r.iters):
-                for o, t in bufs.ops:
-                    if o.kind == "gemm":
-                        a, bt, bias, c = t
-                        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
-                    else:
-                        x, y, z = t
-                        loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
-        finally:
-            if h is not None:
-                h.set_xcd_mask(0)
-                h.set_gemm_tile(0)
+        for _ in range(r.iters):
+            for o, t in bufs.ops:
+                if o.kind == "gemm":
+                    a, bt, bias, c = t
+                    loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+                else:
+                    x, y, z = t
+                    loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
 
     def _graph_for(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> "torch.cuda.CUDAGraph":
         """One HIP graph per (workload, unit slot, QoS, iters): captured on the pod's own
         stream, so replaying it there keeps the stream's CU mask and its ordering."""
-        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks, self.xcd_confine)
+        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks)
         g = self._graphs.get(k)
         if g is None:
             torch.cuda.synchronize(self.device)
@@ -229,29 +150,13 @@ class DeviceExecutor:
         pod of the epoch completes (work-conserving), while two pods never overlap on the
         same CUs -- exactly the ledger's capacity model."""
         for r in runs:
-            split = self.phase_split > 0 and not r.masked
-            key = (r.first_unit, r.n_units, r.masked, split)
+            key = (r.first_unit, r.n_units, r.masked)
             w = CATALOG[r.workload]
             bufs = self.buffers(w, r.first_unit, r.n_units)
             budget = self._budget(r)
             r.start = torch.cuda.Event(enable_timing=True)
             r.end = torch.cuda.Event(enable_timing=True)
-            if split:
-                # the pod's end event is on whichever class stream ran its last op, and the
-                # other stream's tail is ordered before it by the switch events
-                deps, seen = [], set()
-                for u in range(r.first_unit, r.first_unit + r.n_units):
-                    last = self._unit_last.get(u)
-                    if last is not None and id(last[1]) not in seen:
-                        deps.append(last[1])
-                        seen.add(id(last[1]))
-                self._enqueue_split(r, bufs, budget, deps)
-                for u in range(r.first_unit, r.first_unit + r.n_units):
-                    self._unit_last[u] = (key, r.end)
-                self.flops_done += w.flops * r.iters
-                self.bytes_done += w.bytes * r.iters
-                continue
-            st = self.stream_for(*key[:3]).stream
+            st = self.stream_for(*key).stream
             waited = set()
             for u in range(r.first_unit, r.first_unit + r.n_units):
                 last = self._unit_last.get(u)
@@ -311,15 +216,6 @@ class DeviceExecutor:
         for s in self._streams.values():
             s.close()
         self._streams.clear()
-
-
-class _StreamPair:
-    def __init__(self, hbm, mfma):
-        self.hbm, self.mfma = hbm, mfma
-
-    def close(self) -> None:
-        self.hbm.close()
-        self.mfma.close()
 
 
 class _PlainStream:

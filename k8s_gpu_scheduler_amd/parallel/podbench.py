@@ -468,7 +468,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
-    ap.add_argument("--gemm-policy", type=int, default=1, choices=[0, 1, 2, 3, 4],
+    ap.add_argument("--gemm-policy", type=int, default=1, choices=[0, 1, 2],
                     help="GEMM tile policy: 1 (default) 8-phase 256x256 also for co-running pods it fills, 0 128x128 for co-running pods")
     ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],
                     help="GEMM epilogue (A/B knob): 1 LDS-staged 16-B row stores, 0 scattered 8-B stores")
@@ -480,18 +480,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="GEMM tile order: each XCD takes a near-square block of output tiles (1) or a "
                          "tall GROUP_M strip (0)")
     ap.add_argument("--xcd-group", type=int, default=4, help="tile rows per group inside an XCD block")
-    ap.add_argument("--xcd-confine", type=int, default=0, choices=[0, 1],
-                    help="study: each Burstable pod's kernels confined to the XCDs of its unit slot")
-    ap.add_argument("--c-nt", type=int, default=0, choices=[0, 1], help="study: non-temporal GEMM output stores")
     ap.add_argument("--gemm-share", type=int, default=1, choices=[0, 1],
                     help="1: the GEMM tile picker sizes a pod's GEMMs for its CU share (co-running pods fill the "
                          "rest); 0: for the whole chip")
-    ap.add_argument("--unit-rotate", type=int, default=0, choices=[0, 1],
-                    help="study knob: rotate each epoch's CU-slice slots on the executor (the scheduler's "
-                         "first-fit gives the longest pod of every epoch the same slot)")
-    ap.add_argument("--slot-balance", type=int, default=0, choices=[0, 1],
-                    help="study knob: the executor maps each epoch's pods (longest predicted first) onto the "
-                         "CU-slice slots with the least predicted backlog (per-workload EMA of measured pod time)")
     ap.add_argument("--prewarm-ms", type=float, default=300.0,
                     help="untimed device warm-up before the warm-up epochs: this long of back-to-back MFMA "
                          "GEMMs.  It does not change pods/s (interleaved A/B, profiles/r02_prewarm_ab.txt) but "
@@ -499,9 +490,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
-    ap.add_argument("--triad-aux", type=int, default=2, choices=(0, 1, 2, 3, 16, 17, 18, 19),
-                    help="cache-policy bits of --triad-variant 5 (buffer instructions): sc0 1, nt 2, sc1 16")
-    ap.add_argument("--triad-variant", type=int, default=6, choices=range(7),
+    ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 6),
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
                     help="amd-smi activity sampling period across warmup + timed region (0 = off)")
@@ -583,12 +572,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
         _native.hip(required=True).set_xcd_blocks(a.xcd_blocks)
         _native.hip(required=True).set_xcd_group(a.xcd_group)
-        _native.hip(required=True).set_c_nontemporal(a.c_nt)
         _native.hip(required=True).set_triad_variant(a.triad_variant)
-        _native.hip(required=True).set_triad_aux(a.triad_aux)
         ex.triad_blocks = a.triad_blocks
         ex.gemm_share = bool(a.gemm_share)
-        ex.xcd_confine = bool(a.xcd_confine)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
     smi_s = None
@@ -650,11 +636,6 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         if timed:
             state["collected"] = state.get("collected", 0) + 1
         st = ex.collect(runs)
-        if a.slot_balance:
-            est = state.setdefault("est_ms", {})
-            for r in runs:
-                if r.ms > 0:
-                    est[r.workload] = 0.7 * est.get(r.workload, r.ms) + 0.3 * r.ms
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
         smi_vec = [-1.0, -1.0]
         if smi_s is not None:
@@ -702,23 +683,6 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             runs: List[Any] = []
             for g in gpus_here:
                 runs += _runs_for(arr, g)
-            if a.slot_balance and runs and all(r.n_units == 2 for r in runs):
-                now = time.perf_counter() * 1e3
-                bl = state.setdefault("backlog", [0.0] * (UNITS_PER_GPU // 2))
-                dt = now - state.get("bl_t", now)
-                state["bl_t"] = now
-                bl[:] = [max(0.0, b - dt) for b in bl]
-                est = state.setdefault("est_ms", {})
-                order = sorted(runs, key=lambda r: -est.get(r.workload, 5.0))
-                for r in order:
-                    k = min(range(len(bl)), key=lambda i: bl[i])
-                    r.first_unit = 2 * k
-                    bl[k] += est.get(r.workload, 5.0)
-            if a.unit_rotate:
-                shift = 2 * (state.setdefault("epochs", 0) % (UNITS_PER_GPU // 2))
-                for r in runs:
-                    if UNITS_PER_GPU % max(r.n_units, 1) == 0 and shift % max(r.n_units, 1) == 0:
-                        r.first_unit = (r.first_unit + shift) % UNITS_PER_GPU
             state["epochs"] = state.get("epochs", 0) + 1
             t1 = time.perf_counter()
             if rank == 0 and async_cp:

@@ -36,10 +36,7 @@ void set_gemm_policy(int p);
 void set_wide_epilogue(int on);
 void set_xcd_blocks(int on);
 void set_xcd_group(int rows);
-void set_c_nontemporal(int on);
-void set_xcd_mask(int mask);
 void xcd_probe(uintptr_t out, int blocks, uintptr_t stream);
-void set_triad_aux(int aux);
 int pick_xcd_map(int tiles_m, int tiles_n);
 int pick_gemm_tile(int M, int N, int cu_budget);
 std::vector<int> peer_access_matrix();

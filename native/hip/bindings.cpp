@@ -67,10 +67,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_wide_epilogue", &gs::set_wide_epilogue, py::arg("on"));
   m.def("set_xcd_blocks", &gs::set_xcd_blocks, py::arg("on"));
   m.def("set_xcd_group", &gs::set_xcd_group, py::arg("rows"));
-  m.def("set_c_nontemporal", &gs::set_c_nontemporal, py::arg("on"));
-  m.def("set_xcd_mask", &gs::set_xcd_mask, py::arg("mask"));
   m.def("xcd_probe", &gs::xcd_probe, py::arg("out"), py::arg("blocks"), py::arg("stream"));
-  m.def("set_triad_aux", &gs::set_triad_aux, py::arg("aux"));
   m.def("pick_xcd_map", &gs::pick_xcd_map, py::arg("tiles_m"), py::arg("tiles_n"));
   m.def("pick_gemm_tile", &gs::pick_gemm_tile, py::arg("M"), py::arg("N"), py::arg("cu_budget") = 0);
   m.def("peer_access_matrix", &gs::peer_access_matrix);

@@ -20,11 +20,11 @@
 //  * stream_triad -- a = b + s*c over float4 (16 B/lane) -- the HBM-bound pod phase.
 //
 // Launch settings (set_gemm_policy, set_gemm_tile, set_split_k, set_wide_epilogue,
-// set_xcd_blocks, set_xcd_group, set_c_nontemporal, set_xcd_mask, set_triad_variant,
-// set_triad_aux) are process-wide values read on the launching host thread when a kernel is
+// set_xcd_blocks, set_xcd_group, set_triad_variant) are process-wide values read on the launching host thread when a kernel is
 // enqueued (a captured HIP graph keeps the values of its capture).  One host thread per rank
 // launches every pod kernel (parallel.executor), so they are plain statics; the defaults are
-// the measured winners, the rest are A/B knobs whose results are recorded in profiles/.
+// the measured winners; every selectable variant computes the same result (GPU-tested against
+// fp32 PyTorch), the rest of the A/B record lives in profiles/.
 #include <algorithm>
 #include <cstdint>
 
@@ -105,26 +105,12 @@ __device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld,
   }
 }
 
-// ---- XCD confinement (study) -------------------------------------------------------------
-// A pod's kernel may be confined to a set of XCDs (8-bit mask over the block residues b % 8):
-// workgroups of other residues exit at once, the rest share the work, so the pod's GEMM operand
-// strips live in only its own XCDs' L2s -- a software QPX partition.  Residue r runs on XCD
-// (r + rot) % 8 for a rotation that depends on earlier dispatches, so concurrently launched
-// pods' masks are disjoint only in residue space (a study; measured and rejected,
-// profiles/r02_xcd_confine_rejected.json).
+// XCC id of the executing workgroup (HW_REG_XCC_ID): tests/test_gpu_native.py reads it through
+// xcd_probe to check the round-robin block -> XCD dispatch the tile order relies on.
 __device__ __forceinline__ int xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xF; }
 
 __global__ void xcd_probe_kernel(int* out) {
   if (threadIdx.x == 0) out[blockIdx.x] = xcc_id();
-}
-
-// confined block -> (participant index, participants), -1 when this block sits out
-__device__ __forceinline__ int xcd_part(int xmask, int& nparts) {
-  const int slot = blockIdx.x % kXcds;
-  const int nx = __popc(xmask);
-  nparts = (gridDim.x / kXcds) * nx;
-  if (!((xmask >> slot) & 1)) return -1;
-  return (blockIdx.x / kXcds) * nx + __popc(xmask & ((1 << slot) - 1));
 }
 
 template <int KT = BK>
@@ -169,8 +155,7 @@ __device__ __forceinline__ void wide_put(char* img, int row, int col, bf16x4 o) 
 }
 
 template <int BM, int BN, int NT>
-__device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__ C, int ldc, int m0, int n0,
-                                           bool nt = false) {
+__device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__ C, int ldc, int m0, int n0) {
   constexpr int MASK = (BN / 8 - 1) < 15 ? (BN / 8 - 1) : 15;
   constexpr int CPR = BN / 8;                           // 16-B chunks per row
   static_assert(BM * CPR % NT == 0, "wide epilogue split");
@@ -179,11 +164,7 @@ __device__ __forceinline__ void wide_store(const char* img, __bf16* __restrict__
     const int id = k * NT + (int)threadIdx.x;
     const int row = id / CPR, c = id % CPR;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * (BN * 2) + ((c ^ (row & MASK)) << 4));
-    bf16x8* dst = reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8);
-    if (nt)                                             // xmap bit 16: streaming C stores (study)
-      __builtin_nontemporal_store(v, dst);
-    else
-      *dst = v;
+    *reinterpret_cast<bf16x8*>(C + (size_t)(m0 + row) * ldc + n0 + c * 8) = v;
   }
 }
 
@@ -320,7 +301,7 @@ gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
       }
     }
     __syncthreads();
-    wide_store<BM, BN, NT>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
+    wide_store<BM, BN, NT>(smem, C, ldc, m0, n0);
     return;
   }
 
@@ -506,23 +487,7 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     Bt += (size_t)split * K;
   }
   int tm, tn;
-  const int xmask = (xmap >> 24) & 0xFF;
-  if (xmask) {
-    // confined: allowed XCD r (rank among the mask) takes row band r of the tile grid (host:
-    // tiles_m % popcount(mask) == 0, grid = 8 x band tiles), GROUP_M-grouped inside
-    const int slot = b % kXcds;
-    if (!((xmask >> slot) & 1)) return;
-    const int nx = __popc(xmask), rank = __popc(xmask & ((1 << slot) - 1));
-    const int tiles_n = N / 256, band = (M / 256) / nx;
-    const int l = b / kXcds;
-    if (l >= band * tiles_n) return;
-    const int per_group = 4 * tiles_n;
-    const int g = l / per_group, gsize = min(band - g * 4, 4), r = l - g * per_group;
-    tm = rank * band + g * 4 + r % gsize;
-    tn = r / gsize;
-  } else {
-    tile_coords(b, nwg, M / 256, N / 256, xmap, tm, tn);
-  }
+  tile_coords(b, nwg, M / 256, N / 256, xmap, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -703,7 +668,7 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
           }
       }
     __syncthreads();
-    wide_store<256, 256, 512>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
+    wide_store<256, 256, 512>(smem, C, ldc, m0, n0);
     return;
   }
 
@@ -727,354 +692,6 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
           *reinterpret_cast<bf16x4*>(C + (size_t)row * ldc + col) = o;
         }
     }
-}
-
-// ---------------------------------------------------------------------------------------
-// 256x256 "one wave per SIMD" GEMM (tiles 11 / 12, study against the 8-phase kernel): 4 waves
-// as 2 x 2, each owning a 128x128 output block = 8 x 8 MFMA 16x16 tiles (256 fp32 accumulators,
-// AGPR-resident).  PMC of hipBLASLt's MT256x256x64 kernel at 8192^3 (4 waves, 128x128 wave
-// tiles; profiles/r02_gemm_clock_8192.json) shows what the bigger wave tile buys: 34 % fewer
-// LDS instructions per FLOP than the 8-phase kernel's 128x64 wave tiles and 4.7 % vs 29 %
-// of wave cycles waiting, 88 % vs 79 % MFMA-busy per SIMD at the same clock.
-// K-tile KT = 32 (16 KiB per operand), S LDS stages (128 KiB for S = 4).  Iteration t:
-//   MFMAs of rows 0-3 of tile t (fragments already in registers)
-//   lgkmcnt(0); counted vmcnt (tile t+1 landed: tiles t+2 .. t+S-1 may stay in flight); barrier
-//   glds of tile t+S into tile t's buffer (every wave finished reading it before the barrier)
-//   ds_reads of tile t+1's fragments into the other register slot
-//   MFMAs of rows 4-7 of tile t (hide the fragment-read and barrier latency)
-// so a K-tile's glds have S-1 iterations (~(S-1) x 64 MFMAs) to land, and every LDS-DMA write is
-// read only after the issuing waves' vmcnt + a barrier the reader passed (RAW), into a buffer no
-// wave reads any more (WAR).  The wide epilogue assembles the block tile in the 128 KiB.
-// PROBE (timing-only study arms, wrong results): 1 = no barrier in the steady-state loop,
-// 2 = no barrier and no vmcnt wait there either.
-template <bool RELU, bool BIAS, int S, int PROBE = 0>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
-gemm_bf16_nt_256_4w(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
-                    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
-  constexpr int KT = 32;
-  constexpr int OPB = 256 * KT * 2;                // bytes of one operand's K-tile image
-  constexpr int BUF = 2 * OPB;                     // A then B
-  constexpr int G = 2 * 256 * KT * 2 / 16 / 256;   // glds per thread per K-tile (8)
-  static_assert(S >= 2 && S * BUF <= 128 * 1024, "stages");
-  __shared__ __attribute__((aligned(16))) char smem[128 * 1024];
-
-  int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, M / 256, N / 256, xmap, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int frow = lane & 15, fk = lane >> 4;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ra[2][8], rb[2][8];
-
-  const int T = K / KT;
-  // LDS-DMA through buffer_load ... lds: the per-lane byte offset (row, swizzled chunk: the
-  // stage_tile image) is one VGPR fixed for the whole K loop -- row-group and K-tile offsets go
-  // in the scalar soffset -- so the 16 loads of a K-tile hold no 64-bit address registers (the
-  // global_load_lds form spilled at 256 accumulators + 2 fragment slots).
-  constexpr int CH = KT / 8, RPI = 256 / CH;       // 16-B chunks per row, rows per load
-  const int tid = threadIdx.x, r = tid / CH;
-  const unsigned voff_a = (unsigned)(r * lda * 2 + (((tid % CH) ^ ((r >> 1) % CH)) * 16));
-  const unsigned voff_b = (unsigned)(r * ldb * 2 + (((tid % CH) ^ ((r >> 1) % CH)) * 16));
-  const __amdgpu_buffer_rsrc_t rsa =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(Bt + (size_t)n0 * ldb), 0, 256 * ldb * 2, 0x00020000);
-  auto stage = [&](int u) {
-    char* buf = smem + (u % S) * BUF;
-#pragma unroll
-    for (int i = 0; i < 256 * KT * 2 / 16 / 256; ++i) {
-      char* dst = buf + (i * 256 + wave * 64) * 16;            // wave-uniform base
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)dst, 16, voff_a, i * RPI * lda * 2 + u * KT * 2, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(dst + OPB), 16, voff_b, i * RPI * ldb * 2 + u * KT * 2, 0, 0);
-    }
-  };
-  auto read = [&](int u, bf16x8 (&a)[8], bf16x8 (&b)[8]) {
-    const char* buf = smem + (u % S) * BUF;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = lds_frag<KT>(buf + OPB, wc * 128 + j * 16 + frow, fk);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = lds_frag<KT>(buf, wr * 128 + i * 16 + frow, fk);
-  };
-  auto mfma_rows = [&](int i0, const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
-#pragma unroll
-    for (int i = i0; i < i0 + 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        // AGPR-pinned, tied accumulator: with the builtin the compiler's AGPR-form MFMAs here
-        // renamed every accumulator through v_accvgpr_read/write copies (~4 per MFMA)
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b[j]), "v"(a[i]));
-  };
-  auto barrier = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto mfma1 = [&](int i, int j, const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b[j]), "v"(a[i]));
-  };
-  // Steady-state halves with the memory work spread between MFMAs: one wave per SIMD has no
-  // partner wave to issue MFMAs while it stalls on a load issue, so each group of 4 MFMAs is
-  // followed by one LDS-DMA load and two fragment reads (sched_barrier pins the order).
-  // First half: rows 0-3, column-major so the fragments read last (b[7]) are needed last.
-  auto half1 = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) mfma1(i, j, a, b);
-  };
-  auto half2 = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[8], int us, int ur, bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
-    char* sbuf = smem + (us % S) * BUF;
-    const char* rbuf = smem + (ur % S) * BUF;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-#pragma unroll
-      for (int i = 4; i < 8; ++i) mfma1(i, q, a, b);
-      const int c = q & 3;
-      char* dst = sbuf + (q >= 4 ? OPB : 0) + (c * 256 + wave * 64) * 16;
-      if (q < 4)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)dst, 16, voff_a, c * RPI * lda * 2 + us * KT * 2, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)dst, 16, voff_b, c * RPI * ldb * 2 + us * KT * 2, 0, 0);
-      // next tile's fragments: a[0..3] and b[0..3] in the first four groups (half1 needs them first)
-      na[q] = lds_frag<KT>(rbuf, wr * 128 + q * 16 + frow, fk);
-      nb[q] = lds_frag<KT>(rbuf + OPB, wc * 128 + q * 16 + frow, fk);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // vmcnt at iteration t: tiles t+2 .. min(T-1, t+S-1) may stay in flight
-  auto wait_tile = [&](int t) {
-    const int n = max(0, min(T - 1, t + S - 1) - (t + 1));
-    if (n >= 2) wait_vmcnt<2 * G>();
-    else if (n == 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
-  };
-  // lgkmcnt(0) (vmcnt / expcnt fields at their no-wait maxima)
-  auto wait_lds = [] { __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4)); };
-
-#pragma unroll
-  for (int u = 0; u < S; ++u)
-    if (u < T) stage(u);
-  // tile 0 landed: tiles 1 .. min(T, S) - 1 may stay in flight
-  {
-    const int n = min(T, S) - 1;
-    if (n >= 3) wait_vmcnt<3 * G>();
-    else if (n == 2) wait_vmcnt<2 * G>();
-    else if (n == 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
-  }
-  barrier();
-  read(0, ra[0], rb[0]);
-
-  // two K-tiles per trip so the register slots are compile-time
-  int t = 0;
-  {
-    // steady state: every iteration restages and tiles t+2 .. t+S-1 stay in flight
-    for (; t + S + 1 < T; t += 2) {
-      half1(ra[0], rb[0]);
-      wait_lds();
-      if (PROBE < 2) wait_vmcnt<(S - 2) * G>();
-      if (PROBE < 1) barrier();
-      half2(ra[0], rb[0], t + S, t + 1, ra[1], rb[1]);
-
-      half1(ra[1], rb[1]);
-      wait_lds();
-      if (PROBE < 2) wait_vmcnt<(S - 2) * G>();
-      if (PROBE < 1) barrier();
-      half2(ra[1], rb[1], t + 1 + S, t + 2, ra[0], rb[0]);
-    }
-  }
-  for (; t < T; t += 2) {
-    mfma_rows(0, ra[0], rb[0]);
-    wait_lds();
-    wait_tile(t);
-    barrier();
-    if (t + S < T) stage(t + S);
-    if (t + 1 < T) read(t + 1, ra[1], rb[1]);
-    mfma_rows(4, ra[0], rb[0]);
-    if (t + 1 >= T) break;
-    mfma_rows(0, ra[1], rb[1]);
-    wait_lds();
-    wait_tile(t + 1);
-    barrier();
-    if (t + 1 + S < T) stage(t + 1 + S);
-    if (t + 2 < T) read(t + 2, ra[0], rb[0]);
-    mfma_rows(4, ra[1], rb[1]);
-  }
-  // every wave past its last LDS read and every LDS-DMA retired (the last wait was vmcnt(0));
-  // the s_nops cover the MFMA-result -> VALU-read latency the hazard pass cannot see in asm
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-  barrier();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = wc * 128 + j * 16 + fk * 4;
-    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      f32x4 v = acc[i][j] + bv;
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
-      wide_put<256>(smem, wr * 128 + i * 16 + frow, col, o);
-    }
-  }
-  __syncthreads();
-  wide_store<256, 256, 256>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
-}
-
-// Register-staged variant (tile 15): the LDS-DMA piece costs its wave 60-185 issue cycles among
-// MFMAs (MI355X_MICROARCH.md, LDS-DMA issue cost), which one wave per SIMD cannot hide, so here
-// every K-tile goes global -> VGPRs (buffer_load_dwordx4, issued two K-tiles ahead: two register
-// buffers of 8 x 16 B) -> LDS (ds_write_b128 into the swizzled image lds_frag reads), hipBLASLt's
-// "prefetch global read 2" shape.  Iteration t (LDS buffer t % 2 holds tile t, its fragments are
-// in register slot t & 1):
-//   rows 0-3 MFMAs, with the ds_writes of tile t+1 (registers R[(t+1) & 1]) into buffer (t+1) % 2
-//     (free: tile t-1's fragment reads retired before the previous barrier)
-//   lgkmcnt(0) (tile t+1 written, tile t's reads done); barrier
-//   rows 4-7 MFMAs, with tile t+1's fragment reads and the global loads of tile t+3 into R[(t+1) & 1]
-// vmcnt(8) before the ds_writes of tile t+1 leaves only tile t+2's 8 loads in flight.
-template <bool RELU, bool BIAS>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
-gemm_bf16_nt_256_4wr(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
-                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
-  constexpr int KT = 32;
-  constexpr int OPB = 256 * KT * 2;                // bytes of one operand's K-tile image
-  constexpr int BUF = 2 * OPB;                     // A then B
-  __shared__ __attribute__((aligned(16))) char smem[128 * 1024];
-
-  int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, M / 256, N / 256, xmap, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int frow = lane & 15, fk = lane >> 4;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ra[2][8], rb[2][8];
-  f32x4 rg[2][8];                                  // staged K-tiles: [buffer][A chunks 0-3, B chunks 0-3]
-
-  const int T = K / KT;
-  // thread -> (row tid / 4 + 64 c, logical 16-B chunk tid % 4) of every K-tile, c = 0..3
-  const int tid = threadIdx.x, r = tid >> 2, kc = tid & 3;
-  const unsigned voff_a = (unsigned)(r * lda * 2 + kc * 16);
-  const unsigned voff_b = (unsigned)(r * ldb * 2 + kc * 16);
-  const int wofs = r * (KT * 2) + ((kc ^ ((r >> 1) & 3)) << 4);   // swizzled LDS byte offset
-  const __amdgpu_buffer_rsrc_t rsa =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(Bt + (size_t)n0 * ldb), 0, 256 * ldb * 2, 0x00020000);
-  auto gload = [&](int u, int q, f32x4 (&g)[8]) {  // q: A chunks 0-3, B chunks 4-7
-    const int c = q & 3;
-    if (q < 4)
-      g[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, voff_a, c * 64 * lda * 2 + u * KT * 2, 0));
-    else
-      g[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsb, voff_b, c * 64 * ldb * 2 + u * KT * 2, 0));
-  };
-  auto lwrite = [&](int u, int q, const f32x4 (&g)[8]) {
-    char* buf = smem + (u & 1) * BUF + (q < 4 ? 0 : OPB);
-    *reinterpret_cast<f32x4*>(buf + (q & 3) * 64 * (KT * 2) + wofs) = g[q];
-  };
-  auto frag_a = [&](int u, int i) { return lds_frag<KT>(smem + (u & 1) * BUF, wr * 128 + i * 16 + frow, fk); };
-  auto frag_b = [&](int u, int j) { return lds_frag<KT>(smem + (u & 1) * BUF + OPB, wc * 128 + j * 16 + frow, fk); };
-  auto mfma1 = [&](int i, int j, const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b[j]), "v"(a[i]));
-  };
-  auto barrier = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto wait_lds = [] { __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4)); };
-  // one K-tile step; W / L / R = ds_write tile t+1 / global-load tile t+3 / read tile t+1 frags
-  auto step = [&](int t, bf16x8 (&a)[8], bf16x8 (&b)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], f32x4 (&gw)[8],
-                  bool W, bool L, bool R, bool more) {
-    if (more) wait_vmcnt<8>(); else wait_vmcnt<0>();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) mfma1(i, q, a, b);
-      if (W) lwrite(t + 1, q, gw);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    wait_lds();
-    barrier();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-#pragma unroll
-      for (int i = 4; i < 8; ++i) mfma1(i, q, a, b);
-      if (L) gload(t + 3, q, gw);
-      if (R) {
-        na[q] = frag_a(t + 1, q);
-        nb[q] = frag_b(t + 1, q);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  // prologue: tiles 0, 1 -> registers; tile 0 -> LDS; tile 2 -> registers; tile 0 fragments
-#pragma unroll
-  for (int q = 0; q < 8; ++q) gload(0, q, rg[0]);
-  if (T > 1) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) gload(1, q, rg[1]);
-    wait_vmcnt<8>();
-  } else {
-    wait_vmcnt<0>();
-  }
-#pragma unroll
-  for (int q = 0; q < 8; ++q) lwrite(0, q, rg[0]);
-  if (T > 2) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) gload(2, q, rg[0]);
-  }
-  wait_lds();
-  barrier();
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    ra[0][q] = frag_a(0, q);
-    rb[0][q] = frag_b(0, q);
-  }
-
-  int t = 0;
-  for (; t + 4 < T; t += 2) {                      // steady state: every step writes, loads and reads
-    step(t, ra[0], rb[0], ra[1], rb[1], rg[1], true, true, true, true);
-    step(t + 1, ra[1], rb[1], ra[0], rb[0], rg[0], true, true, true, true);
-  }
-  for (; t < T; t += 2) {
-    step(t, ra[0], rb[0], ra[1], rb[1], rg[1], t + 1 < T, t + 3 < T, t + 1 < T, t + 2 < T);
-    if (t + 1 >= T) break;
-    step(t + 1, ra[1], rb[1], ra[0], rb[0], rg[0], t + 2 < T, t + 4 < T, t + 2 < T, t + 3 < T);
-  }
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-  barrier();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = wc * 128 + j * 16 + fk * 4;
-    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      f32x4 v = acc[i][j] + bv;
-      bf16x4 o;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) o[rr] = (__bf16)(RELU ? (v[rr] > 0.f ? v[rr] : 0.f) : v[rr]);
-      wide_put<256>(smem, wr * 128 + i * 16 + frow, col, o);
-    }
-  }
-  __syncthreads();
-  wide_store<256, 256, 256>(smem, C, ldc, m0, n0, (xmap >> 16) & 1);
 }
 
 // C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
@@ -1148,88 +765,10 @@ __global__ void __launch_bounds__(256) stream_triad_u(float4* __restrict__ a_, c
   }
 }
 
-// Buffer-instruction variant with an explicit cache policy (AUX = the gfx950 CPol bits of the
-// raw buffer builtins: 1 = sc0, 2 = nt, 16 = sc1): the study of how the co-running streams'
-// lines share the XCD L2 and the MALL with the GEMMs' operand strips (variant 5 + aux).
-// Buffer byte offsets are 32-bit: arrays up to 4 GiB (checked on the host).
-template <int U, int AUX>
-__global__ void __launch_bounds__(256) stream_triad_buf(float4* __restrict__ a_, const float4* __restrict__ b_,
-                                                        const float4* __restrict__ c_, float s, size_t n4) {
-  const unsigned bytes = (unsigned)(n4 * 16);
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(a_, 0, bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)b_, 0, bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)c_, 0, bytes, 0x00020000);
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const size_t tile = (size_t)blockDim.x * U;
-  const size_t step = (size_t)gridDim.x * tile;
-  for (size_t base = (size_t)blockIdx.x * tile + threadIdx.x; base < n4; base += step) {
-    f32x4 x[U], y[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const size_t i = base + (size_t)k * blockDim.x;
-      if (i < n4) {
-        x[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)(i * 16), 0, AUX));
-        y[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (unsigned)(i * 16), 0, AUX));
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const size_t i = base + (size_t)k * blockDim.x;
-      if (i < n4) {
-        const f32x4 r = x[k] + s * y[k];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), ra, (unsigned)(i * 16), 0, AUX);
-      }
-    }
-  }
-}
-
-template <int U>
-__global__ void __launch_bounds__(256) stream_triad_xcd(float4* __restrict__ a_, const float4* __restrict__ b_,
-                                                        const float4* __restrict__ c_, float s, size_t n4, int xmask) {
-  int nparts;
-  const int part = xcd_part(xmask, nparts);
-  if (part < 0) return;
-  auto a = reinterpret_cast<f32x4*>(a_);
-  auto b = reinterpret_cast<const f32x4*>(b_);
-  auto c = reinterpret_cast<const f32x4*>(c_);
-  const size_t tile = (size_t)blockDim.x * U;
-  const size_t step = (size_t)nparts * tile;
-  for (size_t base = (size_t)part * tile + threadIdx.x; base < n4; base += step) {
-    f32x4 x[U], y[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const size_t i = base + (size_t)k * blockDim.x;
-      if (i < n4) {
-        x[k] = __builtin_nontemporal_load(b + i);
-        y[k] = __builtin_nontemporal_load(c + i);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const size_t i = base + (size_t)k * blockDim.x;
-      if (i < n4) __builtin_nontemporal_store(x[k] + s * y[k], a + i);
-    }
-  }
-}
-
-static int g_triad_aux = 2;
-static int g_xcd_mask = 0;          // study: confine GEMMs / stream kernels to these XCDs (0 = all)
-
-void set_xcd_mask(int mask) {
-  if (mask < 0 || mask > 0xFF) throw std::runtime_error("xcd mask must be 8 bits");
-  g_xcd_mask = mask == 0xFF ? 0 : mask;
-}
-
 void xcd_probe(uintptr_t out, int blocks, uintptr_t stream) {
   hipLaunchKernelGGL(xcd_probe_kernel, dim3(blocks), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<int*>(out));
   HIP_CHECK(hipGetLastError());
-}
-
-void set_triad_aux(int aux) {
-  if (aux != 0 && aux != 1 && aux != 2 && aux != 3 && aux != 16 && aux != 17 && aux != 18 && aux != 19)
-    throw std::runtime_error("triad aux must be a combination of sc0 (1), nt (2), sc1 (16)");
-  g_triad_aux = aux;
 }
 
 // 6 = auto: working set (3 arrays) <= 96 MiB -> cached 2x-unrolled loads (the stream
@@ -1238,7 +777,7 @@ void set_triad_aux(int aux) {
 static int g_triad_variant = 6;
 
 void set_triad_variant(int v) {
-  if (v < 0 || v > 6) throw std::runtime_error("triad variant must be 0..6");
+  if (v < 0 || v > 6 || v == 5) throw std::runtime_error("triad variant must be 0..4 or 6 (auto)");
   g_triad_variant = v;
 }
 
@@ -1269,10 +808,6 @@ static void launch_gemm_v(const __bf16* A, const __bf16* B, __bf16* Cp, const fl
 // the whole grid (A/B knob).
 static int g_xcd_blocks = 1;
 static int g_xcd_group = 4;         // tile rows per group inside an XCD block
-static int g_c_nt = 0;              // study: non-temporal C stores in the wide epilogue
-
-void set_c_nontemporal(int on) { g_c_nt = on ? 1 : 0; }
-
 void set_xcd_blocks(int on) { g_xcd_blocks = on ? 1 : 0; }
 
 void set_xcd_group(int rows) {
@@ -1283,8 +818,7 @@ void set_xcd_group(int rows) {
 // px (XCD-block rows, 8 / px columns) minimising the strips one XCD fetches, A rows + B
 // columns of its block, among the splits that divide the grid; 0 = none (legacy order).
 int pick_xcd_map(int tiles_m, int tiles_n) {
-  const int flags = g_c_nt << 16;
-  if (!g_xcd_blocks || (tiles_m * tiles_n) % kXcds) return flags;
+  if (!g_xcd_blocks || (tiles_m * tiles_n) % kXcds) return 0;
   int best = 0, best_cost = 1 << 30;
   for (int px = 1; px <= kXcds; px *= 2) {
     const int py = kXcds / px;
@@ -1292,7 +826,7 @@ int pick_xcd_map(int tiles_m, int tiles_n) {
     const int cost = tiles_m / px + tiles_n / py;
     if (cost < best_cost) best = px, best_cost = cost;
   }
-  return (best ? best | (g_xcd_group << 8) : 0) | flags;
+  return best ? best | (g_xcd_group << 8) : 0;
 }
 
 // Wide (LDS-staged, 16-B row stores) epilogue whenever C rows are 16-B aligned; g_wide_epi = 0
@@ -1317,13 +851,7 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
 template <bool PEEL, bool WIDE>
 static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                          int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
-  int xmap = pick_xcd_map(M / 256, N / 256);
-  if (g_xcd_mask) {
-    const int nx = __builtin_popcount(g_xcd_mask);
-    if ((M / 256) % nx) throw std::runtime_error("xcd-confined GEMM: tile rows must divide by the XCD count");
-    xmap = (xmap & 0x10000) | (g_xcd_mask << 24);
-    grid = dim3(kXcds * ((M / 256) / nx) * (N / 256));
-  }
+  const int xmap = pick_xcd_map(M / 256, N / 256);
   if (relu && bp)
     hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (relu)
@@ -1366,10 +894,10 @@ static int g_gemm_tile = 0;
 // non-hoisted 128x128 kept as the A/B reference.
 // 9 = 256x256 8-phase (gemm_bf16_nt_256_8ph; needs K >= 128); 10 = the same with the
 // steady-state K loop peeled (constant vmcnt, no per-phase stage conditions).
-// 11 / 12 = 256x256 with 4 waves of 128x128 (gemm_bf16_nt_256_4w), K-tile 32, 4 / 3 LDS stages
-// (wide epilogue only: falls back to tile 10 when C rows are not 16-B aligned).
-static const int kTileBM[16] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 256, 256, 256, 256, 256};
-static const int kTileBN[16] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 256, 256, 256, 256, 256};
+// (Measured and removed: a 256x256 kernel with 4 waves of 128x128 wave tiles, 3-4 LDS stages --
+// slower than the 8-phase kernel at every catalog shape, profiles/r02_gemm_4wave_study.json.)
+static const int kTileBM[11] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256};
+static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -1390,12 +918,12 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 4) throw std::runtime_error("gemm policy must be 0..4");
+  if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");
   g_gemm_policy = p;
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 15) throw std::runtime_error("gemm tile must be 0..15");
+  if (t < 0 || t > 10) throw std::runtime_error("gemm tile must be 0..10");
   g_gemm_tile = t;
 }
 
@@ -1414,11 +942,6 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
   if (alone && fits256) return g_gemm_policy == 2 ? 4 : 10;
   if (!alone && fits256 && g_gemm_policy >= 1) return 10;
-  // study policies: 3 / 4 = co-running pods also take the 8-phase 256x256 when its tiles fill
-  // half / a quarter of their CU share (fewer, more efficient blocks; other pods fill the rest)
-  if (!alone && g_gemm_policy >= 3 && M % 256 == 0 && N % 256 == 0 &&
-      (M / 256) * (N / 256) * (g_gemm_policy == 3 ? 2 : 4) >= budget)
-    return 10;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
@@ -1446,32 +969,6 @@ size_t splitk_workspace_floats(int M, int N, int K, int cu_budget) {
 void set_split_k(int s) {
   if (s < -1 || s > 8) throw std::runtime_error("split_k must be 0 (off) .. 8, or -1 (auto)");
   g_split_k = s == 1 ? 0 : s;
-}
-
-template <int S, int PROBE = 0>
-static void launch_4w(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
-                      int ldb, int ldc, bool relu, hipStream_t s) {
-  const dim3 grid((M / 256) * (N / 256)), block(256);
-  const int xmap = pick_xcd_map(M / 256, N / 256);
-  if constexpr (S == 0) {
-    if (relu && bp)
-      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<true, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-    else if (relu)
-      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<true, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-    else if (bp)
-      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<false, true>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-    else
-      hipLaunchKernelGGL((gemm_bf16_nt_256_4wr<false, false>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-  } else if (PROBE)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, false, S, PROBE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-  else if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<true, true, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-  else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<true, false, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-  else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, true, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
-  else
-    hipLaunchKernelGGL((gemm_bf16_nt_256_4w<false, false, S>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
 }
 
 template <bool RELU, bool BIAS>
@@ -1513,7 +1010,6 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     return;
   }
   int t = pick_gemm_tile(M, N, cu_budget);
-  if (t >= 11 && !wide_ok(Cp, ldc)) t = 10;
   if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
   switch (t) {
@@ -1533,11 +1029,6 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
         launch_8ph<false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
       break;
     }
-    case 11: launch_4w<4>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    case 12: launch_4w<3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    case 13: launch_4w<4, 1>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;   // timing probes
-    case 14: launch_4w<4, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
-    case 15: launch_4w<0>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;     // register-staged
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
   }
   HIP_CHECK(hipGetLastError());
@@ -1597,12 +1088,6 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
   auto B = reinterpret_cast<const float4*>(b);
   auto Cc = reinterpret_cast<const float4*>(c);
   const size_t n4 = n_floats / 4;
-  if (g_xcd_mask) {
-    blocks = (blocks + kXcds - 1) / kXcds * kXcds;
-    hipLaunchKernelGGL((stream_triad_xcd<4>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4, g_xcd_mask);
-    HIP_CHECK(hipGetLastError());
-    return;
-  }
   int variant = g_triad_variant;
   if (variant == 6) variant = (n_floats * 12 <= (size_t)96 << 20) ? 1 : 3;
   switch (variant) {
@@ -1611,16 +1096,6 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
     case 2: hipLaunchKernelGGL((stream_triad_u<4, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 3: hipLaunchKernelGGL((stream_triad_u<4, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 4: hipLaunchKernelGGL((stream_triad_u<8, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
-    case 5: {
-      if (n_floats * 4 > 0xFFFFFFFFull) throw std::runtime_error("triad variant 5: arrays above 4 GiB");
-#define GS_TRIAD_BUF(X) case X: hipLaunchKernelGGL((stream_triad_buf<4, X>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
-      switch (g_triad_aux) {
-        GS_TRIAD_BUF(0) GS_TRIAD_BUF(1) GS_TRIAD_BUF(2) GS_TRIAD_BUF(3)
-        GS_TRIAD_BUF(16) GS_TRIAD_BUF(17) GS_TRIAD_BUF(18) GS_TRIAD_BUF(19)
-      }
-#undef GS_TRIAD_BUF
-      break;
-    }
     default: hipLaunchKernelGGL((stream_triad_u<2, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
   }
   HIP_CHECK(hipGetLastError());
