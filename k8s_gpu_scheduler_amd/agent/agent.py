@@ -61,7 +61,8 @@ class NodeAgent:
                  poll_s: float = C.PROFILER_POLL_S, exporter: Any = None, telemetry: Any = None,
                  apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None,
                  health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
-                 drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1):
+                 drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1,
+                 hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc"):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -79,6 +80,11 @@ class NodeAgent:
         self._overuse_published: Optional[str] = None
         self._overuse_flagged: set = set()
         self.evict_hbm_overuse = evict_hbm_overuse
+        # slack over a pod's HBM cap before it counts as overuse: amd-smi's per-process VRAM
+        # includes the HIP runtime's own allocations (~0.3 GiB per process on MI355X), which
+        # the pod's amd.com/gpu-memory request does not -- the tolerance must cover them
+        self.hbm_tolerance_gib = hbm_tolerance_gib
+        self.host_proc = host_proc
         self.history_every = max(1, history_every)
         self._steps = 0
         self.health = health or HealthMonitor()
@@ -240,16 +246,20 @@ class NodeAgent:
             n += 1
         return n
 
-    def check_hbm(self, usage: Optional[Dict[str, Dict[str, Any]]] = None, tolerance_gib: float = 0.25,
+    def check_hbm(self, usage: Optional[Dict[str, Dict[str, Any]]] = None, tolerance_gib: Optional[float] = None,
                   evict: Optional[bool] = None) -> Dict[str, Dict[str, float]]:
         """HBM share enforcement by detection (the driver does not cap a process's VRAM the
         way MPS's CUDA_MPS_PINNED_DEVICE_MEM_LIMIT does, reference gpu_plugins.go:896-903):
         a pod whose processes hold more VRAM than its cap -- its amd.com/gpu-memory request
         (= the GPU_SCHED_HBM_LIMIT_GIB the scheduler gave it) -- is flagged in the node
         annotation `hbm-overuse`, the exporter gauge `amd_gpu_pod_hbm_overuse` and a Warning
-        event, and with `evict_hbm_overuse` deleted (its controller recreates it)."""
+        event, and with `evict_hbm_overuse` evicted through the Eviction API (PodDisruptionBudgets
+        apply; its controller recreates it).  A pod is marked handled only once its event (and,
+        when evicting, its eviction) went through, so a failed attempt is retried next step
+        while the pod keeps overusing."""
         usage = self.pod_usage() if usage is None else usage
         evict = self.evict_hbm_overuse if evict is None else evict
+        tolerance_gib = self.hbm_tolerance_gib if tolerance_gib is None else tolerance_gib
         over: Dict[str, Dict[str, float]] = {}
         for key, u in usage.items():
             pod = u.get("pod")
@@ -266,22 +276,23 @@ class NodeAgent:
                 self._overuse_published = raw
             except Exception as e:
                 log.warning("hbm-overuse annotation on %s failed: %s", self.node, e)
-            for key in set(over) - self._overuse_flagged:
-                pod = usage[key].get("pod")
-                msg = f"HBM {over[key]['used_gib']:.2f} GiB exceeds the pod's {over[key]['cap_gib']:g} GiB share"
-                log.warning("%s: %s", key, msg)
-                if pod is not None:
-                    try:
-                        self.client.create_event(pod, "GPUMemoryOveruse", msg, "Warning")
-                    except Exception:
-                        pass
-                    if evict:
-                        try:
-                            self.client.delete("pods", O.name(pod), O.namespace(pod))
-                            self.evicted.append(key)
-                        except Exception as e:
-                            log.warning("evicting %s failed: %s", key, e)
-        self._overuse_flagged = set(over)
+        handled = self._overuse_flagged & set(over)         # still over, already handled
+        for key in set(over) - self._overuse_flagged:
+            pod = usage[key].get("pod")
+            msg = f"HBM {over[key]['used_gib']:.2f} GiB exceeds the pod's {over[key]['cap_gib']:g} GiB share"
+            log.warning("%s: %s", key, msg)
+            if pod is None or self.client is None:
+                handled.add(key)
+                continue
+            try:
+                self.client.create_event(pod, "GPUMemoryOveruse", msg, "Warning")
+                if evict:
+                    self.client.evict(O.namespace(pod), O.name(pod))
+                    self.evicted.append(key)
+                handled.add(key)
+            except Exception as e:              # retried at the next step
+                log.warning("%s %s failed: %s", "evicting" if evict else "flagging", key, e)
+        self._overuse_flagged = handled
         return over
 
     # ------------------------------------------------------------------ partitions
@@ -346,14 +357,29 @@ class NodeAgent:
                 return
         self._caps_published = raw
 
+    def _is_own_process(self, host_pid: int) -> bool:
+        """Does a host PID (what amd-smi reports) belong to this agent's container?  Its PID
+        namespace hides the host PID from os.getpid(), so the match is by cgroup: the host
+        process's /host/proc/<pid>/cgroup equals our own /proc/self/cgroup.  Without the host
+        proc mount only a same-namespace PID compare is possible."""
+        if host_pid == os.getpid():
+            return True
+        try:
+            with open(os.path.join(self.host_proc, str(host_pid), "cgroup")) as f:
+                theirs = f.read()
+            with open("/proc/self/cgroup") as f:
+                mine = f.read()
+        except OSError:
+            return False
+        return bool(mine.strip()) and theirs == mine
+
     def busy_reasons(self) -> List[str]:
-        """Why the GPUs are not idle: processes in amd-smi's list (other than this agent)
-        and non-terminal GPU pods bound to the node.  Empty = safe to repartition."""
+        """Why the GPUs are not idle: processes in amd-smi's list (other than this agent's
+        own) and non-terminal GPU pods bound to the node.  Empty = safe to repartition."""
         out = []
-        me = os.getpid()
         for i, d in enumerate(self.source.devices()):
             for p in self.source.processes(i):
-                if int(p.get("pid", 0)) != me:
+                if not self._is_own_process(int(p.get("pid", 0))):
                     out.append(f"gpu{d.get('gpu', i)}: pid {p.get('pid')} ({p.get('name', '?')})")
         if self.client is not None:
             try:

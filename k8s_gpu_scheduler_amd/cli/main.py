@@ -251,6 +251,7 @@ def cmd_agent(args) -> int:
     proc_root = args.proc_root or ("/host/proc" if os.path.isdir("/host/proc") else "/proc")
     agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy,
                       evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout,
+                      hbm_tolerance_gib=args.hbm_tolerance, host_proc=proc_root,
                       pod_resolver=lambda pid: pod_of_pid(pid, proc_root))
     mgr = None
     if args.device_plugin:
@@ -407,7 +408,11 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--evict-unhealthy", action="store_true",
                    help="delete pods assigned to a GPU that turns unhealthy (controllers reschedule them)")
     s.add_argument("--evict-hbm-overuse", action="store_true",
-                   help="delete pods whose processes hold more VRAM than their amd.com/gpu-memory share")
+                   help="evict (Eviction API, PodDisruptionBudgets apply) pods whose processes hold more VRAM "
+                        "than their amd.com/gpu-memory share")
+    s.add_argument("--hbm-tolerance", type=float, default=0.5,
+                   help="GiB over a pod's HBM share before it counts as overuse; must cover the HIP runtime's "
+                        "per-process VRAM (~0.3 GiB on MI355X), which amd-smi counts and the request does not")
     s.add_argument("--proc-root", default="", help="host /proc for pid -> pod attribution (default /host/proc)")
     s.add_argument("--drain-timeout", type=float, default=300.0,
                    help="seconds a partition request waits for the GPUs to go idle before it is refused")

@@ -27,13 +27,14 @@ NAMESPACED = {"pods": True, "configmaps": True, "events": True, "leases": True,
               "persistentvolumeclaims": True, "persistentvolumes": False, "storageclasses": False,
               "csinodes": False,
               # workload owners (SelectorSpread, ServiceAffinity, PodTopologySpread system defaults)
-              "services": True, "replicationcontrollers": True, "replicasets": True, "statefulsets": True}
-KIND_OF = {"pods": "Pod", "configmaps": "ConfigMap", "events": "Event", "leases": "Lease",
+              "services": True, "replicationcontrollers": True, "replicasets": True, "statefulsets": True,
+              "poddisruptionbudgets": True}
+KIND_OF = {"poddisruptionbudgets": "PodDisruptionBudget", "pods": "Pod", "configmaps": "ConfigMap", "events": "Event", "leases": "Lease",
            "nodes": "Node", "namespaces": "Namespace", "persistentvolumeclaims": "PersistentVolumeClaim",
            "persistentvolumes": "PersistentVolume", "storageclasses": "StorageClass", "csinodes": "CSINode",
            "services": "Service", "replicationcontrollers": "ReplicationController", "replicasets": "ReplicaSet",
            "statefulsets": "StatefulSet"}
-API_VERSION_OF = {"leases": "coordination.k8s.io/v1", "storageclasses": "storage.k8s.io/v1",
+API_VERSION_OF = {"poddisruptionbudgets": "policy/v1", "leases": "coordination.k8s.io/v1", "storageclasses": "storage.k8s.io/v1",
                   "csinodes": "storage.k8s.io/v1", "replicasets": "apps/v1", "statefulsets": "apps/v1"}
 
 
@@ -46,6 +47,13 @@ class ApiError(Exception):
 class NotFound(ApiError):
     def __init__(self, message: str = ""):
         super().__init__(404, "NotFound", message)
+
+
+class TooManyRequests(ApiError):
+    """429: an eviction the pod's PodDisruptionBudget does not allow right now."""
+
+    def __init__(self, message: str = ""):
+        super().__init__(429, "TooManyRequests", message)
 
 
 class Conflict(ApiError):
@@ -100,6 +108,11 @@ class KubeClient:
         annotations without a separate PATCH."""
         raise NotImplementedError
 
+    def evict(self, namespace: str, pod_name: str, grace_period_seconds: Optional[int] = None) -> None:
+        """POST pods/eviction (policy/v1 Eviction): a delete that honours the pod's
+        PodDisruptionBudgets -- raises TooManyRequests (429) when a budget forbids it."""
+        raise NotImplementedError
+
     def watch(self, resource: str, namespace: Optional[str] = None, resource_version: str = "",
               timeout_s: Optional[float] = None) -> Iterator[WatchEvent]:
         raise NotImplementedError
@@ -145,6 +158,7 @@ class FakeCluster(KubeClient):
         self.auto_run = auto_run
         self.latency_s = 0.0
         self.bindings: List[Tuple[str, str, str]] = []
+        self.evictions: List[Tuple[str, str]] = []
         self.calls: Dict[str, int] = {}
 
     # ------------------------------------------------------------------ fault injection
@@ -329,6 +343,28 @@ class FakeCluster(KubeClient):
             self._store["pods"][k] = new
             self.bindings.append((namespace, pod_name, node_name))
             self._emit("pods", "MODIFIED", new)
+
+    def evict(self, namespace, pod_name, grace_period_seconds=None):
+        """The eviction subresource: refused (429) while a PodDisruptionBudget selecting the
+        pod has status.disruptionsAllowed == 0, else the pod is deleted and the budget's
+        allowance drops by one (the disruption controller would recompute it)."""
+        with self._lock:
+            self._maybe_fail("evict", "pods")
+            pod = self._store["pods"].get(self._k("pods", pod_name, namespace))
+            if pod is None:
+                raise NotFound(f"pods {namespace}/{pod_name}")
+            budgets = [b for b in self._store["poddisruptionbudgets"].values()
+                       if O.namespace(b) == namespace
+                       and match_label_selector(O.labels(pod), (b.get("spec") or {}).get("selector") or {})]
+            for b in budgets:
+                if int((b.get("status") or {}).get("disruptionsAllowed", 0)) <= 0:
+                    raise TooManyRequests(f"Cannot evict pod as it would violate the pod's disruption budget "
+                                          f"{O.name(b)}")
+            for b in budgets:
+                st = b.setdefault("status", {})
+                st["disruptionsAllowed"] = int(st.get("disruptionsAllowed", 0)) - 1
+            self.evictions.append((namespace, pod_name))
+        self.delete("pods", pod_name, namespace, grace_period_seconds)
 
     def set_pod_phase(self, namespace: str, pod_name: str, phase: str) -> Obj:
         return self.patch("pods", pod_name, {"status": {"phase": phase}}, "merge", namespace)

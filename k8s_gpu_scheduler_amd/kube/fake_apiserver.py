@@ -19,9 +19,10 @@ from .client import ApiError, FakeCluster
 
 _CORE = re.compile(r"^/api/v1(?:/namespaces/(?P<ns>[^/]+))?/(?P<res>pods|nodes|configmaps|events|namespaces|"
                    r"persistentvolumeclaims|persistentvolumes|services|replicationcontrollers)"
-                   r"(?:/(?P<name>[^/]+))?(?:/(?P<sub>binding|status))?$")
-_COORD = re.compile(r"^/apis/(?:coordination\.k8s\.io|storage\.k8s\.io|apps)/v1(?:/namespaces/(?P<ns>[^/]+))?/"
-                    r"(?P<res>leases|storageclasses|csinodes|replicasets|statefulsets)(?:/(?P<name>[^/]+))?$")
+                   r"(?:/(?P<name>[^/]+))?(?:/(?P<sub>binding|status|eviction))?$")
+_COORD = re.compile(r"^/apis/(?:coordination\.k8s\.io|storage\.k8s\.io|apps|policy)/v1(?:/namespaces/(?P<ns>[^/]+))?/"
+                    r"(?P<res>leases|storageclasses|csinodes|replicasets|statefulsets|poddisruptionbudgets)"
+                    r"(?:/(?P<name>[^/]+))?$")
 _PT = {"application/json-patch+json": "json", "application/merge-patch+json": "merge",
        "application/strategic-merge-patch+json": "strategic"}
 
@@ -127,6 +128,9 @@ class FakeApiServer:
                         outer.cluster.bind(r["ns"], r["name"], body["target"]["name"],
                                            body.get("metadata", {}).get("uid", ""),
                                            body.get("metadata", {}).get("annotations"))
+                        return self._send(201, {"kind": "Status", "status": "Success", "code": 201})
+                    if r.get("sub") == "eviction":
+                        outer.cluster.evict(r["ns"], r["name"])
                         return self._send(201, {"kind": "Status", "status": "Success", "code": 201})
                     self._send(201, outer.cluster.create(r["res"], body, r["ns"]))
                 except ApiError as e:

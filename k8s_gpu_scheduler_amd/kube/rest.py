@@ -23,7 +23,7 @@ from typing import Any, Dict, Iterator, Optional
 
 import yaml
 
-from .client import AlreadyExists, ApiError, Conflict, Gone, KubeClient, NotFound, WatchEvent
+from .client import AlreadyExists, ApiError, Conflict, Gone, KubeClient, NotFound, TooManyRequests, WatchEvent
 
 Obj = Dict[str, Any]
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
@@ -33,7 +33,7 @@ GROUP_PATH = {"pods": "/api/v1", "nodes": "/api/v1", "configmaps": "/api/v1", "e
               "persistentvolumeclaims": "/api/v1", "persistentvolumes": "/api/v1",
               "storageclasses": "/apis/storage.k8s.io/v1", "csinodes": "/apis/storage.k8s.io/v1",
               "services": "/api/v1", "replicationcontrollers": "/api/v1", "replicasets": "/apis/apps/v1",
-              "statefulsets": "/apis/apps/v1"}
+              "statefulsets": "/apis/apps/v1", "poddisruptionbudgets": "/apis/policy/v1"}
 CLUSTER_SCOPED = {"nodes", "namespaces", "persistentvolumes", "storageclasses", "csinodes"}
 PATCH_CT = {"json": "application/json-patch+json", "merge": "application/merge-patch+json",
             "strategic": "application/strategic-merge-patch+json"}
@@ -96,6 +96,8 @@ def _raise_for(code: int, body: bytes) -> None:
         raise AlreadyExists(msg) if reason == "AlreadyExists" else Conflict(msg)
     if code == 410:
         raise Gone(msg)
+    if code == 429:
+        raise TooManyRequests(msg)
     raise ApiError(code, reason or "Error", msg)
 
 
@@ -201,6 +203,12 @@ class RestClient(KubeClient):
         body = {"apiVersion": "v1", "kind": "Binding", "metadata": md,
                 "target": {"apiVersion": "v1", "kind": "Node", "name": node_name}}
         self._json("POST", self._path("pods", namespace, pod_name, "binding"), body)
+
+    def evict(self, namespace, pod_name, grace_period_seconds=None):
+        body = {"apiVersion": "policy/v1", "kind": "Eviction", "metadata": {"name": pod_name, "namespace": namespace}}
+        if grace_period_seconds is not None:
+            body["deleteOptions"] = {"gracePeriodSeconds": grace_period_seconds}
+        self._json("POST", self._path("pods", namespace, pod_name, "eviction"), body)
 
     def watch(self, resource, namespace=None, resource_version="", timeout_s=None):
         q = {"watch": "1", "allowWatchBookmarks": "true"}

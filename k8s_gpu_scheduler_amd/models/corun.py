@@ -1,0 +1,500 @@
+"""Multi-way co-run model: the throughput each pod of a GPU's pod group achieves.
+
+The reference predicts a pod's throughput on a shared GPU as its configuration prediction
+minus the SUM of pairwise interference entries of its co-residents
+(reference pkg/plugins/gpu_plugin/gpu_plugins.go:589-612, 695-714; pairs measured offline in
+pkg/recommender/recommender/interference_train.ods).  On MI355X that additive form is a poor
+fit for the 3- and 4-way groups a node actually runs (round-2 virtual node: 22 % MAE), for
+two reasons a pairwise table cannot express:
+
+* pods of one group do not co-run for their whole lifetime -- the short ones finish first
+  and the rest speed up, so what a pod achieves depends on how LONG its co-runners are,
+  not only on who they are;
+* contention is asymmetric and resource-shaped -- next to an HBM stream a GEMM loses ~75 %
+  of its rate while the stream keeps ~97 % (profiles/r02_contention_probe.json).
+
+So this model is a small fluid simulation of the group instead.  Pod i carries W_i =
+iterations x its alone whole-GPU time per iteration (the MFMA / HBM work it brings).  While a
+set A of pods is active, pod i progresses at rate
+
+    r_i = 1 / (1 + sum_{j in A, j != i} u_i . v_j)        (work-ms per wall-ms)
+
+u_i in R^2_+ = how sensitive workload i is to MFMA / HBM pressure, v_j = how much of each
+workload j exerts (initialised from the roofline split; fitted per workload on measured
+co-run groups).  Events: a pod starts (staggered starts allowed) or finishes; between events
+rates are constant.  Predicted throughput = iterations / predicted wall time.  With u.v = 1
+everywhere this is plain processor sharing; the fitted values say how far MI355X is from it.
+
+Collection (`collect`, GPU): random 1..4-pod Burstable groups of the workload catalog, run
+co-located through the bench's DeviceExecutor (HIP graphs, per-pod HW queues) with per-pod
+HIP-event times.  `fit` estimates alone times from the 1-pod groups and u, v by
+Levenberg-Marquardt on log wall-time residuals (ridge toward the roofline init); the result
+ships as data/corun_mi355x.json and is served by the recommender (`ExportTable`) and used by
+the GPU plugin's Score and the burst planner.  `OnlineCorun` refines it from what co-running
+pods achieve in the running cluster (prequential error bookkeeping, as recommender.online).
+
+    python -m k8s_gpu_scheduler_amd.models.corun collect --groups 2400 --out gpurun_out/corun.json   (GPU)
+    python -m k8s_gpu_scheduler_amd.models.corun fit gpurun_out/corun.json --out k8s_gpu_scheduler_amd/data/corun_mi355x.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "corun_mi355x.json")
+MAXK = 8                      # pods per GPU the vectorised simulator handles (8 units of 32 CUs)
+
+
+# ----------------------------------------------------------------------------- simulator
+def simulate(work: np.ndarray, coup: np.ndarray, mask: np.ndarray, start: Optional[np.ndarray] = None) -> np.ndarray:
+    """Wall time at which each pod of each group finishes (same units as `work`).
+
+    work [G, K] >= 0, coup [G, K, K] (u_i . v_j; the diagonal is ignored), mask [G, K] bool,
+    start [G, K] (None = all start at 0).  Returns finish times [G, K] (0 where masked out)."""
+    G, K = work.shape
+    rem = np.where(mask, np.maximum(work, 1e-12), 0.0).astype(np.float64)
+    c = coup * (1.0 - np.eye(K))[None]
+    st = np.zeros((G, K)) if start is None else np.where(mask, start, 0.0).astype(np.float64)
+    done = ~mask.copy()
+    started = np.zeros((G, K), bool)
+    now = np.zeros(G)
+    fin = np.zeros((G, K))
+    big = 1e30
+    for _ in range(2 * K + 1):
+        live = ~done.all(axis=1)
+        if not live.any():
+            break
+        started = started | ((st <= now[:, None] + 1e-12) & mask)
+        act = started & ~done
+        load = 1.0 + np.einsum("gij,gj->gi", c, act.astype(np.float64))
+        rate = np.where(act, 1.0 / load, 0.0)
+        t_fin = np.where(act, rem / np.maximum(rate, 1e-30), big)
+        t_arr = np.where(mask & ~started, st - now[:, None], big)
+        dt = np.minimum(t_fin.min(axis=1), t_arr.min(axis=1))
+        dt = np.where(live, dt, 0.0)
+        rem = rem - rate * dt[:, None]
+        now = now + dt
+        newly = act & (rem <= 1e-9 * np.maximum(work, 1.0))
+        # the argmin pod always finishes (guards rounding)
+        am = np.argmin(t_fin, axis=1)
+        hit = (t_fin[np.arange(G), am] <= dt + 1e-12) & live
+        newly[np.arange(G)[hit], am[hit]] = True
+        fin = np.where(newly, now[:, None], fin)
+        done = done | newly
+    return fin
+
+
+_CORE: Any = False
+
+
+def _native_core() -> Any:
+    """The host C++ core (native/core/corun.cpp: same event simulation, identical results to
+    `simulate` up to rounding), or None on a build without it."""
+    global _CORE
+    if _CORE is False:
+        try:
+            from .. import _native
+            c = _native.core()
+            _CORE = c if c is not None and hasattr(c, "corun_times") else None
+        except Exception:
+            _CORE = None
+    return _CORE
+
+
+# ----------------------------------------------------------------------------- model
+class CorunModel:
+    """Per-workload alone time (ms per iteration on the whole GPU, Burstable pod alone) and
+    the u (sensitivity) / v (pressure) vectors of the fluid model."""
+
+    def __init__(self, names: Sequence[str], alone_ms: Sequence[float], u: np.ndarray, v: np.ndarray,
+                 meta: Optional[Dict[str, Any]] = None):
+        self.names = list(names)
+        self.index = {n: i for i, n in enumerate(self.names)}
+        self.alone_ms = np.asarray(alone_ms, dtype=np.float64)
+        self.u = np.asarray(u, dtype=np.float64).reshape(len(self.names), -1)
+        self.v = np.asarray(v, dtype=np.float64).reshape(len(self.names), -1)
+        self.meta = dict(meta or {})
+        self.version = str(self.meta.get("version", "prior"))
+        self._cmat = self.u @ self.v.T
+
+    # -- construction
+    @classmethod
+    def prior(cls, names: Optional[Sequence[str]] = None, alone_ms: Optional[Sequence[float]] = None) -> "CorunModel":
+        """Roofline init: u = v = (MFMA share, HBM share) of the workload's alone time, so a
+        GEMM pod presses on GEMM pods, a stream pod on stream pods (c = 1 for equal kinds:
+        processor sharing) and unlike kinds overlap."""
+        from . import workloads as W
+        names = list(names or W.NAMES)
+        fr = []
+        for n in names:
+            rf = W.roofline_split(n.replace("_", "-"))
+            m, h = rf if rf else (0.5, 0.5)
+            fr.append(m / max(m + h, 1e-30))
+        fr = np.asarray(fr)
+        uv = np.stack([fr, 1.0 - fr], axis=1)
+        if alone_ms is None:
+            alone_ms = [W.roofline_seconds(W.CATALOG[n], 1.0) * 1e3 if n in W.CATALOG else 1.0 for n in names]
+        return cls(names, alone_ms, uv.copy(), uv.copy(), {"version": "roofline-prior"})
+
+    @classmethod
+    def load(cls, path: str = DATA) -> Optional["CorunModel"]:
+        if not os.path.isfile(path):
+            return None
+        d = json.load(open(path))
+        return cls(d["names"], d["alone_ms"], np.asarray(d["u"]), np.asarray(d["v"]), d.get("meta"))
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"names": self.names, "alone_ms": [round(float(x), 6) for x in self.alone_ms],
+                "u": np.round(self.u, 6).tolist(), "v": np.round(self.v, 6).tolist(), "meta": self.meta}
+
+    def save(self, path: str) -> None:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(self.to_json(), f, indent=1)
+
+    # -- table form (the recommender's ExportTable "corun": one row per workload)
+    def table_columns(self) -> List[str]:
+        R = self.u.shape[1]
+        return ["alone_ms"] + [f"u{r}" for r in range(R)] + [f"v{r}" for r in range(R)]
+
+    def table_rows(self) -> List[List[float]]:
+        return [[float(self.alone_ms[i])] + [float(x) for x in self.u[i]] + [float(x) for x in self.v[i]]
+                for i in range(len(self.names))]
+
+    @classmethod
+    def from_table(cls, index: Sequence[str], columns: Sequence[str], rows: Sequence[Sequence[float]],
+                   version: str) -> Optional["CorunModel"]:
+        cols = list(columns)
+        if not index or not cols or cols[0] != "alone_ms":
+            return None
+        R = sum(1 for c in cols if c.startswith("u"))
+        a = np.asarray(rows, dtype=np.float64)
+        if a.shape != (len(index), 1 + 2 * R):
+            return None
+        return cls(list(index), a[:, 0], a[:, 1:1 + R], a[:, 1 + R:], {"version": version})
+
+    def copy_with(self, u: np.ndarray, v: np.ndarray, version: str) -> "CorunModel":
+        meta = dict(self.meta)
+        meta["version"] = version
+        return CorunModel(self.names, self.alone_ms, u, v, meta)
+
+    # -- lookup
+    def wid(self, name: str) -> int:
+        """Workload row of a pod or workload name: exact, else the longest catalog name
+        contained in it with '-' -> '_' (the recommender's substring rule,
+        reference recom_server.py:67-71); -1 if none."""
+        i = self.index.get(name)
+        if i is not None:
+            return i
+        nm = name.replace("-", "_")
+        best = -1
+        for n, j in self.index.items():
+            if n in nm and (best < 0 or len(n) > len(self.names[best])):
+                best = j
+        return best
+
+    def coupling(self) -> np.ndarray:
+        return self._cmat
+
+    # -- prediction
+    def group_times(self, wids: Sequence[int], iters: Sequence[float],
+                    starts: Optional[Sequence[float]] = None) -> np.ndarray:
+        """Predicted wall ms of each pod of ONE group (wids >= 0)."""
+        k = len(wids)
+        if k == 0:
+            return np.zeros(0)
+        w = np.asarray(wids)
+        work = (self.alone_ms[w] * np.asarray(iters, dtype=np.float64))[None]
+        coup = self._cmat[np.ix_(w, w)][None]
+        st = None if starts is None else np.asarray(starts, dtype=np.float64)[None]
+        return simulate(work, coup, np.ones((1, k), bool), st)[0]
+
+    def group_tput(self, wids: Sequence[int], iters: Sequence[float],
+                   starts: Optional[Sequence[float]] = None) -> np.ndarray:
+        t = self.group_times(wids, iters, starts)
+        return np.asarray(iters, dtype=np.float64) / np.maximum(t, 1e-9) * 1e3
+
+    def batch_times(self, wids: np.ndarray, iters: np.ndarray, mask: np.ndarray,
+                    starts: Optional[np.ndarray] = None) -> np.ndarray:
+        core = _native_core()
+        if core is not None and wids.shape[1] <= 64:
+            st = np.zeros(wids.shape) if starts is None else starts
+            return core.corun_times(np.where(mask, wids, 0).astype(np.int32), iters.astype(np.float64),
+                                    mask.astype(np.uint8), st.astype(np.float64), self.alone_ms, self._cmat)
+        w = np.where(mask, wids, 0)
+        work = self.alone_ms[w] * iters
+        coup = self._cmat[w[:, :, None], w[:, None, :]]
+        return simulate(work, coup, mask, starts)
+
+    def alone_tput(self, wid: int) -> float:
+        return 1e3 / self.alone_ms[wid]
+
+
+# ----------------------------------------------------------------------------- data
+def pack_groups(groups: List[Dict[str, Any]], names: Sequence[str], K: int = 4
+                ) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+    """(wids, iters, mask, measured ms, starts) arrays [G, K] from collected groups."""
+    idx = {n: i for i, n in enumerate(names)}
+    G = len(groups)
+    wids = np.zeros((G, K), np.int64)
+    iters = np.zeros((G, K))
+    mask = np.zeros((G, K), bool)
+    ms = np.zeros((G, K))
+    st = np.zeros((G, K))
+    for g, d in enumerate(groups):
+        for k, n in enumerate(d["w"][:K]):
+            wids[g, k] = idx[n]
+            iters[g, k] = d.get("iters", 20) if np.isscalar(d.get("iters", 20)) else d["iters"][k]
+            mask[g, k] = True
+            ms[g, k] = d["ms"][k]
+            st[g, k] = d["start"][k] if "start" in d else 0.0
+    return wids, iters, mask, ms, st
+
+
+def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, ridge: float = 0.05,
+        max_nfev: int = 400, holdout: float = 0.2, seed: int = 0) -> Tuple[CorunModel, Dict[str, Any]]:
+    """Fit alone times (median of 1-pod groups) and u, v (2 x 18 each, log-parameterised)
+    on the multi-pod groups; returns the model and a report with held-out errors of the
+    fitted model, the roofline prior and the pairwise-additive baseline."""
+    from scipy.optimize import least_squares
+    from . import workloads as W
+    names = list(names or W.NAMES)
+    alone = {}
+    for d in groups:
+        if len(d["w"]) == 1:
+            alone.setdefault(d["w"][0], []).append(d["ms"][0] / d.get("iters", 20))
+    prior = CorunModel.prior(names)
+    a_ms = np.array([np.median(alone[n]) if n in alone else prior.alone_ms[i] for i, n in enumerate(names)])
+    multi = [d for d in groups if len(d["w"]) >= 2]
+    rng = random.Random(seed)
+    rng.shuffle(multi)
+    n_te = int(len(multi) * holdout)
+    test, train = multi[:n_te], multi[n_te:]
+    base = CorunModel(names, a_ms, prior.u, prior.v, {"version": "roofline-prior"})
+    K = max(len(d["w"]) for d in multi)
+    tr = pack_groups(train, names, K)
+    te = pack_groups(test, names, K)
+    n_w, R = len(names), prior.u.shape[1]
+    x0 = np.log(np.concatenate([np.maximum(prior.u, 1e-3).ravel(), np.maximum(prior.v, 1e-3).ravel()]))
+    x_prior = x0.copy()
+
+    def unpack(x):
+        e = np.exp(x)
+        return e[:n_w * R].reshape(n_w, R), e[n_w * R:].reshape(n_w, R)
+
+    def resid(x, data):
+        u, v = unpack(x)
+        m = CorunModel(names, a_ms, u, v)
+        wids, iters, mask, ms, st = data
+        t = m.batch_times(wids, iters, mask, st)
+        r = np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[mask]
+        return r
+
+    def obj(x):
+        return np.concatenate([resid(x, tr), np.sqrt(ridge) * (x - x_prior)])
+
+    t0 = time.time()
+    sol = least_squares(obj, x0, method="trf", max_nfev=max_nfev, x_scale=1.0)
+    u, v = unpack(sol.x)
+    model = CorunModel(names, a_ms, u, v, {"version": f"fit-{len(train)}g", "groups_train": len(train),
+                                            "groups_test": len(test), "ridge": ridge})
+
+    def tput_err(m: CorunModel, data) -> Dict[str, float]:
+        wids, iters, mask, ms, st = data
+        t = m.batch_times(wids, iters, mask, st)
+        tp = iters / np.maximum(t, 1e-9) * 1e3
+        tm = iters / np.maximum(ms, 1e-9) * 1e3
+        e = np.abs(tp - tm)[mask]
+        rel = (np.abs(np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))))[mask]
+        return {"mae_iter_s": float(e.mean()), "mean_tput": float(tm[mask].mean()),
+                "mae_pct_of_mean": float(100 * e.mean() / tm[mask].mean()), "mean_abs_log": float(rel.mean())}
+
+    rep = {"fit_seconds": round(time.time() - t0, 1), "nfev": int(sol.nfev), "cost": float(sol.cost),
+           "train": tput_err(model, tr), "test": tput_err(model, te), "test_prior": tput_err(base, te)}
+    model.meta["report"] = rep
+    return model, rep
+
+
+# ----------------------------------------------------------------------------- online
+class OnlineCorun:
+    """The co-run model refined from live observations: every finished pod is one
+    observation (its group's workloads, start offsets and iterations, its measured wall
+    time).  Observations are predicted with the current model before they are learned
+    (prequential error); every `refit_every` observations a few Levenberg-Marquardt steps
+    refit u, v on a sliding window, ridge-pulled toward the offline model."""
+
+    def __init__(self, base: CorunModel, refit_every: int = 32, window: int = 2048, ridge: float = 0.5,
+                 max_nfev: int = 12):
+        self.base = base
+        self.model = base
+        self.refit_every, self.window, self.ridge, self.max_nfev = refit_every, window, ridge, max_nfev
+        # (workload ids, iterations, start offsets ms, pods, measured ms) per observed group
+        self._obs: List[Tuple[Tuple[int, ...], Tuple[float, ...], Tuple[float, ...], int, Tuple[float, ...]]] = []
+        self._pending = 0
+        self.version = 0
+        self.err = {"prior": 0.0, "online": 0.0, "n": 0, "tput_sum": 0.0}
+        self._lock = threading.Lock()
+
+    def observe_group(self, wids: Sequence[int], iters: Sequence[float], ms: Sequence[float],
+                      starts: Optional[Sequence[float]] = None) -> bool:
+        """One GPU's finished pods (workload ids >= 0); returns True when refitted."""
+        k = len(wids)
+        if k == 0:
+            return False
+        st = list(starts) if starts is not None else [0.0] * k
+        t_on = self.model.group_times(wids, iters, st)
+        t_pr = self.base.group_times(wids, iters, st)
+        with self._lock:
+            for i in range(k):
+                if ms[i] <= 0:
+                    continue
+                tm = iters[i] / ms[i] * 1e3
+                self.err["prior"] += abs(iters[i] / max(t_pr[i], 1e-9) * 1e3 - tm)
+                self.err["online"] += abs(iters[i] / max(t_on[i], 1e-9) * 1e3 - tm)
+                self.err["n"] += 1
+                self.err["tput_sum"] += tm
+            self._obs.append((tuple(wids), tuple(float(x) for x in iters), tuple(float(x) for x in st), k,
+                              tuple(float(x) for x in ms)))
+            if len(self._obs) > self.window:
+                del self._obs[: len(self._obs) - self.window]
+            self._pending += k
+            if self._pending >= self.refit_every:
+                self._pending = 0
+                self._refit()
+                return True
+        return False
+
+    def _refit(self) -> None:
+        from scipy.optimize import least_squares
+        obs = self._obs
+        K = max(o[3] for o in obs)
+        G = len(obs)
+        wids = np.zeros((G, K), np.int64)
+        iters = np.zeros((G, K))
+        mask = np.zeros((G, K), bool)
+        ms = np.ones((G, K))
+        st = np.zeros((G, K))
+        for g, (w, it, s, k, m) in enumerate(obs):
+            wids[g, :k], iters[g, :k], st[g, :k], ms[g, :k] = w, it, s, m
+            mask[g, :k] = True
+        mask &= ms > 0
+        base = self.base
+        n_w, R = base.u.shape
+        x_prior = np.log(np.maximum(np.concatenate([base.u.ravel(), base.v.ravel()]), 1e-6))
+        x0 = np.log(np.maximum(np.concatenate([self.model.u.ravel(), self.model.v.ravel()]), 1e-6))
+        a_ms = base.alone_ms
+
+        def obj(x):
+            e = np.exp(x)
+            m = CorunModel(base.names, a_ms, e[:n_w * R].reshape(n_w, R), e[n_w * R:].reshape(n_w, R))
+            t = m.batch_times(wids, iters, mask, st)
+            r = np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[mask]
+            return np.concatenate([r, np.sqrt(self.ridge) * (x - x_prior)])
+
+        sol = least_squares(obj, x0, method="trf", max_nfev=self.max_nfev)
+        e = np.exp(sol.x)
+        self.version += 1
+        self.model = base.copy_with(e[:n_w * R].reshape(n_w, R), e[n_w * R:].reshape(n_w, R),
+                                    f"{base.version}+online-{self.version}")
+
+    def mae(self) -> Dict[str, Optional[float]]:
+        n = self.err["n"]
+        if not n:
+            return {"n": 0, "prior": None, "online": None, "mean_tput": None}
+        return {"n": n, "prior": self.err["prior"] / n, "online": self.err["online"] / n,
+                "mean_tput": self.err["tput_sum"] / n}
+
+
+# ----------------------------------------------------------------------------- collection (GPU)
+def collect(n_groups: int = 2400, iters: int = 20, seed: int = 0, sizes=(2, 3, 4), alone_reps: int = 3,
+            repeat_frac: float = 0.05) -> Dict[str, Any]:
+    """Run random Burstable pod groups co-located on the GPU; per pod its HIP-event wall ms
+    and start offset.  Workloads are drawn half from the bench's Zipf-like arrival mix, half
+    uniformly; a few groups are re-run to measure the noise floor."""
+    import torch
+    from ..parallel.executor import DeviceExecutor, PodRun
+    from . import workloads as W
+    rng = random.Random(seed)
+    ex = DeviceExecutor(0, use_cu_masks=True)
+    ex.use_graphs = True
+    slots = (0, 2, 4, 6)
+    ex.warm([PodRun(0, wl, u, 2, iters, masked=False) for wl in W.NAMES for u in slots])
+    weights = [1.0 / (1 + (i % 6)) for i in range(len(W.NAMES))]
+
+    def draw() -> str:
+        return rng.choices(W.NAMES, weights)[0] if rng.random() < 0.5 else rng.choice(W.NAMES)
+
+    def run(wls: List[str]) -> Dict[str, Any]:
+        runs = [PodRun(i, wl, slots[i], 2, iters, masked=False) for i, wl in enumerate(wls)]
+        torch.cuda.synchronize()
+        ref = torch.cuda.Event(enable_timing=True)
+        ref.record()
+        ex.launch_epoch(runs)
+        ex.join_current()
+        torch.cuda.synchronize()
+        ms = [r.start.elapsed_time(r.end) for r in runs]
+        st = [ref.elapsed_time(r.start) for r in runs]
+        s0 = min(st)
+        return {"w": wls, "iters": iters, "ms": [round(x, 4) for x in ms], "start": [round(x - s0, 4) for x in st]}
+
+    out: List[Dict[str, Any]] = []
+    for _ in range(alone_reps):
+        for wl in W.NAMES:
+            out.append(run([wl]))
+    t0 = time.time()
+    for g in range(n_groups):
+        k = sizes[g % len(sizes)] if len(sizes) > 1 else sizes[0]
+        if rng.random() < 0.5:
+            k = 4 if 4 in sizes else k         # the bench's shape dominates
+        wls = [draw() for _ in range(k)]
+        out.append(run(wls))
+        if rng.random() < repeat_frac:
+            d = run(wls)
+            d["repeat_of"] = len(out) - 1
+            out.append(d)
+        if g % 200 == 0:
+            print(f"[corun] {g}/{n_groups} groups, {time.time() - t0:.1f}s", flush=True)
+    ex.close()
+    return {"iters": iters, "groups": out, "names": list(W.NAMES)}
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(description="MI355X multi-way co-run model: collect (GPU) / fit (CPU)")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    c = sub.add_parser("collect")
+    c.add_argument("--groups", type=int, default=2400)
+    c.add_argument("--iters", type=int, default=20)
+    c.add_argument("--seed", type=int, default=0)
+    c.add_argument("--out", default="gpurun_out/corun.json")
+    f = sub.add_parser("fit")
+    f.add_argument("data", nargs="+")
+    f.add_argument("--ridge", type=float, default=0.05)
+    f.add_argument("--out", default=DATA)
+    a = ap.parse_args(argv)
+    if a.cmd == "collect":
+        q = int(os.environ.get("GPUSCHED_HW_QUEUES", "16"))
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < q <= 32:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(q)     # as bench.py: one HW queue per pod stream
+        d = collect(a.groups, a.iters, a.seed)
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        json.dump(d, open(a.out, "w"))
+        print(json.dumps({"groups": len(d["groups"]), "out": a.out}))
+        return 0
+    groups: List[Dict[str, Any]] = []
+    for p in a.data:
+        groups += json.load(open(p))["groups"]
+    model, rep = fit(groups, ridge=a.ridge)
+    model.save(a.out)
+    print(json.dumps(rep, indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

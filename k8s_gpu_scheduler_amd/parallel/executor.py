@@ -178,11 +178,24 @@ class DeviceExecutor:
         self._last_events = [ev for _, ev in {id(e): (k, e) for k, e in self._unit_last.values()}.values()]
         self.epoch_runs.append(runs)
 
+    # host poll period while waiting for an epoch's end events
+    poll_s = 20e-6
+
     def wait_epoch(self, runs: List[PodRun]) -> None:
-        """Host-wait until every pod of an epoch finished (its end events)."""
+        """Host-wait until every pod of an epoch finished (its end events), by polling the
+        events.  A blocking hipEventSynchronize sleeps until the runtime is woken, and on a
+        device with no other completion interrupts in flight (the 1-rank plain path) that
+        wake-up came ~6 ms after the last pod kernel ended -- every epoch (rocprof + pod
+        traces, profiles/r03_window/).  Behind the launch-ahead pipeline that lateness is
+        hidden, except after the LAST epoch, where it adds ~6 ms to the timed region (4.4 %
+        of a 20-step window: the whole 'window effect' of round 2).  Polling wakes within
+        tens of microseconds on every path."""
         for r in runs:
-            if r.end is not None:
-                r.end.synchronize()
+            ev = r.end
+            if ev is None:
+                continue
+            while not ev.query():
+                time.sleep(self.poll_s)
 
     def join_current(self) -> None:
         """Make the default stream wait for all enqueued work (no host sync)."""

@@ -60,10 +60,12 @@ MAX_PODS_GPU = 8              # per-pod co-run records per GPU and epoch
 COST0 = 4
 POD0 = COST0 + 2 * len(W.NAMES)
 # busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods), then per pod of
-# this GPU's epoch: (workload id or -1, achieved iterations/s) -- the co-run observations the
-# online interference model learns from; last, amd-smi's view of the GPU over the epoch
-# (gfx activity 0..1, VRAM used GiB; -1 = no amd-smi sample)
-SMI0 = POD0 + 2 * MAX_PODS_GPU
+# this GPU's epoch: (workload id or -1, achieved iterations/s, start ms after the epoch's first
+# pod started) -- the co-run observations the online interference / co-run models learn from;
+# last, amd-smi's view of the GPU over the epoch (gfx activity 0..1, VRAM used GiB; -1 = no
+# amd-smi sample)
+POD_F = 3
+SMI0 = POD0 + POD_F * MAX_PODS_GPU
 TELE = SMI0 + 2
 
 
@@ -101,7 +103,7 @@ class ControlPlane:
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
                  plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0,
-                 online_scale: bool = False):
+                 online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -113,9 +115,19 @@ class ControlPlane:
         self.workcost = WorkCostModel()
         self.ledger = DeviceLedger()
         self.predictions = predictions or measured_predictions() or analytic_predictions()
+        # the multi-way co-run model (models.corun, data/corun_mi355x.json): served to the
+        # scheduler as the recommender would, refined online from the pods' achieved rates
+        self.corun = None
+        if slo_objective != "terms":
+            from ..models.corun import CorunModel, OnlineCorun
+            base = corun_model or CorunModel.load()
+            if base is not None:
+                self.predictions.install_corun(base)
+                self.corun = OnlineCorun(base, refit_every=max(32, 4 * n_gpus * pods_per_gpu))
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
-                "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement}
+                "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement,
+                "slo_objective": slo_objective}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
         # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
@@ -218,25 +230,48 @@ class ControlPlane:
                 pass
 
     def _learn_interference(self, pods: np.ndarray) -> None:
-        """pods[g] = MAX_PODS_GPU x (workload id, achieved iterations/s) of GPU g's epoch:
-        each pod's loss against its predicted alone-throughput at its share is one
-        observation of the additive interference model (recommender.online)."""
-        refit = False
+        """pods[g] = MAX_PODS_GPU x (workload id, achieved iterations/s, start offset ms) of
+        GPU g's epoch.  Each pod's loss against its predicted alone-throughput at its share is
+        one observation of the additive interference model (recommender.online); each GPU's
+        group -- who co-ran, from when, at what rate -- one observation of the co-run model
+        (models.corun.OnlineCorun)."""
+        refit = refit_c = False
         for g in range(pods.shape[0]):
-            rec = pods[g].reshape(MAX_PODS_GPU, 2)
-            wids = [int(w) for w, _ in rec if w >= 0]
-            for i, (w, tput) in enumerate(rec):
-                if w < 0:
-                    continue
-                w = int(w)
-                others = wids[:i] + wids[i + 1:]
-                refit |= self.online.observe(w, others, self.quarter_tput[W.NAMES[w]] - float(tput))
-        if refit:       # serve the refitted table to the scheduler (next cycles' predictions)
+            rec = pods[g].reshape(MAX_PODS_GPU, POD_F)
+            wids = [int(r[0]) for r in rec if r[0] >= 0]
+            if self.online is not None:
+                for i, r in enumerate(rec):
+                    if r[0] < 0:
+                        continue
+                    w = int(r[0])
+                    others = wids[:i] + wids[i + 1:]
+                    refit |= self.online.observe(w, others, self.quarter_tput[W.NAMES[w]] - float(r[1]))
+            if self.corun is not None and wids:
+                live = [r for r in rec if r[0] >= 0 and r[1] > 0]
+                if live:
+                    cw = [self.corun.base.wid(W.NAMES[int(r[0])]) for r in live]
+                    if min(cw) >= 0:
+                        refit_c |= self.corun.observe_group(cw, [float(self.iters)] * len(live),
+                                                            [self.iters / float(r[1]) * 1e3 for r in live],
+                                                            [float(r[2]) for r in live])
+        if refit and self.online is not None:       # serve the refitted table (next cycles' predictions)
             self.predictions.install_interference(self._online_rows, W.NAMES, self.online.rows(),
                                                   f"online-{self.online.version}")
+        if refit_c:
+            self.predictions.install_corun(self.corun.model)
 
     def interference_mae(self) -> Optional[Dict[str, Any]]:
-        return self.online.mae() if self.online is not None else None
+        out = self.online.mae() if self.online is not None else None
+        if self.corun is not None:
+            m = self.corun.mae()
+            q = float(np.mean(list(self.quarter_tput.values())))
+            out = dict(out or {})
+            out["corun"] = {**m, "version": self.corun.model.version,
+                            "online_pct_of_mean_quarter_tput":
+                                round(100.0 * m["online"] / q, 2) if m["online"] is not None else None,
+                            "prior_pct_of_mean_quarter_tput":
+                                round(100.0 * m["prior"] / q, 2) if m["prior"] is not None else None}
+        return out
 
     def update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
         """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib[, per-workload
@@ -248,7 +283,7 @@ class ControlPlane:
             for wid, (tot, n) in enumerate(cost):
                 if n > 0:
                     self.workcost.observe(W.NAMES[wid], float(tot / n), int(n))
-            if self.online is not None:
+            if self.online is not None or self.corun is not None:
                 self._learn_interference(per_gpu[:, POD0:SMI0])
         for st in self.ledger.devices(NODE):
             g = st.device.gpu
@@ -338,12 +373,23 @@ class SimExecutor:
 
 
 def _pod_rows(runs: List[Any]) -> List[float]:
-    """(workload id, achieved iterations/s) of up to MAX_PODS_GPU pods of one GPU's epoch;
-    (-1, 0) pads."""
+    """(workload id, achieved iterations/s, start ms after the first pod of the group) of up
+    to MAX_PODS_GPU pods of one GPU's epoch; (-1, 0, 0) pads."""
     out: List[float] = []
-    for r in runs[:MAX_PODS_GPU]:
-        out += [float(W.INDEX[r.workload]), float(r.throughput)]
-    return out + [-1.0, 0.0] * (MAX_PODS_GPU - min(len(runs), MAX_PODS_GPU))
+    rs = runs[:MAX_PODS_GPU]
+    t0 = None
+    offs = []
+    for r in rs:
+        ev = getattr(r, "start", None)
+        try:
+            offs.append(rs[0].start.elapsed_time(ev) if ev is not None and rs[0].start is not None else 0.0)
+        except Exception:
+            offs.append(0.0)
+    if offs:
+        t0 = min(offs)
+    for r, o in zip(rs, offs):
+        out += [float(W.INDEX[r.workload]), float(r.throughput), float(o - t0)]
+    return out + [-1.0, 0.0, 0.0] * (MAX_PODS_GPU - len(rs))
 
 
 def _cost_rows(runs: List[Any]) -> np.ndarray:
@@ -448,6 +494,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--online-scale", type=int, default=1,
                     help="online interference learning: shrink rows toward the prior SCALED by a learned "
                          "global / per-row factor (recommender.online) instead of the prior itself")
+    ap.add_argument("--slo-objective", default="terms", choices=["terms", "corun"],
+                    help="GPU plugin SLO objective: 'corun' = the multi-way co-run model (data/corun_mi355x.json, "
+                         "refined online) as a constraint on Score and in the burst planner; 'terms' = the "
+                         "reference's pairwise interference terms")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
                     help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
                          "'slo' = most predicted SLOs met first (within --plan-tolerance)")
@@ -533,7 +583,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
                      plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective,
-                     online_scale=bool(a.online_scale))
+                     online_scale=bool(a.online_scale), slo_objective=a.slo_objective)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -548,12 +598,22 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx) if use_gpu else torch.device("cpu")
     backend = a.backend or ("nccl" if use_gpu else "gloo")
+    dist_note = ""
     if dist_on and not dist.is_initialized():
         kw: Dict[str, Any] = {}
         if world == 1:                      # --dist-single outside a launcher: private rendezvous
             from .launch import free_port
             kw = dict(init_method=f"tcp://127.0.0.1:{free_port()}", world_size=1, rank=0)
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None, **kw)
+        try:
+            dist.init_process_group(backend, device_id=dev if backend == "nccl" else None, **kw)
+        except Exception as e:
+            if world > 1 or a.dist_single == 1:
+                raise
+            # the 1-rank group is an option of the N=1 run, not a requirement: keep going on
+            # the plain path (recorded in the result's config) instead of failing the bench
+            print(f"[bench] 1-rank {backend} group failed ({e}); running without collectives",
+                  file=sys.stderr, flush=True)
+            dist_on, dist_note = False, f"1-rank {backend} init failed: {str(e)[:200]}"
     if use_gpu and world > 1 and "GPUSCHED_FORCE_DEVICE" not in os.environ and torch.cuda.device_count() < world:
         raise SystemExit(f"rank {rank}: WORLD_SIZE {world} but only {torch.cuda.device_count()} GPU(s) visible")
     n_gpus = world if world > 1 else max(1, a.gpus)
@@ -779,7 +839,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
                        "balance": a.balance, "plan_bursts": a.plan_bursts,
                        "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
-                       "online_scale": a.online_scale,
+                       "online_scale": a.online_scale, "slo_objective": a.slo_objective,
+                       # which code path N=1 took: collectives over a 1-rank group or the plain path
+                       "collectives": bool(dist_on), "dist_single": a.dist_single,
+                       **({"collectives_note": dist_note} if dist_note else {}),
                        "note": "global_batch = pods per scheduling epoch; seq_len = query batches per pod"},
             "gpu_util_pct": round(util, 2),
             "cu_share_occupancy_pct": round(occ, 2),

@@ -152,6 +152,7 @@ class PodUse:
     units: Tuple[int, int]       # (first unit, count) inside the device
     whole: bool = False
     work: float = 0.0            # predicted whole-GPU seconds of this pod on this device
+    iters: float = 0.0           # iterations a batch pod runs (0 = a long-running service): co-run model
 
 
 @dataclass
@@ -252,7 +253,7 @@ class DeviceLedger:
         return node in self.nodes
 
     def reserve(self, node: str, pod_key: str, pod_name: str, slo: float,
-                allocs: List[Tuple[str, int, int, float, bool]], work: float = 0.0) -> bool:
+                allocs: List[Tuple[str, int, int, float, bool]], work: float = 0.0, iters: float = 0.0) -> bool:
         """allocs: (uuid, first_unit, n_units, hbm_gib, whole).  All-or-nothing.  `work` is
         the pod's predicted GPU time (split evenly over its devices), summed per device for
         the plugin's load-balance term."""
@@ -273,7 +274,7 @@ class DeviceLedger:
                     st.used_units[u] = True
                 st.hbm_used += hbm
                 share = work / max(len(allocs), 1)
-                st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole, share)
+                st.pods[pod_key] = PodUse(pod_key, pod_name, slo, n * CUS_PER_XCD, hbm, (u0, n), whole, share, iters)
                 st.work += share
                 st.invalidate()
             self.pod_index[pod_key] = (node, [a[0] for a in allocs])

@@ -28,6 +28,10 @@ Here the decision is a controller next to the GPU plugin, never inside Score:
      the node), taints `amd.com/partitioning=NoSchedule`, applies through amd-smi,
      republishes the UUIDs (64 on a CPX node) and untaints (agent.NodeAgent.reconcile_partitions);
      the scheduler re-reads the inventory on the node update and the pending pods bind.
+  5. A request the agent refused or failed (node annotation `partition-state`, or a request
+     of ours whose label came back reverted without the mode being applied -- e.g. the node
+     was busy with GPU work the ledger cannot see) backs that node off for that mode for
+     `backoff_s`, so an unledgered busy node is not tainted, drained and reverted in a loop.
 """
 from __future__ import annotations
 
@@ -37,7 +41,7 @@ import threading
 import time
 from collections import Counter
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from ...api import constants as C
 from ...api import objects as O
@@ -82,11 +86,14 @@ class Decision:
 
 
 class PartitionController:
-    def __init__(self, plugin: Any, period_s: float = 2.0, max_nodes_per_step: int = 4):
+    def __init__(self, plugin: Any, period_s: float = 2.0, max_nodes_per_step: int = 4, backoff_s: float = 600.0):
         self.plugin = plugin
         self.period_s = period_s
         self.max_nodes_per_step = max_nodes_per_step
+        self.backoff_s = backoff_s
         self.decisions: List[Decision] = []
+        self._requested: Dict[str, Decision] = {}          # node -> our outstanding request
+        self._backoff: Dict[Tuple[str, str], float] = {}    # (node, mode) -> until (wall clock)
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
 
@@ -132,6 +139,42 @@ class PartitionController:
     def node_idle(self, node: str) -> bool:
         return all(not st.pods for st in self.plugin.ledger.devices(node))
 
+    # ---------------------------------------------------------------- backoff
+    def _note_outcomes(self, nodes: Dict[str, Obj], now: float) -> None:
+        """Back off (node, mode) pairs whose last request was refused or failed."""
+        for name, node in nodes.items():
+            raw = O.annotations(node).get(C.ANNOT_PARTITION_STATE)
+            if not raw:
+                continue
+            try:
+                st = json.loads(raw)
+            except ValueError:
+                continue
+            if st.get("state") in ("refused", "failed") and st.get("mode"):
+                until = float(st.get("ts", now)) + self.backoff_s
+                key = (name, str(st["mode"]).upper())
+                if until > now and until > self._backoff.get(key, 0.0):
+                    self._backoff[key] = until
+                    log.info("partitioning: %s -> %s %s (%s); backing off %.0fs", name, key[1], st["state"],
+                             st.get("reason") or st.get("errors"), until - now)
+        for name, d in list(self._requested.items()):
+            node = nodes.get(name)
+            if node is None:
+                del self._requested[name]
+                continue
+            want = O.labels(node).get(C.LABEL_COMPUTE_PARTITION, "").upper()
+            tainted = any(t.get("key") == C.TAINT_PARTITIONING for t in O.node_taints(node))
+            if want == d.mode or tainted:
+                if self.current_mode(name) == d.mode:
+                    del self._requested[name]          # applied
+                continue
+            del self._requested[name]                  # label reverted, mode not applied: refused
+            if self.current_mode(name) != d.mode:
+                self._backoff[(name, d.mode)] = max(self._backoff.get((name, d.mode), 0.0), now + self.backoff_s)
+
+    def backed_off(self, node: str, mode: str, now: Optional[float] = None) -> bool:
+        return self._backoff.get((node, mode), 0.0) > (time.time() if now is None else now)
+
     # ---------------------------------------------------------------- decision
     def size_pod(self, pod: Obj) -> Optional[int]:
         """CUs of the partition a pending isolated pod needs (writes the annotation when the
@@ -169,6 +212,8 @@ class PartitionController:
         if not demand:
             return []
         nodes = {O.name(n): n for n in self._nodes()}
+        now = time.time()
+        self._note_outcomes(nodes, now)
         ledger = self.plugin.ledger
         # supply per size: free partitions now + partitions of nodes already asked to switch
         supply: Counter = Counter()
@@ -200,6 +245,8 @@ class PartitionController:
                         continue                     # never a node with pods, never twice
                     if self.current_mode(name) == mode or not ledger.devices(name):
                         continue
+                    if self.backed_off(name, mode, now):
+                        continue                     # refused / failed recently for this mode
                     caps = self.node_caps(node)
                     if caps is not None and caps.check(mode) is not None:
                         continue
@@ -222,6 +269,7 @@ class PartitionController:
                                                  f"{supply[size]} available")
                 log.info("partitioning: %s -> %s (%s)", name, mode, d.reason)
                 out.append(d)
+                self._requested[name] = d
                 busy_or_changing.add(name)
                 supply[size] += gpus * parts
                 deficit -= gpus * parts

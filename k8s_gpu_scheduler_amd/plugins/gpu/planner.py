@@ -24,6 +24,14 @@ pod together with every pending fractional pod of the queue:
 The plan is a hint: each pod still runs the full Filter/Score/Reserve cycle; Score ranks
 the planned device first and every other choice after it, and a plan that no longer fits
 (capacity taken meanwhile) is simply ignored.
+
+With a co-run model (models.corun, served by the recommender) the plan is made on it
+instead (`_plan_corun`, native `_core.plan_corun`): every GPU's pod group is simulated as a
+whole, so the objective sees what the pairwise table cannot -- how long each co-runner
+runs and how asymmetric the contention is.  Phase A balances the predicted group makespans
+(the slowest GPU paces a coupled multi-GPU epoch), phase B then maximises the number of
+pods -- burst and residents -- predicted to meet their SLO without letting any GPU's
+makespan exceed (1 + planTolerance) x the balanced plan's longest.
 """
 from __future__ import annotations
 
@@ -89,6 +97,9 @@ class BurstPlanner:
             return hit
         from ... import _native
         core = _native.core()
+        model = self.plugin.corun_model()
+        if model is not None and core is not None and hasattr(core, "plan_corun"):
+            return self._plan_corun(pod, nodes, model, core)
         mat = self._matrix()
         if core is None or mat is None or not hasattr(core, "plan_assignment"):
             return None
@@ -198,6 +209,111 @@ class BurstPlanner:
             np.array(res_slo, dtype=np.float64), np.array(res_pred, dtype=np.float64), M, 0.0,
             self.sweeps, float(self.tolerance), int(self.load_first))
         for (p, _, _, _, _), d in zip(assign, out[:n]):
+            self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
+            plugin._pending_by_key[O.key(p)] = p
+        self.planned_bursts += 1
+        return self.plans.get(key)
+
+    # ---------------------------------------------------------------- co-run plan
+    def _burst(self, pod: Obj) -> List[Tuple[Obj, Any]]:
+        """This pod + the pending fractional pods of this scheduler not planned yet."""
+        plugin = self.plugin
+        key = O.key(pod)
+        burst, seen = [], {key}
+        for p in [pod] + list(plugin.handle.pending_pods() if plugin.handle is not None else []):
+            k = O.key(p)
+            if (k in seen and p is not pod) or k in self.plans or O.node_name_of(p):
+                continue
+            seen.add(k)
+            req = plugin.parse_request(p)
+            if req.units and not req.whole and req.gpu_pod:
+                burst.append((p, req))
+        return burst
+
+    def _plan_corun(self, pod: Obj, nodes: List[str], model: Any, core: Any) -> Optional[Tuple[str, str]]:
+        plugin = self.plugin
+        key = O.key(pod)
+        placed = [(nd, st) for nd in nodes for st in plugin.ledger.devices(nd) if st.device.healthy]
+        if not placed:
+            return None
+        states = [st for _, st in placed]
+        owner = [nd for nd, _ in placed]
+        burst = [(p, r) for p, r in self._burst(pod) if model.wid(O.name(p)) >= 0]
+        if len(burst) < 2 or not any(O.key(p) == key for p, _ in burst):
+            return None
+        gkey = {}
+        dev_group = []
+        for nd, st in placed:
+            dev_group.append(gkey.setdefault((nd,) + plugin.corun_group_key(st), len(gkey)))
+        n_groups = len(gkey)
+        free_units = [st.free_units for st in states]
+        free_hbm = [st.hbm_free for st in states]
+        per: List[List[Tuple[int, float, float]]] = [[] for _ in range(n_groups)]
+        seen = set()
+        for d, st in enumerate(states):
+            g = dev_group[d]
+            for k, use in st.pods.items():
+                if (k, g) in seen:
+                    continue
+                seen.add((k, g))
+                w = model.wid(use.name)
+                if w >= 0:
+                    per[g].append((w, use.iters, use.slo))
+        dev_index = {(owner[d], st.device.uuid): d for d, st in enumerate(states)}
+        # pods planned earlier and still pending hold their capacity and co-run as residents
+        for k, (n, u) in self.plans.items():
+            d = dev_index.get((n, u))
+            p = plugin._pending_by_key.get(k)
+            if d is None or p is None:
+                continue
+            req = plugin.parse_request(p)
+            free_units[d] -= req.units
+            free_hbm[d] -= req.hbm_gib
+            w = model.wid(O.name(p))
+            if w >= 0:
+                per[dev_group[d]].append((w, req.iters, req.slo))
+        # initial assignment: longest predicted work first onto the group with the least
+        # predicted work that has room (units and HBM)
+        load = [sum(model.alone_ms[w] * (it if it > 0 else 0.0) for w, it, _ in m) for m in per]
+        items = sorted(((model.alone_ms[model.wid(O.name(p))] * max(r.iters, 0.0), p, r) for p, r in burst),
+                       key=lambda t: -t[0])
+        rot = (self.planned_bursts * 5 + 1) % max(len(states), 1)
+        nst = len(states)
+        assign = []
+        for work, p, r in items:
+            best = None
+            for d in range(nst):
+                if free_units[d] < r.units or free_hbm[d] + 1e-6 < r.hbm_gib:
+                    continue
+                k2 = (load[dev_group[d]], (d - rot) % nst)
+                if best is None or k2 < best[0]:
+                    best = (k2, d)
+            if best is None:
+                continue
+            d = best[1]
+            free_units[d] -= r.units
+            free_hbm[d] -= r.hbm_gib
+            load[dev_group[d]] += work
+            assign.append((p, r, d))
+        if len(assign) < 2:
+            return None
+        if max((len(m) for m in per), default=0) + len(assign) > 64:
+            return None
+        off = np.zeros(n_groups + 1, np.int64)
+        off[1:] = np.cumsum([len(m) for m in per])
+        flat = [x for m in per for x in m]
+        dev0 = np.array([d for _, _, d in assign], np.int32)
+        units = np.array([r.units for _, r, _ in assign], np.int32)
+        # capacity before the burst (the native planner subtracts the initial assignment)
+        cap = np.array(free_units, np.int32)
+        np.add.at(cap, dev0, units)
+        out = core.plan_corun(
+            dev0, units, np.array([model.wid(O.name(p)) for p, _, _ in assign], np.int32),
+            np.array([r.iters for _, r, _ in assign], np.float64), np.array([r.slo for _, r, _ in assign], np.float64),
+            np.array(dev_group, np.int32), cap, off, np.array([x[0] for x in flat], np.int32),
+            np.array([x[1] for x in flat], np.float64), np.array([x[2] for x in flat], np.float64),
+            model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0)
+        for (p, _, _), d in zip(assign, out):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
             plugin._pending_by_key[O.key(p)] = p
         self.planned_bursts += 1

@@ -71,6 +71,7 @@ class GpuRequest:
     implicit: bool = False  # SLO env only, no amd.com/* request: GPU preferred, not required
     isolated: bool = False  # needs its own compute partition (ANNOT_ISOLATION = "partition")
     part_cus: int = 0       # ... of this many CUs (0 = not sized yet)
+    iters: float = 0.0      # iterations of a batch pod (ITERATIONS env; 0 = long-running service)
 
 
 PARTITION_SIZES = tuple(C.MI355X_CUS // p for p in sorted(C.COMPUTE_PARTITIONS.values(), reverse=True))  # 32..256
@@ -116,6 +117,12 @@ class GPUArgs:
     # "slo": most predicted SLOs met first, then the lower busier GPU; "load": the lower
     # interference-adjusted load of the busier GPU first, SLO count as the tie-break
     plan_objective: str = "slo"
+    # SLO objective of Score: "auto" = the co-run constraint when the prediction provider
+    # serves a co-run model (models.corun), else the reference's per-pod terms; "corun" /
+    # "terms" force one.  Co-run constraint: a device whose GPU group would, with this pod,
+    # miss fewer predicted SLOs always ranks first (bands by the number of NEW misses), the
+    # other terms (packing, balance by predicted group makespan, telemetry) order a band.
+    slo_objective: str = "auto"
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
@@ -134,6 +141,7 @@ class GPUArgs:
     # pending pods that ask for an isolated partition; "off" never requests a change
     partitioning: str = "auto"
     partition_period_s: float = 2.0
+    partition_backoff_s: float = 600.0     # a node that refused / failed a mode is not asked again for it
 
     @classmethod
     def from_dict(cls, d: Dict[str, Any]) -> "GPUArgs":
@@ -142,11 +150,11 @@ class GPUArgs:
                  "weightBalance": "w_balance", "weightComplement": "w_complement",
                  "lptWindowSeconds": "lpt_window_s",
                  "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
-                 "planObjective": "plan_objective",
+                 "planObjective": "plan_objective", "sloObjective": "slo_objective",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle",
-                 "partitionPeriodSeconds": "partition_period_s"}
+                 "partitionPeriodSeconds": "partition_period_s", "partitionBackoffSeconds": "partition_backoff_s"}
         for k, v in (d or {}).items():
             k = alias.get(k, k)
             if hasattr(a, k):
@@ -188,6 +196,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self._score_memo: Dict[str, Tuple[Any, Optional[Choice]]] = {}
         self._col_cache: Dict[Tuple[int, int], str] = {}
         self._pending_by_key: Dict[str, Obj] = {}
+        self._corun_packs: Dict[str, Tuple[Any, Dict[str, Any]]] = {}
         self.planner = None
         if self.args.plan_bursts:
             from .planner import BurstPlanner
@@ -213,7 +222,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             self._wire_informers()
             if self.args.mode != "parity" and self.args.partitioning == "auto":
                 from .partitioner import PartitionController
-                self.partitioner = PartitionController(self, period_s=self.args.partition_period_s)
+                self.partitioner = PartitionController(self, period_s=self.args.partition_period_s,
+                                                       backoff_s=self.args.partition_backoff_s)
 
     # ------------------------------------------------------------------ wiring
     def _wire_informers(self) -> None:
@@ -267,7 +277,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                 except Exception as e:
                     log.debug("recovery: node %s of %s unavailable: %s", node, O.key(pod), e)
             work = self.pod_work(pod, self._pod_predictions(O.name(pod))[0])
-            self.ledger.reserve(node, O.key(pod), O.name(pod), O.pod_slo(pod), allocs, work=work)
+            self.ledger.reserve(node, O.key(pod), O.name(pod), O.pod_slo(pod), allocs, work=work,
+                                iters=float(O.pod_iterations(pod)))
 
     def _on_pod_delete(self, pod: Obj) -> None:
         self.ledger.release(O.key(pod))
@@ -278,7 +289,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
     def parse_request(self, pod: Obj) -> GpuRequest:
         g, cu, mem = O.gpu_request(pod)
         slo = O.pod_slo(pod)
-        r = GpuRequest(slo=slo, hbm_gib=mem, burstable=O.gpu_qos(pod) == "Burstable")
+        r = GpuRequest(slo=slo, hbm_gib=mem, burstable=O.gpu_qos(pod) == "Burstable",
+                       iters=float(O.pod_iterations(pod)))
         ann = O.annotations(pod)
         if ann.get(C.ANNOT_ISOLATION) == "partition":
             # one whole compute partition of the requested (or controller-chosen) size
@@ -456,7 +468,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if self.parity is not None or self.planner is not None:
             return None
         req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
-        rsig = (req.whole, req.units, req.cu, req.hbm_gib, req.isolated, req.part_cus, req.implicit, req.gpu_pod)
+        rsig = (req.whole, req.units, req.cu, req.hbm_gib, req.isolated, req.part_cus, req.implicit, req.gpu_pod,
+                req.iters)
         if phase != "score":
             return rsig
         if self.args.pack == "random":
@@ -468,7 +481,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if req.whole:
             return rsig, tok
         sig = self._pod_ctx(state, pod, req)[4]
-        return None if sig is None else (rsig, sig, tok, self._pred_version)
+        return None if sig is None else (rsig, sig, tok, self._pred_version, id(self.corun_model()))
 
     def _planned_choice(self, state: CycleState, req: GpuRequest, node: str, plan: Any) -> Optional[Choice]:
         """The plan's device on its node as a top-scored Choice, if it is still a candidate."""
@@ -520,7 +533,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         work = self.pod_work(pod, (state.read(_PRED) or self._pod_predictions(O.name(pod)))[0]) \
             if choice is not None else 0.0
         if choice is None or not self.ledger.reserve(node_name, O.key(pod), O.name(pod), req.slo, choice.allocs,
-                                                     work=work):
+                                                     work=work, iters=req.iters):
             return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
         state.write(_CHOICE + "/reserved", choice)
         if self.planner is not None:
@@ -796,7 +809,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         sig = None
         if a.pack != "random":
             x_col = self._workload_col(name, intf) if intf else None
-            sig = (req.units, req.hbm_gib, req.slo, work, x_col, self.mfma_fraction(name) if a.w_complement else None,
+            sig = (req.units, req.hbm_gib, req.slo, req.iters, work, x_col,
+                   self.mfma_fraction(name) if a.w_complement else None,
                    tuple(sorted(conf.items())) if conf else (),
                    () if x_col is not None or not intf else tuple(sorted(intf.items())))
         ctx = (name, conf, intf, work, sig)
@@ -1001,6 +1015,12 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                      conf: Dict[str, float], intf: Dict[str, float], work: float = 0.0) -> Optional[Choice]:
         a = self.args
         states = self.ledger.devices(node)
+        if a.w_slo and a.pack != "random":
+            model = self.corun_model()
+            if model is not None:
+                choice = self._score_cands_corun(node, cands, req, name, states, model)
+                if choice is not None:
+                    return choice
         if self.native_score and a.pack != "random" and len(cands) >= self.NATIVE_MIN_CANDS:
             core = self._core()
             # the node's pack is built on the SECOND score of one node version: a node that
@@ -1071,6 +1091,129 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                 best_i, best_sc = i, sc
         if best_i < 0:
             return None
+        st, u0 = cands[best_i]
+        return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], best_sc, [st.device])
+
+    # ------------------------------------------------------------------ co-run SLO objective
+    def corun_model(self) -> Any:
+        """The co-run model of the prediction provider (models.corun.CorunModel) when Score
+        uses the co-run constraint, else None."""
+        if self.args.slo_objective == "terms" or self.predictions is None:
+            return None
+        fn = getattr(self.predictions, "corun", None)
+        return fn() if fn is not None else None
+
+    @staticmethod
+    def corun_group_key(st: DeviceState) -> Tuple[int, ...]:
+        """Pods that co-run: every fractional pod on a physical GPU in SPX (they share its CUs
+        and HBM), only the pods of one partition on a partitioned GPU."""
+        d = st.device
+        return (d.gpu,) if d.partitions <= 1 else (d.gpu, d.partition)
+
+    def _corun_pack(self, node: str, states: List[DeviceState], model: Any) -> Optional[Dict[str, Any]]:
+        """A node's co-run groups (residents per group as CSR arrays) and their current SLO
+        misses / makespans, memoised per node version x model."""
+        import numpy as np
+        key = (self.ledger.node_gen.get(node, 0), id(model), len(states))
+        hit = self._corun_packs.get(node)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        core = self._core()
+        if core is None or not hasattr(core, "corun_gpu_eval"):
+            return None
+        gids: Dict[Tuple[int, ...], int] = {}
+        dev_group: Dict[str, int] = {}
+        for st in states:
+            dev_group[st.device.uuid] = gids.setdefault(self.corun_group_key(st), len(gids))
+        per: List[List[Tuple[int, float, float]]] = [[] for _ in gids]
+        seen = set()
+        for st in states:
+            g = dev_group[st.device.uuid]
+            for k, use in st.pods.items():
+                if (k, g) in seen:
+                    continue
+                seen.add((k, g))
+                w = model.wid(use.name)
+                if w >= 0:                  # a workload the model does not know is not modelled
+                    per[g].append((w, use.iters, use.slo))
+        off = np.zeros(len(per) + 1, np.int64)
+        off[1:] = np.cumsum([len(m) for m in per])
+        flat = [x for m in per for x in m]
+        r_wid = np.asarray([x[0] for x in flat], np.int32)
+        r_iters = np.asarray([x[1] for x in flat], np.float64)
+        r_slo = np.asarray([x[2] for x in flat], np.float64)
+        if max((len(m) for m in per), default=0) >= 64:
+            return None
+        bad, mk = core.corun_groups_eval(off, r_wid, r_iters, r_slo, model.alone_ms, model.coupling())
+        pack = {"dev_group": dev_group, "off": off, "r_wid": r_wid, "r_iters": r_iters, "r_slo": r_slo,
+                "bad": bad, "mk": mk, "mk_max": float(mk.max(initial=0.0))}
+        if len(self._corun_packs) > 65536:
+            self._corun_packs.clear()
+        self._corun_packs[node] = (key, pack)
+        return pack
+
+    @staticmethod
+    def corun_band(new_bad: int, blend: float) -> float:
+        """Score band of a placement causing `new_bad` predicted SLO misses (its own or its
+        co-runners'): [50, 100) with none, [50/(k+1), 50/k) with k -- strictly ordered by k;
+        `blend` (0..100, the packing / balance / telemetry terms) orders inside a band."""
+        k = max(0, int(new_bad))
+        lo = 50.0 / (k + 1)
+        hi = 100.0 if k == 0 else 50.0 / k
+        return lo + (hi - lo) * min(max(blend, 0.0), 100.0) / 100.0 * 0.999
+
+    def _score_cands_corun(self, node: str, cands: List[Tuple[DeviceState, int]], req: GpuRequest, name: str,
+                           states: List[DeviceState], model: Any) -> Optional[Choice]:
+        """Co-run constraint Score of one node's candidate devices (see GPUArgs.slo_objective):
+        each candidate's co-run group is simulated with and without the pod (native
+        corun_gpu_eval); new predicted SLO misses pick the band, packing / makespan balance /
+        telemetry order within it.  None = the pod's workload is unknown to the model."""
+        import numpy as np
+        xw = model.wid(name)
+        if xw < 0:
+            return None
+        pack = self._corun_pack(node, states, model)
+        if pack is None:
+            return None
+        a = self.args
+        dg = pack["dev_group"]
+        cg = np.asarray([dg[st.device.uuid] for st, _ in cands], np.int32)
+        ug, inv = np.unique(cg, return_inverse=True)
+        bb, ba, mb, ma, _ = self._core().corun_gpu_eval(
+            pack["off"], pack["r_wid"], pack["r_iters"], pack["r_slo"], int(xw), float(req.iters), float(req.slo),
+            ug.astype(np.int32), model.alone_ms, model.coupling())
+        top = max(pack["mk_max"], float(ma.max(initial=0.0)))
+        fill: Dict[int, Tuple[int, int]] = {}
+        if a.w_pack:
+            for s2 in states:
+                t, u = fill.get(s2.device.gpu, (0, 0))
+                fill[s2.device.gpu] = (t + s2.device.units, u + s2.device.units - s2.free_units)
+        samples = self.telemetry.node(node) if a.w_telemetry else {}
+        binpack = a.pack == "binpack"
+        hbm_mb = req.hbm_gib * 1024
+        best_i, best_sc = -1, 0.0
+        for i, (st, u0) in enumerate(cands):
+            j = int(inv[i])
+            num = den = 0.0
+            g = st.device.gpu
+            if a.w_pack:
+                tot, used = fill[g]
+                frac = (used + req.units) / max(tot, 1)
+                num += a.w_pack * (100.0 * frac if binpack else 100.0 * (1.0 - frac))
+                den += a.w_pack
+            if a.w_balance:
+                # the group's predicted makespan after placement against the node's longest
+                num += a.w_balance * (100.0 * (1.0 - float(ma[j]) / top) if top > 0 else 100.0)
+                den += a.w_balance
+            if samples:
+                smp = samples.get(st.device.uuid)
+                if smp is not None:
+                    hbm_ok = 1.0 if smp.vram_total_mb - smp.vram_used_mb >= hbm_mb else 0.0
+                    num += a.w_telemetry * 100.0 * (1.0 - min(1.0, smp.gfx_activity)) * hbm_ok
+                    den += a.w_telemetry
+            sc = self.corun_band(int(ba[j]) - int(bb[j]), num / den if den > 0 else 100.0)
+            if best_i < 0 or sc > best_sc:
+                best_i, best_sc = i, sc
         st, u0 = cands[best_i]
         return Choice(node, [(st.device.uuid, u0, req.units, req.hbm_gib, False)], best_sc, [st.device])
 

@@ -90,6 +90,11 @@ class PredictionProvider:
     def interference(self, name: str) -> Dict[str, float]:
         raise NotImplementedError
 
+    def corun(self) -> Any:
+        """The multi-way co-run model (models.corun.CorunModel) the recommender serves, or
+        None (then Score falls back to the reference's pairwise interference terms)."""
+        return None
+
 
 class RpcPredictions(PredictionProvider):
     def __init__(self, client: RecommenderClient):
@@ -131,7 +136,7 @@ class CachedPredictions(PredictionProvider):
 
     def __init__(self, client: Optional[RecommenderClient] = None,
                  conf: Optional[TrainedTable] = None, intf: Optional[TrainedTable] = None,
-                 refresh_s: float = 30.0, retry_s: float = 2.0, background: bool = True):
+                 refresh_s: float = 30.0, retry_s: float = 2.0, background: bool = True, corun: Any = None):
         self.client = client
         self.refresh_s = refresh_s
         self.retry_s = retry_s
@@ -140,6 +145,7 @@ class CachedPredictions(PredictionProvider):
         self._thread: Optional[threading.Thread] = None
         self._conf: Optional[_Tab] = None
         self._intf: Optional[_Tab] = None
+        self._corun: Any = corun            # models.corun.CorunModel
         if conf is not None:
             self._conf = _Tab(conf.table.index, conf.table.columns, conf.completed().tolist(), conf.version)
         if intf is not None:
@@ -183,6 +189,19 @@ class CachedPredictions(PredictionProvider):
                 self._conf = tab
             else:
                 self._intf = tab
+        # the co-run model (an older recommender answers with an empty table: keep what we have)
+        try:
+            t = self.client.export_table("corun")
+        except Exception as e:
+            log.debug("co-run model unavailable: %s", e)
+            return
+        cur = self._corun
+        if t.rows and (cur is None or cur.version != t.version):
+            from ..models.corun import CorunModel
+            m = CorunModel.from_table([r.index for r in t.rows], list(t.columns), [list(r.values) for r in t.rows],
+                                      t.version)
+            if m is not None:
+                self._corun = m
 
     def configurations(self, name: str) -> Dict[str, float]:
         return self._conf.lookup(name) if self._conf else {}
@@ -190,14 +209,21 @@ class CachedPredictions(PredictionProvider):
     def interference(self, name: str) -> Dict[str, float]:
         return self._intf.lookup(name) if self._intf else {}
 
+    def corun(self) -> Any:
+        return self._corun
+
+    def install_corun(self, model: Any) -> None:
+        """Swap in a new co-run model (e.g. the online-refined one)."""
+        self._corun = model
+
     def tables(self) -> "tuple[Optional[_Tab], Optional[_Tab]]":
         return self._conf, self._intf
 
     def version(self) -> tuple:
-        """Changes whenever a new configurations / interference table is installed (callers
-        memoising per-pod lookups key their memo by it)."""
-        c, i = self._conf, self._intf
-        return (id(c), c.version if c else None, id(i), i.version if i else None)
+        """Changes whenever a new configurations / interference table or co-run model is
+        installed (callers memoising per-pod lookups key their memo by it)."""
+        c, i, m = self._conf, self._intf, self._corun
+        return (id(c), c.version if c else None, id(i), i.version if i else None, id(m))
 
     def install_interference(self, index: List[str], columns: List[str], rows: List[List[float]],
                              version: str) -> None:

@@ -507,6 +507,8 @@ py::tuple select_nodes(py::array_t<int8_t, py::array::c_style | py::array::force
 
 }  // namespace
 
+void register_corun(py::module_& m);   // corun.cpp: multi-way co-run model
+
 PYBIND11_MODULE(_core, m) {
   m.doc() = "native scoring core for the GPU scheduler plugin";
   m.def("slo_scores", &slo_scores, py::arg("offsets"), py::arg("r_slo"), py::arg("r_pred"), py::arg("r_intf"),
@@ -535,4 +537,5 @@ PYBIND11_MODULE(_core, m) {
       .def("score", &NodePack::score);
   m.def("select_nodes", &select_nodes, py::arg("feasible"), py::arg("raw"), py::arg("norm"), py::arg("weights"),
         py::arg("start"), py::arg("limit"));
+  register_corun(m);
 }

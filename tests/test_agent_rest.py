@@ -290,3 +290,61 @@ def test_agent_evicts_hbm_overuse_when_asked():
     assert ag.evicted == ["default/greedy"]
     with pytest.raises(NotFound):
         fc.get("pods", "greedy", "default")
+
+
+def test_hbm_overuse_eviction_honours_pdb_and_retries():
+    """Eviction goes through the Eviction API: a PodDisruptionBudget with no disruptions
+    allowed refuses it (429); the pod is NOT marked handled, so the next step retries and
+    succeeds once the budget allows one disruption."""
+    from k8s_gpu_scheduler_amd.kube.client import TooManyRequests
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=1))
+    pod = O.make_pod("greedy", gpu_cu=64, gpu_mem_gib=2, node_name="n1", phase="Running",
+                     labels_={"app": "greedy"})
+    fc.create("pods", pod)
+    a = fc.get("pods", "greedy", "default")
+    fc.create("poddisruptionbudgets", {"metadata": {"name": "greedy-pdb", "namespace": "default"},
+                                       "spec": {"selector": {"matchLabels": {"app": "greedy"}}},
+                                       "status": {"disruptionsAllowed": 0}})
+    with pytest.raises(TooManyRequests):
+        fc.evict("default", "greedy")
+    src = synthetic_node(1, node="n1")
+    src.procs = {0: [{"pid": 7, "vram_bytes": 40 * 2**30}]}
+    ag = NodeAgent("n1", rds(), src, client=fc, pod_resolver={7: O.uid(a)}.get, evict_hbm_overuse=True)
+    ag.step()
+    assert ag.evicted == [] and fc.get("pods", "greedy", "default")
+    assert "default/greedy" not in ag._overuse_flagged
+    fc.patch("poddisruptionbudgets", "greedy-pdb", {"status": {"disruptionsAllowed": 1}}, "merge", "default")
+    ag.step()
+    assert ag.evicted == ["default/greedy"] and fc.evictions == [("default", "greedy")]
+    with pytest.raises(NotFound):
+        fc.get("pods", "greedy", "default")
+
+
+def test_hbm_tolerance_is_configurable():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=1))
+    a = _bound_pod(fc, "p", 4)
+    src = synthetic_node(1, node="n1")
+    src.procs = {0: [{"pid": 7, "vram_bytes": int(4.4 * 2**30)}]}     # 0.4 GiB of runtime overhead
+    ag = NodeAgent("n1", rds(), src, client=fc, pod_resolver={7: O.uid(a)}.get)
+    assert ag.check_hbm() == {}                                       # default 0.5 GiB covers it
+    ag.hbm_tolerance_gib = 0.25
+    assert list(ag.check_hbm()) == ["default/p"]
+
+
+def test_agent_recognises_its_own_host_pid_by_cgroup(tmp_path):
+    """amd-smi reports host PIDs; the agent's container PID namespace hides its host PID,
+    so its own GPU context is recognised through the host /proc cgroup instead."""
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=1))
+    mine = open("/proc/self/cgroup").read()
+    (tmp_path / "31337").mkdir()
+    (tmp_path / "31337" / "cgroup").write_text(mine)
+    (tmp_path / "4242").mkdir()
+    (tmp_path / "4242" / "cgroup").write_text("0::/kubepods/other-pod\n")
+    src = synthetic_node(1, node="n1")
+    src.procs = {0: [{"pid": 31337, "name": "agent"}, {"pid": 4242, "name": "train.py"}]}
+    ag = NodeAgent("n1", rds(), src, client=fc, host_proc=str(tmp_path))
+    reasons = ag.busy_reasons()
+    assert len(reasons) == 1 and "4242" in reasons[0]

@@ -110,6 +110,21 @@ def test_agent_daemonset_serves_the_device_plugin():
     assert {"patch", "delete", "list"} <= pod_verbs
 
 
+def test_agent_role_covers_what_the_agent_does():
+    """The node agent creates GPUMemoryOveruse Warning events and evicts through the
+    Eviction API: its ClusterRole must allow both (create_event swallows a 403)."""
+    rules = [r for f, d in _docs() if f.startswith("profiler") and d.get("kind") == "ClusterRole"
+             for r in d["rules"]]
+
+    def allowed(resource, verb, group=""):
+        return any(resource in r.get("resources", []) and group in r.get("apiGroups", [""])
+                   and (verb in r.get("verbs", []) or "*" in r.get("verbs", [])) for r in rules)
+    assert allowed("events", "create")
+    assert allowed("events", "create", "events.k8s.io")
+    assert allowed("pods/eviction", "create")
+    assert allowed("nodes", "patch")
+
+
 def _replication_script():
     import yaml
     docs = list(yaml.safe_load_all(open(os.path.join(ROOT, "deploy/redis/redis-statefulset.yaml"))))

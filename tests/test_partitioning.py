@@ -192,3 +192,47 @@ def test_memory_partition_applied_before_compute():
     assert [m for _, m in src.partition_calls[2:]] == ["DPX", "DPX"]
     caps = partition_capabilities(src.partition_info(0))
     assert caps.current_memory == "NPS2" and caps.current_compute == "DPX"
+
+
+def test_unledgered_busy_node_is_requested_once_then_backed_off():
+    """A node busy with GPU work the ledger cannot see (a process of another scheduler):
+    the controller asks once, the agent drains, times out and refuses, and while the
+    isolated pod stays pending the controller does not re-taint that node for that mode
+    until the backoff expires (advisor round 2: the request/refuse loop)."""
+    fc, r, agents, s, plugin = _cluster()
+    agents["n1"].source.procs = {2: [{"pid": 999, "name": "other-scheduler-job", "vram_bytes": 2**30}]}
+    agents["n1"].drain_timeout_s = 0.0
+    for i in range(8):
+        fc.create("pods", O.make_pod(f"iso-{i}", gpu_cu=32, annotations_=ISO))
+    s.schedule_pending()
+    pc = plugin.partitioner
+    assert [(d.node, d.mode) for d in pc.step()] == [("n1", "CPX")]
+    assert not agents["n1"].reconcile_partitions()          # busy: starts draining (taint)
+    time.sleep(0.01)
+    assert not agents["n1"].reconcile_partitions()          # drain timed out: refused + reverted
+    node = fc.get("nodes", "n1")
+    assert json.loads(O.annotations(node)[C.ANNOT_PARTITION_STATE])["state"] == "refused"
+    assert O.labels(node)[C.LABEL_COMPUTE_PARTITION] == "SPX" and not O.node_taints(node)
+    for _ in range(3):                                      # pods still pending: no new request
+        s.schedule_pending(timeout_s=0.05)
+        assert pc.step() == []
+    assert O.labels(fc.get("nodes", "n1"))[C.LABEL_COMPUTE_PARTITION] == "SPX"
+    assert pc.backed_off("n1", "CPX") and not pc.backed_off("n1", "QPX")
+    # once the backoff has expired the node is eligible again
+    pc._backoff[("n1", "CPX")] = 0.0
+    fc.patch("nodes", "n1", {"metadata": {"annotations": {C.ANNOT_PARTITION_STATE: json.dumps(
+        {"state": "refused", "mode": "CPX", "ts": time.time() - 2 * pc.backoff_s})}}}, "merge")
+    assert [(d.node, d.mode) for d in pc.step()] == [("n1", "CPX")]
+
+
+def test_request_reverted_without_state_annotation_backs_off():
+    """If the agent could not write partition-state, a request of ours whose label came back
+    reverted without the mode being applied still counts as refused."""
+    fc, r, agents, s, plugin = _cluster()
+    for i in range(8):
+        fc.create("pods", O.make_pod(f"iso-{i}", gpu_cu=32, annotations_=ISO))
+    s.schedule_pending()
+    pc = plugin.partitioner
+    assert [d.mode for d in pc.step()] == ["CPX"]
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "SPX"}}}, "merge")
+    assert pc.step() == [] and pc.backed_off("n1", "CPX")

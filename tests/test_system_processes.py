@@ -141,7 +141,11 @@ def test_agent_serves_device_plugin_to_kubelet_as_process(tmp_path):
         procs.append(sc)
         client.create("pods", O.make_pod("frac-0", gpu_cu=64, gpu_mem_gib=8, gpu_limits=True))
         pod = _wait(lambda: (lambda p: p if O.node_name_of(p) else None)(client.get("pods", "frac-0", "default")), 90)
-        assert pod, "pod not bound"
+        if not pod:
+            for p in procs:
+                p.terminate()
+            logs = "\n".join(f"--- {p.args[3:5]}\n" + (p.communicate(timeout=10)[0] or "")[-3000:] for p in procs)
+            raise AssertionError("pod not bound; process output:\n" + logs)
         ch = grpc.insecure_channel(f"unix://{tmp_path}/{dp.socket_name(C.RESOURCE_GPU_CU)}")
         alloc = ch.unary_unary(f"/{dp.PLUGIN_SERVICE}/Allocate", request_serializer=dp.AllocateRequest.SerializeToString,
                                response_deserializer=dp.AllocateResponse.FromString)

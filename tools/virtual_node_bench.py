@@ -11,9 +11,12 @@ time), the mean group (the work-conserving bound), the node's epoch time when th
 group times are replayed through the bench's 2-deep launch-ahead pipeline (ranks meet only
 at the placement broadcast, so per-epoch imbalance averages out) and the SLO attainment, for placement policies side by side (interleaved per epoch, same arrivals):
 
-  * greedy (balance + LPT)
-  * planned (`planBursts`: joint SLO / interference-adjusted-load search; `planned_t0` with
-    no load tolerance, `planned_load` with the load-first objective)
+  * greedy (balance + LPT, the reference's pairwise interference terms)
+  * corun (Score under the multi-way co-run model's SLO constraint, models.corun)
+  * corun_plan_tXX (burst planner on the co-run model: balanced group makespans, then the
+    most predicted SLOs met within XX % of the balanced plan's slowest GPU)
+  * planned (`planBursts` on the pairwise table; `planned_t0` with no load tolerance,
+    `planned_load` with the load-first objective)
   * random
 
     python tools/virtual_node_bench.py [--epochs 12] [--out gpurun_out/virtual_node.json]
@@ -27,6 +30,10 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+# one HW queue per pod stream, as bench.py (before HIP initialises)
+_q = int(os.environ.get("GPUSCHED_HW_QUEUES", "16"))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _q <= 32:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_q)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -43,6 +50,11 @@ POLICIES = {
     "planned_t0": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.0),
     "planned_load": dict(balance=1.0, plan_bursts=True, plan_objective="load"),
     "random": dict(policy="random", balance=0.0, plan_bursts=False),
+    "corun": dict(balance=1.0, plan_bursts=False, slo_objective="corun"),
+    "corun_plan_t05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.05, slo_objective="corun"),
+    "corun_plan_t10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun"),
+    "corun_plan_t15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.15, slo_objective="corun"),
+    "corun_plan_t20": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun"),
     # roofline complementarity term (GPU plugin weightComplement) on top of greedy
     "greedy_comp": dict(balance=1.0, plan_bursts=False, complement=1.0),
     "greedy_comp3": dict(balance=1.0, plan_bursts=False, complement=3.0),
@@ -109,11 +121,13 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/virtual_node.json")
     ap.add_argument("--dump-groups", default="", help="write every group's workloads and wall ms (JSON)")
-    ap.add_argument("--policies", nargs="+", default=["greedy", "planned", "random"], choices=sorted(POLICIES))
+    ap.add_argument("--policies", nargs="+", default=["greedy", "corun", "corun_plan_t10", "random"],
+                    choices=sorted(POLICIES))
     a = ap.parse_args()
     policies = {k: POLICIES[k] for k in a.policies}
     cps = {k: ControlPlane(n_gpus=N_GPUS, pods_per_gpu=4, iters=20, seed=a.seed, **kw) for k, kw in policies.items()}
     ex = DeviceExecutor(0, use_cu_masks=True)
+    ex.use_graphs = True                # as the bench (and the co-run model's measurements)
     ex.warm([PodRun(0, wl, u, 2, 20, masked=False) for wl in W.NAMES for u in (0, 2, 4, 6)])
     stats = {k: {"max_ms": [], "mean_ms": [], "walls": [], "ok": 0, "n": 0} for k in policies}
     for e in range(a.warmup + a.epochs):
@@ -135,6 +149,7 @@ def main() -> None:
         out[k] = {"epoch_ms_slowest_gpu": round(mx, 3), "epoch_ms_mean_gpu": round(mn, 3),
                   "imbalance": round(mx / mn, 4), "pods_per_s_8gpu_coupled": round(4 * N_GPUS / mx * 1e3, 1),
                   "slo_attainment_pct": round(100.0 * st["ok"] / max(st["n"], 1), 2), "pods": st["n"],
+                  "interference_mae": cps[k].interference_mae(),
                   "epoch_ms_pipelined_l2": round(pipelined_ms(np.array(st["walls"]), 2), 3),
                   "epoch_ms_pipelined_l3": round(pipelined_ms(np.array(st["walls"]), 3), 3),
                   "epoch_ms_pipelined_l4": round(pipelined_ms(np.array(st["walls"]), 4), 3),
