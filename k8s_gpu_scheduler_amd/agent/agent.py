@@ -62,7 +62,7 @@ class NodeAgent:
                  apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None,
                  health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
                  drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1,
-                 hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc"):
+                 hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc", profile_dir: str = ""):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -85,6 +85,13 @@ class NodeAgent:
         # the pod's amd.com/gpu-memory request does not -- the tolerance must cover them
         self.hbm_tolerance_gib = hbm_tolerance_gib
         self.host_proc = host_proc
+        # per-pod rocprofv3 output the profiling webhook (agent.profile_webhook) routes to a
+        # hostPath: finished runs become workload-history samples (pod_profiler.ProfileIngestor)
+        self.profiles = None
+        if profile_dir:
+            from ..recommender.admission import RedisHistory
+            from .pod_profiler import ProfileIngestor
+            self.profiles = ProfileIngestor(profile_dir, RedisHistory(redis))
         self.history_every = max(1, history_every)
         self._steps = 0
         self.health = health or HealthMonitor()
@@ -500,6 +507,11 @@ class NodeAgent:
                 self.check_hbm(usage)
             except Exception as e:
                 log.warning("per-pod usage / HBM check failed: %s", e)
+        if self.profiles is not None:
+            try:
+                self.profiles.step()
+            except Exception as e:
+                log.warning("ingesting per-pod profiles failed: %s", e)
 
     def run(self) -> None:
         while not self._stop.is_set():

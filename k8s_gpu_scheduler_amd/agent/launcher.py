@@ -55,6 +55,36 @@ class LaunchResult:
         return None
 
 
+_VAR = None
+
+
+def _expand(s: str, env: Dict[str, str]) -> str:
+    """Kubernetes' $(VAR) expansion (an undefined reference stays as written, $$ escapes)."""
+    global _VAR
+    if "$(" not in s and "$$" not in s:
+        return s
+    if _VAR is None:
+        import re
+        _VAR = re.compile(r"\$\$|\$\(([A-Za-z_][A-Za-z0-9_.-]*)\)")
+    return _VAR.sub(lambda m: "$" if m.group(0) == "$$" else env.get(m.group(1), m.group(0)), s)
+
+
+def _field_ref(pod: Obj, path: str) -> Optional[str]:
+    """Downward API fieldRef values a kubelet resolves for env."""
+    if path == "metadata.name":
+        return O.name(pod)
+    if path == "metadata.namespace":
+        return O.namespace(pod)
+    if path == "metadata.uid":
+        return O.uid(pod)
+    if path == "spec.nodeName":
+        return O.node_name_of(pod) or ""
+    if path.startswith("metadata.annotations['") or path.startswith("metadata.labels['"):
+        key = path.split("['", 1)[1].rstrip("']")
+        return (O.annotations(pod) if path.startswith("metadata.annotations") else O.labels(pod)).get(key, "")
+    return None
+
+
 class PodLauncher:
     def __init__(self, client: KubeClient, node_name: str, command: Optional[List[str]] = None,
                  timeout_s: float = 120.0, base_env: Optional[Dict[str, str]] = None,
@@ -94,7 +124,11 @@ class PodLauncher:
         env.update(from_cms)
         for e in ctr.get("env") or []:
             if "value" in e:
-                env[e["name"]] = str(e["value"])
+                env[e["name"]] = _expand(str(e["value"]), env)
+            elif "valueFrom" in e:
+                v = _field_ref(pod, ((e.get("valueFrom") or {}).get("fieldRef") or {}).get("fieldPath", ""))
+                if v is not None:
+                    env[e["name"]] = v
         ann = O.annotations(pod)
         devices = ann.get(C.ANNOT_DEVICES, "")
         if devices:
@@ -112,6 +146,12 @@ class PodLauncher:
         ctr = O.containers(pod)[0] if O.containers(pod) else {}
         argv = (self.command_for(pod) if self.command_for else None) or \
             (list(ctr.get("command") or []) + list(ctr.get("args") or [])) or self.command
+        # kubelet: $(VAR) in command/args expands from the container env; a process runtime
+        # has no mount namespace, so hostPath volumeMounts become path rewrites
+        mounts = self.host_mounts(pod, ctr)
+        argv = [self._remap(_expand(a, env), mounts) for a in argv]
+        for mp, hp in mounts.items():
+            os.makedirs(self.host_root + hp, exist_ok=True)     # hostPath type DirectoryOrCreate
         full_env = dict(self.base_env)
         full_env.update(self.extra_env)
         full_env.update(env)
@@ -130,6 +170,25 @@ class PodLauncher:
         except NotFound:
             pass
         return res
+
+    @staticmethod
+    def host_mounts(pod: Obj, ctr: Obj) -> Dict[str, str]:
+        """mountPath -> hostPath of the container's hostPath volume mounts."""
+        vols = {v.get("name"): (v.get("hostPath") or {}).get("path") for v in (pod.get("spec") or {}).get("volumes") or []}
+        out = {}
+        for m in ctr.get("volumeMounts") or []:
+            hp = vols.get(m.get("name"))
+            if hp and m.get("mountPath"):
+                out[m["mountPath"].rstrip("/")] = hp
+        return out
+
+    def _remap(self, arg: str, mounts: Dict[str, str]) -> str:
+        for mp, hp in sorted(mounts.items(), key=lambda kv: -len(kv[0])):
+            if arg == mp or arg.startswith(mp + "/"):
+                return self.host_root + hp + arg[len(mp):]
+        return arg
+
+    host_root = ""      # prefix for hostPath volumes (tests point it at a scratch directory)
 
     def run_bound(self) -> List[LaunchResult]:
         """Launch every pod bound to this node that has not run yet (one pass)."""

@@ -17,11 +17,12 @@ time, counter totals -- and appended to the pod's workload history
 from __future__ import annotations
 
 import csv
+import logging
 import os
 import shutil
 import tempfile
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from ..api import constants as C
 from ..api import objects as O
@@ -29,6 +30,7 @@ from ..recommender.admission import RedisHistory, workload_key
 from .launcher import LaunchResult, PodLauncher
 
 ROCPROF = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+log = logging.getLogger(__name__)
 
 
 def summarize_kernel_stats(path: str, top: int = 5) -> Dict[str, Any]:
@@ -116,3 +118,106 @@ class ProfiledLauncher(PodLauncher):
                     shutil.copytree(out_dir, dst)
             shutil.rmtree(work, ignore_errors=True)
         return res
+
+
+def summarize_kernel_trace(path: str) -> Dict[str, Any]:
+    """Span (first kernel start .. last kernel end) and busy time (union of kernel intervals)
+    of a rocprofv3 kernel_trace.csv, in ms."""
+    iv = []
+    for r in csv.DictReader(open(path)):
+        try:
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        except (KeyError, ValueError):
+            continue
+    if not iv:
+        return {}
+    iv.sort()
+    busy, cs, ce = 0, iv[0][0], iv[0][1]
+    for a, b in iv[1:]:
+        if a > ce:
+            busy += ce - cs
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    busy += ce - cs
+    span = max(b for _, b in iv) - iv[0][0]
+    return {"span_ms": span / 1e6, "busy_union_ms": busy / 1e6}
+
+
+class ProfileIngestor:
+    """Node-agent side of the profiling webhook (agent.profile_webhook): every finished
+    rocprofv3 output directory under the hostPath -- <root>/<ns>/<pod>/<uid>/<container>/<tag>
+    -- becomes one sample of the pod's workload history (what the resize admission reads):
+    GPU busy time, kernel count, top kernels, the kernel span and busy fraction, the CU share
+    and HBM it was admitted with, and -- for a batch pod with ITERATIONS -- its throughput
+    (iterations / kernel span).  A directory is finished when rocprofv3 has written its
+    stats (kernel_stats.csv, or counter_collection.csv for a PMC pass); ingested ones are
+    removed, so each run is counted once."""
+
+    def __init__(self, root: str, history: RedisHistory, keep_dir: str = ""):
+        self.root = root
+        self.history = history
+        self.keep_dir = keep_dir
+        self.ingested: List[Dict[str, Any]] = []
+
+    def _finished(self) -> List[Tuple[str, List[str]]]:
+        out = []
+        if not os.path.isdir(self.root):
+            return out
+        for dirpath, _, files in os.walk(self.root):
+            rel = os.path.relpath(dirpath, self.root).split(os.sep)
+            if len(rel) != 5:
+                continue
+            if any(f.endswith("kernel_stats.csv") or f.endswith("counter_collection.csv") for f in files):
+                out.append((dirpath, rel))
+        return out
+
+    def step(self) -> int:
+        from .profile_webhook import parse_tag
+        n = 0
+        for d, (ns, name, uid, container, tag) in self._finished():
+            sample: Dict[str, Any] = {"ts": time.time(), "pod": f"{ns}/{name}", "uid": uid, "container": container,
+                                      "source": "rocprof"}
+            req = parse_tag(tag)
+            for root, _, files in os.walk(d):
+                for f in files:
+                    p = os.path.join(root, f)
+                    try:
+                        if f.endswith("kernel_stats.csv"):
+                            sample.update(summarize_kernel_stats(p))
+                        elif f.endswith("kernel_trace.csv"):
+                            sample.update(summarize_kernel_trace(p))
+                        elif f.endswith("counter_collection.csv"):
+                            sample["counters"] = summarize_counters(p)
+                    except (OSError, csv.Error, KeyError, ValueError) as e:
+                        log.warning("profile %s: %s unreadable: %s", d, f, e)
+            if "cu" in req:
+                sample["cu"] = int(req["cu"])
+            if req.get("hbm_gib"):
+                sample["hbm_gib"] = req["hbm_gib"]
+            span = sample.get("span_ms")
+            if span:
+                sample["busy_frac"] = min(1.0, sample.get("busy_union_ms", 0.0) / span)
+                sample["cu_busy"] = sample["busy_frac"]
+                if req.get("iters"):
+                    sample["throughput"] = req["iters"] / (span / 1e3)
+            pod = {"metadata": {"name": name, "namespace": ns, "annotations": {}}}
+            try:
+                self.history.append(workload_key(pod), sample)
+            except Exception as e:          # Redis blip: keep the directory for the next pass
+                log.warning("profile %s: history append failed: %s", d, e)
+                continue
+            self.ingested.append(sample)
+            n += 1
+            if self.keep_dir:
+                dst = os.path.join(self.keep_dir, ns, name, uid, container)
+                shutil.rmtree(dst, ignore_errors=True)
+                shutil.copytree(d, dst)
+            shutil.rmtree(d, ignore_errors=True)
+            # drop the now-empty parents (<uid>/<container>) so the tree does not grow
+            for up in (os.path.dirname(d), os.path.dirname(os.path.dirname(d))):
+                try:
+                    os.rmdir(up)
+                except OSError:
+                    break
+        return n

@@ -210,7 +210,15 @@ def cmd_resize_webhook(args) -> int:
         cp = CachedPredictions(RecommenderClient(args.recommender))
         preds = cp.configurations
     adm = ResizeAdmission(hist.read, preds, min_samples=args.min_samples, shrink_only=args.shrink_only)
-    srv = AdmissionServer(adm, "0.0.0.0", args.port, args.tls_cert, args.tls_key).start()
+    routes = {}
+    if args.profile:
+        # per-pod rocprofv3 injection (agent.profile_webhook): /profile alone, and chained
+        # after the resize on /mutate so a pod gets both with one webhook call
+        from ..agent.profile_webhook import ChainAdmission, ProfileInjector
+        inj = ProfileInjector(rocprof=args.rocprof, host_dir=args.profile_host_dir)
+        routes["/profile"] = inj
+        adm = ChainAdmission(adm, inj)
+    srv = AdmissionServer(adm, "0.0.0.0", args.port, args.tls_cert, args.tls_key, routes=routes).start()
     logging.info("resize webhook on %s", srv.url)
     try:
         while True:
@@ -251,7 +259,7 @@ def cmd_agent(args) -> int:
     proc_root = args.proc_root or ("/host/proc" if os.path.isdir("/host/proc") else "/proc")
     agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy,
                       evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout,
-                      hbm_tolerance_gib=args.hbm_tolerance, host_proc=proc_root,
+                      hbm_tolerance_gib=args.hbm_tolerance, host_proc=proc_root, profile_dir=args.profile_dir,
                       pod_resolver=lambda pid: pod_of_pid(pid, proc_root))
     mgr = None
     if args.device_plugin:
@@ -392,6 +400,10 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--tls-key", default="")
     s.add_argument("--min-samples", type=int, default=3)
     s.add_argument("--shrink-only", action="store_true")
+    s.add_argument("--profile", action="store_true",
+                   help="also wrap opted-in pods (label gpu-scheduler.amd.com/profile=trace|pmc) in rocprofv3")
+    s.add_argument("--rocprof", default="rocprofv3", help="rocprofv3 path inside the pods' images")
+    s.add_argument("--profile-host-dir", default="/var/lib/gpusched/prof")
     s.set_defaults(fn=cmd_resize_webhook)
     s = sub.add_parser("agent")
     common(s)
@@ -410,6 +422,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--evict-hbm-overuse", action="store_true",
                    help="evict (Eviction API, PodDisruptionBudgets apply) pods whose processes hold more VRAM "
                         "than their amd.com/gpu-memory share")
+    s.add_argument("--profile-dir", default="",
+                   help="hostPath where profiled pods' rocprofv3 output lands (mounted from /var/lib/gpusched/prof; "
+                        "see the resize webhook's --profile): finished runs go to the workload history in Redis")
     s.add_argument("--hbm-tolerance", type=float, default=0.5,
                    help="GiB over a pod's HBM share before it counts as overuse; must cover the HIP runtime's "
                         "per-process VRAM (~0.3 GiB on MI355X), which amd-smi counts and the request does not")

@@ -216,9 +216,15 @@ class CorunModel:
         st = None if starts is None else np.asarray(starts, dtype=np.float64)[None]
         return simulate(work, coup, np.ones((1, k), bool), st)[0]
 
+    def group_durations(self, wids: Sequence[int], iters: Sequence[float],
+                        starts: Optional[Sequence[float]] = None) -> np.ndarray:
+        """Predicted wall ms each pod runs (finish - its own start)."""
+        t = self.group_times(wids, iters, starts)
+        return t - (np.asarray(starts, dtype=np.float64) if starts is not None else 0.0)
+
     def group_tput(self, wids: Sequence[int], iters: Sequence[float],
                    starts: Optional[Sequence[float]] = None) -> np.ndarray:
-        t = self.group_times(wids, iters, starts)
+        t = self.group_durations(wids, iters, starts)
         return np.asarray(iters, dtype=np.float64) / np.maximum(t, 1e-9) * 1e3
 
     def batch_times(self, wids: np.ndarray, iters: np.ndarray, mask: np.ndarray,
@@ -293,7 +299,7 @@ def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, rid
         u, v = unpack(x)
         m = CorunModel(names, a_ms, u, v)
         wids, iters, mask, ms, st = data
-        t = m.batch_times(wids, iters, mask, st)
+        t = m.batch_times(wids, iters, mask, st) - st      # durations: finish - own start
         r = np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[mask]
         return r
 
@@ -308,7 +314,7 @@ def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, rid
 
     def tput_err(m: CorunModel, data) -> Dict[str, float]:
         wids, iters, mask, ms, st = data
-        t = m.batch_times(wids, iters, mask, st)
+        t = m.batch_times(wids, iters, mask, st) - st
         tp = iters / np.maximum(t, 1e-9) * 1e3
         tm = iters / np.maximum(ms, 1e-9) * 1e3
         e = np.abs(tp - tm)[mask]
@@ -324,92 +330,164 @@ def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, rid
 
 # ----------------------------------------------------------------------------- online
 class OnlineCorun:
-    """The co-run model refined from live observations: every finished pod is one
-    observation (its group's workloads, start offsets and iterations, its measured wall
-    time).  Observations are predicted with the current model before they are learned
-    (prequential error); every `refit_every` observations a few Levenberg-Marquardt steps
-    refit u, v on a sliding window, ridge-pulled toward the offline model."""
+    """The co-run model refined from live observations.  Every observed GPU group (its
+    workloads, start offsets, iterations, measured wall times; `targets` marks the pods whose
+    time is an observation -- the others are co-runners from neighbouring epochs) is predicted
+    with the current model before it is learned (prequential error).  Every `refit_every`
+    observed pods a refit runs in a background thread on a sliding window: a per-workload
+    scale of the alone time and a global scale of the coupling matrix (19 parameters for the
+    18-workload catalog), ridge-pulled toward the offline model, a few Levenberg-Marquardt
+    steps -- so a scheduler never waits for it; callers pick the new model up via `model`
+    (its `version` changes).  Two stages: from `min_calib` observations on, a global time
+    scale (the median measured / predicted duration of the window: e.g. clocks under a
+    power cap the offline groups did not hit) calibrates the model; from `min_obs` on, the
+    per-workload refit -- fitted on the older 3/4 of the window and adopted only if it
+    predicts the newest 1/4 better than the current model."""
 
-    def __init__(self, base: CorunModel, refit_every: int = 32, window: int = 2048, ridge: float = 0.5,
-                 max_nfev: int = 12):
+    def __init__(self, base: CorunModel, refit_every: int = 32, window: int = 512, ridge: float = 8.0,
+                 max_nfev: int = 8, background: bool = True, min_obs: int = 256, min_calib: int = 256):
         self.base = base
         self.model = base
         self.refit_every, self.window, self.ridge, self.max_nfev = refit_every, window, ridge, max_nfev
-        # (workload ids, iterations, start offsets ms, pods, measured ms) per observed group
-        self._obs: List[Tuple[Tuple[int, ...], Tuple[float, ...], Tuple[float, ...], int, Tuple[float, ...]]] = []
+        self.background = background
+        # no refit before this many observed pods: the offline model is fitted on thousands of
+        # measured groups, a refit on a few dozen only adds noise (replayed bench timelines:
+        # 20 steps of one GPU make the online model WORSE than the offline one)
+        self.min_obs = min_obs
+        self.min_calib = min_calib
+        self.time_scale = 1.0
+        self.rejected = 0
+        # (workload ids, iterations, start offsets ms, measured ms, target mask) per group
+        self._obs: List[Tuple[Tuple[int, ...], Tuple[float, ...], Tuple[float, ...], Tuple[float, ...],
+                              Tuple[bool, ...]]] = []
         self._pending = 0
         self.version = 0
+        self.refits = 0
         self.err = {"prior": 0.0, "online": 0.0, "n": 0, "tput_sum": 0.0}
         self._lock = threading.Lock()
+        self._busy = False
+        self._x = np.zeros(len(base.names) + 1)
 
     def observe_group(self, wids: Sequence[int], iters: Sequence[float], ms: Sequence[float],
-                      starts: Optional[Sequence[float]] = None) -> bool:
-        """One GPU's finished pods (workload ids >= 0); returns True when refitted."""
+                      starts: Optional[Sequence[float]] = None, targets: Optional[Sequence[bool]] = None) -> bool:
+        """One GPU's group; returns True when a refit was started (or, synchronously, done)."""
         k = len(wids)
         if k == 0:
             return False
-        st = list(starts) if starts is not None else [0.0] * k
-        t_on = self.model.group_times(wids, iters, st)
-        t_pr = self.base.group_times(wids, iters, st)
+        st = [float(x) for x in starts] if starts is not None else [0.0] * k
+        tg = [bool(x) for x in targets] if targets is not None else [True] * k
+        t_on = self.model.group_durations(wids, iters, st)
+        t_pr = self.base.group_durations(wids, iters, st)
+        start_refit = False
         with self._lock:
             for i in range(k):
-                if ms[i] <= 0:
+                if not tg[i] or ms[i] <= 0 or iters[i] <= 0:
                     continue
                 tm = iters[i] / ms[i] * 1e3
                 self.err["prior"] += abs(iters[i] / max(t_pr[i], 1e-9) * 1e3 - tm)
                 self.err["online"] += abs(iters[i] / max(t_on[i], 1e-9) * 1e3 - tm)
                 self.err["n"] += 1
                 self.err["tput_sum"] += tm
-            self._obs.append((tuple(wids), tuple(float(x) for x in iters), tuple(float(x) for x in st), k,
-                              tuple(float(x) for x in ms)))
+                self._pending += 1
+            self._obs.append((tuple(int(w) for w in wids), tuple(float(x) for x in iters), tuple(st),
+                              tuple(float(x) for x in ms), tuple(tg)))
             if len(self._obs) > self.window:
                 del self._obs[: len(self._obs) - self.window]
-            self._pending += k
-            if self._pending >= self.refit_every:
+            if self._pending >= self.refit_every and not self._busy and self.err["n"] >= self.min_calib:
                 self._pending = 0
-                self._refit()
-                return True
-        return False
+                self._busy = True
+                start_refit = True
+                snap = list(self._obs)
+        if not start_refit:
+            return False
+        if self.background:
+            threading.Thread(target=self._refit, args=(snap,), daemon=True, name="corun-refit").start()
+        else:
+            self._refit(snap)
+        return True
 
-    def _refit(self) -> None:
-        from scipy.optimize import least_squares
-        obs = self._obs
-        K = max(o[3] for o in obs)
-        G = len(obs)
-        wids = np.zeros((G, K), np.int64)
-        iters = np.zeros((G, K))
-        mask = np.zeros((G, K), bool)
-        ms = np.ones((G, K))
-        st = np.zeros((G, K))
-        for g, (w, it, s, k, m) in enumerate(obs):
-            wids[g, :k], iters[g, :k], st[g, :k], ms[g, :k] = w, it, s, m
-            mask[g, :k] = True
-        mask &= ms > 0
-        base = self.base
-        n_w, R = base.u.shape
-        x_prior = np.log(np.maximum(np.concatenate([base.u.ravel(), base.v.ravel()]), 1e-6))
-        x0 = np.log(np.maximum(np.concatenate([self.model.u.ravel(), self.model.v.ravel()]), 1e-6))
-        a_ms = base.alone_ms
+    def _refit(self, obs) -> None:
+        try:
+            from scipy.optimize import least_squares
+            K = max(len(o[0]) for o in obs)
+            G = len(obs)
+            wids = np.zeros((G, K), np.int64)
+            iters = np.zeros((G, K))
+            mask = np.zeros((G, K), bool)
+            tgt = np.zeros((G, K), bool)
+            ms = np.ones((G, K))
+            st = np.zeros((G, K))
+            for g, (w, it, s, m, t) in enumerate(obs):
+                k = len(w)
+                wids[g, :k], iters[g, :k], st[g, :k], ms[g, :k], tgt[g, :k] = w, it, s, m, t
+                mask[g, :k] = True
+            tgt &= mask & (ms > 0) & (iters > 0)
+            base = self.base
+            n_w = len(base.names)
 
-        def obj(x):
-            e = np.exp(x)
-            m = CorunModel(base.names, a_ms, e[:n_w * R].reshape(n_w, R), e[n_w * R:].reshape(n_w, R))
-            t = m.batch_times(wids, iters, mask, st)
-            r = np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[mask]
-            return np.concatenate([r, np.sqrt(self.ridge) * (x - x_prior)])
+            def model_of(x):
+                m = CorunModel(base.names, base.alone_ms * np.exp(x[:n_w]), base.u * np.exp(x[n_w]), base.v)
+                return m
 
-        sol = least_squares(obj, x0, method="trf", max_nfev=self.max_nfev)
-        e = np.exp(sol.x)
-        self.version += 1
-        self.model = base.copy_with(e[:n_w * R].reshape(n_w, R), e[n_w * R:].reshape(n_w, R),
-                                    f"{base.version}+online-{self.version}")
+            def resid(model, sel):
+                t = model.batch_times(wids, iters, mask, st) - st
+                return np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[sel]
+
+            # stage 1: global time scale of the (possibly refitted) model
+            cur = model_of(self._x)
+            r = resid(cur, tgt)
+            scale = float(np.exp(-np.median(r))) if r.size else 1.0
+            stage2 = self.err["n"] >= self.min_obs
+            x_new = self._x
+            if stage2:
+                n_fit = max(1, (3 * G) // 4)
+                fit_m = tgt.copy()
+                fit_m[n_fit:] = False
+                hold = tgt.copy()
+                hold[:n_fit] = False
+
+                def obj(x):
+                    m2 = model_of(x)
+                    m2.alone_ms = m2.alone_ms * scale
+                    return np.concatenate([resid(m2, fit_m), np.sqrt(self.ridge) * x])
+
+                sol = least_squares(obj, self._x, method="trf", max_nfev=self.max_nfev)
+                cand = model_of(sol.x)
+                cand.alone_ms = cand.alone_ms * scale
+                keep = model_of(self._x)
+                keep.alone_ms = keep.alone_ms * scale
+                if not hold.any() or np.abs(resid(cand, hold)).mean() < np.abs(resid(keep, hold)).mean():
+                    x_new = sol.x
+                else:
+                    self.rejected += 1
+            m = model_of(x_new)
+            with self._lock:
+                self._x = x_new
+                self.time_scale = scale
+                self.version += 1
+                self.refits += 1
+                self.model = CorunModel(base.names, m.alone_ms * scale, m.u, m.v,
+                                        dict(base.meta, version=f"{base.version}+online-{self.version}"))
+        except Exception as e:      # a failed refit keeps the current model
+            import logging
+            logging.getLogger(__name__).warning("co-run refit failed: %s", e)
+        finally:
+            with self._lock:
+                self._busy = False
+
+    def wait_idle(self, timeout_s: float = 10.0) -> None:
+        t = time.time()
+        while self._busy and time.time() - t < timeout_s:
+            time.sleep(0.005)
 
     def mae(self) -> Dict[str, Optional[float]]:
         n = self.err["n"]
         if not n:
-            return {"n": 0, "prior": None, "online": None, "mean_tput": None}
+            return {"n": 0, "prior": None, "online": None, "mean_tput": None, "refits": self.refits,
+                    "rejected": self.rejected}
         return {"n": n, "prior": self.err["prior"] / n, "online": self.err["online"] / n,
-                "mean_tput": self.err["tput_sum"] / n}
+                "mean_tput": self.err["tput_sum"] / n, "refits": self.refits, "rejected": self.rejected,
+                "time_scale": round(self.time_scale, 4)}
 
 
 # ----------------------------------------------------------------------------- collection (GPU)

@@ -82,6 +82,10 @@ class DeviceExecutor:
         self._graphs: Dict[Tuple, "torch.cuda.CUDAGraph"] = {}
         self.flops_done = 0.0
         self.bytes_done = 0.0
+        # the executor's clock: pod start / end events are reported as ms after this event
+        # (the co-run learner rebuilds which pods of neighbouring epochs overlapped)
+        self.clock = torch.cuda.Event(enable_timing=True)
+        self.clock.record(torch.cuda.current_stream(self.device))
 
     def stream_for(self, first_unit: int, n_units: int, masked: bool = True):
         key = (first_unit, n_units, masked)

@@ -60,11 +60,11 @@ MAX_PODS_GPU = 8              # per-pod co-run records per GPU and epoch
 COST0 = 4
 POD0 = COST0 + 2 * len(W.NAMES)
 # busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods), then per pod of
-# this GPU's epoch: (workload id or -1, achieved iterations/s, start ms after the epoch's first
-# pod started) -- the co-run observations the online interference / co-run models learn from;
-# last, amd-smi's view of the GPU over the epoch (gfx activity 0..1, VRAM used GiB; -1 = no
-# amd-smi sample)
-POD_F = 3
+# this GPU's epoch: (workload id or -1, achieved iterations/s, start ms, end ms on the rank's
+# executor clock; -1 = no timeline, the group ran isolated) -- the co-run observations the
+# online interference / co-run models learn from; last, amd-smi's view of the GPU over the
+# epoch (gfx activity 0..1, VRAM used GiB; -1 = no amd-smi sample)
+POD_F = 4
 SMI0 = POD0 + POD_F * MAX_PODS_GPU
 TELE = SMI0 + 2
 
@@ -103,7 +103,8 @@ class ControlPlane:
                  cu_per_pod: int = 64, predictions: Optional[CachedPredictions] = None, qos: str = "burstable",
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
                  plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0,
-                 online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None):
+                 online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
+                 corun_margin: float = 0.0, corun_sigma: float = 0.0):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -127,7 +128,7 @@ class ControlPlane:
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
                 "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement,
-                "slo_objective": slo_objective}
+                "slo_objective": slo_objective, "corun_margin": corun_margin, "corun_sigma": corun_sigma}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
         # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
@@ -160,6 +161,7 @@ class ControlPlane:
                                                  refit_every=max(32, 4 * n_gpus * pods_per_gpu),
                                                  scale=online_scale)
                 self._online_rows = rows
+        self._timeline: Dict[int, List[Any]] = {}     # per GPU: the last epochs' pod rows (co-run learner)
         self.epoch = 0
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -230,35 +232,62 @@ class ControlPlane:
                 pass
 
     def _learn_interference(self, pods: np.ndarray) -> None:
-        """pods[g] = MAX_PODS_GPU x (workload id, achieved iterations/s, start offset ms) of
+        """pods[g] = MAX_PODS_GPU x (workload id, achieved iterations/s, start ms, end ms) of
         GPU g's epoch.  Each pod's loss against its predicted alone-throughput at its share is
-        one observation of the additive interference model (recommender.online); each GPU's
-        group -- who co-ran, from when, at what rate -- one observation of the co-run model
-        (models.corun.OnlineCorun)."""
-        refit = refit_c = False
+        one observation of the additive interference model (recommender.online).  For the
+        co-run model (models.corun.OnlineCorun) an observation is what actually co-ran: with a
+        timeline (the bench's launch-ahead pipeline overlaps consecutive epochs on a GPU),
+        epoch e is learned once e+2 is known, as the group of every pod of e-2 .. e+2 whose
+        interval overlaps e's, at its real start offset, with e's pods as the targets;
+        without one (isolated groups) the epoch's group alone."""
+        refit = False
         for g in range(pods.shape[0]):
-            rec = pods[g].reshape(MAX_PODS_GPU, POD_F)
-            wids = [int(r[0]) for r in rec if r[0] >= 0]
+            rec = [r for r in pods[g].reshape(MAX_PODS_GPU, POD_F) if r[0] >= 0]
+            wids = [int(r[0]) for r in rec]
             if self.online is not None:
                 for i, r in enumerate(rec):
-                    if r[0] < 0:
-                        continue
-                    w = int(r[0])
                     others = wids[:i] + wids[i + 1:]
-                    refit |= self.online.observe(w, others, self.quarter_tput[W.NAMES[w]] - float(r[1]))
-            if self.corun is not None and wids:
-                live = [r for r in rec if r[0] >= 0 and r[1] > 0]
-                if live:
-                    cw = [self.corun.base.wid(W.NAMES[int(r[0])]) for r in live]
-                    if min(cw) >= 0:
-                        refit_c |= self.corun.observe_group(cw, [float(self.iters)] * len(live),
-                                                            [self.iters / float(r[1]) * 1e3 for r in live],
-                                                            [float(r[2]) for r in live])
+                    refit |= self.online.observe(wids[i], others, self.quarter_tput[W.NAMES[wids[i]]] - float(r[1]))
+            if self.corun is not None:
+                self._observe_corun(g, [r for r in rec if r[1] > 0])
         if refit and self.online is not None:       # serve the refitted table (next cycles' predictions)
             self.predictions.install_interference(self._online_rows, W.NAMES, self.online.rows(),
                                                   f"online-{self.online.version}")
-        if refit_c:
+        if self.corun is not None and self.corun.model is not self.predictions.corun():
             self.predictions.install_corun(self.corun.model)
+
+    def _observe_corun(self, g: int, rec: List[Any]) -> None:
+        base = self.corun.base
+        if not rec:
+            return
+        if rec[0][2] < 0:                               # isolated group
+            w = [base.wid(W.NAMES[int(r[0])]) for r in rec]
+            if min(w) >= 0:
+                self.corun.observe_group(w, [float(self.iters)] * len(rec),
+                                         [self.iters / float(r[1]) * 1e3 for r in rec], None)
+            return
+        hist = self._timeline.setdefault(g, [])
+        hist.append(rec)
+        if len(hist) > 5:
+            del hist[0]
+        if len(hist) < 3:
+            return
+        # epoch e-2 once e is known: a long pod of e-2 overlaps pods of several later epochs
+        # on the other slots; two epochs of look-ahead cover all but the longest tails
+        tgt = hist[-3]
+        lo, hi = min(r[2] for r in tgt), max(r[3] for r in tgt)
+        members, flags = [], []
+        for ep in hist:
+            for r in ep:
+                if r[3] > lo and r[2] < hi:                 # overlaps the target epoch
+                    members.append(r)
+                    flags.append(ep is tgt)
+        t0 = min(r[2] for r in members)
+        w = [base.wid(W.NAMES[int(r[0])]) for r in members]
+        if min(w) < 0 or len(members) > 60:
+            return
+        self.corun.observe_group(w, [float(self.iters)] * len(members), [float(r[3] - r[2]) for r in members],
+                                 [float(r[2] - t0) for r in members], flags)
 
     def interference_mae(self) -> Optional[Dict[str, Any]]:
         out = self.online.mae() if self.online is not None else None
@@ -372,24 +401,21 @@ class SimExecutor:
         pass
 
 
-def _pod_rows(runs: List[Any]) -> List[float]:
-    """(workload id, achieved iterations/s, start ms after the first pod of the group) of up
-    to MAX_PODS_GPU pods of one GPU's epoch; (-1, 0, 0) pads."""
+def _pod_rows(runs: List[Any], ref: Any = None) -> List[float]:
+    """(workload id, achieved iterations/s, start ms, end ms) of up to MAX_PODS_GPU pods of one
+    GPU's epoch, times on the clock of `ref` (a HIP event of the executor; None = no
+    timeline: start = end = -1); (-1, 0, -1, -1) pads."""
     out: List[float] = []
     rs = runs[:MAX_PODS_GPU]
-    t0 = None
-    offs = []
     for r in rs:
-        ev = getattr(r, "start", None)
-        try:
-            offs.append(rs[0].start.elapsed_time(ev) if ev is not None and rs[0].start is not None else 0.0)
-        except Exception:
-            offs.append(0.0)
-    if offs:
-        t0 = min(offs)
-    for r, o in zip(rs, offs):
-        out += [float(W.INDEX[r.workload]), float(r.throughput), float(o - t0)]
-    return out + [-1.0, 0.0, 0.0] * (MAX_PODS_GPU - len(rs))
+        t0 = t1 = -1.0
+        if ref is not None and getattr(r, "start", None) is not None and getattr(r, "end", None) is not None:
+            try:
+                t0, t1 = ref.elapsed_time(r.start), ref.elapsed_time(r.end)
+            except Exception:
+                t0 = t1 = -1.0
+        out += [float(W.INDEX[r.workload]), float(r.throughput), float(t0), float(t1)]
+    return out + [-1.0, 0.0, -1.0, -1.0] * (MAX_PODS_GPU - len(rs))
 
 
 def _cost_rows(runs: List[Any]) -> np.ndarray:
@@ -676,7 +702,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     totals = {"pods": 0.0, "busy_unit_ms": 0.0, "slo_ok": 0.0}
     state: Dict[str, Any] = {"next": cp.schedule_epoch() if rank == 0 else None}
 
-    host = {"launch": 0.0, "schedule": 0.0, "wait": 0.0, "comm": 0.0}
+    host = {"launch": 0.0, "schedule": 0.0, "wait": 0.0, "comm": 0.0, "collect": 0.0}
     intervals: List[Tuple[float, float]] = []
     trace: Optional[List[Any]] = [] if (os.environ.get("GPUSCHED_BENCH_TRACE") and rank == 0) else None
     t_start = time.perf_counter()
@@ -695,6 +721,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                                       intervals[-1][1], (time.perf_counter() - t_start) * 1e3))
         if timed:
             state["collected"] = state.get("collected", 0) + 1
+        t_post = time.perf_counter()
         st = ex.collect(runs)
         hbm = sum(W.CATALOG[r.workload].hbm_gib for r in runs)
         smi_vec = [-1.0, -1.0]
@@ -703,7 +730,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             if sm["gfx_activity_pct_mean"] is not None:
                 smi_vec = [sm["gfx_activity_pct_mean"] / 100.0, (sm["vram_used_mb_max"] or 0.0) / 1024.0]
         vec = [st["busy_unit_ms"], st["pods"], st["slo_ok"], hbm] + _cost_rows(runs).ravel().tolist() + \
-            _pod_rows(runs) + smi_vec
+            _pod_rows(runs, getattr(ex, "clock", None)) + smi_vec
         if dist_on:
             with torch.cuda.stream(side) if (side is not None and backend == "nccl") else _null():
                 tele.copy_(torch.tensor(vec, dtype=torch.float64))
@@ -725,6 +752,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         if rank == 0:
             cp.update_telemetry(per_gpu, max(st["span_ms"], 1e-3))
         if timed:
+            host["collect"] += time.perf_counter() - t_post      # event reads, telemetry, all-gather
+            if trace is not None and trace:
+                trace[-1] = tuple(trace[-1]) + ((time.perf_counter() - t_start) * 1e3,)
             tot = per_gpu[:, :4].sum(axis=0)
             totals["pods"] += tot[1]
             totals["busy_unit_ms"] += tot[0]

@@ -246,9 +246,12 @@ class BurstPlanner:
         for nd, st in placed:
             dev_group.append(gkey.setdefault((nd,) + plugin.corun_group_key(st), len(gkey)))
         n_groups = len(gkey)
+        if n_groups < 2:
+            return None                     # one co-run group (one GPU): nothing to plan
         free_units = [st.free_units for st in states]
         free_hbm = [st.hbm_free for st in states]
         per: List[List[Tuple[int, float, float]]] = [[] for _ in range(n_groups)]
+        margin = 1.0 + plugin.args.corun_margin      # SLOs as the model must predict them
         seen = set()
         for d, st in enumerate(states):
             g = dev_group[d]
@@ -258,7 +261,7 @@ class BurstPlanner:
                 seen.add((k, g))
                 w = model.wid(use.name)
                 if w >= 0:
-                    per[g].append((w, use.iters, use.slo))
+                    per[g].append((w, use.iters, use.slo * margin))
         dev_index = {(owner[d], st.device.uuid): d for d, st in enumerate(states)}
         # pods planned earlier and still pending hold their capacity and co-run as residents
         for k, (n, u) in self.plans.items():
@@ -271,7 +274,7 @@ class BurstPlanner:
             free_hbm[d] -= req.hbm_gib
             w = model.wid(O.name(p))
             if w >= 0:
-                per[dev_group[d]].append((w, req.iters, req.slo))
+                per[dev_group[d]].append((w, req.iters, req.slo * margin))
         # initial assignment: longest predicted work first onto the group with the least
         # predicted work that has room (units and HBM)
         load = [sum(model.alone_ms[w] * (it if it > 0 else 0.0) for w, it, _ in m) for m in per]
@@ -309,10 +312,11 @@ class BurstPlanner:
         np.add.at(cap, dev0, units)
         out = core.plan_corun(
             dev0, units, np.array([model.wid(O.name(p)) for p, _, _ in assign], np.int32),
-            np.array([r.iters for _, r, _ in assign], np.float64), np.array([r.slo for _, r, _ in assign], np.float64),
+            np.array([r.iters for _, r, _ in assign], np.float64),
+            np.array([r.slo * margin for _, r, _ in assign], np.float64),
             np.array(dev_group, np.int32), cap, off, np.array([x[0] for x in flat], np.int32),
             np.array([x[1] for x in flat], np.float64), np.array([x[2] for x in flat], np.float64),
-            model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0)
+            model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0, float(plugin.args.corun_sigma))
         for (p, _, _), d in zip(assign, out):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
             plugin._pending_by_key[O.key(p)] = p

@@ -140,7 +140,7 @@ class ResizeAdmission:
     __call__ = mutate
 
 
-def webhook_handler(adm: ResizeAdmission, review: Dict[str, Any]) -> Dict[str, Any]:
+def webhook_handler(adm: Any, review: Dict[str, Any]) -> Dict[str, Any]:
     """admission.k8s.io/v1 AdmissionReview in -> AdmissionReview out (JSONPatch)."""
     req = review.get("request") or {}
     uid = req.get("uid", "")
@@ -162,8 +162,10 @@ class AdmissionServer:
     webhooks over TLS: pass certfile/keyfile (the deploy manifest mounts them from a
     Secret); plain HTTP is for tests and local runs."""
 
-    def __init__(self, adm: ResizeAdmission, host: str = "0.0.0.0", port: int = 8443,
-                 certfile: str = "", keyfile: str = ""):
+    def __init__(self, adm: Any, host: str = "0.0.0.0", port: int = 8443,
+                 certfile: str = "", keyfile: str = "", routes: Optional[Dict[str, Any]] = None):
+        # POST /mutate -> adm; extra paths -> their own admission (anything with patch_ops)
+        paths = {"/mutate": adm, **(routes or {})}
         import threading
         from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
@@ -187,13 +189,14 @@ class AdmissionServer:
                     self._send(404, b"")
 
             def do_POST(self):
-                if self.path.rstrip("/") != "/mutate":
+                target = paths.get(self.path.rstrip("/"))
+                if target is None:
                     self._send(404, b"")
                     return
                 n = int(self.headers.get("Content-Length") or 0)
                 try:
                     review = json.loads(self.rfile.read(n) or b"{}")
-                    self._send(200, json.dumps(webhook_handler(adm, review)).encode())
+                    self._send(200, json.dumps(webhook_handler(target, review)).encode())
                 except json.JSONDecodeError as e:
                     self._send(400, json.dumps({"error": str(e)}).encode())
 

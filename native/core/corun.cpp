@@ -95,11 +95,21 @@ struct GroupEval {
   int ok = 0, bad = 0;          // members meeting / missing their SLO (SLO <= 0 counts as met)
   double makespan = 0.0;        // last finish of a batch pod (services excluded)
   double deficit = 0.0;         // sum over missing members of 1 - tput / SLO (how far they are)
+  double expected = 0.0;        // expected members meeting their SLO under model error (sigma)
 };
+
+// P(true throughput >= SLO) when log(true / predicted) ~ N(0, sigma^2): the planner's soft
+// objective -- a plan of pods that clear their SLO by a model error's worth is worth more
+// than one that meets the same number on paper by a hair.
+inline double p_meet(double tput, double slo, double sigma) {
+  if (slo <= 0) return 1.0;
+  if (sigma <= 0) return tput >= slo ? 1.0 : 0.0;
+  return 0.5 * std::erfc(-std::log(std::max(tput, 1e-12) / slo) / (sigma * std::sqrt(2.0)));
+}
 
 // Evaluate one group: SLO verdicts and makespan.  slo = minimum iterations/s.
 GroupEval eval_group(int k, const int32_t* w, const double* iters, const double* slo, const double* alone,
-                     const double* C, int W, double* tput_out = nullptr) {
+                     const double* C, int W, double* tput_out = nullptr, double sigma = 0.0) {
   GroupEval g;
   if (k == 0) return g;
   if (k > kMaxK) throw std::runtime_error("corun: group larger than 64 pods");
@@ -114,6 +124,7 @@ GroupEval eval_group(int k, const int32_t* w, const double* iters, const double*
       g.makespan = std::max(g.makespan, fin[i]);
     }
     if (tput_out) tput_out[i] = tput;
+    g.expected += p_meet(tput, slo[i], sigma);
     if (slo[i] <= 0 || tput >= slo[i]) {
       ++g.ok;
     } else {
@@ -258,14 +269,15 @@ py::tuple corun_groups_eval(I64 off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alon
 // swaps of equal-unit pods across GPUs):
 //   A  makespan: lower the pair's longer predicted group makespan (sum of squares as the
 //      tie-break) -- the balanced plan, M0 = its longest GPU;
-//   B  SLO: more members (burst + residents) predicted to meet their SLO, never taking a GPU
+//   B  SLO: more members (burst + residents) predicted to meet their SLO (sigma > 0: the
+//      EXPECTED number under lognormal model error of that sigma), never taking a GPU
 //      above cap = (1 + tolerance) * M0 (or above its current makespan, if already over);
 //      equal count -> the smaller total SLO deficit (sum of 1 - tput / SLO over the misses: a
 //      gradient toward placements one swap away from meeting more), then the lower makespan.
 // mode: 0 = A then B, 1 = A only (balance), 2 = B only (cap from the initial plan).
 py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 slo, I32 dev_gpu, I32 dev_free,
                                 I64 res_off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alone, F64 cmat, int sweeps,
-                                double tolerance, int mode) {
+                                double tolerance, int mode, double sigma) {
   int W;
   check_model(alone, cmat, W);
   const py::ssize_t P = dev_in.shape(0), D = dev_gpu.shape(0), NR = r_wid.shape(0);
@@ -315,7 +327,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         it[i] = a >= 0 ? iters.data()[a] : r_iters.data()[-1 - a];
         sl[i] = a >= 0 ? slo.data()[a] : r_slo.data()[-1 - a];
       }
-      return eval_group(k, w, it, sl, A, Cm, W);
+      return eval_group(k, w, it, sl, A, Cm, W, nullptr, sigma);
     };
     std::vector<GroupEval> ge(NG);
     for (int g = 0; g < NG; ++g) ge[g] = eval(g);
@@ -398,6 +410,12 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         const bool over = (ai.makespan > cap * (1 + eps) && ai.makespan > bi.makespan * (1 + eps)) ||
                           (aj.makespan > cap * (1 + eps) && aj.makespan > bj.makespan * (1 + eps));
         if (over) return false;
+        if (sigma > 0) {          // soft objective: expected SLOs met under model error
+          const double eb = bi.expected + bj.expected, ea = ai.expected + aj.expected;
+          if (ea > eb + 1e-6) return true;
+          if (ea < eb - 1e-6) return false;
+          return std::max(ai.makespan, aj.makespan) < std::max(bi.makespan, bj.makespan) * (1 - eps);
+        }
         const int ob = bi.ok + bj.ok, oa = ai.ok + aj.ok;
         if (oa != ob) return oa > ob;
         const double fb = bi.deficit + bj.deficit, fa = ai.deficit + aj.deficit;
@@ -424,5 +442,5 @@ void register_corun(py::module_& m) {
   m.def("plan_corun", &plan_corun, py::arg("dev"), py::arg("units"), py::arg("wid"), py::arg("iters"), py::arg("slo"),
         py::arg("dev_gpu"), py::arg("dev_free"), py::arg("res_off"), py::arg("r_wid"), py::arg("r_iters"),
         py::arg("r_slo"), py::arg("alone_ms"), py::arg("cmat"), py::arg("sweeps") = 8, py::arg("tolerance") = 0.03,
-        py::arg("mode") = 0);
+        py::arg("mode") = 0, py::arg("sigma") = 0.0);
 }

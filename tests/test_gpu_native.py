@@ -4,10 +4,14 @@ Numerics of every HIP kernel are checked against a plain PyTorch fp32 reference 
 same op.  The HIP module is loaded unconditionally (no fallback): if it is missing these
 tests fail loudly.
 """
+import json
+import os
+
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
 
 
 @pytest.fixture(scope="module")
@@ -450,6 +454,50 @@ def test_profiled_pod_writes_rocprof_history():
     (h,) = hist.read("onnx_resnet50_1024")
     assert h["gpu_busy_ms"] > 0 and h["kernels"] >= 60, h
     assert any("gemm_bf16" in k["name"] for k in h["top"]), h["top"]
+
+
+def test_profile_webhook_pod_under_rocprof_lands_in_redis_history(tmp_path):
+    """The deployable per-pod profiler end to end on the box: the admission webhook wraps an
+    opted-in pod's container in rocprofv3 (agent.profile_webhook), the kubelet-style launcher
+    resolves the downward-API env / $(VAR)s / hostPath and runs it (ops.podrun: the workload's
+    native GEMM + stream kernels), and the node agent's ingestor turns the finished output
+    directory into the workload's Redis history -- GEMM kernels included."""
+    import sys
+    from k8s_gpu_scheduler_amd.agent import profile_webhook as PW
+    from k8s_gpu_scheduler_amd.agent.launcher import PodLauncher
+    from k8s_gpu_scheduler_amd.agent.pod_profiler import ROCPROF, ProfileIngestor
+    from k8s_gpu_scheduler_amd.api import constants as C
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.recommender.admission import RedisHistory
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("box", gpus=1))
+    fc.add_admission("pods", PW.ProfileInjector(rocprof=ROCPROF))
+    pod = O.make_pod("onnx-resnet50-1024-wh", gpu_cu=64, gpu_mem_gib=8, env={C.ENV_ITERATIONS: "30"},
+                     labels_={PW.LABEL_PROFILE: "trace"}, node_name="box", phase="Running")
+    pod["spec"]["containers"][0]["command"] = [sys.executable, "-m", "k8s_gpu_scheduler_amd.ops.podrun"]
+    pod["spec"]["containers"][0]["args"] = ["--workload", "onnx_resnet50_1024", "--cu-budget", "64"]
+    fc.create("pods", pod)
+    pod = fc.get("pods", "onnx-resnet50-1024-wh", "default")
+    assert pod["spec"]["containers"][0]["command"][0] == ROCPROF
+    la = PodLauncher(fc, "box", timeout_s=300)
+    la.host_root = str(tmp_path)
+    la.cwd = str(tmp_path)
+    la.extra_env = {"TMPDIR": str(tmp_path), "PYTHONPATH": root}
+    res = la.run(pod)
+    assert res.rc == 0, res.stderr[-3000:]
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    ing = ProfileIngestor(str(tmp_path) + PW.HOST_DIR, RedisHistory(r))
+    assert ing.step() == 1
+    (h,) = RedisHistory(r).read("onnx_resnet50_1024")
+    assert h["source"] == "rocprof" and h["cu"] == 64 and h["uid"] == O.uid(pod)
+    assert any("gemm_bf16" in k["name"] for k in h["top"]), h["top"]
+    assert h["kernels"] >= 90 and h["span_ms"] > 0 and h["throughput"] > 0 and 0 < h["busy_frac"] <= 1.0
+    with open(os.path.join(OUT, "profile_webhook_sample.json"), "w") as f:
+        json.dump(h, f, indent=1)
 
 
 def test_device_plugin_allocates_real_device_nodes():

@@ -55,10 +55,32 @@ POLICIES = {
     "corun_plan_t10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun"),
     "corun_plan_t15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.15, slo_objective="corun"),
     "corun_plan_t20": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun"),
+    "corun_plan_t20_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
+                               corun_sigma=0.10),
+    "corun_plan_t30_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun",
+                               corun_sigma=0.10),
+    "corun_plan_t20_s15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
+                               corun_sigma=0.15),
+    "corun_plan_t30": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun"),
+    "corun_plan_t20_m05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
+                               corun_margin=0.05),
+    "corun_plan_t10_m05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun",
+                               corun_margin=0.05),
+    "corun_plan_t10_m10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun",
+                               corun_margin=0.10),
+    "corun_plan_t20_m10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
+                               corun_margin=0.10),
+    "corun_plan_t20_m15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
+                               corun_margin=0.15),
     # roofline complementarity term (GPU plugin weightComplement) on top of greedy
     "greedy_comp": dict(balance=1.0, plan_bursts=False, complement=1.0),
     "greedy_comp3": dict(balance=1.0, plan_bursts=False, complement=3.0),
 }
+
+
+from k8s_gpu_scheduler_amd.models.corun import CorunModel  # noqa: E402
+
+MODEL = CorunModel.load()      # the shipped co-run model: predictions logged next to measurements
 
 
 def run_group(ex: DeviceExecutor, runs):
@@ -77,7 +99,7 @@ def run_group(ex: DeviceExecutor, runs):
     return s.elapsed_time(e)
 
 
-GROUPS: list = []      # (policy, [workloads], wall ms) of every group, for --dump-groups
+GROUPS: list = []      # per group: policy, workloads, wall ms, per pod (SLO, achieved, predicted), for --dump-groups
 
 
 def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
@@ -87,7 +109,14 @@ def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
     for g in range(N_GPUS):
         runs = _runs_for(arr, g)
         walls.append(run_group(ex, runs))
-        GROUPS.append((tag, [r.workload for r in runs], walls[-1]))
+        pred = [None] * len(runs)
+        model = MODEL
+        if model is not None and runs:
+            pred = [round(float(x), 1) for x in model.group_tput([model.wid(r.workload) for r in runs],
+                                                                 [r.iters for r in runs])]
+        GROUPS.append({"policy": tag, "epoch": cp.epoch, "w": [r.workload for r in runs], "wall_ms": round(walls[-1], 4),
+                       "slo": [round(r.slo, 1) for r in runs], "tput": [round(r.throughput, 1) for r in runs],
+                       "pred": pred})
         for r in runs:
             per_gpu[g, :4] += (r.ms * r.n_units, 1, 1 if r.throughput >= r.slo else 0,
                                W.CATALOG[r.workload].hbm_gib)
