@@ -62,7 +62,8 @@ class NodeAgent:
                  apply_partitions: bool = True, pod_resolver: Optional[Callable[[int], Optional[str]]] = None,
                  health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
                  drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1,
-                 hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc", profile_dir: str = ""):
+                 hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc", profile_dir: str = "",
+                 partition_dry_run: bool = False, fabric: Any = None):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -85,6 +86,14 @@ class NodeAgent:
         # the pod's amd.com/gpu-memory request does not -- the tolerance must cover them
         self.hbm_tolerance_gib = hbm_tolerance_gib
         self.host_proc = host_proc
+        # dry run: a partition request goes through every check (capabilities, idleness) but
+        # instead of calling amd-smi the agent records the exact calls it would make
+        # (node annotation partition-state "dry-run", `dry_run_calls`)
+        self.partition_dry_run = partition_dry_run
+        # measured per-pair xGMI copy rates (agent.fabric.FabricProber), published with the
+        # topology for the multi-GPU placement
+        self.fabric = fabric
+        self.dry_run_calls: List[Dict[str, Any]] = []
         # per-pod rocprofv3 output the profiling webhook (agent.profile_webhook) routes to a
         # hostPath: finished runs become workload-history samples (pod_profiler.ProfileIngestor)
         self.profiles = None
@@ -118,9 +127,7 @@ class NodeAgent:
             return False
         schema.publish_uuids(self.redis, self.node, uuids)
         schema.publish_devices(self.redis, self.node, devs)
-        topo = self.source.topology()
-        if topo:
-            self.redis.set(schema.topology_key(self.node), json.dumps(topo, separators=(",", ":")))
+        self.publish_topology()
         self.prev_uuids = uuids
         self.publishes += 1
         for cb in self.on_inventory_change:
@@ -129,6 +136,31 @@ class NodeAgent:
             except Exception as e:
                 log.warning("inventory-change callback failed: %s", e)
         log.info("published %d devices for %s", len(uuids), self.node)
+        return True
+
+    def publish_topology(self) -> None:
+        """`gpusched:topology:<node>`: the static link matrix plus, once probed, the measured
+        per-pair bandwidth (`bw_gbps`)."""
+        topo = self.source.topology()
+        last = self.fabric.last if self.fabric is not None else None
+        if last and last.get("bw_gbps"):
+            topo = dict(topo or {"n": len(last["bw_gbps"])})
+            topo["bw_gbps"] = last["bw_gbps"]
+        if topo:
+            self.redis.set(schema.topology_key(self.node), json.dumps(topo, separators=(",", ":")))
+
+    def probe_fabric(self) -> bool:
+        """Measure the fabric when due and the GPUs are idle; republish the topology."""
+        if self.fabric is None:
+            return False
+        res = self.fabric.maybe_probe(self.busy_reasons)
+        if res is None:
+            return False
+        from .fabric import degraded_pairs
+        bad = degraded_pairs(res.get("bw_gbps") or [])
+        if bad:
+            log.warning("fabric on %s: degraded GPU pairs %s", self.node, bad)
+        self.publish_topology()
         return True
 
     # ------------------------------------------------------------------ telemetry
@@ -460,6 +492,18 @@ class NodeAgent:
                 self._set_partition_state("waiting-idle", mode=target_c, memory=target_m, busy=busy[:8])
             return False
         self._drain_since = None
+        if self.partition_dry_run:
+            calls = []
+            for step, mode, cur, fn in (("memory", target_m, cur_m, "amdsmi_set_gpu_memory_partition"),
+                                        ("compute", target_c, cur_c, "amdsmi_set_gpu_compute_partition")):
+                if mode != cur:
+                    for g in sorted(self._gpu_indices()):
+                        calls.append({"gpu": g, "device_index": self._gpu_indices()[g], "call": fn, "mode": mode})
+            if calls != self.dry_run_calls:
+                self.dry_run_calls = calls
+                log.info("partition dry run on %s: %s", self.node, calls)
+                self._set_partition_state("dry-run", mode=target_c, memory=target_m, calls=calls)
+            return False
         res.taint_node(self.node, C.TAINT_PARTITIONING, target_c, "NoSchedule")
         self._set_partition_state("applying", mode=target_c, memory=target_m)
         errs: List[str] = []
@@ -474,6 +518,8 @@ class NodeAgent:
                     errs.append(f"gpu{g} {step} {mode}: {e}")
             if errs:
                 break                   # never apply the compute mode after a failed memory change
+        if self.fabric is not None:
+            self.fabric.invalidate()            # partitions changed: re-measure when idle
         self.publish(force=True)
         self.publish_caps(force=True)
         res.untaint_node(self.node, C.TAINT_PARTITIONING)
@@ -489,6 +535,10 @@ class NodeAgent:
         except Exception as e:
             log.warning("partition reconcile failed: %s", e)
         self.publish()
+        try:
+            self.probe_fabric()
+        except Exception as e:
+            log.warning("fabric probe failed: %s", e)
         try:
             self.publish_caps()
         except Exception as e:

@@ -228,6 +228,15 @@ def cmd_resize_webhook(args) -> int:
     return 0
 
 
+def _fabric_prober(args):
+    """Per-pair xGMI copy-rate probe for the agent (agent.fabric): on real devices unless
+    --fabric-probe off; never with --synthetic GPUs."""
+    if args.fabric_probe == "off" or args.synthetic:
+        return None
+    from ..agent.fabric import FabricProber
+    return FabricProber()
+
+
 def cmd_agent(args) -> int:
     from ..agent.agent import NodeAgent
     from ..agent.devices import best_source, synthetic_node
@@ -260,6 +269,8 @@ def cmd_agent(args) -> int:
     agent = NodeAgent(node, redis, src, client, args.poll, exporter=exp, evict_unhealthy=args.evict_unhealthy,
                       evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout,
                       hbm_tolerance_gib=args.hbm_tolerance, host_proc=proc_root, profile_dir=args.profile_dir,
+                      partition_dry_run=args.partition_dry_run,
+                      fabric=_fabric_prober(args),
                       pod_resolver=lambda pid: pod_of_pid(pid, proc_root))
     mgr = None
     if args.device_plugin:
@@ -422,6 +433,12 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--evict-hbm-overuse", action="store_true",
                    help="evict (Eviction API, PodDisruptionBudgets apply) pods whose processes hold more VRAM "
                         "than their amd.com/gpu-memory share")
+    s.add_argument("--fabric-probe", default="auto", choices=["auto", "off"],
+                   help="measure every GPU pair's copy rate (child process, idle GPUs only) at start-up and "
+                        "after partition changes; published with the topology for multi-GPU placement")
+    s.add_argument("--partition-dry-run", action="store_true",
+                   help="check partition requests (capabilities, idleness) but only record the amd-smi calls "
+                        "that would apply them (node annotation partition-state: dry-run)")
     s.add_argument("--profile-dir", default="",
                    help="hostPath where profiled pods' rocprofv3 output lands (mounted from /var/lib/gpusched/prof; "
                         "see the resize webhook's --profile): finished runs go to the workload history in Redis")

@@ -115,10 +115,19 @@ class PartitionController:
             return self.client.list("nodes")[0]
 
     def pending_isolated(self) -> List[Obj]:
+        """Pending pods of this scheduler that need an isolated partition: annotated
+        `isolation: partition`, or SLO-only pods whose SLO no fractional share can meet
+        (the GPU plugin's parse_request turns them into partition requests)."""
         ours = getattr(self.plugin.handle, "framework_for", None)
-        return [p for p in self._pods() if not O.node_name_of(p) and not O.is_terminal(p)
-                and (ours(p) is not None if ours else O.scheduler_name(p) == C.SCHEDULER_NAME)
-                and O.annotations(p).get(C.ANNOT_ISOLATION) == "partition"]
+        out = []
+        for p in self._pods():
+            if O.node_name_of(p) or O.is_terminal(p):
+                continue
+            if not (ours(p) is not None if ours else O.scheduler_name(p) == C.SCHEDULER_NAME):
+                continue
+            if O.annotations(p).get(C.ANNOT_ISOLATION) == "partition" or self.plugin.parse_request(p).isolated:
+                out.append(p)
+        return out
 
     @staticmethod
     def node_caps(node: Obj):
@@ -183,6 +192,15 @@ class PartitionController:
         if cu > 0:
             from .plugin import partition_size
             return partition_size(cu)
+        req = self.plugin.parse_request(pod)
+        if req.isolated and req.part_cus and not O.annotations(pod).get(C.ANNOT_PARTITION_CUS):
+            # an SLO-only pod the plugin sized from its predictions: record the size
+            try:
+                self.client.patch("pods", O.name(pod), {"metadata": {"annotations": {
+                    C.ANNOT_PARTITION_CUS: str(req.part_cus)}}}, "merge", O.namespace(pod))
+            except Exception as e:
+                log.warning("annotating %s with its partition size failed: %s", O.key(pod), e)
+            return req.part_cus
         ann = O.annotations(pod).get(C.ANNOT_PARTITION_CUS)
         if ann:
             try:

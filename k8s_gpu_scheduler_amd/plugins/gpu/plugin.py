@@ -147,6 +147,11 @@ class GPUArgs:
     # partition controller (plugins.gpu.partitioner): "auto" re-partitions idle nodes for
     # pending pods that ask for an isolated partition; "off" never requests a change
     partitioning: str = "auto"
+    # an SLO-only pod (no amd.com/* request) whose SLO no fractional share can meet -- its
+    # predicted throughput at the default share is below it -- becomes an isolated-partition
+    # request sized from its predictions (the reference drives the MIG layout from every A30
+    # pod's predictions, gpu_plugins.go:357-399,478-496)
+    slo_partitioning: bool = True
     partition_period_s: float = 2.0
     partition_backoff_s: float = 600.0     # a node that refused / failed a mode is not asked again for it
 
@@ -161,7 +166,7 @@ class GPUArgs:
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle",
-                 "partitionPeriodSeconds": "partition_period_s", "partitionBackoffSeconds": "partition_backoff_s"}
+                 "partitionPeriodSeconds": "partition_period_s", "sloPartitioning": "slo_partitioning", "partitionBackoffSeconds": "partition_backoff_s"}
         for k, v in (d or {}).items():
             k = alias.get(k, k)
             if hasattr(a, k):
@@ -321,6 +326,12 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             # (busybox on a CPU-only cluster still schedules): only an explicit
             # amd.com/* request makes the GPU a hard requirement
             r.implicit = mem <= 0
+            size = self.slo_partition_size(pod, slo) if (r.implicit and slo > 0) else None
+            if size:
+                r.isolated, r.whole, r.implicit = True, 1, False
+                r.part_cus = r.cu = size
+                r.units = 0
+                return r
         # round fractional units up to a power of two (aligned XCD groups)
         if r.units:
             p = 1
@@ -329,6 +340,23 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             r.units = min(p, C.MI355X_XCDS)
             r.cu = r.units * CUS_PER_XCD
         return r
+
+    def slo_partition_size(self, pod: Obj, slo: float) -> Optional[int]:
+        """CUs of the isolated partition an SLO-only pod needs when no fractional share can
+        meet its SLO (predicted throughput at the default share below the SLO), sized like
+        the reference's MIG choice: the smallest partition whose prediction still meets it
+        (partitioner.size_from_predictions); None = a fractional share will do, or no
+        predictions (then the reference's behaviour: score it, never filter it)."""
+        if not self.args.slo_partitioning or self.predictions is None or self.args.mode == "parity":
+            return None
+        conf = self._pod_predictions(O.name(pod))[0]
+        if not conf:
+            return None
+        share = conf.get(self._col(max(1, math.ceil(self.args.default_cu / CUS_PER_XCD)), C.MI355X_XCDS))
+        if share is None or share >= slo:
+            return None
+        from .partitioner import size_from_predictions
+        return size_from_predictions(conf, slo, self.args.model)
 
     # ------------------------------------------------------------------ extension points
     def pre_filter(self, state: CycleState, pod: Obj) -> Optional[Status]:

@@ -10,9 +10,14 @@ adjacency alone rarely discriminates; the selection therefore ranks candidate se
 2. NUMA locality: all GPUs on one NUMA node/socket (host staging stays local);
 3. best fit: take GPUs from the NUMA domain with the fewest free GPUs that still fits,
    so larger future requests keep a whole domain;
-4. least live xGMI traffic on the set's GPUs (telemetry: amd-smi per-link accumulators,
+4. measured fabric (agent.fabric, `bw_gbps`): a set containing a degraded pair (copy rate
+   below half the node's median pair) ranks after every set without one, and among the
+   rest the set whose slowest pair is fastest wins (quantised to 5 % of the median, so
+   measurement noise does not reorder healthy sets) -- ring collectives run at the pace
+   of their slowest link;
+5. least live xGMI traffic on the set's GPUs (telemetry: amd-smi per-link accumulators,
    quantised to 10 % of a GPU's 7-link capacity so noise does not reorder equal sets);
-5. lowest total link weight (amdsmi `topo_get_link_weight`), then lowest indices.
+6. lowest total link weight (amdsmi `topo_get_link_weight`), then lowest indices.
 A set is only eligible if each GPU is entirely free (no fractional residents): RCCL
 rings of a multi-GPU pod are per-link bound and a co-located partition pod would share
 that GPU's links.
@@ -31,6 +36,7 @@ class Topology:
     hops: List[List[int]] = field(default_factory=list)
     weight: List[List[int]] = field(default_factory=list)
     numa: List[int] = field(default_factory=list)
+    bw: List[List[float]] = field(default_factory=list)               # measured GB/s per ordered pair
 
     @classmethod
     def fully_connected(cls, n: int = 8, numa_split: bool = True) -> "Topology":
@@ -43,10 +49,26 @@ class Topology:
     @classmethod
     def from_json(cls, d: Dict) -> "Topology":
         n = int(d["n"])
-        return cls(n, d.get("link_type") or [], d.get("hops") or [], d.get("weight") or [], d.get("numa") or [0] * n)
+        return cls(n, d.get("link_type") or [], d.get("hops") or [], d.get("weight") or [], d.get("numa") or [0] * n,
+                   d.get("bw_gbps") or [])
 
     def to_json(self) -> Dict:
-        return {"n": self.n, "link_type": self.link_type, "hops": self.hops, "weight": self.weight, "numa": self.numa}
+        out = {"n": self.n, "link_type": self.link_type, "hops": self.hops, "weight": self.weight, "numa": self.numa}
+        if self.bw:
+            out["bw_gbps"] = self.bw
+        return out
+
+    def pair_bw(self, i: int, j: int) -> Optional[float]:
+        """Measured rate of the slower direction of a pair (None = not measured)."""
+        if not self.bw or max(i, j) >= len(self.bw):
+            return None
+        a, b = self.bw[i][j], self.bw[j][i]
+        return min(a, b) if a > 0 and b > 0 else None
+
+    def bw_median(self) -> Optional[float]:
+        vals = sorted(v for i in range(len(self.bw)) for j in range(len(self.bw))
+                      if i != j and (v := self.pair_bw(i, j)) is not None)
+        return vals[len(vals) // 2] if vals else None
 
     def connected(self, i: int, j: int) -> bool:
         if i == j:
@@ -77,6 +99,7 @@ def select_gpu_set(topo: Topology, free_gpus: Sequence[int], k: int,
     for g in free:
         free_per_numa[numa_of[g]] = free_per_numa.get(numa_of[g], 0) + 1
     best: Optional[Tuple[Tuple, List[int]]] = None
+    med = topo.bw_median() if k > 1 else None
     combos = itertools.combinations(free, k)
     for combo in combos:
         if not is_clique(topo, combo):
@@ -86,11 +109,16 @@ def select_gpu_set(topo: Topology, free_gpus: Sequence[int], k: int,
         fit = min(free_per_numa[d] for d in domains) if same_numa else 99
         wsum = sum(topo.weight[a][b] if topo.weight else 0 for a, b in itertools.combinations(combo, 2))
         load = sum(round(10 * min(1.0, max(0.0, (link_load or {}).get(g, 0.0)))) for g in combo)
-        key = (0 if same_numa else 1, fit, load, wsum, combo)
+        degraded, bw_q = 0, 0
+        if med:
+            slowest = min((topo.pair_bw(a, b) or med) for a, b in itertools.combinations(combo, 2))
+            degraded = 1 if slowest < 0.5 * med else 0
+            bw_q = -round(20 * slowest / med)
+        key = (degraded, 0 if same_numa else 1, fit, bw_q, load, wsum, combo)
         if best is None or key < best[0]:
             best = (key, list(combo))
     if best is None:
         return None
-    same = best[0][0] == 0
-    quality = (1.0 if same else 0.6) * (1.0 if best[0][1] in (k, 99) else 0.9)
+    same = best[0][1] == 0
+    quality = (1.0 if same else 0.6) * (1.0 if best[0][2] in (k, 99) else 0.9) * (0.5 if best[0][0] else 1.0)
     return best[1], quality

@@ -500,6 +500,33 @@ def test_profile_webhook_pod_under_rocprof_lands_in_redis_history(tmp_path):
         json.dump(h, f, indent=1)
 
 
+def test_fabric_probe_single_device_publishes(tmp_path):
+    """The agent's fabric probe on the box (agent.fabric): run in a child process (the agent
+    never holds a GPU context), it measures every visible device's copy rate -- here one
+    MI355X, so the diagonal (its own HBM copy) -- and the agent publishes it with the
+    topology without error."""
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import synthetic_node
+    from k8s_gpu_scheduler_amd.agent.fabric import FabricProber, measure_in_child
+    from k8s_gpu_scheduler_amd.store import schema
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    res = measure_in_child(mib=64, iters=5, env=env)
+    assert res is not None and res["n"] >= 1
+    assert all(res["bw_gbps"][i][i] > 100.0 for i in range(res["n"])), res
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    ag = NodeAgent("box", r, synthetic_node(1, node="box"),
+                   fabric=FabricProber(lambda: measure_in_child(mib=64, iters=5, env=env)))
+    ag.publish()
+    assert ag.probe_fabric()
+    topo = json.loads(r.get(schema.topology_key("box")))
+    assert topo["bw_gbps"][0][0] > 100.0
+    with open(os.path.join(OUT, "fabric_probe.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
 def test_device_plugin_allocates_real_device_nodes():
     """Device plugin on the real inventory (amd-smi / HIP): every advertised GPU resolves to
     its own /dev/dri/renderD* through sysfs, and Allocate hands a container /dev/kfd plus

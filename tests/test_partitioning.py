@@ -236,3 +236,116 @@ def test_request_reverted_without_state_annotation_backs_off():
     assert [d.mode for d in pc.step()] == ["CPX"]
     fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "SPX"}}}, "merge")
     assert pc.step() == [] and pc.backed_off("n1", "CPX")
+
+
+def _preds_plugin(plugin, conf_row):
+    from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, _Tab
+    cp = CachedPredictions()
+    cols = ["1P_MI355X", "2P_MI355X", "4P_MI355X", "8P_MI355X"]
+    cp._conf = _Tab(["onnx_resnet50_1024"], cols, [conf_row], "t")
+    cp._intf = _Tab(["onnx_resnet50_1024_MI355X"], ["onnx_resnet50_1024"], [[0.0]], "t")
+    plugin.predictions = cp
+
+
+def test_slo_only_pod_no_share_can_satisfy_triggers_partition_and_binds():
+    """An SLO-only pod (no amd.com/* request) whose SLO the default 64-CU share cannot meet
+    (predicted 200 < SLO 250) but a DPX half-GPU can (300): Filter keeps it off shared
+    GPUs, the controller sizes it from its predictions (128 CUs) and asks for DPX on the
+    IDLE node only -- the busy one keeps its mode -- and after the agent applies and
+    republishes, the pod binds to a 128-CU partition."""
+    fc, r, agents, s, plugin = _cluster(("n1", "n2"))
+    _preds_plugin(plugin, [400.0, 300.0, 200.0, 90.0])
+    fc.create("pods", O.make_pod("resident", gpu_cu=64, gpu_mem_gib=4,
+                                 node_selector={"kubernetes.io/hostname": "n1"}))
+    (res,) = s.schedule_pending()
+    assert res.node == "n1"
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-slo", slo=250))
+    (res,) = s.schedule_pending()
+    assert not res.node and "DPX partition" in res.status.message()     # never onto a shared GPU
+    dec = plugin.partitioner.step()
+    assert [(d.node, d.mode) for d in dec] == [("n2", "DPX")]
+    assert O.labels(fc.get("nodes", "n1"))[C.LABEL_COMPUTE_PARTITION] == "SPX"
+    pod = fc.get("pods", "onnx-resnet50-1024-slo", "default")
+    assert O.annotations(pod)[C.ANNOT_PARTITION_CUS] == "128"
+    assert agents["n2"].reconcile_partitions()
+    assert _drain(s, fc, ["onnx-resnet50-1024-slo"])
+    u = O.annotations(fc.get("pods", "onnx-resnet50-1024-slo", "default"))[C.ANNOT_DEVICES]
+    assert {d.device.uuid: d.device.cus for d in plugin.ledger.devices("n2")}[u] == 128
+
+
+def test_slo_only_pod_a_share_can_satisfy_stays_fractional():
+    fc, r, agents, s, plugin = _cluster()
+    _preds_plugin(plugin, [400.0, 300.0, 200.0, 90.0])
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-ok", slo=150))      # 200 at 64 CUs meets 150
+    (res,) = s.schedule_pending()
+    assert res.node == "n1" and plugin.partitioner.step() == []
+    plugin.args.slo_partitioning = False                                   # opt-out: reference behaviour
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-hard", slo=250))
+    (res,) = s.schedule_pending()
+    assert res.node == "n1"
+
+
+def test_agent_partition_dry_run_records_amd_smi_calls():
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=2))
+    src = synthetic_node(2, node="n1")
+    ag = NodeAgent("n1", rds(), src, client=fc, partition_dry_run=True)
+    ag.step()
+    fc.patch("nodes", "n1", {"metadata": {"labels": {C.LABEL_COMPUTE_PARTITION: "QPX",
+                                                     C.LABEL_MEMORY_PARTITION: "NPS2"}}}, "merge")
+    assert not ag.reconcile_partitions()
+    assert src.partition_calls == [] and not O.node_taints(fc.get("nodes", "n1"))
+    st = json.loads(O.annotations(fc.get("nodes", "n1"))[C.ANNOT_PARTITION_STATE])
+    assert st["state"] == "dry-run"
+    assert st["calls"] == [
+        {"gpu": 0, "device_index": 0, "call": "amdsmi_set_gpu_memory_partition", "mode": "NPS2"},
+        {"gpu": 1, "device_index": 1, "call": "amdsmi_set_gpu_memory_partition", "mode": "NPS2"},
+        {"gpu": 0, "device_index": 0, "call": "amdsmi_set_gpu_compute_partition", "mode": "QPX"},
+        {"gpu": 1, "device_index": 1, "call": "amdsmi_set_gpu_compute_partition", "mode": "QPX"}]
+
+
+def test_measured_fabric_steers_quad_away_from_degraded_link():
+    """Scripted fabric probe: pair (1, 2) copies at a third of the other pairs' rate.  The
+    agent publishes the matrix with the topology (only while idle), and a 4-GPU pod takes
+    a quad without that pair although GPUs 0-3 are the first same-NUMA quad."""
+    from k8s_gpu_scheduler_amd.agent.fabric import FabricProber, degraded_pairs
+    from k8s_gpu_scheduler_amd.plugins.gpu.topology import Topology, select_gpu_set
+    bw = [[0.0 if i == j else 120.0 for j in range(8)] for i in range(8)]
+    bw[1][2] = bw[2][1] = 40.0
+    calls = []
+
+    def probe():
+        calls.append(1)
+        return {"n": 8, "bw_gbps": bw}
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=8))
+    r = rds()
+    src = synthetic_node(8, node="n1")
+    src.procs = {0: [{"pid": 77, "name": "busy"}]}
+    ag = NodeAgent("n1", r, src, client=fc, fabric=FabricProber(probe))
+    ag.step()                                                 # publish + probe attempt
+    assert calls == []                                        # busy GPUs: deferred
+    src.procs = {}
+    assert ag.probe_fabric() and not ag.probe_fabric()
+    assert calls == [1]                                       # once, when idle
+    topo = Topology.from_json(json.loads(r.get(schema.topology_key("n1"))))
+    assert topo.pair_bw(1, 2) == 40.0 and degraded_pairs(bw) == [(1, 2), (2, 1)]
+    gpus, q = select_gpu_set(topo, list(range(8)), 4)
+    assert not {1, 2} <= set(gpus) and q == 1.0
+    assert select_gpu_set(Topology.fully_connected(8), list(range(8)), 4)[0] == [0, 1, 2, 3]
+    # end to end through the scheduler: the plugin reads the published topology
+    s = Scheduler(fc, default_gpu_config({}), full_registry(), bind_async=False, record_events=False,
+                  extras={"redis": r})
+    s.start_informers()
+    fc.create("pods", O.make_pod("ring-4", gpus=4))
+    (res,) = s.schedule_pending()
+    assert res.node == "n1"
+    idx = json.loads(O.annotations(fc.get("pods", "ring-4", "default"))[C.ANNOT_DEVICE_INDICES])
+    plugin = s.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+    gpu_of = {d.device.uuid: d.device.gpu for d in plugin.ledger.devices("n1")}
+    assert not {1, 2} <= {gpu_of[a[0]] for a in idx}
+    # a partition change makes the probe due again
+    ag.fabric.invalidate()
+    assert not ag.probe_fabric() and calls == [1]             # the 4-GPU pod runs: not now
+    fc.delete("pods", "ring-4", "default")
+    assert ag.probe_fabric() and calls == [1, 1]

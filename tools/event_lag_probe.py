@@ -37,7 +37,7 @@ from k8s_gpu_scheduler_amd.models import workloads as W  # noqa: E402
 from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun  # noqa: E402
 
 
-def run(ex: DeviceExecutor, side, mode: str, epochs: int, rng: random.Random, dist=None):
+def run(ex: DeviceExecutor, side, mode: str, epochs: int, rng: random.Random, dist=None, cp=None):
     lags = []
     torch.cuda.synchronize()
     ref = torch.cuda.Event(enable_timing=True)
@@ -75,10 +75,14 @@ def run(ex: DeviceExecutor, side, mode: str, epochs: int, rng: random.Random, di
                 buf.copy_(torch.arange(64, dtype=torch.int32))
                 dist.broadcast(buf, 0)
                 buf.cpu()
+        if cp is not None:
+            cp.request_schedule()          # the bench's order: ask, launch, collect, receive
         ex.launch_epoch(runs)
         pending.append(runs)
         while len(pending) > 2:
             wait(pending.pop(0))
+        if cp is not None:
+            cp.get_schedule()
     while pending:
         wait(pending.pop(0))
     return lags
@@ -94,6 +98,11 @@ def main() -> None:
     ap.add_argument("--control-plane", action="store_true",
                     help="also run the bench's control-plane process, asked for a schedule every epoch")
     a = ap.parse_args()
+    cp = None
+    if a.control_plane:        # spawned before anything touches the GPU, as in the bench
+        from k8s_gpu_scheduler_amd.parallel.controlplane_proc import ControlPlaneProc
+        cp = ControlPlaneProc(n_gpus=1, pods_per_gpu=4, iters=20, seed=0)
+        cp.schedule_epoch()
     smi = None
     if a.smi_period_ms > 0:
         from k8s_gpu_scheduler_amd.telemetry.smi_sampler import ActivitySampler
@@ -113,7 +122,7 @@ def main() -> None:
             td.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", world_size=1, rank=0,
                                   device_id=torch.device("cuda", 0))
             dist = td
-        lags = run(ex, side, "sync" if mode == "bcast" else mode, a.epochs, rng, dist)
+        lags = run(ex, side, "sync" if mode == "bcast" else mode, a.epochs, rng, dist, cp)
         body = lags[3:]
         out[mode] = {"median_ms": round(statistics.median(body), 3), "max_ms": round(max(body), 3),
                      "min_ms": round(min(body), 3), "last_epoch_ms": round(lags[-1], 3)}
@@ -122,6 +131,8 @@ def main() -> None:
     json.dump(out, open(a.out, "w"), indent=1)
     if smi is not None:
         smi.stop()
+    if cp is not None:
+        cp.close()
     ex.close()
 
 
