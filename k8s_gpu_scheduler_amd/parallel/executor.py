@@ -12,6 +12,7 @@ Working buffers are allocated once per (workload, slot) and reused -- a warm con
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
@@ -63,8 +64,14 @@ class DeviceExecutor:
     # co-run launch policy (tools/pod_mix.py measures these on the catalog mix):
     #   gemm_share   -- tell the GEMM tile picker the pod's CU share instead of the chip
     #   triad_blocks -- workgroups per stream-kernel launch (0 = the kernel's default)
+    #   triad_wg_per_cu -- k > 0: a pod's stream kernels launch k workgroups per CU of its
+    #                   share instead (caps the stream's resident waves next to co-running
+    #                   GEMMs: alone on the chip, 256 workgroups kept 96 % of the stream's rate
+    #                   and lifted a co-running GEMM from 180 to 319 TF,
+    #                   profiles/r02_contention_probe.json triad_sweep)
     gemm_share = True
     triad_blocks = 0
+    triad_wg_per_cu = 0
     #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
     #                   HIP graph on the pod's stream (captured once per workload/slot)
     use_graphs = False
@@ -99,8 +106,13 @@ class DeviceExecutor:
             self._streams[key] = st
         return st
 
+    # one buffer set per workload instead of per (workload, slot): ~1/4 of the HBM, for
+    # multi-rank rehearsals that map every rank onto one GPU (GPUSCHED_FORCE_DEVICE);
+    # co-running pods of one workload then share operands (load generation only)
+    shared_buffers = os.environ.get("GPUSCHED_SHARED_BUFFERS", "") == "1"
+
     def buffers(self, w: Workload, first_unit: int, n_units: int) -> _Buffers:
-        k = (w.name, first_unit, n_units)
+        k = (w.name, 0, 0) if self.shared_buffers else (w.name, first_unit, n_units)
         b = self._bufs.get(k)
         if b is None:
             b = _Buffers(w, self.dev)
@@ -120,7 +132,13 @@ class DeviceExecutor:
     def _budget(self, r: PodRun) -> int:
         return r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
 
+    def triad_grid(self, r: PodRun) -> int:
+        if self.triad_wg_per_cu > 0:
+            return max(1, r.n_units * CUS_PER_UNIT * self.triad_wg_per_cu)
+        return self.triad_blocks
+
     def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:
+        blocks = self.triad_grid(r)
         for _ in range(r.iters):
             for o, t in bufs.ops:
                 if o.kind == "gemm":
@@ -128,12 +146,12 @@ class DeviceExecutor:
                     loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
                 else:
                     x, y, z = t
-                    loadgen.triad(x, y, z, 1.0001, blocks=self.triad_blocks, stream=st)
+                    loadgen.triad(x, y, z, 1.0001, blocks=blocks, stream=st)
 
     def _graph_for(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> "torch.cuda.CUDAGraph":
         """One HIP graph per (workload, unit slot, QoS, iters): captured on the pod's own
         stream, so replaying it there keeps the stream's CU mask and its ordering."""
-        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks)
+        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_grid(r))
         g = self._graphs.get(k)
         if g is None:
             torch.cuda.synchronize(self.device)

@@ -566,6 +566,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
+    ap.add_argument("--triad-wg-per-cu", type=int, default=0,
+                    help="k > 0: each pod's HBM-stream kernels launch k workgroups per CU of its share "
+                         "(caps the stream's resident waves next to co-running GEMMs); 0 = --triad-blocks")
     ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 6),
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
@@ -660,6 +663,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_xcd_group(a.xcd_group)
         _native.hip(required=True).set_triad_variant(a.triad_variant)
         ex.triad_blocks = a.triad_blocks
+        ex.triad_wg_per_cu = a.triad_wg_per_cu
         ex.gemm_share = bool(a.gemm_share)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
@@ -848,6 +852,13 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     smi_all = [smi_t.clone() for _ in range(world)]
     if dist_on:
         dist.all_gather(smi_all, smi_t)
+    # every rank's host time per step (launch / schedule / wait / comm / collect): the
+    # multi-rank rehearsal's view of host-side contention
+    hkeys = sorted(host)
+    host_t = torch.tensor([host[k] / a.steps * 1e3 for k in hkeys], dtype=torch.float64, device=dev)
+    host_all = [host_t.clone() for _ in range(world)]
+    if dist_on:
+        dist.all_gather(host_all, host_t)
     smi_rows = [t.cpu().tolist() for t in smi_all]
     flops_tot, elapsed, busy_tot_ms = float(flops[0]), float(flops[1]), float(flops[2])
     bytes_tot, floor_peak, floor_ach = float(flops[3]), float(flops[4]), float(flops[5])
@@ -870,6 +881,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                        "balance": a.balance, "plan_bursts": a.plan_bursts,
                        "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
                        "online_scale": a.online_scale, "slo_objective": a.slo_objective,
+                       "triad_wg_per_cu": a.triad_wg_per_cu,
                        # which code path N=1 took: collectives over a 1-rank group or the plain path
                        "collectives": bool(dist_on), "dist_single": a.dist_single,
                        **({"collectives_note": dist_note} if dist_note else {}),
@@ -895,6 +907,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "interference_mae": cp.interference_mae(),
             "unscheduled": cp.unscheduled,
             "host_ms_per_step_rank0": {k: round(v / a.steps * 1e3, 3) for k, v in host.items()},
+            "host_ms_per_step_by_rank": [{k: round(float(v), 3) for k, v in zip(hkeys, t.cpu().tolist())}
+                                         for t in host_all] if world > 1 else None,
+            "control_plane_ms_per_epoch": round(cp.sched_s / max(a.steps, 1) * 1e3, 3),
             "simulated": not use_gpu,
         }
         print(json.dumps(result), flush=True)

@@ -16,6 +16,11 @@ epoch:
      (agent.NodeAgent.pod_usage / record_history: process -> pod attribution through the
      apiserver, history keyed by workload) appends it to Redis, where the admission reads
      it; then the pod is deleted.
+     `--history rocprof` (GPU): the pods are real containers-as-processes instead
+     (ops.podrun through the kubelet-style launcher), wrapped in rocprofv3 by the profiling
+     webhook chained behind the resize admission, and the history comes from the node
+     agent's ProfileIngestor reading their rocprofv3 output (agent.profile_webhook) --
+     the deployed path, with kernel-level samples (throughput = iterations / kernel span).
 
 Reported per run: pods completed/s, mean CU request at admission, SLO attainment, backlog,
 GPU CU-share occupancy -- with and without the loop.
@@ -27,6 +32,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import os
 import random
 import time
 from typing import Any, Dict, List, Optional
@@ -91,9 +97,14 @@ def _poisson(rng: random.Random, lam: float) -> int:
 
 
 def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 128, iters: int = 20,
-        resize: bool = True, sim: bool = False, seed: int = 0, device: int = 0) -> Dict[str, Any]:
+        resize: bool = True, sim: bool = False, seed: int = 0, device: int = 0,
+        history: str = "executor", workdir: str = "") -> Dict[str, Any]:
     if n_gpus > 1 and not sim:
         raise ValueError("one process drives one GPU: multi-GPU resize loops run with sim=True")
+    if history == "rocprof":
+        if sim:
+            raise ValueError("--history rocprof runs real pod processes under rocprofv3 (GPU)")
+        return _run_rocprof(epochs, rate, request_cu, iters, resize, seed, workdir)
     rng = random.Random(seed)
     preds = measured_predictions() or analytic_predictions()
     conf = preds._conf
@@ -191,6 +202,98 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
                         "samples": stats.get("history_samples", 0)}}
 
 
+def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: bool, seed: int,
+                 workdir: str) -> Dict[str, Any]:
+    """The resize loop fed by the deployable profiler: pods run as processes under the
+    webhook-injected rocprofv3, the agent's ingestor turns their output into history."""
+    import sys
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    from ..agent import profile_webhook as PW
+    from ..agent.launcher import PodLauncher
+    from ..agent.pod_profiler import ROCPROF, ProfileIngestor
+    rng = random.Random(seed)
+    preds = measured_predictions() or analytic_predictions()
+    conf = preds._conf
+    quarter = {n: conf.by_label[n][f"4P_{C.MI355X}"] for n in W.NAMES}
+    work = workdir or tempfile.mkdtemp(prefix="resize-rocprof-", dir=os.environ.get("TMPDIR") or None)
+    fc = FakeCluster(sync_watch=True, auto_run=True)
+    fc.create("nodes", O.make_node(NODE, gpus=1))
+    hist = RedisHistory(Redis(FakeRedisBackend(FakeRedisEngine())))
+    adm = ResizeAdmission(hist.read, preds.configurations) if resize else None
+    fc.add_admission("pods", PW.ChainAdmission(adm, PW.ProfileInjector(rocprof=ROCPROF)))
+    cfg = default_gpu_config({"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.0, "compat_env": False},
+                             disable_defaults=True)
+    cfg.pod_initial_backoff_s = 0.0
+    ledger = DeviceLedger()
+    sched = Scheduler(fc, cfg, full_registry(), bind_async=False, record_events=False, seed=seed,
+                      extras={"ledger": ledger, "predictions": preds})
+    sched.keep_results = False
+    sched.start_informers()
+    sched.queue.initial_backoff_s = 0.0
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    la = PodLauncher(fc, NODE, timeout_s=240)
+    la.host_root = work
+    la.cwd = work
+    la.extra_env = {"TMPDIR": work, "PYTHONPATH": root}
+    base_env_for = la.env_for
+
+    def env_for(pod):           # the fake node's UUIDs are not this box's: keep the share, run unfiltered
+        env = {k: v for k, v in base_env_for(pod).items()
+               if k not in (C.ENV_ROCR_VISIBLE, C.ENV_HIP_VISIBLE, C.ENV_CU_MASK)}
+        env["GPU_SCHED_CU"] = str(O.gpu_request(pod)[1])
+        return env
+    la.env_for = env_for
+    ing = ProfileIngestor(work + PW.HOST_DIR, hist)
+    weights = [1.0 / (1 + (i % 6)) for i in range(len(W.NAMES))]
+    stats = {"created": 0, "completed": 0, "slo_ok": 0, "req_cu": [], "backlog": [], "samples": 0, "failed": 0}
+    serial = 0
+    t_all = time.perf_counter()
+    for e in range(epochs):
+        for _ in range(_poisson(rng, rate)):
+            wl = rng.choices(W.NAMES, weights)[0]
+            w = W.CATALOG[wl]
+            pod = O.make_pod(f"{wl.replace('_', '-')}-{serial}", gpu_cu=request_cu,
+                             gpu_mem_gib=round(2 * w.hbm_gib, 1), slo=round(quarter[wl] * rng.uniform(0.5, 0.95), 3),
+                             env={C.ENV_ITERATIONS: str(iters)}, labels_={PW.LABEL_PROFILE: "trace"})
+            pod["spec"]["containers"][0]["command"] = [sys.executable, "-m", "k8s_gpu_scheduler_amd.ops.podrun"]
+            pod["spec"]["containers"][0]["args"] = ["--workload", wl]
+            serial += 1
+            fc.create("pods", pod, owned=True)
+            stats["created"] += 1
+        sched.queue.move_all_to_active_or_backoff("epoch")
+        results = sched.schedule_pending()
+        pods = []
+        for r in results:
+            if r.node:
+                ns, name = r.pod_key.split("/", 1)
+                pods.append(fc.get("pods", name, ns))
+                stats["req_cu"].append(O.gpu_request(pods[-1])[1])
+        with ThreadPoolExecutor(max_workers=max(1, len(pods))) as tp:
+            res = list(tp.map(la.run, pods))
+        stats["failed"] += sum(1 for x in res if x.rc != 0)
+        before = len(ing.ingested)
+        stats["samples"] += ing.step()
+        by_uid = {smp["uid"]: smp for smp in ing.ingested[before:]}
+        for pod in pods:
+            smp = by_uid.get(O.uid(pod))
+            if smp is not None and smp.get("throughput"):
+                stats["completed"] += 1
+                stats["slo_ok"] += int(O.pod_slo(pod) <= 0 or smp["throughput"] >= O.pod_slo(pod))
+            fc.delete("pods", O.name(pod), O.namespace(pod))
+        stats["backlog"].append(sum(sched.queue.pending().values()))
+    return {"resize": resize, "history": {"source": "rocprofv3 via the profiling webhook -> node agent ingestor",
+                                          "samples": stats["samples"]},
+            "epochs": epochs, "rate_per_gpu": rate, "request_cu": request_cu, "created": stats["created"],
+            "completed": stats["completed"], "failed_pods": stats["failed"],
+            "mean_cu_request_placed": round(float(np.mean(stats["req_cu"])) if stats["req_cu"] else 0.0, 1),
+            "slo_attainment_pct": round(100.0 * stats["slo_ok"] / max(stats["completed"], 1), 2),
+            "final_backlog": stats["backlog"][-1] if stats["backlog"] else 0,
+            "mean_backlog": round(float(np.mean(stats["backlog"])) if stats["backlog"] else 0.0, 2),
+            "admission": adm.stats if adm is not None else None,
+            "wall_s": round(time.perf_counter() - t_all, 1)}
+
+
 def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap = argparse.ArgumentParser(description="recommender resize loop under Poisson arrivals (config 5)")
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,10 +305,14 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--no-resize", action="store_true")
     ap.add_argument("--both", action="store_true", help="run with and without the loop")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--history", default="executor", choices=["executor", "rocprof"],
+                    help="where the workload history comes from: the executor's accounting reported as a "
+                         "process list (default), or rocprofv3 output of real pod processes (GPU)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     modes = [True, False] if a.both else [not a.no_resize]
-    out = {"runs": [run(a.gpus, a.epochs, a.rate, a.request_cu, a.iters, m, a.sim, a.seed) for m in modes]}
+    out = {"runs": [run(a.gpus, a.epochs, a.rate, a.request_cu, a.iters, m, a.sim, a.seed, history=a.history)
+                    for m in modes]}
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as f:

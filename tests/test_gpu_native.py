@@ -500,6 +500,19 @@ def test_profile_webhook_pod_under_rocprof_lands_in_redis_history(tmp_path):
         json.dump(h, f, indent=1)
 
 
+def test_resize_loop_fed_by_rocprof_history(tmp_path):
+    """Config 5 on the deployed path: Poisson pods run as processes under the webhook's
+    rocprofv3, the agent's ingestor writes their kernel-level samples to the workload
+    history, and the resize admission of later pods reads them."""
+    from k8s_gpu_scheduler_amd.parallel.resize_loop import run
+    out = run(epochs=4, rate=2.0, request_cu=128, iters=10, resize=True, history="rocprof", workdir=str(tmp_path))
+    with open(os.path.join(OUT, "resize_loop_rocprof.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    assert out["failed_pods"] == 0, out
+    assert out["history"]["samples"] == out["completed"] > 0, out
+    assert out["admission"]["seen"] >= out["created"]
+
+
 def test_fabric_probe_single_device_publishes(tmp_path):
     """The agent's fabric probe on the box (agent.fabric): run in a child process (the agent
     never holds a GPU context), it measures every visible device's copy rate -- here one

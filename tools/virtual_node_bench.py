@@ -61,6 +61,12 @@ POLICIES = {
                                corun_sigma=0.10),
     "corun_plan_t20_s15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
                                corun_sigma=0.15),
+    "corun_plan_t40_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.40, slo_objective="corun",
+                               corun_sigma=0.10),
+    "corun_plan_t50_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.50, slo_objective="corun",
+                               corun_sigma=0.10),
+    "corun_plan_t30_s15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun",
+                               corun_sigma=0.15),
     "corun_plan_t30": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun"),
     "corun_plan_t20_m05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
                                corun_margin=0.05),
