@@ -811,6 +811,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         ref["ev"] = torch.cuda.Event(enable_timing=True)
         ref["ev"].record(side)
+        if trace is not None:        # clock alignment: when the host sees the reference event done
+            ref["ev"].synchronize()
+            ref["host_ms"] = (time.perf_counter() - t_start) * 1e3
     flops0, bytes0 = ex.flops_done, ex.bytes_done
     if rank == 0:
         if async_cp:
@@ -825,6 +828,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     wall1 = time.time()
+    if use_gpu and trace is not None:
+        fin = torch.cuda.Event(enable_timing=True)
+        fin.record(side)
+        fin.synchronize()
+        ref["align_end"] = ((time.perf_counter() - t_start) * 1e3, ref["ev"].elapsed_time(fin))
     smi_sum: Dict[str, Any] = {}
     if smi_s is not None:
         smi_s.poll()
@@ -915,7 +923,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         print(json.dumps(result), flush=True)
         if trace is not None:
             with open(os.environ["GPUSCHED_BENCH_TRACE"], "w") as f:
-                json.dump({"ms_total": elapsed * 1e3, "pods": trace}, f)
+                json.dump({"ms_total": elapsed * 1e3, "pods": trace, "ref_host_ms": ref.get("host_ms"),
+                           "align_end_host_gpu_ms": ref.get("align_end")}, f)
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(result, f)

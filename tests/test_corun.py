@@ -1,0 +1,186 @@
+"""Multi-way co-run model (models.corun + native/core/corun.cpp) and the GPU plugin's co-run
+SLO constraint: fluid-sharing simulation, native/numpy agreement, fitting on measured-style
+groups, the online refit, the Score bands and the burst planner."""
+import numpy as np
+import pytest
+
+from k8s_gpu_scheduler_amd import _native
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.framework.config import default_gpu_config
+from k8s_gpu_scheduler_amd.framework.scheduler import Scheduler
+from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+from k8s_gpu_scheduler_amd.models import corun as CR
+from k8s_gpu_scheduler_amd.models import workloads as W
+from k8s_gpu_scheduler_amd.plugins import full_registry
+from k8s_gpu_scheduler_amd.plugins.gpu.devices import DeviceLedger
+from k8s_gpu_scheduler_amd.plugins.gpu.plugin import GPUPlugin
+from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, _Tab
+from k8s_gpu_scheduler_amd.telemetry.cache import TelemetryCache
+
+core = _native.core()
+has_core = core is not None and hasattr(core, "plan_corun")
+I32, I64, F64 = np.int32, np.int64, np.float64
+
+
+def test_simulator_is_processor_sharing_with_unit_coupling():
+    # two pods, u.v = 1: each runs at 1/2 while both are active
+    work = np.array([[10.0, 10.0]])
+    coup = np.ones((1, 2, 2))
+    fin = CR.simulate(work, coup, np.ones((1, 2), bool))
+    assert np.allclose(fin, [[20.0, 20.0]])
+    # the short one finishes at 10 (5 of work at rate 1/2), the long one then runs alone
+    fin = CR.simulate(np.array([[5.0, 10.0]]), coup, np.ones((1, 2), bool))
+    assert np.allclose(fin, [[10.0, 15.0]])
+    # no coupling: both run at full rate; a staggered start shifts only that pod
+    fin = CR.simulate(np.array([[5.0, 10.0]]), np.zeros((1, 2, 2)), np.ones((1, 2), bool), np.array([[0.0, 3.0]]))
+    assert np.allclose(fin, [[5.0, 13.0]])
+    # masked-out slots finish at 0 and do not press on the others
+    fin = CR.simulate(np.array([[4.0, 99.0]]), coup, np.array([[True, False]]))
+    assert np.allclose(fin, [[4.0, 0.0]])
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_native_simulation_matches_numpy():
+    rng = np.random.default_rng(0)
+    m = CR.CorunModel.load()
+    G, K = 300, 4
+    wids = rng.integers(0, len(m.names), (G, K))
+    iters = rng.integers(5, 40, (G, K)).astype(F64)
+    mask = rng.random((G, K)) < 0.85
+    mask[:, 0] = True
+    starts = np.where(rng.random((G, K)) < 0.3, rng.random((G, K)) * 5.0, 0.0)
+    nat = m.batch_times(wids, iters, mask, starts)
+    w = np.where(mask, wids, 0)
+    ref = CR.simulate(m.alone_ms[w] * iters, m.coupling()[w[:, :, None], w[:, None, :]], mask, starts)
+    assert np.allclose(nat[mask], ref[mask], rtol=1e-9, atol=1e-9)
+
+
+def test_shipped_model_covers_the_catalog_and_beats_the_prior():
+    m = CR.CorunModel.load()
+    assert m is not None and m.names == list(W.NAMES)
+    rep = m.meta["report"]
+    assert rep["test"]["mae_pct_of_mean"] < 12.0 < rep["test_prior"]["mae_pct_of_mean"]
+    # alone, a pod runs at its alone rate; next to another pod it cannot get faster
+    i = m.wid("onnx_resnet50_2048")
+    assert i >= 0 and m.wid("my-onnx-resnet50-2048-pod") == i
+    alone = m.group_tput([i], [20])[0]
+    assert alone == pytest.approx(m.alone_tput(i), rel=1e-9)
+    pair = m.group_tput([i, m.wid("tensorflow_mobilenet_2048")], [20, 20])
+    assert pair[0] < alone
+
+
+def _synthetic_groups(model, n, rng, noise=0.0):
+    out = []
+    for i, name in enumerate(model.names):
+        out.append({"w": [name], "iters": 20, "ms": [float(model.alone_ms[i] * 20)], "start": [0.0]})
+    for _ in range(n):
+        k = int(rng.integers(2, 5))
+        ws = [int(x) for x in rng.integers(0, len(model.names), k)]
+        st = [0.0] + [float(x) for x in rng.random(k - 1) * 0.2]
+        t = model.group_durations(ws, [20] * k, st) * np.exp(rng.normal(0.0, noise, k))
+        out.append({"w": [model.names[j] for j in ws], "iters": 20, "ms": [float(x) for x in t], "start": st})
+    return out
+
+
+def test_fit_recovers_a_synthetic_coupling():
+    names = list(W.NAMES[:5])
+    prior = CR.CorunModel.prior(names)
+    rng = np.random.default_rng(1)
+    u = np.exp(rng.normal(0.0, 0.5, prior.u.shape)) * 0.7
+    v = np.exp(rng.normal(0.0, 0.5, prior.v.shape)) * 0.7
+    truth = CR.CorunModel(names, prior.alone_ms, u, v)
+    groups = _synthetic_groups(truth, 400, rng, noise=0.01)
+    model, rep = CR.fit(groups, names=names, ridge=1e-4, max_nfev=200)
+    assert rep["test"]["mean_abs_log"] < 0.03
+    assert rep["test"]["mae_pct_of_mean"] < 0.5 * rep["test_prior"]["mae_pct_of_mean"]
+    # the model round-trips through the recommender's table form
+    t = CR.CorunModel.from_table(model.names, model.table_columns(), model.table_rows(), "v")
+    assert np.allclose(t.coupling(), model.coupling(), rtol=1e-9)
+
+
+def test_online_corun_learns_a_slower_world():
+    """The cluster runs 30 % slower than the offline model says (e.g. a power cap): the
+    online model's prequential error falls below the offline one once refits start."""
+    base = CR.CorunModel.load()
+    world = CR.CorunModel(base.names, base.alone_ms * 1.3, base.u, base.v)
+    on = CR.OnlineCorun(base, refit_every=32, window=256, background=False, min_obs=64, min_calib=64)
+    rng = np.random.default_rng(2)
+    for _ in range(160):
+        ws = [int(x) for x in rng.integers(0, len(base.names), 4)]
+        ms = world.group_durations(ws, [20] * 4)
+        on.observe_group(ws, [20] * 4, ms)
+    e = on.mae()
+    assert on.refits > 0 and e["online"] < 0.6 * e["prior"]
+    assert on.model.version != base.version
+
+
+def test_corun_band_orders_by_new_misses_then_blend():
+    band = GPUPlugin.corun_band
+    assert band(0, 0) > band(1, 100) > band(1, 0) > band(2, 100) > band(3, 100)
+    assert band(0, 100) < 100.0 and band(0, 0) == pytest.approx(50.0)
+    assert band(0, 80) > band(0, 20)
+
+
+def _toy_model():
+    # memwl presses on memwl only, cmpwl on cmpwl only; 1 ms per iteration alone
+    return CR.CorunModel(["memwl", "cmpwl"], [1.0, 1.0], np.array([[0.0, 1.0], [1.0, 0.0]]),
+                         np.array([[0.0, 1.0], [1.0, 0.0]]), {"version": "toy"})
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_native_burst_planner_pairs_complementary_pods():
+    m = _toy_model()
+    # 2 GPUs (one device each, 8 free units); start with like pods together: 20 ms each ->
+    # 500 it/s < the 800 it/s SLO for all four
+    args = dict(units=np.full(4, 2, I32), wid=np.array([0, 0, 1, 1], I32), iters=np.full(4, 10.0),
+                slo=np.full(4, 800.0), dev_gpu=np.array([0, 1], I32), dev_free=np.array([8, 8], I32),
+                res_off=np.zeros(3, I64), r_wid=np.zeros(0, I32), r_iters=np.zeros(0), r_slo=np.zeros(0),
+                alone_ms=m.alone_ms, cmat=m.coupling())
+    out = list(core.plan_corun(np.array([0, 0, 1, 1], I32), **args))
+    assert out[0] != out[1] and out[2] != out[3]
+    off = np.array([0, 2, 4], I64)
+    rw = np.array([m_ for _, m_ in sorted(zip(out, [0, 0, 1, 1]))], I32)
+    bad, mk = core.corun_groups_eval(off, rw, np.full(4, 10.0), np.full(4, 800.0), m.alone_ms, m.coupling())
+    assert list(bad) == [0, 0] and np.allclose(mk, 10.0)
+    # a resident memory pod on GPU 0: the incoming memory pod belongs on GPU 1
+    args1 = dict(args, units=np.full(1, 2, I32), wid=np.array([0], I32), iters=np.full(1, 10.0),
+                 slo=np.full(1, 800.0), res_off=np.array([0, 1, 1], I64), r_wid=np.array([0], I32),
+                 r_iters=np.array([10.0]), r_slo=np.array([800.0]))
+    assert list(core.plan_corun(np.array([0], I32), **args1)) == [1]
+    with pytest.raises(RuntimeError):
+        core.plan_corun(np.array([0, 0, 0, 0, 0], I32), **dict(args, units=np.full(5, 2, I32),
+                                                                wid=np.zeros(5, I32), iters=np.ones(5),
+                                                                slo=np.zeros(5)))
+
+
+def _predictions(corun):
+    cp = CachedPredictions(corun=corun)
+    names = ["memwl", "cmpwl"]
+    cp._conf = _Tab(names, [f"{p}P_{C.MI355X}" for p in (1, 2, 4, 8)],
+                    [[1000.0] * 4, [1000.0] * 4], "t")
+    cp._intf = _Tab(names, names, [[0.0, 0.0], [0.0, 0.0]], "t")
+    return cp
+
+
+def _place(objective: str):
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n0", gpus=2))
+    ledger = DeviceLedger()
+    args = {"w_slo": 1.0, "w_pack": 1.0, "w_telemetry": 0.0, "w_balance": 0.0, "slo_objective": objective}
+    s = Scheduler(fc, default_gpu_config(args, disable_defaults=True), full_registry(), bind_async=False, seed=0,
+                  extras={"ledger": ledger, "telemetry": TelemetryCache(stale_s=0),
+                          "predictions": _predictions(_toy_model())})
+    s.start_informers()
+    for name in ("memwl-0", "memwl-1"):
+        fc.create("pods", O.make_pod(name, gpu_cu=64, slo=800, env={C.ENV_ITERATIONS: "10"}))
+        assert all(r.status.ok for r in s.schedule_pending())
+    return sorted(len(st.pods) for st in ledger.devices("n0"))
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_corun_objective_keeps_an_slo_that_binpacking_would_break():
+    # the reference-style terms (no interference in the pairwise table) pack both memory pods
+    # on one GPU; the co-run constraint predicts 500 < 800 it/s there and spreads them
+    assert _place("terms") == [0, 2]
+    assert _place("auto") == [1, 1]
