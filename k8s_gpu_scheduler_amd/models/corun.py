@@ -515,7 +515,7 @@ def collect(n_groups: int = 2400, iters: int = 20, seed: int = 0, sizes=(2, 3, 4
         ref = torch.cuda.Event(enable_timing=True)
         ref.record()
         ex.launch_epoch(runs)
-        ex.join_current()
+        ex.wait_all()
         torch.cuda.synchronize()
         ms = [r.start.elapsed_time(r.end) for r in runs]
         st = [ref.elapsed_time(r.start) for r in runs]

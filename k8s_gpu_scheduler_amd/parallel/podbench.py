@@ -681,6 +681,15 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     # default stream would implicitly wait for every queued pod kernel and serialise the
     # host with the GPU (measured: 11.7 ms/epoch vs ~3 ms of host work).
     side = torch.cuda.Stream(device=dev) if use_gpu else None
+    if side is not None:
+        # The HIP runtime creates a stream's hardware queue at its FIRST dispatch, and doing so
+        # stalls every other launch for 5-11 ms.  On the collective path the placement
+        # broadcast touches `side` during warm-up; on the plain path its first use was the
+        # timed region's reference event -- a one-off 5.6-11 ms inside the timed window, the
+        # whole 20-step "window effect" (profiles/r03_window/README.md).  Touch it now.
+        _touch = torch.cuda.Event()
+        _touch.record(side)
+        _touch.synchronize()
     cdev = dev if (dist_on and backend == "nccl") else torch.device("cpu")
     assign = torch.zeros((P, FIELDS), dtype=torch.int32, device=cdev)
     tele = torch.zeros((TELE,), dtype=torch.float64, device=cdev)

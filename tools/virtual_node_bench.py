@@ -51,33 +51,11 @@ POLICIES = {
     "planned_load": dict(balance=1.0, plan_bursts=True, plan_objective="load"),
     "random": dict(policy="random", balance=0.0, plan_bursts=False),
     "corun": dict(balance=1.0, plan_bursts=False, slo_objective="corun"),
-    "corun_plan_t05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.05, slo_objective="corun"),
-    "corun_plan_t10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun"),
-    "corun_plan_t15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.15, slo_objective="corun"),
-    "corun_plan_t20": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun"),
-    "corun_plan_t20_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
-                               corun_sigma=0.10),
-    "corun_plan_t30_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun",
-                               corun_sigma=0.10),
-    "corun_plan_t20_s15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
-                               corun_sigma=0.15),
-    "corun_plan_t40_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.40, slo_objective="corun",
-                               corun_sigma=0.10),
-    "corun_plan_t50_s10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.50, slo_objective="corun",
-                               corun_sigma=0.10),
-    "corun_plan_t30_s15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun",
-                               corun_sigma=0.15),
-    "corun_plan_t30": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.30, slo_objective="corun"),
-    "corun_plan_t20_m05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
-                               corun_margin=0.05),
-    "corun_plan_t10_m05": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun",
-                               corun_margin=0.05),
-    "corun_plan_t10_m10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.10, slo_objective="corun",
-                               corun_margin=0.10),
-    "corun_plan_t20_m10": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
-                               corun_margin=0.10),
-    "corun_plan_t20_m15": dict(balance=1.0, plan_bursts=True, plan_tolerance=0.20, slo_objective="corun",
-                               corun_margin=0.15),
+    # corun_plan_tTT[_sSS]: burst planner on the co-run model, load tolerance TT %, soft
+    # objective with model-error sigma 0.SS (none = hard SLO counts)
+    **{f"corun_plan_t{t:02d}" + (f"_s{sg:02d}" if sg else ""):
+       dict(balance=1.0, plan_bursts=True, plan_tolerance=t / 100.0, slo_objective="corun", corun_sigma=sg / 100.0)
+       for t in (5, 10, 20, 30, 40, 50) for sg in (0, 3, 5, 8, 10)},
     # roofline complementarity term (GPU plugin weightComplement) on top of greedy
     "greedy_comp": dict(balance=1.0, plan_bursts=False, complement=1.0),
     "greedy_comp3": dict(balance=1.0, plan_bursts=False, complement=3.0),
@@ -94,15 +72,13 @@ def run_group(ex: DeviceExecutor, runs):
     if not runs:
         return 0.0
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s = torch.cuda.Event(enable_timing=True)
     s.record()
     ex.launch_epoch(runs)
-    ex.join_current()
-    e.record()
-    e.synchronize()
+    ex.wait_all()         # host-side: a stream-wait here would slow one pod stream (executor.wait_all)
     for r in runs:
         r.ms = r.start.elapsed_time(r.end)
-    return s.elapsed_time(e)
+    return max(s.elapsed_time(r.end) for r in runs)
 
 
 GROUPS: list = []      # per group: policy, workloads, wall ms, per pod (SLO, achieved, predicted), for --dump-groups
