@@ -64,14 +64,10 @@ class DeviceExecutor:
     # co-run launch policy (tools/pod_mix.py measures these on the catalog mix):
     #   gemm_share   -- tell the GEMM tile picker the pod's CU share instead of the chip
     #   triad_blocks -- workgroups per stream-kernel launch (0 = the kernel's default)
-    #   triad_wg_per_cu -- k > 0: a pod's stream kernels launch k workgroups per CU of its
-    #                   share instead (caps the stream's resident waves next to co-running
-    #                   GEMMs: alone on the chip, 256 workgroups kept 96 % of the stream's rate
-    #                   and lifted a co-running GEMM from 180 to 319 TF,
-    #                   profiles/r02_contention_probe.json triad_sweep)
+    #   (capping the stream kernels at k workgroups per CU of the pod's share was measured and
+    #   dropped: 380 / 509 / 550 pods/s at k = 1 / 2 / 4 vs 586 uncapped, profiles/r03_triad_cap_ab.json)
     gemm_share = True
     triad_blocks = 0
-    triad_wg_per_cu = 0
     #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
     #                   HIP graph on the pod's stream (captured once per workload/slot)
     use_graphs = False
@@ -132,13 +128,8 @@ class DeviceExecutor:
     def _budget(self, r: PodRun) -> int:
         return r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
 
-    def triad_grid(self, r: PodRun) -> int:
-        if self.triad_wg_per_cu > 0:
-            return max(1, r.n_units * CUS_PER_UNIT * self.triad_wg_per_cu)
-        return self.triad_blocks
-
     def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:
-        blocks = self.triad_grid(r)
+        blocks = self.triad_blocks
         for _ in range(r.iters):
             for o, t in bufs.ops:
                 if o.kind == "gemm":
@@ -151,7 +142,7 @@ class DeviceExecutor:
     def _graph_for(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> "torch.cuda.CUDAGraph":
         """One HIP graph per (workload, unit slot, QoS, iters): captured on the pod's own
         stream, so replaying it there keeps the stream's CU mask and its ordering."""
-        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_grid(r))
+        k = (r.workload, r.first_unit, r.n_units, r.masked, r.iters, budget, self.triad_blocks)
         g = self._graphs.get(k)
         if g is None:
             torch.cuda.synchronize(self.device)

@@ -524,6 +524,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     help="GPU plugin SLO objective: 'corun' = the multi-way co-run model (data/corun_mi355x.json, "
                          "refined online) as a constraint on Score and in the burst planner; 'terms' = the "
                          "reference's pairwise interference terms")
+    ap.add_argument("--corun-sigma", type=float, default=0.05,
+                    help="co-run burst planner: expected SLOs met under the model's log error of this sigma "
+                         "(held-out ~0.05, profiles/r03_corun_v2/); 0 = hard predicted counts")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
                     help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
                          "'slo' = most predicted SLOs met first (within --plan-tolerance)")
@@ -566,9 +569,6 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
-    ap.add_argument("--triad-wg-per-cu", type=int, default=0,
-                    help="k > 0: each pod's HBM-stream kernels launch k workgroups per CU of its share "
-                         "(caps the stream's resident waves next to co-running GEMMs); 0 = --triad-blocks")
     ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 6),
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
@@ -576,9 +576,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--dist-single", type=int, default=-1, choices=[-1, 0, 1],
                     help="a 1-rank process group takes the multi-rank collective path (placement broadcast, "
                          "telemetry all-gather, result all-reduce, barriers): 1 always, 0 never, -1 (default) "
-                         "on a GPU -- N=1 then runs the same code as the N-GPU scaling run, and it measured "
-                         "faster in the driver's 20-step window (593 vs 569 pods/s, 6/6 interleaved pairs, GPU "
-                         "util 99.5 vs 95.6 %%; a tie over 60 steps; profiles/r02_rccl_single_rank/)")
+                         "on a GPU, so N=1 runs the same code as the N-GPU scaling run.  The two paths measure "
+                         "the same (593/594 vs 594/592 pods/s at 20 steps, 625 vs 618 at 60; "
+                         "profiles/r03_window/README.md)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     a.lookahead = max(1, a.lookahead)
@@ -612,7 +612,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     cp_kwargs = dict(n_gpus=n_gpus_planned, pods_per_gpu=a.pods_per_gpu, iters=a.iters, seed=a.seed,
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
                      plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective,
-                     online_scale=bool(a.online_scale), slo_objective=a.slo_objective)
+                     online_scale=bool(a.online_scale), slo_objective=a.slo_objective, corun_sigma=a.corun_sigma)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -663,7 +663,6 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_xcd_group(a.xcd_group)
         _native.hip(required=True).set_triad_variant(a.triad_variant)
         ex.triad_blocks = a.triad_blocks
-        ex.triad_wg_per_cu = a.triad_wg_per_cu
         ex.gemm_share = bool(a.gemm_share)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
@@ -897,8 +896,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
                        "balance": a.balance, "plan_bursts": a.plan_bursts,
                        "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
-                       "online_scale": a.online_scale, "slo_objective": a.slo_objective,
-                       "triad_wg_per_cu": a.triad_wg_per_cu,
+                       "online_scale": a.online_scale, "slo_objective": a.slo_objective, "corun_sigma": a.corun_sigma,
                        # which code path N=1 took: collectives over a 1-rank group or the plain path
                        "collectives": bool(dist_on), "dist_single": a.dist_single,
                        **({"collectives_note": dist_note} if dist_note else {}),
