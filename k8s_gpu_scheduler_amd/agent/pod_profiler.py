@@ -150,7 +150,9 @@ class ProfileIngestor:
     -- becomes one sample of the pod's workload history (what the resize admission reads):
     GPU busy time, kernel count, top kernels, the kernel span and busy fraction, the CU share
     and HBM it was admitted with, and -- for a batch pod with ITERATIONS -- its throughput
-    (iterations / kernel span).  A directory is finished when rocprofv3 has written its
+    (iterations / GPU-busy time: the union of its kernel intervals, not the span -- rocprofv3's
+    per-dispatch tracing adds host gaps between an eagerly launching pod's kernels that the
+    unprofiled pod does not have).  A directory is finished when rocprofv3 has written its
     stats (kernel_stats.csv, or counter_collection.csv for a PMC pass); ingested ones are
     removed, so each run is counted once."""
 
@@ -200,7 +202,8 @@ class ProfileIngestor:
                 sample["busy_frac"] = min(1.0, sample.get("busy_union_ms", 0.0) / span)
                 sample["cu_busy"] = sample["busy_frac"]
                 if req.get("iters"):
-                    sample["throughput"] = req["iters"] / (span / 1e3)
+                    busy = sample.get("busy_union_ms") or span
+                    sample["throughput"] = req["iters"] / (busy / 1e3)
             pod = {"metadata": {"name": name, "namespace": ns, "annotations": {}}}
             try:
                 self.history.append(workload_key(pod), sample)

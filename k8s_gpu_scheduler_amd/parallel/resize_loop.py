@@ -203,9 +203,13 @@ def run(n_gpus: int = 1, epochs: int = 40, rate: float = 3.0, request_cu: int = 
 
 
 def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: bool, seed: int,
-                 workdir: str) -> Dict[str, Any]:
-    """The resize loop fed by the deployable profiler: pods run as processes under the
-    webhook-injected rocprofv3, the agent's ingestor turns their output into history."""
+                 workdir: str, profile_samples: int = 3) -> Dict[str, Any]:
+    """The resize loop fed by the deployable profiler: pods run as processes; the first
+    `profile_samples` pods of each workload opt in to the profiling webhook (label), so they
+    run under the injected rocprofv3 and the agent's ingestor turns their output into the
+    history the resize admission reads -- a sampling profiler, as a cluster would run it.
+    Throughput and SLOs are accounted from every pod's own report (unprofiled pods carry no
+    profiler overhead)."""
     import sys
     import tempfile
     from concurrent.futures import ThreadPoolExecutor
@@ -246,16 +250,22 @@ def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: 
     la.env_for = env_for
     ing = ProfileIngestor(work + PW.HOST_DIR, hist)
     weights = [1.0 / (1 + (i % 6)) for i in range(len(W.NAMES))]
-    stats = {"created": 0, "completed": 0, "slo_ok": 0, "req_cu": [], "backlog": [], "samples": 0, "failed": 0}
+    stats = {"created": 0, "completed": 0, "slo_ok": 0, "req_cu": [], "backlog": [], "samples": 0, "failed": 0,
+             "profiled": 0}
+    profiled_by_wl: Dict[str, int] = {}
     serial = 0
     t_all = time.perf_counter()
     for e in range(epochs):
         for _ in range(_poisson(rng, rate)):
             wl = rng.choices(W.NAMES, weights)[0]
             w = W.CATALOG[wl]
+            prof = profiled_by_wl.get(wl, 0) < profile_samples
+            if prof:
+                profiled_by_wl[wl] = profiled_by_wl.get(wl, 0) + 1
+                stats["profiled"] += 1
             pod = O.make_pod(f"{wl.replace('_', '-')}-{serial}", gpu_cu=request_cu,
                              gpu_mem_gib=round(2 * w.hbm_gib, 1), slo=round(quarter[wl] * rng.uniform(0.5, 0.95), 3),
-                             env={C.ENV_ITERATIONS: str(iters)}, labels_={PW.LABEL_PROFILE: "trace"})
+                             env={C.ENV_ITERATIONS: str(iters)}, labels_={PW.LABEL_PROFILE: "trace"} if prof else None)
             pod["spec"]["containers"][0]["command"] = [sys.executable, "-m", "k8s_gpu_scheduler_amd.ops.podrun"]
             pod["spec"]["containers"][0]["args"] = ["--workload", wl]
             serial += 1
@@ -272,18 +282,17 @@ def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: 
         with ThreadPoolExecutor(max_workers=max(1, len(pods))) as tp:
             res = list(tp.map(la.run, pods))
         stats["failed"] += sum(1 for x in res if x.rc != 0)
-        before = len(ing.ingested)
         stats["samples"] += ing.step()
-        by_uid = {smp["uid"]: smp for smp in ing.ingested[before:]}
-        for pod in pods:
-            smp = by_uid.get(O.uid(pod))
-            if smp is not None and smp.get("throughput"):
+        for pod, x in zip(pods, res):
+            rep = x.json() if x.rc == 0 else None
+            if rep and rep.get("throughput"):
                 stats["completed"] += 1
-                stats["slo_ok"] += int(O.pod_slo(pod) <= 0 or smp["throughput"] >= O.pod_slo(pod))
+                stats["slo_ok"] += int(O.pod_slo(pod) <= 0 or rep["throughput"] >= O.pod_slo(pod))
             fc.delete("pods", O.name(pod), O.namespace(pod))
         stats["backlog"].append(sum(sched.queue.pending().values()))
     return {"resize": resize, "history": {"source": "rocprofv3 via the profiling webhook -> node agent ingestor",
-                                          "samples": stats["samples"]},
+                                          "samples": stats["samples"], "profiled_pods": stats["profiled"],
+                                          "profile_samples_per_workload": profile_samples},
             "epochs": epochs, "rate_per_gpu": rate, "request_cu": request_cu, "created": stats["created"],
             "completed": stats["completed"], "failed_pods": stats["failed"],
             "mean_cu_request_placed": round(float(np.mean(stats["req_cu"])) if stats["req_cu"] else 0.0, 1),
