@@ -350,10 +350,12 @@ class OnlineCorun:
     predicts the newest 1/4 better than the current model."""
 
     def __init__(self, base: CorunModel, refit_every: int = 32, window: int = 512, ridge: float = 8.0,
-                 max_nfev: int = 8, background: bool = True, min_obs: int = 256, min_calib: int = 256):
+                 max_nfev: int = 8, background: Any = True, min_obs: int = 256, min_calib: int = 256):
         self.base = base
         self.model = base
         self.refit_every, self.window, self.ridge, self.max_nfev = refit_every, window, ridge, max_nfev
+        # True / "thread": refit in a thread; "process": in a worker process (the scheduler's
+        # control plane: no interpreter-lock contention); False: synchronously
         self.background = background
         # no refit before this many observed pods: the offline model is fitted on thousands of
         # measured groups, a refit on a few dozen only adds noise (replayed bench timelines:
@@ -373,7 +375,10 @@ class OnlineCorun:
         self._busy = False
         # import the optimiser now: its first import (~0.5-1 s of interpreter work under the
         # GIL) would otherwise land in the first background refit, inside a timed region
-        from scipy.optimize import least_squares  # noqa: F401
+        if background == "process":
+            _RefitWorker.shared()           # start (and let it import) before any timed work
+        else:
+            from scipy.optimize import least_squares  # noqa: F401
         self._x = np.zeros(len(base.names) + 1)
 
     def observe_group(self, wids: Sequence[int], iters: Sequence[float], ms: Sequence[float],
@@ -414,74 +419,51 @@ class OnlineCorun:
             self._refit(snap)
         return True
 
+    def _payload(self, obs) -> Dict[str, Any]:
+        K = max(len(o[0]) for o in obs)
+        G = len(obs)
+        wids = np.zeros((G, K), np.int64)
+        iters = np.zeros((G, K))
+        mask = np.zeros((G, K), bool)
+        tgt = np.zeros((G, K), bool)
+        ms = np.ones((G, K))
+        st = np.zeros((G, K))
+        for g, (w, it, s, m, t) in enumerate(obs):
+            k = len(w)
+            wids[g, :k], iters[g, :k], st[g, :k], ms[g, :k], tgt[g, :k] = w, it, s, m, t
+            mask[g, :k] = True
+        b = self.base
+        return {"names": b.names, "alone_ms": b.alone_ms, "u": b.u, "v": b.v, "wids": wids, "iters": iters,
+                "mask": mask, "tgt": tgt, "ms": ms, "st": st, "x": self._x, "ridge": self.ridge,
+                "max_nfev": self.max_nfev, "stage2": self.err["n"] >= self.min_obs}
+
     def _refit(self, obs) -> None:
         try:
-            from scipy.optimize import least_squares
-            K = max(len(o[0]) for o in obs)
-            G = len(obs)
-            wids = np.zeros((G, K), np.int64)
-            iters = np.zeros((G, K))
-            mask = np.zeros((G, K), bool)
-            tgt = np.zeros((G, K), bool)
-            ms = np.ones((G, K))
-            st = np.zeros((G, K))
-            for g, (w, it, s, m, t) in enumerate(obs):
-                k = len(w)
-                wids[g, :k], iters[g, :k], st[g, :k], ms[g, :k], tgt[g, :k] = w, it, s, m, t
-                mask[g, :k] = True
-            tgt &= mask & (ms > 0) & (iters > 0)
-            base = self.base
-            n_w = len(base.names)
-
-            def model_of(x):
-                m = CorunModel(base.names, base.alone_ms * np.exp(x[:n_w]), base.u * np.exp(x[n_w]), base.v)
-                return m
-
-            def resid(model, sel):
-                t = model.batch_times(wids, iters, mask, st) - st
-                return np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[sel]
-
-            # stage 1: global time scale of the (possibly refitted) model
-            cur = model_of(self._x)
-            r = resid(cur, tgt)
-            scale = float(np.exp(-np.median(r))) if r.size else 1.0
-            stage2 = self.err["n"] >= self.min_obs
-            x_new = self._x
-            if stage2:
-                n_fit = max(1, (3 * G) // 4)
-                fit_m = tgt.copy()
-                fit_m[n_fit:] = False
-                hold = tgt.copy()
-                hold[:n_fit] = False
-
-                def obj(x):
-                    m2 = model_of(x)
-                    m2.alone_ms = m2.alone_ms * scale
-                    return np.concatenate([resid(m2, fit_m), np.sqrt(self.ridge) * x])
-
-                sol = least_squares(obj, self._x, method="trf", max_nfev=self.max_nfev)
-                cand = model_of(sol.x)
-                cand.alone_ms = cand.alone_ms * scale
-                keep = model_of(self._x)
-                keep.alone_ms = keep.alone_ms * scale
-                if not hold.any() or np.abs(resid(cand, hold)).mean() < np.abs(resid(keep, hold)).mean():
-                    x_new = sol.x
-                else:
-                    self.rejected += 1
-            m = model_of(x_new)
-            with self._lock:
-                self._x = x_new
-                self.time_scale = scale
-                self.version += 1
-                self.refits += 1
-                self.model = CorunModel(base.names, m.alone_ms * scale, m.u, m.v,
-                                        dict(base.meta, version=f"{base.version}+online-{self.version}"))
+            if self.background == "process":
+                res = _RefitWorker.shared().solve(self._payload(obs))
+            else:
+                res = solve_refit(self._payload(obs))
+            self._install(res)
         except Exception as e:      # a failed refit keeps the current model
             import logging
             logging.getLogger(__name__).warning("co-run refit failed: %s", e)
         finally:
             with self._lock:
                 self._busy = False
+
+    def _install(self, res: Dict[str, Any]) -> None:
+        base = self.base
+        n_w = len(base.names)
+        x_new, scale = np.asarray(res["x"]), float(res["scale"])
+        with self._lock:
+            self.rejected += int(res["rejected"])
+            self._x = x_new
+            self.time_scale = scale
+            self.version += 1
+            self.refits += 1
+            self.model = CorunModel(base.names, base.alone_ms * np.exp(x_new[:n_w]) * scale,
+                                    base.u * np.exp(x_new[n_w]), base.v,
+                                    dict(base.meta, version=f"{base.version}+online-{self.version}"))
 
     def wait_idle(self, timeout_s: float = 10.0) -> None:
         t = time.time()
@@ -496,6 +478,122 @@ class OnlineCorun:
         return {"n": n, "prior": self.err["prior"] / n, "online": self.err["online"] / n,
                 "mean_tput": self.err["tput_sum"] / n, "refits": self.refits, "rejected": self.rejected,
                 "time_scale": round(self.time_scale, 4)}
+
+
+def solve_refit(p: Dict[str, Any]) -> Dict[str, Any]:
+    """One OnlineCorun refit on a window of observed groups (pure: arrays in, parameters out).
+    Stage 1: the global time scale = exp(-median log(predicted / measured)) of the current
+    model; stage 2 (p["stage2"]): a per-workload log-scale of the alone time and a global
+    log-scale of the coupling, a few Levenberg-Marquardt steps ridge-pulled to 0, fitted on the
+    older 3/4 of the window and kept only if it predicts the newest 1/4 better."""
+    from scipy.optimize import least_squares
+    names, alone, u, v = p["names"], np.asarray(p["alone_ms"]), np.asarray(p["u"]), np.asarray(p["v"])
+    wids, iters, mask, ms, st = p["wids"], p["iters"], p["mask"], p["ms"], p["st"]
+    tgt = p["tgt"] & mask & (ms > 0) & (iters > 0)
+    n_w = len(names)
+    G = wids.shape[0]
+
+    def model_of(x, scale=1.0):
+        return CorunModel(names, alone * np.exp(x[:n_w]) * scale, u * np.exp(x[n_w]), v)
+
+    def resid(model, sel):
+        t = model.batch_times(wids, iters, mask, st) - st
+        return np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[sel]
+
+    x0 = np.asarray(p["x"], dtype=np.float64)
+    r = resid(model_of(x0), tgt)
+    scale = float(np.exp(-np.median(r))) if r.size else 1.0
+    x_new, rejected = x0, 0
+    if p["stage2"]:
+        n_fit = max(1, (3 * G) // 4)
+        fit_m, hold = tgt.copy(), tgt.copy()
+        fit_m[n_fit:] = False
+        hold[:n_fit] = False
+        ridge = float(p["ridge"])
+        sol = least_squares(lambda x: np.concatenate([resid(model_of(x, scale), fit_m), np.sqrt(ridge) * x]), x0,
+                            method="trf", max_nfev=int(p["max_nfev"]))
+        if not hold.any() or (np.abs(resid(model_of(sol.x, scale), hold)).mean()
+                              < np.abs(resid(model_of(x0, scale), hold)).mean()):
+            x_new = sol.x
+        else:
+            rejected = 1
+    return {"x": x_new, "scale": scale, "rejected": rejected}
+
+
+class _RefitWorker:
+    """A child PROCESS that runs `solve_refit`, so a refit (hundreds of ms of numpy / scipy
+    between native simulations on a window of 10-20-member timeline groups) never competes
+    with the scheduler for the interpreter lock: in a thread it stalled the 8-GPU control
+    plane by ~50 ms per epoch.  A plain subprocess (the bench's control plane is itself a
+    daemonic multiprocessing child, which may not start multiprocessing children); frames are
+    length-prefixed pickles of arrays this process built itself."""
+    _inst: Optional["_RefitWorker"] = None
+    _guard = threading.Lock()
+
+    def __init__(self):
+        import subprocess
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        # one BLAS / OpenMP thread: a multi-threaded least-squares step would take every core
+        # the scheduler and the GPU ranks need
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                   OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+        self.p = subprocess.Popen([sys.executable, "-m", "k8s_gpu_scheduler_amd.models.corun", "refit-worker"],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env)
+        self.lock = threading.Lock()
+
+    @classmethod
+    def shared(cls) -> "_RefitWorker":
+        with cls._guard:
+            if cls._inst is None or cls._inst.p.poll() is not None:
+                cls._inst = cls()
+            return cls._inst
+
+    def solve(self, payload: Dict[str, Any]) -> Dict[str, Any]:
+        import pickle
+        import struct
+        data = pickle.dumps(payload, protocol=pickle.HIGHEST_PROTOCOL)
+        with self.lock:
+            self.p.stdin.write(struct.pack("<Q", len(data)) + data)
+            self.p.stdin.flush()
+            n = struct.unpack("<Q", _read_exact(self.p.stdout, 8))[0]
+            res = pickle.loads(_read_exact(self.p.stdout, n))
+        if "error" in res:
+            raise RuntimeError(res["error"])
+        return res
+
+
+def _read_exact(f, n: int) -> bytes:
+    buf = b""
+    while len(buf) < n:
+        chunk = f.read(n - len(buf))
+        if not chunk:
+            raise EOFError("refit worker closed its pipe")
+        buf += chunk
+    return buf
+
+
+def _refit_worker_main() -> int:
+    """`python -m k8s_gpu_scheduler_amd.models.corun refit-worker`: solve frames until EOF."""
+    import pickle
+    import struct
+    import sys
+    from scipy.optimize import least_squares  # noqa: F401  (import now, not in the first refit)
+    inp, out = sys.stdin.buffer, sys.stdout.buffer
+    sys.stdout = sys.stderr             # frames only on the real stdout
+    while True:
+        try:
+            n = struct.unpack("<Q", _read_exact(inp, 8))[0]
+            payload = pickle.loads(_read_exact(inp, n))
+        except EOFError:
+            return 0
+        try:
+            res = solve_refit(payload)
+        except Exception as e:          # report, keep serving
+            res = {"error": repr(e)}
+        data = pickle.dumps(res, protocol=pickle.HIGHEST_PROTOCOL)
+        out.write(struct.pack("<Q", len(data)) + data)
+        out.flush()
 
 
 # ----------------------------------------------------------------------------- collection (GPU)
@@ -559,11 +657,14 @@ def main(argv: Optional[List[str]] = None) -> int:
     c.add_argument("--iters", type=int, default=20)
     c.add_argument("--seed", type=int, default=0)
     c.add_argument("--out", default="gpurun_out/corun.json")
+    sub.add_parser("refit-worker", help="internal: OnlineCorun's refit process")
     f = sub.add_parser("fit")
     f.add_argument("data", nargs="+")
     f.add_argument("--ridge", type=float, default=0.05)
     f.add_argument("--out", default=DATA)
     a = ap.parse_args(argv)
+    if a.cmd == "refit-worker":
+        return _refit_worker_main()
     if a.cmd == "collect":
         q = int(os.environ.get("GPUSCHED_HW_QUEUES", "16"))
         if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < q <= 32:

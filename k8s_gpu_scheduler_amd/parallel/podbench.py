@@ -124,9 +124,10 @@ class ControlPlane:
             base = corun_model or CorunModel.load()
             if base is not None:
                 self.predictions.install_corun(base)
-                # a refit is ~30 ms of control-plane CPU (GIL) and the offline model's error is
-                # ~3.5 %: refit about every 8 epochs of the whole node
-                self.corun = OnlineCorun(base, refit_every=max(128, 8 * n_gpus * pods_per_gpu))
+                # refits run in a worker process (a refit in a thread stalled this control plane
+                # by ~50 ms per 8-GPU epoch through the interpreter lock), about every 8 epochs
+                self.corun = OnlineCorun(base, refit_every=max(128, 8 * n_gpus * pods_per_gpu),
+                                         background="process")
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
                 "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement,

@@ -115,6 +115,21 @@ def test_online_corun_learns_a_slower_world():
     assert on.model.version != base.version
 
 
+def test_online_corun_refits_in_a_worker_process():
+    """The control plane's mode: refits run in a child process (no interpreter-lock
+    contention with the scheduler) and the refitted model is installed on return."""
+    base = CR.CorunModel.load()
+    world = CR.CorunModel(base.names, base.alone_ms * 1.3, base.u, base.v)
+    on = CR.OnlineCorun(base, refit_every=64, window=256, background="process", min_obs=64, min_calib=64)
+    rng = np.random.default_rng(3)
+    for _ in range(120):
+        ws = [int(x) for x in rng.integers(0, len(base.names), 4)]
+        on.observe_group(ws, [20] * 4, world.group_durations(ws, [20] * 4))
+        on.wait_idle(30.0)
+    assert on.refits > 0 and abs(on.time_scale - 1.3) < 0.05
+    assert on.mae()["online"] < 0.6 * on.mae()["prior"]
+
+
 def test_corun_band_orders_by_new_misses_then_blend():
     band = GPUPlugin.corun_band
     assert band(0, 0) > band(1, 100) > band(1, 0) > band(2, 100) > band(3, 100)
