@@ -71,6 +71,14 @@ class DeviceExecutor:
     #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
     #                   HIP graph on the pod's stream (captured once per workload/slot)
     use_graphs = False
+    #   balance_slots -- Burstable pods of one size are interchangeable across their CU-slice
+    #                   slots (the share is accounting, not a mask), so the executor puts each
+    #                   epoch's pods, longest first, on the slot streams with the least
+    #                   cumulative work (LPT).  The scheduler's first-fit gives the epoch's
+    #                   longest pod (LPT queue order) slot 0 every time, so slot 0's stream
+    #                   carried 131 ms of a 134 ms window and slot 6's 100 ms: the launch-ahead
+    #                   pipeline then waits on slot 0 while the others idle.
+    balance_slots = os.environ.get("GPUSCHED_BALANCE_SLOTS", "1") == "1"
 
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
         self.device = device
@@ -85,6 +93,7 @@ class DeviceExecutor:
         self._graphs: Dict[Tuple, "torch.cuda.CUDAGraph"] = {}
         self.flops_done = 0.0
         self.bytes_done = 0.0
+        self._slot_work: Dict[Tuple[int, int], float] = {}     # (first unit, units) -> cumulative work
         # the executor's clock: pod start / end events are reported as ms after this event
         # (the co-run learner rebuilds which pods of neighbouring epochs overlapped)
         self.clock = torch.cuda.Event(enable_timing=True)
@@ -162,6 +171,8 @@ class DeviceExecutor:
         finished early starts its next pod at once instead of idling until the slowest
         pod of the epoch completes (work-conserving), while two pods never overlap on the
         same CUs -- exactly the ledger's capacity model."""
+        if self.balance_slots:
+            self._balance(runs)
         for r in runs:
             key = (r.first_unit, r.n_units, r.masked)
             w = CATALOG[r.workload]
@@ -195,18 +206,37 @@ class DeviceExecutor:
         self._last_events = [ev for _, ev in {id(e): (k, e) for k, e in self._unit_last.values()}.values()]
         self.epoch_runs.append(runs)
 
+    @staticmethod
+    def pod_work(r: PodRun) -> float:
+        """Relative work of a pod (its kernels' roofline time alone on the GPU x iterations)."""
+        from ..models.workloads import roofline_seconds
+        return roofline_seconds(CATALOG[r.workload], 1.0) * max(r.iters, 1)
+
+    def _balance(self, runs: List[PodRun]) -> None:
+        """Reassign the slots of each group of same-size Burstable pods of this epoch: longest
+        pod first onto the slot with the least cumulative work (ties: the lower slot)."""
+        groups: Dict[int, List[PodRun]] = {}
+        for r in runs:
+            if not r.masked:
+                groups.setdefault(r.n_units, []).append(r)
+        for n, rs in groups.items():
+            if len(rs) < 2:
+                continue
+            slots = sorted(r.first_unit for r in rs)
+            if len(set(slots)) != len(slots):
+                continue
+            for r in sorted(rs, key=self.pod_work, reverse=True):
+                u = min(slots, key=lambda s: (self._slot_work.get((s, n), 0.0), s))
+                slots.remove(u)
+                r.first_unit = u
+                self._slot_work[(u, n)] = self._slot_work.get((u, n), 0.0) + self.pod_work(r)
+
     # host poll period while waiting for an epoch's end events
     poll_s = 20e-6
 
     def wait_epoch(self, runs: List[PodRun]) -> None:
         """Host-wait until every pod of an epoch finished (its end events), by polling the
-        events.  A blocking hipEventSynchronize sleeps until the runtime is woken, and on a
-        device with no other completion interrupts in flight (the 1-rank plain path) that
-        wake-up came ~6 ms after the last pod kernel ended -- every epoch (rocprof + pod
-        traces, profiles/r03_window/).  Behind the launch-ahead pipeline that lateness is
-        hidden, except after the LAST epoch, where it adds ~6 ms to the timed region (4.4 %
-        of a 20-step window: the whole 'window effect' of round 2).  Polling wakes within
-        tens of microseconds on every path."""
+        events (wakes within tens of microseconds; never a stream-wait, see wait_all)."""
         for r in runs:
             ev = r.end
             if ev is None:

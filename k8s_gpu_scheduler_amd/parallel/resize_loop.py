@@ -262,7 +262,6 @@ def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: 
             prof = profiled_by_wl.get(wl, 0) < profile_samples
             if prof:
                 profiled_by_wl[wl] = profiled_by_wl.get(wl, 0) + 1
-                stats["profiled"] += 1
             pod = O.make_pod(f"{wl.replace('_', '-')}-{serial}", gpu_cu=request_cu,
                              gpu_mem_gib=round(2 * w.hbm_gib, 1), slo=round(quarter[wl] * rng.uniform(0.5, 0.95), 3),
                              env={C.ENV_ITERATIONS: str(iters)}, labels_={PW.LABEL_PROFILE: "trace"} if prof else None)
@@ -279,6 +278,7 @@ def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: 
                 ns, name = r.pod_key.split("/", 1)
                 pods.append(fc.get("pods", name, ns))
                 stats["req_cu"].append(O.gpu_request(pods[-1])[1])
+        stats["profiled"] += sum(1 for p in pods if O.labels(p).get(PW.LABEL_PROFILE))
         with ThreadPoolExecutor(max_workers=max(1, len(pods))) as tp:
             res = list(tp.map(la.run, pods))
         stats["failed"] += sum(1 for x in res if x.rc != 0)

@@ -272,3 +272,24 @@ def test_complement_term_prefers_the_gpu_with_the_other_roofline_class():
     assert g["big-gemmy-0"] == g["big-streamy-0"]
     g = place(0.0)                      # balance alone spreads the two pods
     assert g["big-gemmy-0"] != g["big-streamy-0"]
+
+
+def test_executor_balances_burstable_slots_by_cumulative_work():
+    """DeviceExecutor._balance (CPU-testable part): each epoch's same-size Burstable pods go
+    longest first onto the slot with the least cumulative work, so the slot that first-fit
+    always hands the epoch's longest pod does not become the pipeline's bottleneck; masked
+    (Guaranteed) pods keep their slots."""
+    import types
+    from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun
+    ex = types.SimpleNamespace(_slot_work={}, pod_work=lambda r: {"a": 4.0, "b": 3.0, "c": 2.0, "d": 1.0}[r.pod_id])
+    tot = {}
+    for e in range(8):
+        runs = [PodRun(p, "onnx_resnet50_1024", u, 2, 20, masked=False) for p, u in zip("abcd", (0, 2, 4, 6))]
+        DeviceExecutor._balance(ex, runs)
+        assert sorted(r.first_unit for r in runs) == [0, 2, 4, 6]
+        for r in runs:
+            tot[r.first_unit] = tot.get(r.first_unit, 0.0) + ex.pod_work(r)
+    assert max(tot.values()) - min(tot.values()) <= 4.0          # first-fit: 32 vs 8
+    g = [PodRun("a", "x", 0, 2, 20, masked=True), PodRun("b", "x", 2, 2, 20, masked=True)]
+    DeviceExecutor._balance(ex, g)
+    assert [r.first_unit for r in g] == [0, 2]
