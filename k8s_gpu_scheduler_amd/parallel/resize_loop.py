@@ -290,6 +290,9 @@ def _run_rocprof(epochs: int, rate: float, request_cu: int, iters: int, resize: 
                 stats["slo_ok"] += int(O.pod_slo(pod) <= 0 or rep["throughput"] >= O.pod_slo(pod))
             fc.delete("pods", O.name(pod), O.namespace(pod))
         stats["backlog"].append(sum(sched.queue.pending().values()))
+        print(f"[resize-rocprof] resize={resize} epoch {e + 1}/{epochs}: ran {len(pods)}, completed "
+              f"{stats['completed']}, backlog {stats['backlog'][-1]}, samples {stats['samples']}",
+              file=sys.stderr, flush=True)
     return {"resize": resize, "history": {"source": "rocprofv3 via the profiling webhook -> node agent ingestor",
                                           "samples": stats["samples"], "profiled_pods": stats["profiled"],
                                           "profile_samples_per_workload": profile_samples},

@@ -12,8 +12,9 @@ Behaviour of the reference server (reference pkg/recommender/recom_server.py):
 Fixes: existence is checked before hashing, the swap is under a lock
 (§5.2 race), the retrain loop survives exceptions, the thread pool size is configurable.
 Extensions (separate `gpusched.recommender.Extended` service): ExportTable (completed
-matrices for the scheduler's in-process cache), RecommendResources (resize from
-Redis history), Version.
+matrices for the scheduler's in-process cache, and table "corun": the multi-way co-run model
+of models.corun, one row per workload), RecommendResources (resize from Redis history),
+Version.
 """
 from __future__ import annotations
 
@@ -107,12 +108,44 @@ class ModelSlot:
             return self.current
 
 
+class CorunSlot:
+    """The multi-way co-run model (models.corun, a JSON file) with the same md5-driven hot
+    reload and locked swap as the matrices; served through ExportTable("corun")."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self._lock = threading.Lock()
+        self.model: Any = None
+        self.version: Optional[str] = None
+        self.file_version: Optional[str] = None
+
+    def load_if_changed(self) -> bool:
+        v = file_version(self.path) if self.path else None
+        if v is None or v == self.file_version:
+            return False
+        from ..models.corun import CorunModel
+        m = CorunModel.load(self.path)
+        if m is None:
+            return False
+        with self._lock:
+            self.model, self.file_version = m, v
+            self.version = f"{m.version}@{v[:8]}"
+        log.info("corun: loaded %s (%d workloads)", self.version, len(m.names))
+        return True
+
+    def get(self) -> Any:
+        with self._lock:
+            return self.model
+
+
 class RecommenderService:
     def __init__(self, configurations_path: str = "", interference_path: str = "",
                  kind: str = "iterative", job_delay_s: float = C.RECOMMENDER_JOB_DELAY_S,
-                 history_source: Optional[Callable[[str], Any]] = None, model: str = "MI355X"):
+                 history_source: Optional[Callable[[str], Any]] = None, model: str = "MI355X",
+                 corun_path: str = ""):
         self.conf = ModelSlot("configurations", configurations_path, kind)
         self.intf = ModelSlot("interference", interference_path, kind)
+        self.corun = CorunSlot(corun_path)
         self.job_delay_s = job_delay_s
         self.history_source = history_source
         self.model = model
@@ -126,6 +159,10 @@ class RecommenderService:
 
     @classmethod
     def from_env(cls, **kw: Any) -> "RecommenderService":
+        """Env as the reference's server, plus CORUN_MODEL_PATH (default: the shipped MI355X
+        co-run model, data/corun_mi355x.json)."""
+        from ..models.corun import DATA as CORUN_DATA
+        kw.setdefault("corun_path", os.getenv("CORUN_MODEL_PATH", CORUN_DATA))
         return cls(os.getenv("CONFIGURATIONS_DATA_PATH", DEFAULT_CONF),
                    os.getenv("INTERFERENCE_DATA_PATH", DEFAULT_INTF),
                    job_delay_s=float(os.getenv("JOB_DELAY", C.RECOMMENDER_JOB_DELAY_S)), **kw)
@@ -139,6 +176,10 @@ class RecommenderService:
                     self.restore_online()
             except Exception as e:
                 log.warning("%s: training failed: %s", slot.name, e)
+        try:
+            self.corun.load_if_changed()
+        except Exception as e:
+            log.warning("corun: loading %s failed: %s", self.corun.path, e)
 
     def start_retrain_loop(self) -> None:
         def loop() -> None:
@@ -173,8 +214,19 @@ class RecommenderService:
         return self._impute(self.intf, request.index)
 
     def ExportTable(self, request: Any, context: Any) -> Any:
-        slot = self.conf if request.table in ("", "configurations") else self.intf
         out = P.Table()
+        if request.table == "corun":
+            m = self.corun.get()
+            if m is None:
+                return out
+            out.columns.extend(m.table_columns())
+            out.version = self.corun.version or ""
+            for lab, vals in zip(m.names, m.table_rows()):
+                r = out.rows.add()
+                r.index = lab
+                r.values.extend(float(v) for v in vals)
+            return out
+        slot = self.conf if request.table in ("", "configurations") else self.intf
         t = slot.get()
         if t is None:
             return out

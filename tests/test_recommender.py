@@ -392,3 +392,31 @@ def test_online_table_survives_recommender_restart(ref_data, tmp_path):
     c2.store = store
     c2.train()
     assert not c2.intf.version.startswith("online-")
+
+
+def test_recommender_serves_the_corun_model_and_hot_reloads_it(ref_data, tmp_path):
+    """ExportTable("corun") serves the multi-way co-run model (models.corun) the GPU plugin's
+    co-run objective uses; a changed model file reaches a CachedPredictions without restarts."""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.models.corun import DATA, CorunModel
+    conf, intf = ref_data
+    cm = tmp_path / "corun.json"
+    shutil.copy(DATA, cm)
+    svc = RecommenderService(str(conf), str(intf), job_delay_s=0.2, corun_path=str(cm))
+    svc.train()
+    srv, port = svc.make_server(0, 2, "127.0.0.1")
+    try:
+        cache = CachedPredictions(RecommenderClient(f"127.0.0.1:{port}"), background=False)
+        cache.refresh(force=True)
+        m, ref = cache.corun(), CorunModel.load(str(cm))
+        assert m is not None and m.names == ref.names
+        assert np.allclose(m.coupling(), ref.coupling(), rtol=1e-6) and np.allclose(m.alone_ms, ref.alone_ms)
+        v0 = m.version
+        ref2 = CorunModel(ref.names, ref.alone_ms * 1.1, ref.u, ref.v, dict(ref.meta, version="refit-x"))
+        ref2.save(str(cm))
+        svc.train()
+        cache.refresh(force=True)
+        assert cache.corun().version != v0 and np.allclose(cache.corun().alone_ms, ref.alone_ms * 1.1)
+    finally:
+        svc.stop()
+        srv.stop(0)
