@@ -63,6 +63,21 @@ class RecommenderClient:
     def version(self) -> Any:
         return self._call(f"/{P.EXT_SERVICE}/Version", P.Empty())
 
+    def observe_corun(self, groups: List[Dict[str, Any]]) -> Any:
+        """Send co-run groups (dicts: workloads, iters, ms[, start_ms, target]) for the
+        recommender's online co-run model (ExportTable("corun") then serves the refined one)."""
+        req = P.ObserveCorunRequest()
+        for g in groups:
+            x = req.groups.add()
+            x.workloads.extend(g["workloads"])
+            x.iters.extend(float(v) for v in g["iters"])
+            x.ms.extend(float(v) for v in g["ms"])
+            if g.get("start_ms") is not None:
+                x.start_ms.extend(float(v) for v in g["start_ms"])
+            if g.get("target") is not None:
+                x.target.extend(bool(v) for v in g["target"])
+        return self._call(f"/{P.EXT_SERVICE}/ObserveCorun", req)
+
     def observe_interference(self, observations: List[Tuple[str, List[str], float]]) -> Any:
         """Send (pod, co-runner pods, throughput loss) observations for online learning."""
         req = P.ObserveRequest()

@@ -14,7 +14,8 @@ Wire-identical to the reference's proto (reference pkg/recommender/protos/recom.
 FileDescriptorProto is assembled here and message classes come from the descriptor pool.
 A second service, `gpusched.recommender.Extended`, adds what the MI355X build needs
 (bulk table export for the in-process prediction cache, resource-resize advice, model
-version, co-run observations for online interference learning) without touching the
+version, co-run observations for online interference learning, co-run groups for the online
+co-run model) without touching the
 reference API.
 """
 from __future__ import annotations
@@ -67,6 +68,7 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
     _field(ver, "configurations", 1, _F.TYPE_STRING)
     _field(ver, "interference", 2, _F.TYPE_STRING)
     _field(ver, "model", 3, _F.TYPE_STRING)
+    _field(ver, "corun", 4, _F.TYPE_STRING)              # co-run model version served
     emp = fx.message_type.add(name="Empty")
     del emp
     cr = fx.message_type.add(name="CoRun")                # one pod's co-run observation
@@ -79,6 +81,18 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
     _field(orp, "accepted", 1, _F.TYPE_INT32)
     _field(orp, "interference", 2, _F.TYPE_STRING)       # interference table version now served
     _field(orp, "observations", 3, _F.TYPE_INT32)        # total learned so far
+    cg = fx.message_type.add(name="CorunGroup")          # one GPU's co-running pods (models.corun)
+    _field(cg, "workloads", 1, _F.TYPE_STRING, _F.LABEL_REPEATED)     # pod or workload names
+    _field(cg, "iters", 2, _F.TYPE_FLOAT, _F.LABEL_REPEATED)
+    _field(cg, "start_ms", 3, _F.TYPE_FLOAT, _F.LABEL_REPEATED)       # start offsets in the group
+    _field(cg, "ms", 4, _F.TYPE_FLOAT, _F.LABEL_REPEATED)             # measured wall ms
+    _field(cg, "target", 5, _F.TYPE_BOOL, _F.LABEL_REPEATED)          # observation (else co-runner only)
+    ocq = fx.message_type.add(name="ObserveCorunRequest")
+    _field(ocq, "groups", 1, _F.TYPE_MESSAGE, _F.LABEL_REPEATED, ".gpusched.recommender.CorunGroup")
+    ocp = fx.message_type.add(name="ObserveCorunReply")
+    _field(ocp, "accepted", 1, _F.TYPE_INT32)
+    _field(ocp, "corun", 2, _F.TYPE_STRING)              # co-run model version now served
+    _field(ocp, "observations", 3, _F.TYPE_INT32)
     s2 = fx.service.add(name="Extended")
     s2.method.add(name="ExportTable", input_type=".gpusched.recommender.TableRequest",
                   output_type=".gpusched.recommender.Table")
@@ -88,6 +102,8 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
                   output_type=".gpusched.recommender.VersionReply")
     s2.method.add(name="ObserveInterference", input_type=".gpusched.recommender.ObserveRequest",
                   output_type=".gpusched.recommender.ObserveReply")
+    s2.method.add(name="ObserveCorun", input_type=".gpusched.recommender.ObserveCorunRequest",
+                  output_type=".gpusched.recommender.ObserveCorunReply")
     pool.Add(fx)
     return pool
 
@@ -111,6 +127,9 @@ Empty = _cls("gpusched.recommender.Empty")
 CoRun = _cls("gpusched.recommender.CoRun")
 ObserveRequest = _cls("gpusched.recommender.ObserveRequest")
 ObserveReply = _cls("gpusched.recommender.ObserveReply")
+CorunGroup = _cls("gpusched.recommender.CorunGroup")
+ObserveCorunRequest = _cls("gpusched.recommender.ObserveCorunRequest")
+ObserveCorunReply = _cls("gpusched.recommender.ObserveCorunReply")
 
 SERVICE = "recommender.recommender"
 EXT_SERVICE = "gpusched.recommender.Extended"
@@ -121,6 +140,7 @@ METHODS: Dict[str, Any] = {
     f"/{EXT_SERVICE}/RecommendResources": (ResizeRequest, ResizeReply),
     f"/{EXT_SERVICE}/Version": (Empty, VersionReply),
     f"/{EXT_SERVICE}/ObserveInterference": (ObserveRequest, ObserveReply),
+    f"/{EXT_SERVICE}/ObserveCorun": (ObserveCorunRequest, ObserveCorunReply),
 }
 
 

@@ -137,6 +137,12 @@ class CorunSlot:
         with self._lock:
             return self.model
 
+    def serve(self, model: Any, version: str) -> None:
+        """Serve an online-refined model (the file bookkeeping is untouched: a changed file
+        is loaded again and replaces it)."""
+        with self._lock:
+            self.model, self.version = model, version
+
 
 class RecommenderService:
     def __init__(self, configurations_path: str = "", interference_path: str = "",
@@ -146,6 +152,9 @@ class RecommenderService:
         self.conf = ModelSlot("configurations", configurations_path, kind)
         self.intf = ModelSlot("interference", interference_path, kind)
         self.corun = CorunSlot(corun_path)
+        self._corun_online: Any = None      # models.corun.OnlineCorun on the served file model
+        self._corun_online_base: Optional[str] = None
+        self._corun_refit_mode: Any = "process"
         self.job_delay_s = job_delay_s
         self.history_source = history_source
         self.model = model
@@ -318,9 +327,44 @@ class RecommenderService:
         log.info("interference: restored online table %s", d["version"])
         return True
 
+    def ObserveCorun(self, request: Any, context: Any) -> Any:
+        """Online co-run learning (models.corun.OnlineCorun, refits in a worker process): each
+        group is one GPU's co-running pods with their measured wall ms; the refined model is
+        served through ExportTable("corun") under version `<file version>+online-N` until
+        the model file changes."""
+        from ..models.corun import OnlineCorun
+        reply = P.ObserveCorunReply()
+        with self._online_lock:
+            if self.corun.file_version is None:
+                self.corun.load_if_changed()
+            base = self.corun.get()
+            if base is None:
+                return reply
+            if self._corun_online is None or self._corun_online_base != self.corun.file_version:
+                # the served model may already be an online one: learn on the file's model
+                from ..models.corun import CorunModel
+                fm = CorunModel.load(self.corun.path) if self.corun.path else base
+                self._corun_online = OnlineCorun(fm or base, background=self._corun_refit_mode)
+                self._corun_online_base = self.corun.file_version
+            on = self._corun_online
+            for g in request.groups:
+                w = [base.wid(n) for n in g.workloads]
+                k = len(w)
+                if not k or min(w) < 0 or len(g.ms) != k or len(g.iters) != k:
+                    continue
+                st = list(g.start_ms) if len(g.start_ms) == k else None
+                tg = list(g.target) if len(g.target) == k else None
+                on.observe_group(w, list(g.iters), list(g.ms), st, tg)
+                reply.accepted += 1
+            if on.model is not self.corun.get() and on.refits:
+                self.corun.serve(on.model, f"{self.corun.version.split('+')[0]}+online-{on.version}")
+            reply.corun = self.corun.version or ""
+            reply.observations = int(on.err["n"])
+        return reply
+
     def Version(self, request: Any, context: Any) -> Any:
         return P.VersionReply(configurations=self.conf.version or "", interference=self.intf.version or "",
-                              model=self.conf.kind)
+                              model=self.conf.kind, corun=self.corun.version or "")
 
     # ------------------------------------------------------------------ server
     def make_server(self, port: int = C.RECOMMENDER_PORT, workers: int = C.RECOMMENDER_WORKERS,
@@ -332,7 +376,8 @@ class RecommenderService:
             P.generic_handler(P.EXT_SERVICE, {"ExportTable": self.ExportTable,
                                               "RecommendResources": self.RecommendResources,
                                               "Version": self.Version,
-                                              "ObserveInterference": self.ObserveInterference}),
+                                              "ObserveInterference": self.ObserveInterference,
+                                              "ObserveCorun": self.ObserveCorun}),
         ))
         bound = server.add_insecure_port(f"{host}:{port}")
         server.start()

@@ -420,3 +420,40 @@ def test_recommender_serves_the_corun_model_and_hot_reloads_it(ref_data, tmp_pat
     finally:
         svc.stop()
         srv.stop(0)
+
+
+def test_observe_corun_rpc_serves_a_refined_model(ref_data, tmp_path):
+    """Extended.ObserveCorun: co-run groups measured on the cluster refine the co-run model
+    (models.corun.OnlineCorun) and ExportTable("corun") serves the refined version."""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.models.corun import DATA, CorunModel
+    conf, intf = ref_data
+    cm = tmp_path / "corun.json"
+    shutil.copy(DATA, cm)
+    svc = RecommenderService(str(conf), str(intf), corun_path=str(cm))
+    svc._corun_refit_mode = False                      # refit synchronously in the test
+    svc.train()
+    srv, port = svc.make_server(0, 2, "127.0.0.1")
+    try:
+        cl = RecommenderClient(f"127.0.0.1:{port}")
+        base = CorunModel.load(str(cm))
+        slow = CorunModel(base.names, base.alone_ms * 1.25, base.u, base.v)      # the cluster runs 25 % slower
+        rng = np.random.default_rng(5)
+        v0 = cl.version().corun
+        for _ in range(6):
+            groups = []
+            for _ in range(60):
+                ws = [int(x) for x in rng.integers(0, len(base.names), 4)]
+                groups.append({"workloads": [base.names[w] for w in ws], "iters": [20] * 4,
+                               "ms": list(slow.group_durations(ws, [20] * 4))})
+            rep = cl.observe_corun(groups)
+            assert rep.accepted == 60
+        assert rep.corun != v0 and "+online-" in rep.corun and cl.version().corun == rep.corun
+        cache = CachedPredictions(cl, background=False)
+        cache.refresh(force=True)
+        m = cache.corun()
+        assert m.version == rep.corun
+        assert np.allclose(m.alone_ms / base.alone_ms, 1.25, rtol=0.05)
+    finally:
+        svc.stop()
+        srv.stop(0)
