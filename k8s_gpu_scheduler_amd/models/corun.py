@@ -53,40 +53,48 @@ MAXK = 8                      # pods per GPU the vectorised simulator handles (8
 
 
 # ----------------------------------------------------------------------------- simulator
-def simulate(work: np.ndarray, coup: np.ndarray, mask: np.ndarray, start: Optional[np.ndarray] = None) -> np.ndarray:
+def simulate(work: np.ndarray, coup: np.ndarray, mask: np.ndarray, start: Optional[np.ndarray] = None,
+             pin_end: Optional[np.ndarray] = None) -> np.ndarray:
     """Wall time at which each pod of each group finishes (same units as `work`).
 
     work [G, K] >= 0, coup [G, K, K] (u_i . v_j; the diagonal is ignored), mask [G, K] bool,
-    start [G, K] (None = all start at 0).  Returns finish times [G, K] (0 where masked out)."""
+    start [G, K] (None = all start at 0), pin_end [G, K] (None: none pinned; a member with
+    pin_end > start is present exactly in [start, pin_end) and not simulated -- a co-runner
+    whose interval was measured; native sim_group documents why).  Returns finish times
+    [G, K] (0 where masked out)."""
     G, K = work.shape
-    rem = np.where(mask, np.maximum(work, 1e-12), 0.0).astype(np.float64)
     c = coup * (1.0 - np.eye(K))[None]
     st = np.zeros((G, K)) if start is None else np.where(mask, start, 0.0).astype(np.float64)
+    pin = np.zeros((G, K), bool) if pin_end is None else mask & (pin_end > st)
+    pe = np.where(pin, pin_end if pin_end is not None else 0.0, 0.0)
+    rem = np.where(mask & ~pin, np.maximum(work, 1e-12), 0.0).astype(np.float64)
     done = ~mask.copy()
     started = np.zeros((G, K), bool)
     now = np.zeros(G)
-    fin = np.zeros((G, K))
+    fin = np.where(pin, pe, 0.0)
     big = 1e30
-    for _ in range(2 * K + 1):
-        live = ~done.all(axis=1)
+    for _ in range(3 * K + 1):
+        live = (~done & ~pin).any(axis=1)
         if not live.any():
             break
         started = started | ((st <= now[:, None] + 1e-12) & mask)
+        done = done | (pin & started & (pe <= now[:, None] + 1e-12))
         act = started & ~done
         load = 1.0 + np.einsum("gij,gj->gi", c, act.astype(np.float64))
-        rate = np.where(act, 1.0 / load, 0.0)
-        t_fin = np.where(act, rem / np.maximum(rate, 1e-30), big)
+        rate = np.where(act & ~pin, 1.0 / load, 0.0)
+        t_fin = np.where(act & ~pin, rem / np.maximum(rate, 1e-30), big)
         t_arr = np.where(mask & ~started, st - now[:, None], big)
-        dt = np.minimum(t_fin.min(axis=1), t_arr.min(axis=1))
+        t_pin = np.where(act & pin, pe - now[:, None], big)
+        dt = np.minimum(np.minimum(t_fin.min(axis=1), t_arr.min(axis=1)), t_pin.min(axis=1))
         dt = np.where(live, dt, 0.0)
         rem = rem - rate * dt[:, None]
         now = now + dt
-        newly = act & (rem <= 1e-9 * np.maximum(work, 1.0))
+        newly = act & ~pin & (rem <= 1e-9 * np.maximum(work, 1.0))
         # the argmin pod always finishes (guards rounding)
         am = np.argmin(t_fin, axis=1)
-        hit = (t_fin[np.arange(G), am] <= dt + 1e-12) & live
+        hit = (t_fin[np.arange(G), am] <= dt + 1e-12) & live & (t_fin[np.arange(G), am] < big)
         newly[np.arange(G)[hit], am[hit]] = True
-        fin = np.where(newly, now[:, None], fin)
+        fin = np.where(newly & ~pin, now[:, None], fin)
         done = done | newly
     return fin
 
@@ -205,8 +213,9 @@ class CorunModel:
 
     # -- prediction
     def group_times(self, wids: Sequence[int], iters: Sequence[float],
-                    starts: Optional[Sequence[float]] = None) -> np.ndarray:
-        """Predicted wall ms of each pod of ONE group (wids >= 0)."""
+                    starts: Optional[Sequence[float]] = None, pin_end: Optional[Sequence[float]] = None) -> np.ndarray:
+        """Predicted wall ms of each pod of ONE group (wids >= 0); pin_end: members with a
+        measured end (> their start) are present as measured and not simulated."""
         k = len(wids)
         if k == 0:
             return np.zeros(0)
@@ -214,17 +223,19 @@ class CorunModel:
         core = _native_core()
         if core is not None and k <= 64:         # ~20x faster than the numpy event loop for one group
             st = np.zeros((1, k)) if starts is None else np.asarray(starts, dtype=np.float64).reshape(1, k)
+            pe = None if pin_end is None else np.asarray(pin_end, np.float64).reshape(1, k)
             return core.corun_times(w.astype(np.int32).reshape(1, k), np.asarray(iters, np.float64).reshape(1, k),
-                                    np.ones((1, k), np.uint8), st, self.alone_ms, self._cmat)[0]
+                                    np.ones((1, k), np.uint8), st, self.alone_ms, self._cmat, pe)[0]
         work = (self.alone_ms[w] * np.asarray(iters, dtype=np.float64))[None]
         coup = self._cmat[np.ix_(w, w)][None]
         st = None if starts is None else np.asarray(starts, dtype=np.float64)[None]
-        return simulate(work, coup, np.ones((1, k), bool), st)[0]
+        pe = None if pin_end is None else np.asarray(pin_end, np.float64)[None]
+        return simulate(work, coup, np.ones((1, k), bool), st, pe)[0]
 
     def group_durations(self, wids: Sequence[int], iters: Sequence[float],
-                        starts: Optional[Sequence[float]] = None) -> np.ndarray:
+                        starts: Optional[Sequence[float]] = None, pin_end: Optional[Sequence[float]] = None) -> np.ndarray:
         """Predicted wall ms each pod runs (finish - its own start)."""
-        t = self.group_times(wids, iters, starts)
+        t = self.group_times(wids, iters, starts, pin_end)
         return t - (np.asarray(starts, dtype=np.float64) if starts is not None else 0.0)
 
     def group_tput(self, wids: Sequence[int], iters: Sequence[float],
@@ -233,16 +244,17 @@ class CorunModel:
         return np.asarray(iters, dtype=np.float64) / np.maximum(t, 1e-9) * 1e3
 
     def batch_times(self, wids: np.ndarray, iters: np.ndarray, mask: np.ndarray,
-                    starts: Optional[np.ndarray] = None) -> np.ndarray:
+                    starts: Optional[np.ndarray] = None, pin_end: Optional[np.ndarray] = None) -> np.ndarray:
         core = _native_core()
         if core is not None and wids.shape[1] <= 64:
             st = np.zeros(wids.shape) if starts is None else starts
+            pe = None if pin_end is None else np.asarray(pin_end, np.float64)
             return core.corun_times(np.where(mask, wids, 0).astype(np.int32), iters.astype(np.float64),
-                                    mask.astype(np.uint8), st.astype(np.float64), self.alone_ms, self._cmat)
+                                    mask.astype(np.uint8), st.astype(np.float64), self.alone_ms, self._cmat, pe)
         w = np.where(mask, wids, 0)
         work = self.alone_ms[w] * iters
         coup = self._cmat[w[:, :, None], w[:, None, :]]
-        return simulate(work, coup, mask, starts)
+        return simulate(work, coup, mask, starts, pin_end)
 
     def alone_tput(self, wid: int) -> float:
         return 1e3 / self.alone_ms[wid]
@@ -269,6 +281,35 @@ def pack_groups(groups: List[Dict[str, Any]], names: Sequence[str], K: int = 4
     return wids, iters, mask, ms, st
 
 
+def pack_targets(groups: List[Dict[str, Any]], K: int) -> np.ndarray:
+    """[G, K] bool: which members' times are observations (a group's "target" list; default
+    all -- a timeline group also carries co-runners that only shape the others' rates)."""
+    out = np.zeros((len(groups), K), bool)
+    for g, d in enumerate(groups):
+        t = d.get("target")
+        for k in range(min(len(d["w"]), K)):
+            out[g, k] = bool(t[k]) if t is not None else True
+    return out
+
+
+def timeline_groups(pods: Sequence[Sequence[Any]], iters: int = 20) -> List[Dict[str, Any]]:
+    """Co-run groups from a bench timeline (GPUSCHED_BENCH_TRACE rows of ONE GPU: epoch, slot,
+    workload, start ms, end ms, ...): per epoch, its pods are the targets and every pod whose
+    interval overlaps theirs is a member, at its real start offset -- the continuous-pipeline
+    setting the isolated collection groups do not cover."""
+    by: Dict[int, List[Sequence[Any]]] = {}
+    for r in pods:
+        by.setdefault(int(r[0]), []).append(r)
+    out = []
+    for e, tgt in sorted(by.items()):
+        lo, hi = min(r[3] for r in tgt), max(r[4] for r in tgt)
+        mem = [r for rs in by.values() for r in rs if r[4] > lo and r[3] < hi]
+        t0 = min(r[3] for r in mem)
+        out.append({"w": [r[2] for r in mem], "iters": iters, "ms": [float(r[4] - r[3]) for r in mem],
+                    "start": [float(r[3] - t0) for r in mem], "target": [any(r is x for x in tgt) for r in mem]})
+    return out
+
+
 def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, ridge: float = 0.05,
         max_nfev: int = 400, holdout: float = 0.2, seed: int = 0) -> Tuple[CorunModel, Dict[str, Any]]:
     """Fit alone times (median of 1-pod groups) and u, v (2 x 18 each, log-parameterised)
@@ -292,6 +333,10 @@ def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, rid
     K = max(len(d["w"]) for d in multi)
     tr = pack_groups(train, names, K)
     te = pack_groups(test, names, K)
+    tg_tr, tg_te = pack_targets(train, K), pack_targets(test, K)
+    # timeline groups: co-runners that are not observations are pinned to their measured span
+    pin_tr = np.where(tr[2] & ~tg_tr & (tr[3] > 0), tr[4] + tr[3], 0.0)
+    pin_te = np.where(te[2] & ~tg_te & (te[3] > 0), te[4] + te[3], 0.0)
     n_w, R = len(names), prior.u.shape[1]
     x0 = np.log(np.concatenate([np.maximum(prior.u, 1e-3).ravel(), np.maximum(prior.v, 1e-3).ravel()]))
     x_prior = x0.copy()
@@ -304,8 +349,8 @@ def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, rid
         u, v = unpack(x)
         m = CorunModel(names, a_ms, u, v)
         wids, iters, mask, ms, st = data
-        t = m.batch_times(wids, iters, mask, st) - st      # durations: finish - own start
-        r = np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[mask]
+        t = m.batch_times(wids, iters, mask, st, pin_tr if data is tr else pin_te) - st   # durations
+        r = np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[mask & (tg_tr if data is tr else tg_te)]
         return r
 
     def obj(x):
@@ -319,7 +364,8 @@ def fit(groups: List[Dict[str, Any]], names: Optional[Sequence[str]] = None, rid
 
     def tput_err(m: CorunModel, data) -> Dict[str, float]:
         wids, iters, mask, ms, st = data
-        t = m.batch_times(wids, iters, mask, st) - st
+        mask = mask & (tg_tr if data is tr else tg_te)
+        t = m.batch_times(wids, iters, data[2], st, pin_tr if data is tr else pin_te) - st
         tp = iters / np.maximum(t, 1e-9) * 1e3
         tm = iters / np.maximum(ms, 1e-9) * 1e3
         e = np.abs(tp - tm)[mask]
@@ -389,8 +435,11 @@ class OnlineCorun:
             return False
         st = [float(x) for x in starts] if starts is not None else [0.0] * k
         tg = [bool(x) for x in targets] if targets is not None else [True] * k
-        t_on = self.model.group_durations(wids, iters, st)
-        t_pr = self.base.group_durations(wids, iters, st)
+        # co-runners that are not observations are present as measured (pinned): the targets
+        # are predicted given what their co-runners really did
+        pin = None if all(tg) else [0.0 if t or m <= 0 else s + m for t, s, m in zip(tg, st, ms)]
+        t_on = self.model.group_durations(wids, iters, st, pin)
+        t_pr = self.base.group_durations(wids, iters, st, pin)
         start_refit = False
         with self._lock:
             for i in range(k):
@@ -433,8 +482,9 @@ class OnlineCorun:
             wids[g, :k], iters[g, :k], st[g, :k], ms[g, :k], tgt[g, :k] = w, it, s, m, t
             mask[g, :k] = True
         b = self.base
+        pin = np.where(mask & ~tgt & (ms > 0), st + ms, 0.0)
         return {"names": b.names, "alone_ms": b.alone_ms, "u": b.u, "v": b.v, "wids": wids, "iters": iters,
-                "mask": mask, "tgt": tgt, "ms": ms, "st": st, "x": self._x, "ridge": self.ridge,
+                "mask": mask, "tgt": tgt, "ms": ms, "st": st, "pin": pin, "x": self._x, "ridge": self.ridge,
                 "max_nfev": self.max_nfev, "stage2": self.err["n"] >= self.min_obs}
 
     def _refit(self, obs) -> None:
@@ -496,8 +546,10 @@ def solve_refit(p: Dict[str, Any]) -> Dict[str, Any]:
     def model_of(x, scale=1.0):
         return CorunModel(names, alone * np.exp(x[:n_w]) * scale, u * np.exp(x[n_w]), v)
 
+    pin = p.get("pin")
+
     def resid(model, sel):
-        t = model.batch_times(wids, iters, mask, st) - st
+        t = model.batch_times(wids, iters, mask, st, pin) - st
         return np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[sel]
 
     x0 = np.asarray(p["x"], dtype=np.float64)

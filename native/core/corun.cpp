@@ -30,31 +30,40 @@ constexpr int kMaxK = 64;   // pods per GPU group (CPX: 64 devices of 4 CUs woul
 
 // fin[i] = wall ms at which pod i finishes (kBig for a service pod); tput_ms[i] = ms per
 // iteration achieved (fin / iters, or the steady-state ms/iter of a service pod).
+// pin_end (optional): a member with pin_end[i] > start[i] is PINNED -- present exactly during
+// [start, pin_end) (a co-runner whose interval was measured), pressing on the others but not
+// simulated itself; fin[i] = pin_end[i].  Learning from a pipeline's timeline conditions the
+// observed pods on what their co-runners really did, instead of re-simulating co-runners whose
+// own (earlier) co-runners lie outside the observed window.
 void sim_group(int k, const int32_t* w, const double* iters, const double* start, const double* alone,
-               const double* C, int W, double* fin) {
-  double rem[kMaxK], st[kMaxK];
-  bool started[kMaxK], done[kMaxK], svc[kMaxK];
+               const double* C, int W, double* fin, const double* pin_end = nullptr) {
+  double rem[kMaxK], st[kMaxK], pe[kMaxK];
+  bool started[kMaxK], done[kMaxK], svc[kMaxK], pin[kMaxK];
   for (int i = 0; i < k; ++i) {
     svc[i] = iters[i] <= 0;
-    rem[i] = svc[i] ? kBig : std::max(alone[w[i]] * iters[i], 1e-12);
     st[i] = start ? start[i] : 0.0;
+    pin[i] = pin_end && pin_end[i] > st[i];
+    pe[i] = pin[i] ? pin_end[i] : 0.0;
+    rem[i] = (svc[i] || pin[i]) ? kBig : std::max(alone[w[i]] * iters[i], 1e-12);
     started[i] = done[i] = false;
-    fin[i] = svc[i] ? kBig : 0.0;
+    fin[i] = pin[i] ? pe[i] : svc[i] ? kBig : 0.0;
   }
   double now = 0.0;
-  for (int step = 0; step < 2 * k + 1; ++step) {
+  for (int step = 0; step < 3 * k + 1; ++step) {
     bool live = false;
-    for (int i = 0; i < k; ++i) live |= !done[i] && !svc[i];
+    for (int i = 0; i < k; ++i) live |= !done[i] && !svc[i] && !pin[i];
     if (!live) break;
     for (int i = 0; i < k; ++i)
       if (!started[i] && st[i] <= now + 1e-12) started[i] = true;
+    for (int i = 0; i < k; ++i)
+      if (pin[i] && started[i] && !done[i] && pe[i] <= now + 1e-12) done[i] = true;
     double rate[kMaxK];
     double dt = kBig;
     int am = -1;
     double am_t = kBig;
     for (int i = 0; i < k; ++i) {
       rate[i] = 0.0;
-      if (!started[i] || done[i]) continue;
+      if (!started[i] || done[i] || pin[i]) continue;
       double load = 1.0;
       const double* ci = C + (size_t)w[i] * W;
       for (int j = 0; j < k; ++j)
@@ -66,13 +75,15 @@ void sim_group(int k, const int32_t* w, const double* iters, const double* start
       }
     }
     dt = am_t;
-    for (int i = 0; i < k; ++i)
+    for (int i = 0; i < k; ++i) {
       if (!started[i]) dt = std::min(dt, st[i] - now);
+      else if (pin[i] && !done[i]) dt = std::min(dt, pe[i] - now);
+    }
     for (int i = 0; i < k; ++i)
-      if (started[i] && !done[i] && !svc[i]) rem[i] -= rate[i] * dt;
+      if (started[i] && !done[i] && !svc[i] && !pin[i]) rem[i] -= rate[i] * dt;
     now += dt;
     for (int i = 0; i < k; ++i) {
-      if (!started[i] || done[i] || svc[i]) continue;
+      if (!started[i] || done[i] || svc[i] || pin[i]) continue;
       const double wk = alone[w[i]] * iters[i];
       if (rem[i] <= 1e-9 * std::max(wk, 1.0) || (i == am && am_t <= dt + 1e-12)) {
         done[i] = true;
@@ -153,7 +164,7 @@ void check_wids(const int32_t* w, py::ssize_t n, int W, const char* what) {
 
 // Batch simulation: groups of up to K pods (mask selects members); returns finish ms [G, K]
 // (0 where masked out, 1e300 for service pods).
-py::array_t<double> corun_times(I32 wids, F64 iters, U8 mask, F64 starts, F64 alone, F64 cmat) {
+py::array_t<double> corun_times(I32 wids, F64 iters, U8 mask, F64 starts, F64 alone, F64 cmat, py::object pin_end) {
   int W;
   check_model(alone, cmat, W);
   if (wids.ndim() != 2) throw std::runtime_error("corun_times: wids must be [G, K]");
@@ -162,6 +173,14 @@ py::array_t<double> corun_times(I32 wids, F64 iters, U8 mask, F64 starts, F64 al
       starts.shape(0) != G || starts.shape(1) != K)
     throw std::runtime_error("corun_times: array shapes differ");
   if (K > kMaxK) throw std::runtime_error("corun_times: more than 64 pods per group");
+  F64 pin_a;
+  const double* pp = nullptr;
+  if (!pin_end.is_none()) {
+    pin_a = pin_end.cast<F64>();
+    if (pin_a.ndim() != 2 || pin_a.shape(0) != G || pin_a.shape(1) != K)
+      throw std::runtime_error("corun_times: pin_end must be [G, K]");
+    pp = pin_a.data();
+  }
   py::array_t<double> out({G, K});
   const int32_t* wp = wids.data();
   const double* ip = iters.data();
@@ -174,7 +193,7 @@ py::array_t<double> corun_times(I32 wids, F64 iters, U8 mask, F64 starts, F64 al
     py::gil_scoped_release nogil;
     for (py::ssize_t g = 0; g < G; ++g) {
       int32_t w[kMaxK];
-      double it[kMaxK], st[kMaxK], fin[kMaxK];
+      double it[kMaxK], st[kMaxK], fin[kMaxK], pe[kMaxK];
       int idx[kMaxK], k = 0;
       for (py::ssize_t j = 0; j < K; ++j) {
         op[g * K + j] = 0.0;
@@ -184,9 +203,10 @@ py::array_t<double> corun_times(I32 wids, F64 iters, U8 mask, F64 starts, F64 al
         w[k] = x;
         it[k] = ip[g * K + j];
         st[k] = sp[g * K + j];
+        pe[k] = pp ? pp[g * K + j] : 0.0;
         idx[k++] = (int)j;
       }
-      sim_group(k, w, it, st, A, Cm, W, fin);
+      sim_group(k, w, it, st, A, Cm, W, fin, pp ? pe : nullptr);
       for (int i = 0; i < k; ++i) op[g * K + idx[i]] = fin[i];
     }
   }
@@ -433,7 +453,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
 
 void register_corun(py::module_& m) {
   m.def("corun_times", &corun_times, py::arg("wids"), py::arg("iters"), py::arg("mask"), py::arg("starts"),
-        py::arg("alone_ms"), py::arg("cmat"));
+        py::arg("alone_ms"), py::arg("cmat"), py::arg("pin_end") = py::none());
   m.def("corun_gpu_eval", &corun_gpu_eval, py::arg("off"), py::arg("r_wid"), py::arg("r_iters"), py::arg("r_slo"),
         py::arg("x_wid"), py::arg("x_iters"), py::arg("x_slo"), py::arg("cand_gpu"), py::arg("alone_ms"),
         py::arg("cmat"));

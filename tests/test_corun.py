@@ -40,6 +40,38 @@ def test_simulator_is_processor_sharing_with_unit_coupling():
     assert np.allclose(fin, [[4.0, 0.0]])
 
 
+def test_pinned_co_runner_is_present_exactly_as_measured():
+    # target: 10 ms of work; a co-runner pinned to [0, 4): the target runs at 1/2 for 4 ms
+    # (2 ms of work), then alone: finishes at 4 + 8 = 12; the pinned member "finishes" at 4
+    coup = np.ones((1, 2, 2))
+    fin = CR.simulate(np.array([[10.0, 999.0]]), coup, np.ones((1, 2), bool), np.array([[0.0, 0.0]]),
+                      np.array([[0.0, 4.0]]))
+    assert np.allclose(fin, [[12.0, 4.0]])
+    # a pinned member present in [2, 6) presses only then: 2 ms alone, 4 ms at 1/2, 6 ms alone
+    fin = CR.simulate(np.array([[10.0, 1.0]]), coup, np.ones((1, 2), bool), np.array([[0.0, 2.0]]),
+                      np.array([[0.0, 6.0]]))
+    assert np.allclose(fin, [[12.0, 6.0]])
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_native_simulation_matches_numpy_with_pinned_members():
+    rng = np.random.default_rng(4)
+    m = CR.CorunModel.load()
+    G, K = 200, 8
+    wids = rng.integers(0, len(m.names), (G, K))
+    iters = np.full((G, K), 20.0)
+    mask = rng.random((G, K)) < 0.9
+    mask[:, 0] = True
+    starts = rng.random((G, K)) * 4.0
+    starts[:, 0] = 0.0
+    pin = np.where(rng.random((G, K)) < 0.5, starts + rng.random((G, K)) * 10.0 + 0.1, 0.0)
+    pin[:, 0] = 0.0                                  # at least one simulated member
+    nat = m.batch_times(wids, iters, mask, starts, pin)
+    w = np.where(mask, wids, 0)
+    ref = CR.simulate(m.alone_ms[w] * iters, m.coupling()[w[:, :, None], w[:, None, :]], mask, starts, pin)
+    assert np.allclose(nat[mask], ref[mask], rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.skipif(not has_core, reason="_core not built")
 def test_native_simulation_matches_numpy():
     rng = np.random.default_rng(0)
