@@ -127,6 +127,7 @@ def pipelined_ms(t: np.ndarray, lookahead: int) -> float:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=8, help="GPUs of the virtual node")
     ap.add_argument("--epochs", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
@@ -135,6 +136,8 @@ def main() -> None:
     ap.add_argument("--policies", nargs="+", default=["greedy", "corun", "corun_plan_t10", "random"],
                     choices=sorted(POLICIES))
     a = ap.parse_args()
+    global N_GPUS
+    N_GPUS = a.gpus
     policies = {k: POLICIES[k] for k in a.policies}
     cps = {k: ControlPlane(n_gpus=N_GPUS, pods_per_gpu=4, iters=20, seed=a.seed, **kw) for k, kw in policies.items()}
     ex = DeviceExecutor(0, use_cu_masks=True)
@@ -158,7 +161,7 @@ def main() -> None:
     for k, st in stats.items():
         mx, mn = statistics.mean(st["max_ms"]), statistics.mean(st["mean_ms"])
         out[k] = {"epoch_ms_slowest_gpu": round(mx, 3), "epoch_ms_mean_gpu": round(mn, 3),
-                  "imbalance": round(mx / mn, 4), "pods_per_s_8gpu_coupled": round(4 * N_GPUS / mx * 1e3, 1),
+                  "imbalance": round(mx / mn, 4), "pods_per_s_coupled": round(4 * N_GPUS / mx * 1e3, 1),
                   "slo_attainment_pct": round(100.0 * st["ok"] / max(st["n"], 1), 2), "pods": st["n"],
                   "interference_mae": cps[k].interference_mae(),
                   "epoch_ms_pipelined_l2": round(pipelined_ms(np.array(st["walls"]), 2), 3),
@@ -169,8 +172,8 @@ def main() -> None:
     if a.dump_groups:
         json.dump(GROUPS, open(a.dump_groups, "w"))
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
-    json.dump({"note": "each virtual GPU's 4 pods co-run on the one real MI355X in turn; coupled 8-GPU epoch = "
-                       "slowest group; policies interleaved per epoch, same seed", "epochs": a.epochs,
+    json.dump({"note": "each virtual GPU's 4 pods co-run on the one real MI355X in turn; coupled N-GPU epoch = "
+                       "slowest group; policies interleaved per epoch, same seed", "gpus": N_GPUS, "epochs": a.epochs,
                "results": out}, open(a.out, "w"), indent=1)
 
 
