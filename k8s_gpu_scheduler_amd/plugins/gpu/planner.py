@@ -32,6 +32,12 @@ runs and how asymmetric the contention is.  Phase A balances the predicted group
 (the slowest GPU paces a coupled multi-GPU epoch), phase B then maximises the number of
 pods -- burst and residents -- predicted to meet their SLO without letting any GPU's
 makespan exceed (1 + planTolerance) x the balanced plan's longest.
+
+With `planCarry` > 0 the planner also remembers how much predicted work each GPU took in
+earlier bursts beyond the least-loaded GPU (its backlog, decayed by planCarry per burst) and
+plans on backlog + makespan: the SLO phase's slack then evens out over bursts instead of
+random-walking onto one GPU, whose cumulative work paces a pipelined multi-GPU job
+(tools/virtual_node_bench.py replays the bench's launch-ahead pipeline over measured groups).
 """
 from __future__ import annotations
 
@@ -47,9 +53,14 @@ Obj = Dict[str, Any]
 
 
 class BurstPlanner:
-    def __init__(self, plugin: Any, tolerance: float = 0.05, sweeps: int = 8, objective: str = "slo"):
+    def __init__(self, plugin: Any, tolerance: float = 0.05, sweeps: int = 8, objective: str = "slo",
+                 carry: float = 0.0):
         if objective not in ("slo", "load"):
             raise ValueError(f"plan objective must be 'slo' or 'load', not {objective!r}")
+        if not 0.0 <= carry <= 1.0:
+            raise ValueError(f"plan carry must be in [0, 1], not {carry!r}")
+        self.carry = carry
+        self.backlog: Dict[Tuple, float] = {}             # co-run group key -> predicted ms
         self.plugin = plugin
         self.tolerance = tolerance
         self.load_first = objective == "load"
@@ -310,18 +321,50 @@ class BurstPlanner:
         # capacity before the burst (the native planner subtracts the initial assignment)
         cap = np.array(free_units, np.int32)
         np.add.at(cap, dev0, units)
+        gkeys = sorted(gkey, key=gkey.get)
+        base = None
+        if self.carry > 0:
+            raw = [self.backlog.get(k, 0.0) for k in gkeys]
+            lo = min(raw)
+            base = np.array([x - lo for x in raw], np.float64)
+        r_wid = np.array([x[0] for x in flat], np.int32)
+        r_iters = np.array([x[1] for x in flat], np.float64)
+        r_slo = np.array([x[2] for x in flat], np.float64)
         out = core.plan_corun(
             dev0, units, np.array([model.wid(O.name(p)) for p, _, _ in assign], np.int32),
             np.array([r.iters for _, r, _ in assign], np.float64),
             np.array([r.slo * margin for _, r, _ in assign], np.float64),
-            np.array(dev_group, np.int32), cap, off, np.array([x[0] for x in flat], np.int32),
-            np.array([x[1] for x in flat], np.float64), np.array([x[2] for x in flat], np.float64),
-            model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0, float(plugin.args.corun_sigma))
+            np.array(dev_group, np.int32), cap, off, r_wid, r_iters, r_slo,
+            model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0, float(plugin.args.corun_sigma),
+            base)
+        if self.carry > 0:
+            self._carry(gkeys, per, assign, out, dev_group, model, core, off, r_wid, r_iters, r_slo)
         for (p, _, _), d in zip(assign, out):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid)
             plugin._pending_by_key[O.key(p)] = p
         self.planned_bursts += 1
         return self.plans.get(key)
+
+    def _carry(self, gkeys, per, assign, out, dev_group, model, core, off, r_wid, r_iters, r_slo) -> None:
+        """Backlog bookkeeping after a co-run plan: each group's predicted makespan increase
+        from this burst (residents alone before, residents + planned pods after) is added to
+        its backlog; backlogs decay by `carry` per burst and are kept relative to the least
+        loaded group (only differences steer the plan)."""
+        _, mk0 = core.corun_groups_eval(off, r_wid, r_iters, r_slo, model.alone_ms, model.coupling())
+        groups = [list(m) for m in per]
+        for (p, r, _), d in zip(assign, out):
+            groups[dev_group[int(d)]].append((model.wid(O.name(p)), r.iters, r.slo))
+        off1 = np.zeros(len(groups) + 1, np.int64)
+        off1[1:] = np.cumsum([len(m) for m in groups])
+        flat1 = [x for m in groups for x in m]
+        _, mk1 = core.corun_groups_eval(off1, np.array([x[0] for x in flat1], np.int32),
+                                        np.array([x[1] for x in flat1], np.float64),
+                                        np.array([x[2] for x in flat1], np.float64), model.alone_ms, model.coupling())
+        for g, k in enumerate(gkeys):
+            self.backlog[k] = self.carry * self.backlog.get(k, 0.0) + max(float(mk1[g]) - float(mk0[g]), 0.0)
+        lo = min(self.backlog[k] for k in gkeys)
+        for k in gkeys:
+            self.backlog[k] -= lo
 
     def consume(self, pod_key: str) -> None:
         self.plans.pop(pod_key, None)

@@ -130,6 +130,11 @@ class GPUArgs:
     # the burst planner's soft objective: expected SLOs met when the model's log error is
     # N(0, sigma^2) (held-out: mean |log error| 0.093 -> sigma ~0.12); 0 = hard counts
     corun_sigma: float = 0.0
+    # co-run planner backlog carry: each GPU's predicted work from earlier bursts beyond the
+    # least-loaded GPU's is carried into the next plans (multiplied by this factor per burst;
+    # 0 = every burst planned on its own).  In a pipelined multi-GPU job the busiest GPU's
+    # CUMULATIVE work paces the run, and per-burst slack for SLOs otherwise random-walks
+    plan_carry: float = 0.0
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
@@ -163,6 +168,7 @@ class GPUArgs:
                  "lptWindowSeconds": "lpt_window_s",
                  "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
                  "planObjective": "plan_objective", "sloObjective": "slo_objective", "corunMargin": "corun_margin", "corunSigma": "corun_sigma",
+                 "planCarry": "plan_carry",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle",
@@ -212,7 +218,8 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         self.planner = None
         if self.args.plan_bursts:
             from .planner import BurstPlanner
-            self.planner = BurstPlanner(self, self.args.plan_tolerance, objective=self.args.plan_objective)
+            self.planner = BurstPlanner(self, self.args.plan_tolerance, objective=self.args.plan_objective,
+                                        carry=self.args.plan_carry)
         self._pred_version: Any = None
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)

@@ -295,9 +295,14 @@ py::tuple corun_groups_eval(I64 off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alon
 //      equal count -> the smaller total SLO deficit (sum of 1 - tput / SLO over the misses: a
 //      gradient toward placements one swap away from meeting more), then the lower makespan.
 // mode: 0 = A then B, 1 = A only (balance), 2 = B only (cap from the initial plan).
+// base (optional, per GPU, ms): backlog carried from earlier bursts.  Both phases then see
+// base[g] + makespan[g], and B's cap becomes the balanced plan's longest base + makespan plus
+// tolerance x its longest makespan: a GPU that took extra work for SLOs in one burst gets
+// lighter groups in the next ones, so the per-burst slack does not pile up on one GPU of a
+// pipelined multi-GPU job (the busiest GPU's cumulative work paces it).
 py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 slo, I32 dev_gpu, I32 dev_free,
                                 I64 res_off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alone, F64 cmat, int sweeps,
-                                double tolerance, int mode, double sigma) {
+                                double tolerance, int mode, double sigma, py::object base_obj) {
   int W;
   check_model(alone, cmat, W);
   const py::ssize_t P = dev_in.shape(0), D = dev_gpu.shape(0), NR = r_wid.shape(0);
@@ -315,6 +320,17 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
   if (res_off.shape(0) != NG + 1) throw std::runtime_error("plan_corun: res_off must have n_gpu + 1 entries");
   const int64_t* RO = res_off.data();
   if (RO[0] != 0 || RO[NG] != NR) throw std::runtime_error("plan_corun: bad resident offsets");
+  // base[g]: GPU g's backlog in ms (work planned onto it by earlier bursts beyond the least
+  // loaded GPU's); the objectives see base[g] + the group's makespan
+  std::vector<double> B(NG, 0.0);
+  if (!base_obj.is_none()) {
+    F64 base = base_obj.cast<F64>();
+    if (base.ndim() != 1 || base.shape(0) != NG) throw std::runtime_error("plan_corun: base must have n_gpu entries");
+    for (int g = 0; g < NG; ++g) {
+      B[g] = base.data()[g];
+      if (!std::isfinite(B[g]) || B[g] < 0) throw std::runtime_error("plan_corun: base must be finite and >= 0");
+    }
+  }
   std::vector<int32_t> dev(dev_in.data(), dev_in.data() + P);
   std::vector<int> free(dev_free.data(), dev_free.data() + D);
   const int32_t* U = units.data();
@@ -373,7 +389,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
             remove(g0, (int)p);
             mem[g1].push_back((int)p);
             const GroupEval a0 = eval(g0), a1 = eval(g1);
-            if (accept(ge[g0], ge[g1], a0, a1)) {
+            if (accept(g0, g1, ge[g0], ge[g1], a0, a1)) {
               free[d0] += U[p];
               free[d] -= U[p];
               dev[p] = (int32_t)d;
@@ -394,7 +410,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
             replace(gi, (int)i, (int)j);
             replace(gj, (int)j, (int)i);
             const GroupEval ai = eval(gi), aj = eval(gj);
-            if (accept(ge[gi], ge[gj], ai, aj)) {
+            if (accept(gi, gj, ge[gi], ge[gj], ai, aj)) {
               dev[i] = dj;
               dev[j] = di;
               ge[gi] = ai;
@@ -409,39 +425,43 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         if (!improved) break;
       }
     };
-    auto max_mk = [&]() {
+    auto max_mk = [&](bool eff) {
       double m = 0;
-      for (const auto& g : ge) m = std::max(m, g.makespan);
+      for (int g = 0; g < NG; ++g) m = std::max(m, ge[g].makespan + (eff ? B[g] : 0.0));
       return m;
     };
     if (mode == 0 || mode == 1) {
-      run_phase([&](const GroupEval& bi, const GroupEval& bj, const GroupEval& ai, const GroupEval& aj) {
-        const double mb = std::max(bi.makespan, bj.makespan), ma = std::max(ai.makespan, aj.makespan);
+      run_phase([&](int gi, int gj, const GroupEval& bi, const GroupEval& bj, const GroupEval& ai, const GroupEval& aj) {
+        const double mb = std::max(B[gi] + bi.makespan, B[gj] + bj.makespan);
+        const double ma = std::max(B[gi] + ai.makespan, B[gj] + aj.makespan);
         if (ma < mb * (1 - eps)) return true;
         if (ma > mb * (1 + eps)) return false;
-        const double sb = bi.makespan * bi.makespan + bj.makespan * bj.makespan;
-        const double sa = ai.makespan * ai.makespan + aj.makespan * aj.makespan;
-        return sa < sb * (1 - 1e-6);
+        const double xi = B[gi] + bi.makespan, xj = B[gj] + bj.makespan;
+        const double yi = B[gi] + ai.makespan, yj = B[gj] + aj.makespan;
+        return yi * yi + yj * yj < (xi * xi + xj * xj) * (1 - 1e-6);
       });
     }
     if (mode == 0 || mode == 2) {
-      const double cap = (1.0 + std::max(tolerance, 0.0)) * max_mk();
-      run_phase([&](const GroupEval& bi, const GroupEval& bj, const GroupEval& ai, const GroupEval& aj) {
-        const bool over = (ai.makespan > cap * (1 + eps) && ai.makespan > bi.makespan * (1 + eps)) ||
-                          (aj.makespan > cap * (1 + eps) && aj.makespan > bj.makespan * (1 + eps));
+      // headroom of tolerance x the balanced plan's longest GROUP (not its backlog)
+      const double cap = max_mk(true) + std::max(tolerance, 0.0) * max_mk(false);
+      run_phase([&](int gi, int gj, const GroupEval& bi, const GroupEval& bj, const GroupEval& ai, const GroupEval& aj) {
+        const bool over = (B[gi] + ai.makespan > cap * (1 + eps) && ai.makespan > bi.makespan * (1 + eps)) ||
+                          (B[gj] + aj.makespan > cap * (1 + eps) && aj.makespan > bj.makespan * (1 + eps));
         if (over) return false;
+        const double mb = std::max(B[gi] + bi.makespan, B[gj] + bj.makespan);
+        const double ma = std::max(B[gi] + ai.makespan, B[gj] + aj.makespan);
         if (sigma > 0) {          // soft objective: expected SLOs met under model error
           const double eb = bi.expected + bj.expected, ea = ai.expected + aj.expected;
           if (ea > eb + 1e-6) return true;
           if (ea < eb - 1e-6) return false;
-          return std::max(ai.makespan, aj.makespan) < std::max(bi.makespan, bj.makespan) * (1 - eps);
+          return ma < mb * (1 - eps);
         }
         const int ob = bi.ok + bj.ok, oa = ai.ok + aj.ok;
         if (oa != ob) return oa > ob;
         const double fb = bi.deficit + bj.deficit, fa = ai.deficit + aj.deficit;
         if (fa < fb - 1e-6) return true;
         if (fa > fb + 1e-6) return false;
-        return std::max(ai.makespan, aj.makespan) < std::max(bi.makespan, bj.makespan) * (1 - eps);
+        return ma < mb * (1 - eps);
       });
     }
   }
@@ -462,5 +482,5 @@ void register_corun(py::module_& m) {
   m.def("plan_corun", &plan_corun, py::arg("dev"), py::arg("units"), py::arg("wid"), py::arg("iters"), py::arg("slo"),
         py::arg("dev_gpu"), py::arg("dev_free"), py::arg("res_off"), py::arg("r_wid"), py::arg("r_iters"),
         py::arg("r_slo"), py::arg("alone_ms"), py::arg("cmat"), py::arg("sweeps") = 8, py::arg("tolerance") = 0.03,
-        py::arg("mode") = 0, py::arg("sigma") = 0.0);
+        py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none());
 }

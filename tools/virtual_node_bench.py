@@ -56,6 +56,11 @@ POLICIES = {
     **{f"corun_plan_t{t:02d}" + (f"_s{sg:02d}" if sg else ""):
        dict(balance=1.0, plan_bursts=True, plan_tolerance=t / 100.0, slo_objective="corun", corun_sigma=sg / 100.0)
        for t in (5, 10, 20, 30, 40, 50) for sg in (0, 3, 5, 8, 10)},
+    # ..._cCC: backlog carried between bursts, decay 0.CC per burst (c100 = no decay)
+    **{f"corun_plan_t{t:02d}_s05_c{c:03d}":
+       dict(balance=1.0, plan_bursts=True, plan_tolerance=t / 100.0, slo_objective="corun", corun_sigma=0.05,
+            plan_carry=c / 100.0)
+       for t in (20, 30, 40, 50) for c in (90, 95, 100)},
     # roofline complementarity term (GPU plugin weightComplement) on top of greedy
     "greedy_comp": dict(balance=1.0, plan_bursts=False, complement=1.0),
     "greedy_comp3": dict(balance=1.0, plan_bursts=False, complement=3.0),
@@ -84,13 +89,28 @@ def run_group(ex: DeviceExecutor, runs):
 GROUPS: list = []      # per group: policy, workloads, wall ms, per pod (SLO, achieved, predicted), for --dump-groups
 
 
+SIM = {"on": False, "sigma": 0.05, "rng": None}
+
+
+def sim_group(runs) -> float:
+    """--simulate: the co-run model stands in for the GPU (each pod's predicted wall time
+    times a lognormal error of sigma, its size on held-out groups); CPU-only policy studies."""
+    if not runs:
+        return 0.0
+    t = MODEL.group_times([MODEL.wid(r.workload) for r in runs], [r.iters for r in runs])
+    t = t * np.exp(SIM["rng"].normal(0.0, SIM["sigma"], len(runs)))
+    for r, x in zip(runs, t):
+        r.ms = float(x)
+    return float(t.max())
+
+
 def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
     walls, per_gpu = [], np.zeros((N_GPUS, TELE))
     per_gpu[:, SMI0:] = -1.0          # one real GPU stands in for eight: no per-GPU amd-smi view
     ok = n = 0
     for g in range(N_GPUS):
         runs = _runs_for(arr, g)
-        walls.append(run_group(ex, runs))
+        walls.append(sim_group(runs) if SIM["on"] else run_group(ex, runs))
         pred = [None] * len(runs)
         model = MODEL
         if model is not None and runs:
@@ -135,14 +155,20 @@ def main() -> None:
     ap.add_argument("--dump-groups", default="", help="write every group's workloads and wall ms (JSON)")
     ap.add_argument("--policies", nargs="+", default=["greedy", "corun", "corun_plan_t10", "random"],
                     choices=sorted(POLICIES))
+    ap.add_argument("--simulate", action="store_true",
+                    help="no GPU: group times from the co-run model with lognormal error (--sim-sigma)")
+    ap.add_argument("--sim-sigma", type=float, default=0.05)
     a = ap.parse_args()
+    SIM.update(on=a.simulate, sigma=a.sim_sigma, rng=np.random.default_rng(a.seed))
     global N_GPUS
     N_GPUS = a.gpus
     policies = {k: POLICIES[k] for k in a.policies}
     cps = {k: ControlPlane(n_gpus=N_GPUS, pods_per_gpu=4, iters=20, seed=a.seed, **kw) for k, kw in policies.items()}
-    ex = DeviceExecutor(0, use_cu_masks=True)
-    ex.use_graphs = True                # as the bench (and the co-run model's measurements)
-    ex.warm([PodRun(0, wl, u, 2, 20, masked=False) for wl in W.NAMES for u in (0, 2, 4, 6)])
+    ex = None
+    if not a.simulate:
+        ex = DeviceExecutor(0, use_cu_masks=True)
+        ex.use_graphs = True            # as the bench (and the co-run model's measurements)
+        ex.warm([PodRun(0, wl, u, 2, 20, masked=False) for wl in W.NAMES for u in (0, 2, 4, 6)])
     stats = {k: {"max_ms": [], "mean_ms": [], "walls": [], "ok": 0, "n": 0} for k in policies}
     for e in range(a.warmup + a.epochs):
         for k, cp in cps.items():
@@ -174,6 +200,7 @@ def main() -> None:
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump({"note": "each virtual GPU's 4 pods co-run on the one real MI355X in turn; coupled N-GPU epoch = "
                        "slowest group; policies interleaved per epoch, same seed", "gpus": N_GPUS, "epochs": a.epochs,
+               "simulated": ({"model": getattr(MODEL, "version", ""), "sigma": a.sim_sigma} if a.simulate else False),
                "results": out}, open(a.out, "w"), indent=1)
 
 
