@@ -104,7 +104,8 @@ class ControlPlane:
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
                  plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0,
                  online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
-                 corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0):
+                 corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
+                 plan_feedback: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -166,6 +167,12 @@ class ControlPlane:
                                                  scale=online_scale)
                 self._online_rows = rows
         self._timeline: Dict[int, List[Any]] = {}     # per GPU: the last epochs' pod rows (co-run learner)
+        # planner backlog feedback: the predicted busy ms per GPU of every scheduled epoch not yet
+        # collected (FIFO: epochs are collected in the order they were scheduled), and per GPU
+        # the end of the busy time already accounted on its executor's clock
+        self.plan_feedback = plan_feedback and plan_carry > 0
+        self._carry_pred: "collections.deque[Dict[int, float]]" = collections.deque()
+        self._covered: Dict[int, float] = {}
         self.epoch = 0
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -200,7 +207,12 @@ class ControlPlane:
                              slo=round(p["slo"], 3), gpu_limits=self.qos == "guaranteed",
                              env={C.ENV_ITERATIONS: str(self.iters)})
             self.fc.create("pods", pod, owned=True)
+        planner = getattr(self.plugin, "planner", None)
+        if planner is not None:
+            planner.last_increments = {}
         results = self.sched.schedule_pending()
+        if self.plan_feedback and planner is not None:
+            self._carry_pred.append({k[1]: v for k, v in planner.last_increments.items() if k[0] == NODE})
         arr = np.full((len(pods), FIELDS), -1, dtype=np.int32)
         byname = {p["name"]: p for p in pods}
         dropped = []
@@ -260,6 +272,33 @@ class ControlPlane:
         if self.corun is not None and self.corun.model is not self.predictions.corun():
             self.predictions.install_corun(self.corun.model)
 
+    def _plan_feedback(self, pods: np.ndarray) -> None:
+        """Fold each GPU's measured busy time for the collected epoch, minus what the planner
+        predicted for it, into the planner's backlog.  With a timeline the busy time is the
+        union of the epoch's pod intervals past what earlier epochs already covered (the
+        launch-ahead pipeline overlaps neighbouring epochs); without one (isolated groups) the
+        slowest pod's wall time."""
+        if not self._carry_pred:
+            return
+        pred = self._carry_pred.popleft()
+        planner = self.plugin.planner
+        for g in range(pods.shape[0]):
+            rec = [r for r in pods[g].reshape(MAX_PODS_GPU, POD_F) if r[0] >= 0 and r[1] > 0]
+            if not rec or g not in pred:
+                continue
+            if rec[0][2] >= 0:
+                cov = self._covered.get(g, -float("inf"))
+                busy = 0.0
+                for s0, e0 in sorted((float(r[2]), float(r[3])) for r in rec):
+                    s0 = max(s0, cov)
+                    if e0 > s0:
+                        busy += e0 - s0
+                        cov = e0
+                self._covered[g] = cov
+            else:
+                busy = max(self.iters / float(r[1]) * 1e3 for r in rec)
+            planner.correct((NODE, g), busy - pred[g])
+
     def _observe_corun(self, g: int, rec: List[Any]) -> None:
         base = self.corun.base
         if not rec:
@@ -318,6 +357,8 @@ class ControlPlane:
                     self.workcost.observe(W.NAMES[wid], float(tot / n), int(n))
             if self.online is not None or self.corun is not None:
                 self._learn_interference(per_gpu[:, POD0:SMI0])
+            if self.plan_feedback:
+                self._plan_feedback(per_gpu[:, POD0:SMI0])
         for st in self.ledger.devices(NODE):
             g = st.device.gpu
             if g >= len(per_gpu):
@@ -537,6 +578,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "GPU's cumulative work paces the pipelined N-GPU run; simulated virtual node (co-run "
                          "model +-5 %%): pipelined epoch 2-8 %% shorter and 0.5-5 points more SLOs met than 0 "
                          "at 2/4/8 GPUs.  No effect at N=1 (one GPU group)")
+    ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
+                    help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
+                         "collected epoch (a GPU slower than its siblings, or the model's error on it)")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
                     help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
                          "'slo' = most predicted SLOs met first (within --plan-tolerance)")
@@ -625,7 +669,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
                      plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective,
                      online_scale=bool(a.online_scale), slo_objective=a.slo_objective, corun_sigma=a.corun_sigma,
-                     plan_carry=a.plan_carry)
+                     plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -910,7 +954,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                        "balance": a.balance, "plan_bursts": a.plan_bursts,
                        "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
                        "online_scale": a.online_scale, "slo_objective": a.slo_objective, "corun_sigma": a.corun_sigma,
-                       "plan_carry": a.plan_carry,
+                       "plan_carry": a.plan_carry, "plan_feedback": a.plan_feedback,
                        # which code path N=1 took: collectives over a 1-rank group or the plain path
                        "collectives": bool(dist_on), "dist_single": a.dist_single,
                        **({"collectives_note": dist_note} if dist_note else {}),

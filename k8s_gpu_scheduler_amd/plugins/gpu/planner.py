@@ -61,6 +61,7 @@ class BurstPlanner:
             raise ValueError(f"plan carry must be in [0, 1], not {carry!r}")
         self.carry = carry
         self.backlog: Dict[Tuple, float] = {}             # co-run group key -> predicted ms
+        self.last_increments: Dict[Tuple, float] = {}     # the last burst's predicted ms per group
         self.plugin = plugin
         self.tolerance = tolerance
         self.load_first = objective == "load"
@@ -360,11 +361,22 @@ class BurstPlanner:
         _, mk1 = core.corun_groups_eval(off1, np.array([x[0] for x in flat1], np.int32),
                                         np.array([x[1] for x in flat1], np.float64),
                                         np.array([x[2] for x in flat1], np.float64), model.alone_ms, model.coupling())
+        self.last_increments = {}
         for g, k in enumerate(gkeys):
-            self.backlog[k] = self.carry * self.backlog.get(k, 0.0) + max(float(mk1[g]) - float(mk0[g]), 0.0)
+            inc = max(float(mk1[g]) - float(mk0[g]), 0.0)
+            self.last_increments[k] = inc
+            self.backlog[k] = self.carry * self.backlog.get(k, 0.0) + inc
         lo = min(self.backlog[k] for k in gkeys)
         for k in gkeys:
             self.backlog[k] -= lo
+
+    def correct(self, group: Tuple, delta_ms: float) -> None:
+        """Measured feedback: a group's observed busy time for a planned burst exceeded (or
+        fell short of) the plan's prediction by delta_ms -- e.g. a GPU running a few percent
+        slower than its siblings, or the model's error on that group.  Folded into its
+        backlog, so the next plans see what the GPU really has left."""
+        if self.carry > 0 and group in self.backlog:
+            self.backlog[group] = max(self.backlog[group] + delta_ms, 0.0)
 
     def consume(self, pod_key: str) -> None:
         self.plans.pop(pod_key, None)

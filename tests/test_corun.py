@@ -276,3 +276,24 @@ def test_planner_backlog_carry_evens_out_cumulative_gpu_work():
     # close to the mean
     free, carried = _cumulative_imbalance(0.0), _cumulative_imbalance(1.0)
     assert carried < free and carried < 1.03, (free, carried)
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_planner_feedback_moves_work_off_a_slow_gpu(tmp_path):
+    """Virtual node in --simulate mode (co-run model +-5 % stands in for the GPUs), GPU 0
+    running 8 % slower than the model says: with measured busy-time feedback into the backlog
+    the pipelined node epoch (the busiest GPU's cumulative time) is shorter than without."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "vn.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "virtual_node_bench.py"), "--simulate",
+                        "--gpus", "4", "--epochs", "32", "--seed", "1", "--sim-speed", "1.08",
+                        "--policies", "corun_plan_t30_s05_c100", "corun_plan_t30_s05_c100_nofb", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, PYTHONPATH=root))
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(out.read_text())["results"]
+    fb, nofb = res["corun_plan_t30_s05_c100"], res["corun_plan_t30_s05_c100_nofb"]
+    assert fb["epoch_ms_pipelined_l2"] < nofb["epoch_ms_pipelined_l2"], (fb, nofb)

@@ -61,6 +61,11 @@ POLICIES = {
        dict(balance=1.0, plan_bursts=True, plan_tolerance=t / 100.0, slo_objective="corun", corun_sigma=0.05,
             plan_carry=c / 100.0)
        for t in (20, 30, 40, 50) for c in (90, 95, 100)},
+    # the same without the measured busy-time feedback into the backlog
+    **{f"corun_plan_t{t:02d}_s05_c100_nofb":
+       dict(balance=1.0, plan_bursts=True, plan_tolerance=t / 100.0, slo_objective="corun", corun_sigma=0.05,
+            plan_carry=1.0, plan_feedback=False)
+       for t in (20, 30, 40)},
     # roofline complementarity term (GPU plugin weightComplement) on top of greedy
     "greedy_comp": dict(balance=1.0, plan_bursts=False, complement=1.0),
     "greedy_comp3": dict(balance=1.0, plan_bursts=False, complement=3.0),
@@ -89,16 +94,18 @@ def run_group(ex: DeviceExecutor, runs):
 GROUPS: list = []      # per group: policy, workloads, wall ms, per pod (SLO, achieved, predicted), for --dump-groups
 
 
-SIM = {"on": False, "sigma": 0.05, "rng": None}
+SIM = {"on": False, "sigma": 0.05, "rng": None, "speed": []}
 
 
-def sim_group(runs) -> float:
+def sim_group(runs, g: int = 0) -> float:
     """--simulate: the co-run model stands in for the GPU (each pod's predicted wall time
     times a lognormal error of sigma, its size on held-out groups); CPU-only policy studies."""
     if not runs:
         return 0.0
     t = MODEL.group_times([MODEL.wid(r.workload) for r in runs], [r.iters for r in runs])
     t = t * np.exp(SIM["rng"].normal(0.0, SIM["sigma"], len(runs)))
+    if g < len(SIM["speed"]):
+        t = t * SIM["speed"][g]             # a GPU slower (> 1) or faster than the model's
     for r, x in zip(runs, t):
         r.ms = float(x)
     return float(t.max())
@@ -110,7 +117,7 @@ def epoch(cp: ControlPlane, ex: DeviceExecutor, arr: np.ndarray, tag: str = ""):
     ok = n = 0
     for g in range(N_GPUS):
         runs = _runs_for(arr, g)
-        walls.append(sim_group(runs) if SIM["on"] else run_group(ex, runs))
+        walls.append(sim_group(runs, g) if SIM["on"] else run_group(ex, runs))
         pred = [None] * len(runs)
         model = MODEL
         if model is not None and runs:
@@ -158,8 +165,10 @@ def main() -> None:
     ap.add_argument("--simulate", action="store_true",
                     help="no GPU: group times from the co-run model with lognormal error (--sim-sigma)")
     ap.add_argument("--sim-sigma", type=float, default=0.05)
+    ap.add_argument("--sim-speed", default="", help="per-GPU time multipliers, comma-separated (e.g. 1.06,1,1)")
     a = ap.parse_args()
-    SIM.update(on=a.simulate, sigma=a.sim_sigma, rng=np.random.default_rng(a.seed))
+    SIM.update(on=a.simulate, sigma=a.sim_sigma, rng=np.random.default_rng(a.seed),
+               speed=[float(x) for x in a.sim_speed.split(",") if x])
     global N_GPUS
     N_GPUS = a.gpus
     policies = {k: POLICIES[k] for k in a.policies}
@@ -200,7 +209,8 @@ def main() -> None:
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump({"note": "each virtual GPU's 4 pods co-run on the one real MI355X in turn; coupled N-GPU epoch = "
                        "slowest group; policies interleaved per epoch, same seed", "gpus": N_GPUS, "epochs": a.epochs,
-               "simulated": ({"model": getattr(MODEL, "version", ""), "sigma": a.sim_sigma} if a.simulate else False),
+               "simulated": ({"model": getattr(MODEL, "version", ""), "sigma": a.sim_sigma, "speed": SIM["speed"]}
+                             if a.simulate else False),
                "results": out}, open(a.out, "w"), indent=1)
 
 
