@@ -559,9 +559,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--plan-bursts", type=int, default=1, choices=[0, 1],
                     help="1 (default): plan each epoch's burst of pods jointly.  With the co-run model "
                          "(--slo-objective corun): balanced predicted group makespans, then the most predicted "
-                         "SLOs met within --plan-tolerance -- on the virtual 8-GPU node 77.8 %% of SLOs met vs "
-                         "57.6 %% greedy and 56.0 %% random, at 1.27x greedy's coupled pods/s (48 epochs, "
-                         "profiles/r03_virtual_node.json).  At N=1 there is one GPU group and nothing to plan")
+                         "SLOs met within --plan-tolerance, with the GPUs' backlogs carried between bursts "
+                         "(--plan-carry) -- on the virtual 8-GPU node 83.1 %% of SLOs met vs 57.7 %% greedy and "
+                         "56.0 %% random, at 0.99x greedy's pipelined pods/s (48 epochs, profiles/r03_vn_carry/).  "
+                         "At N=1 there is one GPU group and nothing to plan")
     ap.add_argument("--online-scale", type=int, default=1,
                     help="online interference learning: shrink rows toward the prior SCALED by a learned "
                          "global / per-row factor (recommender.online) instead of the prior itself")
@@ -575,9 +576,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--plan-carry", type=float, default=1.0,
                     help="co-run burst planner: carry each GPU's predicted backlog from earlier bursts into the "
                          "next plans, decayed by this factor per burst (0 = every burst on its own).  The busiest "
-                         "GPU's cumulative work paces the pipelined N-GPU run; simulated virtual node (co-run "
-                         "model +-5 %%): pipelined epoch 2-8 %% shorter and 0.5-5 points more SLOs met than 0 "
-                         "at 2/4/8 GPUs.  No effect at N=1 (one GPU group)")
+                         "GPU's cumulative work paces the pipelined N-GPU run; MI355X virtual node: pipelined "
+                         "epoch 1-4 %% shorter and 3-6 points more SLOs met than 0 at 2/4/8 GPUs "
+                         "(profiles/r03_vn_carry/).  No effect at N=1 (one GPU group)")
     ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
                     help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
                          "collected epoch (a GPU slower than its siblings, or the model's error on it)")
