@@ -112,7 +112,7 @@ def main():
     res["prio_triad_high"] = case("prio_triad_high", S(), S(priority=-1), ng, nt)
     for gu, tu in (((0, 6), (6, 8)), ((0, 4), (4, 8)), ((0, 3), (3, 8)), ((0, 2), (2, 8))):
         res[f"masked_g{gu}_t{tu}"] = case(f"masked g{gu} t{tu}", S(gu), S(tu), ng, nt, gbudget=(gu[1] - gu[0]) * 32)
-    for tu in ((3, 8), (2, 8), (4, 8)):     # only the stream kernel confined; GEMM may use every CU
+    for tu in ((1, 8), (2, 8), (3, 8), (4, 8)):     # only the stream kernel confined; GEMM may use every CU
         res[f"triad_only_masked_t{tu}"] = case(f"triad-only masked t{tu}", S(), S(tu), ng, nt)
     if os.environ.get("PROBE_SHORT"):
         os.makedirs("gpurun_out", exist_ok=True)
