@@ -1,18 +1,44 @@
-"""Control-plane throughput at N GPUs (CPU only): ms to schedule one epoch of N x 4 pods."""
+"""Control-plane throughput at N GPUs (CPU only): ms to schedule one epoch of N x 4 pods.
+
+Two configurations: the plain GPU plugin (no burst planner) and the bench defaults (co-run
+planner with backlog carry and measured feedback; each epoch's telemetry is fed back from the
+co-run model, as `tools/virtual_node_bench.py --simulate` does), so the planner's full
+per-epoch cost is in the figure.
+"""
+import os
 import sys
 import time
 
-sys.path.insert(0, ".")
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 from k8s_gpu_scheduler_amd.parallel.podbench import ControlPlane  # noqa: E402
 
-for n in (1, 2, 4, 8):
-    cp = ControlPlane(n, 4, 20, 0)
-    for _ in range(10):
+BENCH = dict(balance=1.0, plan_bursts=True, plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05,
+             plan_carry=1.0, plan_feedback=True)
+
+
+def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
+    import virtual_node_bench as V
+    V.N_GPUS = n
+    V.SIM.update(on=True, sigma=0.05, rng=np.random.default_rng(0), speed=[])
+    cp = ControlPlane(n, 4, 20, 0, **kwargs)
+    ts = []
+    for e in range(warm + epochs):
         cp.finish_live()
-        cp.schedule_epoch()
-    t = time.perf_counter()
-    for _ in range(100):
-        cp.finish_live()
-        cp.schedule_epoch()
-    dt = (time.perf_counter() - t) / 100
-    print(f"gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}", flush=True)
+        t = time.perf_counter()
+        arr = cp.schedule_epoch()
+        if e >= warm:
+            ts.append(time.perf_counter() - t)
+        if kwargs:
+            V.epoch(cp, None, arr, "t")      # telemetry back into the control plane (not timed)
+    return float(np.median(ts))
+
+
+for name, kw in (("plain", {}), ("bench-defaults", BENCH)):
+    for n in (1, 2, 4, 8):
+        dt = run(n, kw)
+        print(f"{name} gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}",
+              flush=True)
