@@ -374,9 +374,11 @@ class BurstPlanner:
         """Measured feedback: a group's observed busy time for a planned burst exceeded (or
         fell short of) the plan's prediction by delta_ms -- e.g. a GPU running a few percent
         slower than its siblings, or the model's error on that group.  Folded into its
-        backlog, so the next plans see what the GPU really has left."""
+        backlog, so the next plans see what the GPU really has left.  Backlogs are relative
+        (the plans subtract the least one), so a group that ran faster than predicted may go
+        below the others' floor."""
         if self.carry > 0 and group in self.backlog:
-            self.backlog[group] = max(self.backlog[group] + delta_ms, 0.0)
+            self.backlog[group] += delta_ms
 
     def consume(self, pod_key: str) -> None:
         self.plans.pop(pod_key, None)
