@@ -64,6 +64,9 @@ def test_scheduler_profile_loads_and_instantiates():
     fw = Framework(prof, full_registry(), handle=None)
     gpu = fw.plugin("GPU")
     assert gpu.args.w_balance == 0.5 and gpu.args.model == "MI355X"
+    # the deployed burst planner: co-run model, 30 % tolerance, backlog carried between bursts
+    assert gpu.args.plan_bursts and gpu.args.plan_tolerance == 0.3 and gpu.args.plan_carry == 1.0
+    assert gpu.planner is not None and gpu.planner.carry == 1.0
     dep = _find("Deployment", "gpu-scheduler", "kube-system")
     spec = dep["spec"]["template"]["spec"]
     assert (spec.get("serviceAccountName") or spec.get("serviceAccount")) == "sample-sa"   # reference SA name
