@@ -284,9 +284,9 @@ class ControlPlane:
         planner = self.plugin.planner
         for g in range(pods.shape[0]):
             rec = [r for r in pods[g].reshape(MAX_PODS_GPU, POD_F) if r[0] >= 0 and r[1] > 0]
-            if not rec or g not in pred:
+            if not rec:
                 continue
-            if rec[0][2] >= 0:
+            if rec[0][2] >= 0:            # (the covered end advances even for an unplanned epoch)
                 cov = self._covered.get(g, -float("inf"))
                 busy = 0.0
                 for s0, e0 in sorted((float(r[2]), float(r[3])) for r in rec):
@@ -297,7 +297,8 @@ class ControlPlane:
                 self._covered[g] = cov
             else:
                 busy = max(self.iters / float(r[1]) * 1e3 for r in rec)
-            planner.correct((NODE, g), busy - pred[g])
+            if g in pred:
+                planner.correct((NODE, g), busy - pred[g])
 
     def _observe_corun(self, g: int, rec: List[Any]) -> None:
         base = self.corun.base
