@@ -200,6 +200,8 @@ def main() -> None:
                   "slo_attainment_pct": round(100.0 * st["ok"] / max(st["n"], 1), 2), "pods": st["n"],
                   "interference_mae": cps[k].interference_mae(),
                   "epoch_ms_pipelined_l2": round(pipelined_ms(np.array(st["walls"]), 2), 3),
+                  # what paces the bench: its 2-deep launch-ahead pipeline over these group times
+                  "pods_per_s_pipelined_l2": round(4 * N_GPUS / pipelined_ms(np.array(st["walls"]), 2) * 1e3, 1),
                   "epoch_ms_pipelined_l3": round(pipelined_ms(np.array(st["walls"]), 3), 3),
                   "epoch_ms_pipelined_l4": round(pipelined_ms(np.array(st["walls"]), 4), 3),
                   "walls_ms": [[round(x, 3) for x in w] for w in st["walls"]]}
