@@ -10,7 +10,8 @@ Protocol (multiprocessing Pipe, in order):
   ("schedule",)                -> child: finish the live epoch's pods, schedule the next
                                   epoch, reply ("placements", arr, sched_s, unscheduled)
   ("telemetry", per_gpu, ms)   -> child: update the TelemetryCache (no reply)
-  ("reset_stats",)             -> child: zero sched_s / unscheduled counters
+  ("reset_stats",)             -> child: zero sched_s / unscheduled counters, realign the
+                                  planner's backlog (the bench drained every GPU before timing)
   ("interference_mae",)        -> child: reply ("interference_mae", online-model error summary)
   ("stop",)                    -> child exits
 """
@@ -35,8 +36,7 @@ def _serve(conn: Any, kwargs: dict) -> None:
         elif kind == "telemetry":
             cp.update_telemetry(msg[1], msg[2])
         elif kind == "reset_stats":
-            cp.sched_s = 0.0
-            cp.unscheduled = 0
+            cp.reset_stats()
         elif kind == "interference_mae":
             conn.send(("interference_mae", cp.interference_mae()))
         elif kind == "stop":

@@ -272,6 +272,15 @@ class ControlPlane:
         if self.corun is not None and self.corun.model is not self.predictions.corun():
             self.predictions.install_corun(self.corun.model)
 
+    def reset_stats(self) -> None:
+        """The warmup -> timed transition: zero the counters, and realign the planner's backlog,
+        since the bench drained every GPU's pipeline (all idle at once) before timing."""
+        self.sched_s = 0.0
+        self.unscheduled = 0
+        planner = getattr(self.plugin, "planner", None)
+        if planner is not None:
+            planner.realign()
+
     def _plan_feedback(self, pods: np.ndarray) -> None:
         """Fold each GPU's measured busy time for the collected epoch, minus what the planner
         predicted for it, into the planner's backlog.  With a timeline the busy time is the
@@ -883,11 +892,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             ref["host_ms"] = (time.perf_counter() - t_start) * 1e3
     flops0, bytes0 = ex.flops_done, ex.bytes_done
     if rank == 0:
-        if async_cp:
-            cp.reset_stats()
-        else:
-            cp.sched_s = 0.0
-            cp.unscheduled = 0
+        cp.reset_stats()
     run_epochs(a.steps, True)
     if dist_on:
         dist.barrier()

@@ -380,6 +380,15 @@ class BurstPlanner:
         if self.carry > 0 and group in self.backlog:
             self.backlog[group] += delta_ms
 
+    def realign(self) -> None:
+        """Every group has drained (e.g. a pipelined job synchronised its GPUs): the carried
+        backlog is void, except the last planned burst, which has not run yet."""
+        self.backlog = dict(self.last_increments)
+        if self.backlog:
+            lo = min(self.backlog.values())
+            for k in self.backlog:
+                self.backlog[k] -= lo
+
     def consume(self, pod_key: str) -> None:
         self.plans.pop(pod_key, None)
         self.plugin._pending_by_key.pop(pod_key, None)

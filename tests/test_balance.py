@@ -150,9 +150,9 @@ def test_bench_timed_sim_four_ranks_balance_improves_throughput(tmp_path):
     """Rehearsal of the coupled multi-rank run (gloo, modelled device time): spreading
     predicted work must not lose throughput against plain bin-packing."""
     best = {}
-    # wall-clock timed runs on a shared CPU: a second interleaved pair (best of each arm) absorbs
-    # a load spike during one run
-    for attempt in range(2):
+    # wall-clock timed runs on a shared CPU: further interleaved pairs (best of each arm) absorb
+    # a load spike during one run (other test processes under pytest -n)
+    for attempt in range(3):
         for bal in (0, 1):
             env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",

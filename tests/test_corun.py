@@ -346,3 +346,14 @@ def test_default_planner_meets_more_slos_than_greedy_and_random_at_greedy_throug
     g, rnd, p = res["greedy"], res["random"], res["corun_plan_t30_s05_c100"]
     assert p["slo_attainment_pct"] > max(g["slo_attainment_pct"], rnd["slo_attainment_pct"]) + 10
     assert p["epoch_ms_pipelined_l2"] <= 1.03 * g["epoch_ms_pipelined_l2"]
+
+
+def test_planner_realign_keeps_only_the_burst_not_yet_run():
+    """After the bench drains every GPU (warmup -> timed), the carried backlog is void except the
+    last planned burst, which is already scheduled but has not run."""
+    from k8s_gpu_scheduler_amd.plugins.gpu.planner import BurstPlanner
+    p = BurstPlanner(plugin=None, carry=1.0)
+    p.backlog = {("n", 0): 5.0, ("n", 1): 0.0}
+    p.last_increments = {("n", 0): 1.0, ("n", 1): 3.0}
+    p.realign()
+    assert p.backlog == {("n", 0): 0.0, ("n", 1): 2.0}
