@@ -283,6 +283,46 @@ def test_executor_epoch_and_bench_smoke():
     assert r["value"] > 0 and not r["simulated"] and r["unscheduled"] == 0
 
 
+def test_planner_backlog_feedback_on_real_timelines():
+    """The N-GPU bench's planner path on real pod timelines: a 2-GPU control plane (co-run
+    planner + backlog carry + measured feedback) plans each epoch; both GPUs' pods run on the
+    one MI355X (GPU 1's on their own slot streams), and each GPU's telemetry rows, with start /
+    end times on the executor clock, feed the backlog as in bench.py."""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor
+    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=2, iters=4, seed=5, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0)
+    planner = cp.plugin.planner
+    ex = DeviceExecutor(0)
+    corrections = []
+    orig = planner.correct
+
+    def spy(group, delta):
+        corrections.append((group, delta))
+        orig(group, delta)
+    planner.correct = spy
+    for _ in range(4):
+        cp.finish_live()
+        arr = cp.schedule_epoch()
+        per_gpu = np.zeros((2, PB.TELE))
+        per_gpu[:, PB.SMI0:] = -1.0
+        runs = {g: PB._runs_for(arr, g) for g in (0, 1)}
+        for r in runs[1]:                      # GPU 1's pods on the other half of the slots
+            r.first_unit = (r.first_unit + 4) % 8
+        ex.launch_epoch(runs[0] + runs[1])
+        ex.wait_all()
+        for g in (0, 1):
+            ex.collect(runs[g])
+            per_gpu[g, PB.POD0:PB.SMI0] = PB._pod_rows(runs[g], ex.clock)
+        cp.update_telemetry(per_gpu, 1.0)
+    ex.close()
+    assert planner.planned_bursts == 4 and len(planner.backlog) == 2
+    assert len(corrections) == 8 and all(np.isfinite(d) for _, d in corrections)
+    assert {g for g, _ in corrections} == {(PB.NODE, 0), (PB.NODE, 1)}
+    assert all(np.isfinite(v) for v in planner.backlog.values())
+
+
 def test_rccl_probe_single_rank(tmp_path, monkeypatch):
     """RCCL path of the placement probe (world size 1 on the 1-GPU box)."""
     import json
