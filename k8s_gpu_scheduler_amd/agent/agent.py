@@ -63,7 +63,8 @@ class NodeAgent:
                  health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
                  drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1,
                  hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc", profile_dir: str = "",
-                 partition_dry_run: bool = False, fabric: Any = None):
+                 partition_dry_run: bool = False, fabric: Any = None,
+                 corun_send: Optional[Callable[[List[Dict[str, Any]]], Any]] = None):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -97,10 +98,18 @@ class NodeAgent:
         # per-pod rocprofv3 output the profiling webhook (agent.profile_webhook) routes to a
         # hostPath: finished runs become workload-history samples (pod_profiler.ProfileIngestor)
         self.profiles = None
+        self.corun = None
         if profile_dir:
             from ..recommender.admission import RedisHistory
             from .pod_profiler import ProfileIngestor
-            self.profiles = ProfileIngestor(profile_dir, RedisHistory(redis))
+            # co-run observations from the traces (agent.corun_observer): pods that overlapped
+            # on one device, sent to the recommender's online co-run model
+            self.corun = None
+            if corun_send is not None:
+                from .corun_observer import CorunObserver
+                self.corun = CorunObserver(corun_send, running_on=self._running_on if client is not None else None)
+            self.profiles = ProfileIngestor(profile_dir, RedisHistory(redis), node=node, corun=self.corun,
+                                            pod_lookup=self._pod_lookup if client is not None else None)
         self.history_every = max(1, history_every)
         self._steps = 0
         self.health = health or HealthMonitor()
@@ -562,6 +571,29 @@ class NodeAgent:
                 self.profiles.step()
             except Exception as e:
                 log.warning("ingesting per-pod profiles failed: %s", e)
+            if self.corun is not None:
+                try:
+                    self.corun.step()
+                except Exception as e:
+                    log.warning("co-run observations failed: %s", e)
+
+    def _pod_lookup(self, ns: str, name: str) -> Optional[Dict[str, Any]]:
+        from ..kube.client import NotFound
+        try:
+            return self.client.get("pods", name, ns)
+        except NotFound:
+            return None
+
+    def _running_on(self, uuid: str) -> set:
+        """Keys of this node's non-terminal pods assigned to device `uuid`."""
+        pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        out = set()
+        for p in pods:
+            if O.is_terminal(p):
+                continue
+            if uuid in (O.annotations(p).get(C.ANNOT_DEVICES) or "").split(","):
+                out.add(O.key(p))
+        return out
 
     def run(self) -> None:
         while not self._stop.is_set():

@@ -148,7 +148,7 @@ class PodLauncher:
             (list(ctr.get("command") or []) + list(ctr.get("args") or [])) or self.command
         # kubelet: $(VAR) in command/args expands from the container env; a process runtime
         # has no mount namespace, so hostPath volumeMounts become path rewrites
-        mounts = self.host_mounts(pod, ctr)
+        mounts = self.host_mounts(pod, ctr, env)
         argv = [self._remap(_expand(a, env), mounts) for a in argv]
         for mp, hp in mounts.items():
             os.makedirs(self.host_root + hp, exist_ok=True)     # hostPath type DirectoryOrCreate
@@ -172,14 +172,22 @@ class PodLauncher:
         return res
 
     @staticmethod
-    def host_mounts(pod: Obj, ctr: Obj) -> Dict[str, str]:
-        """mountPath -> hostPath of the container's hostPath volume mounts."""
+    def host_mounts(pod: Obj, ctr: Obj, env: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+        """mountPath -> hostPath of the container's hostPath volume mounts (with its subPath,
+        or its subPathExpr expanded from the container env, as the kubelet does; a sub-path
+        that is absolute or climbs out with `..` is refused, as the kubelet refuses it)."""
         vols = {v.get("name"): (v.get("hostPath") or {}).get("path") for v in (pod.get("spec") or {}).get("volumes") or []}
         out = {}
         for m in ctr.get("volumeMounts") or []:
             hp = vols.get(m.get("name"))
-            if hp and m.get("mountPath"):
-                out[m["mountPath"].rstrip("/")] = hp
+            if not hp or not m.get("mountPath"):
+                continue
+            sub = m.get("subPath") or (_expand(m["subPathExpr"], env or {}) if m.get("subPathExpr") else "")
+            if sub:
+                if sub.startswith("/") or ".." in sub.split("/") or "$(" in sub:
+                    raise ValueError(f"volumeMount {m.get('name')}: bad sub-path {sub!r}")
+                hp = hp.rstrip("/") + "/" + sub
+            out[m["mountPath"].rstrip("/")] = hp
         return out
 
     def _remap(self, arg: str, mounts: Dict[str, str]) -> str:

@@ -22,7 +22,7 @@ import os
 import shutil
 import tempfile
 import time
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..api import constants as C
 from ..api import objects as O
@@ -132,6 +132,7 @@ def summarize_kernel_trace(path: str) -> Dict[str, Any]:
     if not iv:
         return {}
     iv.sort()
+    first_ns, last_ns = iv[0][0], max(b for _, b in iv)
     busy, cs, ce = 0, iv[0][0], iv[0][1]
     for a, b in iv[1:]:
         if a > ce:
@@ -140,8 +141,8 @@ def summarize_kernel_trace(path: str) -> Dict[str, Any]:
         else:
             ce = max(ce, b)
     busy += ce - cs
-    span = max(b for _, b in iv) - iv[0][0]
-    return {"span_ms": span / 1e6, "busy_union_ms": busy / 1e6}
+    span = last_ns - first_ns
+    return {"span_ms": span / 1e6, "busy_union_ms": busy / 1e6, "first_ns": first_ns, "last_ns": last_ns}
 
 
 class ProfileIngestor:
@@ -154,13 +155,27 @@ class ProfileIngestor:
     per-dispatch tracing adds host gaps between an eagerly launching pod's kernels that the
     unprofiled pod does not have).  A directory is finished when rocprofv3 has written its
     stats (kernel_stats.csv, or counter_collection.csv for a PMC pass); ingested ones are
-    removed, so each run is counted once."""
+    removed, so each run is counted once.
 
-    def __init__(self, root: str, history: RedisHistory, keep_dir: str = ""):
+    `pod_lookup(ns, name)` (the agent's API client): a directory is ingested only for a pod
+    that exists with that UID on this node -- defence in depth behind the webhook's per-
+    container subPathExpr mount; the pod's own workload annotation names the history it goes
+    to.  Files over `max_file_bytes` are not read.  With a `corun` observer
+    (agent.corun_observer.CorunObserver) each traced pod's kernel interval on its device is
+    also recorded, so pods that overlapped on one GPU become co-run observations."""
+
+    def __init__(self, root: str, history: RedisHistory, keep_dir: str = "",
+                 pod_lookup: Optional[Callable[[str, str], Optional[Dict[str, Any]]]] = None,
+                 node: str = "", corun: Any = None, max_file_bytes: int = 64 << 20):
         self.root = root
         self.history = history
         self.keep_dir = keep_dir
+        self.pod_lookup = pod_lookup
+        self.node = node
+        self.corun = corun
+        self.max_file_bytes = max_file_bytes
         self.ingested: List[Dict[str, Any]] = []
+        self.rejected: List[str] = []
 
     def _finished(self) -> List[Tuple[str, List[str]]]:
         out = []
@@ -174,10 +189,43 @@ class ProfileIngestor:
                 out.append((dirpath, rel))
         return out
 
+    def _owner(self, ns: str, name: str, uid: str) -> Tuple[bool, Optional[Dict[str, Any]]]:
+        """(accept, pod object or None)."""
+        if self.pod_lookup is None:
+            return True, None
+        try:
+            pod = self.pod_lookup(ns, name)
+        except Exception as e:          # apiserver blip: keep the directory for the next pass
+            raise RuntimeError(f"pod lookup failed: {e}") from e
+        if pod is None or O.uid(pod) != uid:
+            return False, None
+        if self.node and O.node_name_of(pod) not in ("", self.node):
+            return False, None
+        return True, pod
+
+    def _drop(self, d: str) -> None:
+        shutil.rmtree(d, ignore_errors=True)
+        # drop the now-empty parents (<uid>/<container>) so the tree does not grow
+        for up in (os.path.dirname(d), os.path.dirname(os.path.dirname(d))):
+            try:
+                os.rmdir(up)
+            except OSError:
+                break
+
     def step(self) -> int:
         from .profile_webhook import parse_tag
         n = 0
         for d, (ns, name, uid, container, tag) in self._finished():
+            try:
+                ok, owner = self._owner(ns, name, uid)
+            except RuntimeError as e:
+                log.warning("profile %s: %s", d, e)
+                continue
+            if not ok:
+                log.warning("profile %s: no pod %s/%s with uid %s on this node: dropped", d, ns, name, uid)
+                self.rejected.append(d)
+                self._drop(d)
+                continue
             sample: Dict[str, Any] = {"ts": time.time(), "pod": f"{ns}/{name}", "uid": uid, "container": container,
                                       "source": "rocprof"}
             req = parse_tag(tag)
@@ -185,6 +233,9 @@ class ProfileIngestor:
                 for f in files:
                     p = os.path.join(root, f)
                     try:
+                        if os.path.getsize(p) > self.max_file_bytes:
+                            log.warning("profile %s: %s larger than %d bytes: skipped", d, f, self.max_file_bytes)
+                            continue
                         if f.endswith("kernel_stats.csv"):
                             sample.update(summarize_kernel_stats(p))
                         elif f.endswith("kernel_trace.csv"):
@@ -204,23 +255,26 @@ class ProfileIngestor:
                 if req.get("iters"):
                     busy = sample.get("busy_union_ms") or span
                     sample["throughput"] = req["iters"] / (busy / 1e3)
-            pod = {"metadata": {"name": name, "namespace": ns, "annotations": {}}}
+            # the pod's own workload name (its annotation) when the object is known; the name
+            # rule of recommender.admission.workload_key otherwise
+            pod = owner or {"metadata": {"name": name, "namespace": ns, "annotations": {}}}
+            wl = workload_key(pod)
+            first, last = sample.pop("first_ns", None), sample.pop("last_ns", None)
             try:
-                self.history.append(workload_key(pod), sample)
+                self.history.append(wl, sample)
             except Exception as e:          # Redis blip: keep the directory for the next pass
                 log.warning("profile %s: history append failed: %s", d, e)
                 continue
+            if self.corun is not None and first is not None and last is not None and last > first:
+                try:
+                    self.corun.add(pod, wl, float(req.get("iters", 0.0)), int(first), int(last))
+                except Exception as e:
+                    log.warning("profile %s: co-run record failed: %s", d, e)
             self.ingested.append(sample)
             n += 1
             if self.keep_dir:
                 dst = os.path.join(self.keep_dir, ns, name, uid, container)
                 shutil.rmtree(dst, ignore_errors=True)
                 shutil.copytree(d, dst)
-            shutil.rmtree(d, ignore_errors=True)
-            # drop the now-empty parents (<uid>/<container>) so the tree does not grow
-            for up in (os.path.dirname(d), os.path.dirname(os.path.dirname(d))):
-                try:
-                    os.rmdir(up)
-                except OSError:
-                    break
+            self._drop(d)
         return n

@@ -10,13 +10,14 @@ the kubelet starts, but admission can rewrite what the kubelet will start:
   pod CREATE (label gpu-scheduler.amd.com/profile=trace) --> ProfileInjector.patch_ops:
     every container with an explicit `command` runs as
       rocprofv3 --kernel-trace --stats --output-format csv -o run -- <command> <args>
-                -d /gpusched-prof/<ns>/<pod>/<uid>/<container>/<tag>
+                -d /gpusched-prof/<tag>
     (the program directly after `--`: no shell, no env hop -- the profiler's preloaded
-    library must see the real program); namespace, name and UID come from the downward API
-    (a controller's pod may get its generated name after admission), <tag> records the
-    request the pod was admitted with (CU share, HBM, iterations: `cu64-hbm8-it20`), so the
-    agent can attribute a profile even after the pod object is gone; a hostPath volume
-    (/var/lib/gpusched/prof) is mounted at /gpusched-prof;
+    library must see the real program); the hostPath volume (/var/lib/gpusched/prof) is
+    mounted with `subPathExpr: <ns>/<pod>/<uid>/<container>` (namespace, name and UID from
+    the downward API: a controller's pod may get its generated name after admission), so a
+    container sees only its own directory -- it cannot read, overwrite or forge another pod's
+    profiles; <tag> records the request the pod was admitted with (CU share, HBM, iterations:
+    `cu64-hbm8-it20`), so the agent can attribute a profile even after the pod object is gone;
   the container exits --> rocprofv3 writes run_kernel_stats.csv / run_kernel_trace.csv
     into the hostPath --> the node agent (pod_profiler.ProfileIngestor, NodeAgent.step)
     summarises each finished directory into the pod's WORKLOAD history in Redis
@@ -123,7 +124,7 @@ class ProfileInjector:
                 self.stats["skipped_no_command"] += 1
                 continue
             name = ctr.get("name") or f"c{i}"
-            out = f"{MOUNT}/$({NS_ENV})/$({NAME_ENV})/$({UID_ENV})/{name}/{tag}"
+            out = f"{MOUNT}/{tag}"
             # the container args stay where they are: kubelet runs command + args, so the
             # original program and its arguments follow `--` unchanged
             ops.append({"op": "add", "path": f"/spec/containers/{i}/command",
@@ -136,7 +137,9 @@ class ProfileInjector:
             if "volumeMounts" not in ctr:
                 ops.append({"op": "add", "path": f"/spec/containers/{i}/volumeMounts", "value": []})
             ops.append({"op": "add", "path": f"/spec/containers/{i}/volumeMounts/-",
-                        "value": {"name": VOLUME, "mountPath": MOUNT}})
+                        "value": {"name": VOLUME, "mountPath": MOUNT,
+                                  # only this container's own directory of the hostPath
+                                  "subPathExpr": f"$({NS_ENV})/$({NAME_ENV})/$({UID_ENV})/{name}"}})
             wrapped.append(name)
         if not wrapped:
             return [], None

@@ -228,6 +228,15 @@ def cmd_resize_webhook(args) -> int:
     return 0
 
 
+def _corun_sender(addr: str):
+    """RecommenderClient.observe_corun for the agent's co-run observer (None: no recommender)."""
+    if not addr:
+        return None
+    from ..recommender.client import RecommenderClient
+    cl = RecommenderClient(addr)
+    return cl.observe_corun
+
+
 def _fabric_prober(args):
     """Per-pair xGMI copy-rate probe for the agent (agent.fabric): on real devices unless
     --fabric-probe off; never with --synthetic GPUs."""
@@ -270,7 +279,7 @@ def cmd_agent(args) -> int:
                       evict_hbm_overuse=args.evict_hbm_overuse, drain_timeout_s=args.drain_timeout,
                       hbm_tolerance_gib=args.hbm_tolerance, host_proc=proc_root, profile_dir=args.profile_dir,
                       partition_dry_run=args.partition_dry_run,
-                      fabric=_fabric_prober(args),
+                      fabric=_fabric_prober(args), corun_send=_corun_sender(args.corun_recommender),
                       pod_resolver=lambda pid: pod_of_pid(pid, proc_root))
     mgr = None
     if args.device_plugin:
@@ -442,6 +451,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--profile-dir", default="",
                    help="hostPath where profiled pods' rocprofv3 output lands (mounted from /var/lib/gpusched/prof; "
                         "see the resize webhook's --profile): finished runs go to the workload history in Redis")
+    s.add_argument("--corun-recommender", default=os.getenv("RECOMMENDER_ADDR", ""),
+                   help="recommender host:port: with --profile-dir, profiled pods that overlapped on one GPU are sent "
+                        "as co-run observations (ObserveCorun) for its online co-run model")
     s.add_argument("--hbm-tolerance", type=float, default=0.5,
                    help="GiB over a pod's HBM share before it counts as overuse; must cover the HIP runtime's "
                         "per-process VRAM (~0.3 GiB on MI355X), which amd-smi counts and the request does not")

@@ -23,7 +23,7 @@ import logging
 import os
 import threading
 from concurrent import futures
-from typing import Any, Callable, Optional
+from typing import Any, Callable, Dict, Optional
 
 import grpc
 import numpy as np
@@ -155,6 +155,8 @@ class RecommenderService:
         self._corun_online: Any = None      # models.corun.OnlineCorun on the served file model
         self._corun_online_base: Optional[str] = None
         self._corun_refit_mode: Any = "process"
+        # OnlineCorun knobs (from_env: CORUN_MIN_OBS, CORUN_MIN_CALIB, CORUN_REFIT_EVERY)
+        self.corun_online_kw: Dict[str, int] = {}
         self.job_delay_s = job_delay_s
         self.history_source = history_source
         self.model = model
@@ -172,9 +174,14 @@ class RecommenderService:
         co-run model, data/corun_mi355x.json)."""
         from ..models.corun import DATA as CORUN_DATA
         kw.setdefault("corun_path", os.getenv("CORUN_MODEL_PATH", CORUN_DATA))
-        return cls(os.getenv("CONFIGURATIONS_DATA_PATH", DEFAULT_CONF),
-                   os.getenv("INTERFERENCE_DATA_PATH", DEFAULT_INTF),
-                   job_delay_s=float(os.getenv("JOB_DELAY", C.RECOMMENDER_JOB_DELAY_S)), **kw)
+        svc = cls(os.getenv("CONFIGURATIONS_DATA_PATH", DEFAULT_CONF),
+                  os.getenv("INTERFERENCE_DATA_PATH", DEFAULT_INTF),
+                  job_delay_s=float(os.getenv("JOB_DELAY", C.RECOMMENDER_JOB_DELAY_S)), **kw)
+        for env, k in (("CORUN_MIN_OBS", "min_obs"), ("CORUN_MIN_CALIB", "min_calib"),
+                       ("CORUN_REFIT_EVERY", "refit_every")):
+            if os.getenv(env):
+                svc.corun_online_kw[k] = int(os.environ[env])
+        return svc
 
     # ------------------------------------------------------------------ training loop
     def train(self) -> None:
@@ -344,7 +351,8 @@ class RecommenderService:
                 # the served model may already be an online one: learn on the file's model
                 from ..models.corun import CorunModel
                 fm = CorunModel.load(self.corun.path) if self.corun.path else base
-                self._corun_online = OnlineCorun(fm or base, background=self._corun_refit_mode)
+                self._corun_online = OnlineCorun(fm or base, background=self._corun_refit_mode,
+                                                 **self.corun_online_kw)
                 self._corun_online_base = self.corun.file_version
             on = self._corun_online
             for g in request.groups:

@@ -1,0 +1,125 @@
+"""The deployed co-run learning loop: profiled pods that overlapped on one GPU -> the node
+agent's co-run observer -> the recommender's ObserveCorun (online refit) -> a new served
+ExportTable("corun") version -> the scheduler's GPU plugin scoring on it.
+
+Reference analog superseded: the recommender retrains only when its training files change
+(reference pkg/recommender/recom_server.py:74-134); nothing in a cluster produces data."""
+import os
+import shutil
+
+import numpy as np
+
+from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+from k8s_gpu_scheduler_amd.agent.corun_observer import CorunObserver
+from k8s_gpu_scheduler_amd.agent.devices import synthetic_node
+from k8s_gpu_scheduler_amd.api import constants as C
+from k8s_gpu_scheduler_amd.api import objects as O
+from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+from k8s_gpu_scheduler_amd.models.corun import DATA, CorunModel
+from k8s_gpu_scheduler_amd.recommender.client import CachedPredictions, RecommenderClient
+from k8s_gpu_scheduler_amd.recommender.service import RecommenderService
+from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+from k8s_gpu_scheduler_amd.store.resp import Redis
+
+UUID = "GPU-aaaaaaaa-0000-0000-0000-000000000001"
+
+
+def _trace_dir(root, pod, tag, t0_ns, t1_ns, n_kernels=8):
+    d = os.path.join(root, O.namespace(pod), O.name(pod), O.uid(pod), "main", tag)
+    os.makedirs(d)
+    with open(os.path.join(d, "run_kernel_stats.csv"), "w") as f:
+        f.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage"\n"k",8,1000,125,100.0\n')
+    step = (t1_ns - t0_ns) // n_kernels
+    with open(os.path.join(d, "run_kernel_trace.csv"), "w") as f:
+        f.write('"Kernel_Name","Start_Timestamp","End_Timestamp"\n')
+        for i in range(n_kernels):
+            a = t0_ns + i * step
+            f.write(f'"k",{a},{t1_ns if i == n_kernels - 1 else a + step - 1000}\n')
+    return d
+
+
+def _pod(fc, name, uuid=UUID, phase="Succeeded"):
+    p = O.make_pod(name, gpu_cu=64, gpu_mem_gib=4, env={C.ENV_ITERATIONS: "20"}, node_name="n1", phase=phase)
+    p["metadata"].setdefault("annotations", {})[C.ANNOT_DEVICES] = uuid
+    fc.create("pods", p)
+    return fc.get("pods", name, "default")
+
+
+def test_observer_groups_overlapping_pods_and_waits_for_running_corunners():
+    sent = []
+    running = {"default/b"}
+    ob = CorunObserver(sent.append, running_on=lambda u: set(running) if u == UUID else set(), settle_s=0.0)
+    a = {"metadata": {"name": "a", "namespace": "default", "annotations": {C.ANNOT_DEVICES: UUID}}}
+    b = {"metadata": {"name": "b", "namespace": "default", "annotations": {C.ANNOT_DEVICES: UUID}}}
+    c = {"metadata": {"name": "c", "namespace": "default", "annotations": {C.ANNOT_DEVICES: "GPU-other"}}}
+    assert ob.add(a, "onnx_resnet50_1024", 20, 0, 10_000_000)
+    assert ob.add(c, "onnx_mobilenet_1024", 20, 0, 10_000_000)        # another GPU: its own group
+    assert ob.step() == 1 and ob.pending() == 1          # a waits: b ran next to it and is still running
+    running.clear()
+    assert ob.add(b, "onnx_mobilenet_2048", 20, 4_000_000, 16_000_000)
+    assert ob.step() == 2
+    groups = [g for batch in sent for g in batch]
+    ga = next(g for g in groups if "onnx_resnet50_1024" in g["workloads"]
+              and g["target"][g["workloads"].index("onnx_resnet50_1024")])
+    assert sorted(ga["workloads"]) == ["onnx_mobilenet_2048", "onnx_resnet50_1024"]
+    i = ga["workloads"].index("onnx_mobilenet_2048")
+    assert ga["start_ms"][i] == 4.0 and ga["ms"][i] == 12.0 and ga["target"] == [x == "onnx_resnet50_1024"
+                                                                                for x in ga["workloads"]]
+
+
+def test_observer_drops_a_target_whose_corunner_left_no_trace():
+    running = {"default/unprofiled"}
+    ob = CorunObserver(lambda g: None, running_on=lambda u: set(running), settle_s=0.0)
+    a = {"metadata": {"name": "a", "namespace": "default", "annotations": {C.ANNOT_DEVICES: UUID}}}
+    ob.add(a, "onnx_resnet50_1024", 20, 0, 10_000_000)
+    running.clear()                                       # finished, never traced
+    assert ob.step() == 0 and ob.dropped == 1
+
+
+def test_profiled_pods_on_one_gpu_refine_the_served_model_and_the_scheduler_scores_on_it(tmp_path):
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=1))
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    cm = tmp_path / "corun.json"
+    shutil.copy(DATA, cm)
+    svc = RecommenderService("", "", corun_path=str(cm))
+    svc._corun_refit_mode = False                       # refit synchronously in the test
+    svc.corun_online_kw = {"min_obs": 8, "min_calib": 8, "refit_every": 8}
+    svc.train()
+    srv, port = svc.make_server(0, 2, "127.0.0.1")
+    try:
+        cl = RecommenderClient(f"127.0.0.1:{port}")
+        v0 = cl.version().corun
+        base = CorunModel.load(str(cm))
+        slow = CorunModel(base.names, base.alone_ms * 1.3, base.u, base.v)      # this node runs 30 % slower
+        root = str(tmp_path / "prof")
+        ag = NodeAgent("n1", r, synthetic_node(1, node="n1"), client=fc, profile_dir=root,
+                       corun_send=cl.observe_corun)
+        ag.corun.settle_s = 0.0
+        pairs = [("onnx_resnet50_1024", "onnx_mobilenet_2048"), ("tensorflow_resnet50_1024", "onnx_ssd_mobilenet_1024"),
+                 ("onnx_mobilenet_1024", "tensorflow_mobilenet_2048")] * 4
+        t = 1_000_000_000
+        for k, (wa, wb) in enumerate(pairs):
+            ia, ib = base.wid(wa), base.wid(wb)
+            fin = slow.group_times([ia, ib], [20, 20], [0.0, 1.0])          # b starts 1 ms after a
+            pa = _pod(fc, f"{wa.replace('_', '-')}-{k}")
+            pb = _pod(fc, f"{wb.replace('_', '-')}-{k}")
+            _trace_dir(root, pa, "cu64-hbm4-it20", t, t + int(fin[0] * 1e6))
+            _trace_dir(root, pb, "cu64-hbm4-it20", t + 1_000_000, t + int(fin[1] * 1e6))
+            t += int(max(fin) * 1e6) + 5_000_000                             # groups do not overlap
+        ag.step()
+        assert ag.corun.sent == 2 * len(pairs) and ag.corun.dropped == 0
+        v1 = cl.version().corun
+        assert v1 != v0 and "+online-" in v1
+        cache = CachedPredictions(cl, background=False)
+        cache.refresh(force=True)
+        m = cache.corun()
+        assert m.version == v1
+        assert float(np.median(m.alone_ms / base.alone_ms)) > 1.15        # learned: the node is slower
+        # the scheduler's GPU plugin scores with the served refined model
+        from k8s_gpu_scheduler_amd.plugins.gpu.plugin import GPUPlugin
+        plugin = GPUPlugin({"sloObjective": "corun"}, predictions=cache)
+        assert plugin.corun_model().version == v1
+    finally:
+        svc.stop()
+        srv.stop(0)

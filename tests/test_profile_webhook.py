@@ -49,12 +49,14 @@ def test_injector_wraps_opted_in_container_program_after_double_dash():
     i = cmd.index("--")
     assert cmd[i + 1:] == ARGV[:3] and ctr["args"] == ARGV[3:]       # program right after --
     d = cmd[cmd.index("-d") + 1]
-    assert d == "/gpusched-prof/$(GPUSCHED_POD_NAMESPACE)/$(GPUSCHED_POD_NAME)/$(GPUSCHED_POD_UID)/" \
-                "main/cu64-hbm8-it20"
+    assert d == "/gpusched-prof/cu64-hbm8-it20"
     envs = {e["name"]: e for e in ctr["env"]}
     assert envs[PW.UID_ENV]["valueFrom"]["fieldRef"]["fieldPath"] == "metadata.uid"
     assert envs[C.ENV_ITERATIONS]["value"] == "20"                  # the pod's own env kept
-    assert {"name": PW.VOLUME, "mountPath": PW.MOUNT} in ctr["volumeMounts"]
+    # the container sees only its own <ns>/<pod>/<uid>/<container> directory of the hostPath
+    assert {"name": PW.VOLUME, "mountPath": PW.MOUNT,
+            "subPathExpr": "$(GPUSCHED_POD_NAMESPACE)/$(GPUSCHED_POD_NAME)/$(GPUSCHED_POD_UID)/main"} \
+        in ctr["volumeMounts"]
     vol = next(v for v in got["spec"]["volumes"] if v["name"] == PW.VOLUME)
     assert vol["hostPath"] == {"path": PW.HOST_DIR, "type": "DirectoryOrCreate"}
     assert O.annotations(got)[PW.ANNOT_PROFILED] == "main"
@@ -188,7 +190,7 @@ def test_kernel_trace_summary_merges_overlaps(tmp_path):
     p = tmp_path / "t.csv"
     p.write_text('"Start_Timestamp","End_Timestamp"\n0,4000000\n1000000,2000000\n5000000,6000000\n')
     s = summarize_kernel_trace(str(p))
-    assert s == {"span_ms": 6.0, "busy_union_ms": 5.0}
+    assert s == {"span_ms": 6.0, "busy_union_ms": 5.0, "first_ns": 0, "last_ns": 6000000}
 
 
 def test_webhook_handler_fails_open():
