@@ -39,6 +39,8 @@ def _serve(conn: Any, kwargs: dict) -> None:
             cp.reset_stats()
         elif kind == "interference_mae":
             conn.send(("interference_mae", cp.interference_mae()))
+        elif kind == "planner_stats":
+            conn.send(("planner_stats", cp.planner_stats()))
         elif kind == "stop":
             conn.close()
             return
@@ -96,6 +98,16 @@ class ControlPlaneProc:
                 raise RuntimeError(f"control-plane process exited (code {self._p.exitcode})")
         msg = self._conn.recv()
         return msg[1] if msg[0] == "interference_mae" else None
+
+    def planner_stats(self):
+        while self._outstanding > 0:
+            self.get_schedule()
+        self._conn.send(("planner_stats",))
+        while not self._conn.poll(1.0):
+            if not self._p.is_alive():
+                raise RuntimeError(f"control-plane process exited (code {self._p.exitcode})")
+        msg = self._conn.recv()
+        return msg[1] if msg[0] == "planner_stats" else None
 
     def close(self) -> None:
         try:

@@ -36,6 +36,7 @@ class PodRun:
     start: Optional[torch.cuda.Event] = None
     end: Optional[torch.cuda.Event] = None
     ms: float = 0.0
+    gpu: int = 0                 # the node's GPU index (simulated executors keep one pipeline per GPU)
 
     @property
     def throughput(self) -> float:
@@ -58,6 +59,28 @@ class _Buffers:
                 y = torch.ones(o.n_floats, dtype=torch.float32, device=device)
                 z = torch.ones(o.n_floats, dtype=torch.float32, device=device)
                 self.ops.append((o, (x, y, z)))
+
+
+def lpt_balance(runs: List[PodRun], slot_work: Dict[Tuple[int, int], float], work=None) -> None:
+    """Reassign the slots of each group of same-size Burstable pods of this epoch: longest pod
+    first onto the slot with the least cumulative work (ties: the lower slot).  `slot_work`
+    ((first unit, units) -> cumulative work) is the caller's running state."""
+    work = work or DeviceExecutor.pod_work
+    groups: Dict[int, List[PodRun]] = {}
+    for r in runs:
+        if not r.masked:
+            groups.setdefault(r.n_units, []).append(r)
+    for n, rs in groups.items():
+        if len(rs) < 2:
+            continue
+        slots = sorted(r.first_unit for r in rs)
+        if len(set(slots)) != len(slots):
+            continue
+        for r in sorted(rs, key=work, reverse=True):
+            u = min(slots, key=lambda s: (slot_work.get((s, n), 0.0), s))
+            slots.remove(u)
+            r.first_unit = u
+            slot_work[(u, n)] = slot_work.get((u, n), 0.0) + work(r)
 
 
 class DeviceExecutor:
@@ -213,23 +236,7 @@ class DeviceExecutor:
         return roofline_seconds(CATALOG[r.workload], 1.0) * max(r.iters, 1)
 
     def _balance(self, runs: List[PodRun]) -> None:
-        """Reassign the slots of each group of same-size Burstable pods of this epoch: longest
-        pod first onto the slot with the least cumulative work (ties: the lower slot)."""
-        groups: Dict[int, List[PodRun]] = {}
-        for r in runs:
-            if not r.masked:
-                groups.setdefault(r.n_units, []).append(r)
-        for n, rs in groups.items():
-            if len(rs) < 2:
-                continue
-            slots = sorted(r.first_unit for r in rs)
-            if len(set(slots)) != len(slots):
-                continue
-            for r in sorted(rs, key=self.pod_work, reverse=True):
-                u = min(slots, key=lambda s: (self._slot_work.get((s, n), 0.0), s))
-                slots.remove(u)
-                r.first_unit = u
-                self._slot_work[(u, n)] = self._slot_work.get((u, n), 0.0) + self.pod_work(r)
+        lpt_balance(runs, self._slot_work, self.pod_work)
 
     # host poll period while waiting for an epoch's end events
     poll_s = 20e-6

@@ -61,10 +61,11 @@ COST0 = 4
 POD0 = COST0 + 2 * len(W.NAMES)
 # busy_unit_ms, pods, slo_ok, hbm_gib, then per workload: (s/iter sum, pods), then per pod of
 # this GPU's epoch: (workload id or -1, achieved iterations/s, start ms, end ms on the rank's
-# executor clock; -1 = no timeline, the group ran isolated) -- the co-run observations the
-# online interference / co-run models learn from; last, amd-smi's view of the GPU over the
-# epoch (gfx activity 0..1, VRAM used GiB; -1 = no amd-smi sample)
-POD_F = 4
+# executor clock; -1 = no timeline, the group ran isolated; first CU-slice unit) -- the co-run
+# observations the online interference / co-run models learn from and the planner's slot
+# timelines; last, amd-smi's view of the GPU over the epoch (gfx activity 0..1, VRAM used GiB;
+# -1 = no amd-smi sample)
+POD_F = 5
 SMI0 = POD0 + POD_F * MAX_PODS_GPU
 TELE = SMI0 + 2
 
@@ -105,7 +106,8 @@ class ControlPlane:
                  plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0,
                  online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
-                 plan_feedback: bool = True):
+                 plan_feedback: bool = True, plan_slots: bool = False, slot_spread_ms: float = 2.0,
+                 slot_sigma: float = 0.2):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -133,7 +135,8 @@ class ControlPlane:
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
                 "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement,
                 "slo_objective": slo_objective, "corun_margin": corun_margin, "corun_sigma": corun_sigma,
-                "plan_carry": plan_carry}
+                "plan_carry": plan_carry, "plan_slots": plan_slots, "slot_spread_ms": slot_spread_ms,
+                "slot_sigma": slot_sigma}
         if policy == "random":
             args.update({"pack": "random", "seed": seed})
         # balance > 0: pods carry ITERATIONS, GPU is also the queueSort plugin (longest
@@ -153,7 +156,10 @@ class ControlPlane:
         conf = self.predictions._conf
         self.quarter_tput = {n: conf.by_label[n][f"{C.MI355X_CUS // cu_per_pod}P_{C.MI355X}"] for n in W.NAMES}
         self.online = None
-        if learn_interference and self.predictions._intf is not None:
+        # the reference-style pairwise table learns online only where Score uses it: under the
+        # co-run objective it is superseded (and its online fit was worse than its prior over a
+        # 20-step window, BENCH_r03.json interference_mae)
+        if learn_interference and slo_objective == "terms" and self.predictions._intf is not None:
             from ..recommender.online import OnlineInterference
             from ..recommender.tables import find_index_for_request
             tab = self.predictions._intf
@@ -309,6 +315,36 @@ class ControlPlane:
             if g in pred:
                 planner.correct((NODE, g), busy - pred[g])
 
+    def _feed_timeline(self, pods: np.ndarray) -> None:
+        """Measured pod intervals (executor clock) into the planner's slot timelines: each
+        pins its pod on the GPU's pipeline, so the next slot plans simulate from what ran."""
+        planner = getattr(self.plugin, "planner", None)
+        tl = getattr(planner, "timeline", None)
+        if tl is None:
+            return
+        for g in range(pods.shape[0]):
+            for r in pods[g].reshape(MAX_PODS_GPU, POD_F):
+                if r[0] >= 0 and r[2] >= 0 and r[3] > r[2]:
+                    tl.measure((NODE, g), int(r[4]), float(r[2]), float(r[3]))
+
+    def planner_stats(self) -> Optional[Dict[str, Any]]:
+        planner = getattr(self.plugin, "planner", None)
+        if planner is None:
+            return None
+        st = dict(planner.stats)
+        n = max(st.get("slot_plans", 0), 1)
+        for k in ("slot_spread_ms", "slot_min_spread_ms"):
+            st[k] = round(st[k] / n, 3)
+        st["slot_expected_met_pct"] = round(100.0 * st.pop("slot_expected_met") / max(st["slot_pods"], 1), 2)
+        tl = getattr(planner, "timeline", None)
+        if tl is not None:
+            st["timeline_measured"] = tl.measured
+            st["timeline_unmatched"] = tl.unmatched
+        if planner.backlog:
+            b = list(planner.backlog.values())
+            st["backlog_spread_ms"] = round(max(b) - min(b), 3)
+        return st
+
     def _observe_corun(self, g: int, rec: List[Any]) -> None:
         base = self.corun.base
         if not rec:
@@ -369,6 +405,7 @@ class ControlPlane:
                 self._learn_interference(per_gpu[:, POD0:SMI0])
             if self.plan_feedback:
                 self._plan_feedback(per_gpu[:, POD0:SMI0])
+            self._feed_timeline(per_gpu[:, POD0:SMI0])
         for st in self.ledger.devices(NODE):
             g = st.device.gpu
             if g >= len(per_gpu):
@@ -457,9 +494,9 @@ class SimExecutor:
 
 
 def _pod_rows(runs: List[Any], ref: Any = None) -> List[float]:
-    """(workload id, achieved iterations/s, start ms, end ms) of up to MAX_PODS_GPU pods of one
-    GPU's epoch, times on the clock of `ref` (a HIP event of the executor; None = no
-    timeline: start = end = -1); (-1, 0, -1, -1) pads."""
+    """(workload id, achieved iterations/s, start ms, end ms, first unit) of up to MAX_PODS_GPU
+    pods of one GPU's epoch, times on the clock of `ref` (a HIP event of the executor; None = no
+    timeline: start = end = -1); (-1, 0, -1, -1, -1) pads."""
     out: List[float] = []
     rs = runs[:MAX_PODS_GPU]
     for r in rs:
@@ -469,8 +506,8 @@ def _pod_rows(runs: List[Any], ref: Any = None) -> List[float]:
                 t0, t1 = ref.elapsed_time(r.start), ref.elapsed_time(r.end)
             except Exception:
                 t0 = t1 = -1.0
-        out += [float(W.INDEX[r.workload]), float(r.throughput), float(t0), float(t1)]
-    return out + [-1.0, 0.0, -1.0, -1.0] * (MAX_PODS_GPU - len(rs))
+        out += [float(W.INDEX[r.workload]), float(r.throughput), float(t0), float(t1), float(r.first_unit)]
+    return out + [-1.0, 0.0, -1.0, -1.0, -1.0] * (MAX_PODS_GPU - len(rs))
 
 
 def _cost_rows(runs: List[Any]) -> np.ndarray:
@@ -526,6 +563,29 @@ def _smi_report(rows: List[List[float]], period_ms: float) -> Optional[Dict[str,
             "period_ms": period_ms}
 
 
+def _effective_config(a: Any) -> Dict[str, Any]:
+    """The policy knobs this run's code path actually reads (a knob the default path ignores
+    is left out, so the recorded config can be audited against what ran)."""
+    corun = a.slo_objective == "corun"
+    planned = bool(a.plan_bursts) and a.policy != "random"
+    out: Dict[str, Any] = {"balance": a.balance, "slo_objective": a.slo_objective, "plan_bursts": int(planned),
+                           "slot_balance": a.slot_balance}
+    if planned:
+        out["plan_tolerance"] = a.plan_tolerance
+        if corun:
+            out.update(corun_sigma=a.corun_sigma, plan_carry=a.plan_carry,
+                       plan_feedback=a.plan_feedback if a.plan_carry > 0 else 0, plan_slots=a.plan_slots)
+            if a.plan_slots:
+                out.update(slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
+        else:
+            out["plan_objective"] = a.plan_objective
+    elif corun:
+        out["corun_sigma"] = a.corun_sigma
+    if not corun:
+        out["online_scale"] = a.online_scale          # the pairwise table's online learner
+    return out
+
+
 def _runs_for(arr: np.ndarray, gpu: int):
     from .executor import PodRun
     out = []
@@ -533,7 +593,7 @@ def _runs_for(arr: np.ndarray, gpu: int):
         g, u0, n, wid, iters, slo_m, masked = (int(x) for x in row)
         if g != gpu or g < 0:
             continue
-        out.append(PodRun(i, W.NAMES[wid], u0, n, iters, slo_m / 1000.0, masked=bool(masked)))
+        out.append(PodRun(i, W.NAMES[wid], u0, n, iters, slo_m / 1000.0, masked=bool(masked), gpu=g))
     return out
 
 
@@ -566,6 +626,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--sim-timed", action="store_true",
                     help="simulated executor sleeps out a modelled device time per epoch (multi-rank CPU rehearsal)")
     ap.add_argument("--sim-scale", type=float, default=1.0, help="modelled device-time multiplier (--sim-timed)")
+    ap.add_argument("--sim-model", action="store_true",
+                    help="with --sim: the bench's slot pipeline simulated with the co-run model (parallel.modelpipe); "
+                         "pods/s and SLO attainment on the simulated clock")
+    ap.add_argument("--sim-noise", type=float, default=0.05, help="--sim-model: per-pod lognormal work noise sigma")
+    ap.add_argument("--sim-perturb", type=float, default=0.0,
+                    help="--sim-model: lognormal sigma on the truth's u / v (a GPU the scheduler's model does not know)")
     ap.add_argument("--plan-bursts", type=int, default=1, choices=[0, 1],
                     help="1 (default): plan each epoch's burst of pods jointly.  With the co-run model "
                          "(--slo-objective corun): balanced predicted group makespans, then the most predicted "
@@ -592,6 +658,15 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
                     help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
                          "collected epoch (a GPU slower than its siblings, or the model's error on it)")
+    ap.add_argument("--plan-slots", type=int, default=0, choices=[0, 1],
+                    help="co-run planner: also choose each pod's CU slot by simulating its GPU's slot pipelines "
+                         "(in-flight pods of earlier epochs, measured ones pinned)")
+    ap.add_argument("--slot-spread-ms", type=float, default=2.0,
+                    help="--plan-slots: how far (ms) the slots' predicted ends may spread beyond the most even "
+                         "assignment's to meet more SLOs")
+    ap.add_argument("--slot-sigma", type=float, default=0.2,
+                    help="--plan-slots: log error of the slot plan's predicted pod times (its co-runners are partly "
+                         "pods placed later: ~0.2 on MI355X bench traces)")
     ap.add_argument("--plan-objective", default="load", choices=["load", "slo"],
                     help="burst planner: 'load' = lowest interference-adjusted load of the busiest GPU first, "
                          "'slo' = most predicted SLOs met first (within --plan-tolerance)")
@@ -602,6 +677,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--balance", type=float, default=1.0,
                     help="weight of the GPU plugin's least-predicted-load term (0 = off; >0 also sorts the "
                          "queue longest-predicted-work first)")
+    ap.add_argument("--slot-balance", type=int, default=int(os.environ.get("GPUSCHED_BALANCE_SLOTS", "1")),
+                    choices=[0, 1],
+                    help="1: the executor re-slots each epoch's Burstable pods longest-first onto the least-loaded "
+                         "CU slot (blind to SLOs); 0: pods run on the slot the scheduler chose")
     ap.add_argument("--no-cu-mask", action="store_true")
     ap.add_argument("--qos", default="burstable", choices=["burstable", "guaranteed"],
                     help="burstable: CU request is an accounted share, kernels may use idle CUs; "
@@ -680,7 +759,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      policy=a.policy, qos=a.qos, balance=a.balance, plan_bursts=bool(a.plan_bursts),
                      plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective,
                      online_scale=bool(a.online_scale), slo_objective=a.slo_objective, corun_sigma=a.corun_sigma,
-                     plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback))
+                     plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=bool(a.plan_slots),
+                     slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -732,8 +812,13 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         _native.hip(required=True).set_triad_variant(a.triad_variant)
         ex.triad_blocks = a.triad_blocks
         ex.gemm_share = bool(a.gemm_share)
+    elif a.sim_model:
+        from .modelpipe import ModelPipelineExecutor
+        ex = ModelPipelineExecutor(noise=a.sim_noise, perturb=a.sim_perturb, seed=a.seed + 1000 * rank)
     else:
         ex = SimExecutor(timed=a.sim_timed, scale=a.sim_scale)
+    if hasattr(ex, "balance_slots"):
+        ex.balance_slots = bool(a.slot_balance)
     smi_s = None
     if use_gpu and a.smi_period_ms > 0:
         from ..telemetry.smi_sampler import ActivitySampler
@@ -798,7 +883,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                     intervals.append((ref["ev"].elapsed_time(r.start), ref["ev"].elapsed_time(r.end)))
                     if trace is not None:   # GPUSCHED_BENCH_TRACE: per-pod timeline of the timed region
                         trace.append((state.get("collected", 0), r.first_unit, r.workload, intervals[-1][0],
-                                      intervals[-1][1], (time.perf_counter() - t_start) * 1e3))
+                                      intervals[-1][1], (time.perf_counter() - t_start) * 1e3, r.slo))
         if timed:
             state["collected"] = state.get("collected", 0) + 1
         t_post = time.perf_counter()
@@ -826,7 +911,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                                    W.CATALOG[r.workload].hbm_gib)
                 per_gpu[g, COST0:POD0] += _cost_rows([r]).ravel()
             for g in range(n_gpus):
-                per_gpu[g, POD0:SMI0] = _pod_rows([r for r in runs if int(arr[r.pod_id][0]) == g])
+                per_gpu[g, POD0:SMI0] = _pod_rows([r for r in runs if int(arr[r.pod_id][0]) == g],
+                                                  getattr(ex, "clock", None))
         else:
             per_gpu = np.asarray(vec, dtype=np.float64)[None, :]
         if rank == 0:
@@ -891,6 +977,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             ref["ev"].synchronize()
             ref["host_ms"] = (time.perf_counter() - t_start) * 1e3
     flops0, bytes0 = ex.flops_done, ex.bytes_done
+    sim_t0 = getattr(ex, "elapsed_ms", None)
     if rank == 0:
         cp.reset_stats()
     run_epochs(a.steps, True)
@@ -914,7 +1001,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                           ("gfx_activity_pct_mean", "umc_activity_pct_mean", "power_w_mean", "vram_used_mb_max",
                            "gfx_activity_pct_max", "samples")], dtype=torch.float64, device=dev)
     if not use_gpu:
-        # simulated executor: wall time = modelled device time of each epoch (+ host time)
+        # simulated executor: wall time = modelled device time of each epoch (+ host time);
+        # the model pipeline reports its simulated clock
+        if sim_t0 is not None:
+            elapsed = (ex.elapsed_ms - sim_t0) / 1e3
         elapsed = max(elapsed, 1e-9)
     busy_ms = _union_ms(intervals)
     # roofline floor of this rank's work: its GEMM FLOPs at the MFMA rate or its modelled HBM
@@ -958,10 +1048,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "config": {"model": "bin-pack fractional-GPU pods onto MI355X by live HBM/CU-util (Score path)",
                        "global_batch": P, "seq_len": a.iters, "parallelism": f"dp{n_gpus}",
                        "pods_per_gpu": a.pods_per_gpu, "cu_per_pod": 64, "policy": a.policy, "qos": a.qos,
-                       "balance": a.balance, "plan_bursts": a.plan_bursts,
-                       "plan_tolerance": a.plan_tolerance, "plan_objective": a.plan_objective,
-                       "online_scale": a.online_scale, "slo_objective": a.slo_objective, "corun_sigma": a.corun_sigma,
-                       "plan_carry": a.plan_carry, "plan_feedback": a.plan_feedback,
+                       **_effective_config(a),
                        # which code path N=1 took: collectives over a 1-rank group or the plain path
                        "collectives": bool(dist_on), "dist_single": a.dist_single,
                        **({"collectives_note": dist_note} if dist_note else {}),
@@ -985,6 +1072,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "slo_attainment_pct": round(100.0 * totals["slo_ok"] / max(totals["pods"], 1), 2),
             "sched_ms_per_pod": round(cp.sched_s / max(totals["pods"], 1) * 1e3, 4),
             "interference_mae": cp.interference_mae(),
+            "planner": cp.planner_stats(),
             "unscheduled": cp.unscheduled,
             "host_ms_per_step_rank0": {k: round(v / a.steps * 1e3, 3) for k, v in host.items()},
             "host_ms_per_step_by_rank": [{k: round(float(v), 3) for k, v in zip(hkeys, t.cpu().tolist())}

@@ -135,6 +135,13 @@ class GPUArgs:
     # 0 = every burst planned on its own).  In a pipelined multi-GPU job the busiest GPU's
     # CUMULATIVE work paces the run, and per-burst slack for SLOs otherwise random-walks
     plan_carry: float = 0.0
+    # co-run planner: also choose each planned pod's CU slot on its GPU, simulating the GPU's
+    # slot pipelines (in-flight pods of earlier placements, measured ones pinned; see
+    # plugins.gpu.timeline) -- the most expected SLOs met among slot assignments whose slot
+    # ends stay within slotSpreadMs of the most even assignment's
+    plan_slots: bool = False
+    slot_spread_ms: float = 2.0
+    slot_sigma: float = 0.2
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
     model: str = C.MI355X
     default_cu: int = 64              # implied request for SLO-only pods (reference-style pods)
@@ -168,7 +175,7 @@ class GPUArgs:
                  "lptWindowSeconds": "lpt_window_s",
                  "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
                  "planObjective": "plan_objective", "sloObjective": "slo_objective", "corunMargin": "corun_margin", "corunSigma": "corun_sigma",
-                 "planCarry": "plan_carry",
+                 "planCarry": "plan_carry", "planSlots": "plan_slots", "slotSpreadMs": "slot_spread_ms", "slotSigma": "slot_sigma",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle",
@@ -219,7 +226,9 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if self.args.plan_bursts:
             from .planner import BurstPlanner
             self.planner = BurstPlanner(self, self.args.plan_tolerance, objective=self.args.plan_objective,
-                                        carry=self.args.plan_carry)
+                                        carry=self.args.plan_carry, slots=bool(self.args.plan_slots),
+                                        spread_ms=float(self.args.slot_spread_ms),
+                                        slot_sigma=float(self.args.slot_sigma))
         self._pred_version: Any = None
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)
@@ -527,11 +536,16 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
 
     def _planned_choice(self, state: CycleState, req: GpuRequest, node: str, plan: Any) -> Optional[Choice]:
         """The plan's device on its node as a top-scored Choice, if it is still a candidate."""
-        pnode, puuid = plan
+        pnode, puuid = plan[0], plan[1]
+        pu0 = plan[2] if len(plan) > 2 else None
         if node != pnode:
             return None
         for st, u0 in (state.read(_CANDS) or {}).get(node) or []:
             if st.device.uuid == puuid:
+                # the planned CU slot when it is still free (else the ledger's best fit)
+                if pu0 is not None and pu0 + req.units <= len(st.used_units) and \
+                        not any(st.used_units[pu0:pu0 + req.units]):
+                    u0 = pu0
                 return Choice(node, [(puuid, u0, req.units, req.hbm_gib, False)], float(C.MAX_NODE_SCORE),
                               [st.device])
         return None
@@ -579,6 +593,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return Status.unschedulable("GPU capacity changed before reserve", self.NAME)
         state.write(_CHOICE + "/reserved", choice)
         if self.planner is not None:
+            self.planner.placed(pod, node_name, choice, req)
             self.planner.consume(O.key(pod))
         return None
 

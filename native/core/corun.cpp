@@ -18,7 +18,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
+#include <unordered_map>
 #include <vector>
 
 namespace py = pybind11;
@@ -79,6 +82,81 @@ void sim_group(int k, const int32_t* w, const double* iters, const double* start
       if (!started[i]) dt = std::min(dt, st[i] - now);
       else if (pin[i] && !done[i]) dt = std::min(dt, pe[i] - now);
     }
+    for (int i = 0; i < k; ++i)
+      if (started[i] && !done[i] && !svc[i] && !pin[i]) rem[i] -= rate[i] * dt;
+    now += dt;
+    for (int i = 0; i < k; ++i) {
+      if (!started[i] || done[i] || svc[i] || pin[i]) continue;
+      const double wk = alone[w[i]] * iters[i];
+      if (rem[i] <= 1e-9 * std::max(wk, 1.0) || (i == am && am_t <= dt + 1e-12)) {
+        done[i] = true;
+        fin[i] = now;
+      }
+    }
+  }
+}
+
+// Pipeline simulation of one GPU: members are chained per CU slot -- member i with prev[i] >= 0
+// starts the moment member prev[i] finishes (a slot's stream runs its pods back to back, the
+// executor's launch-ahead pipeline), but not before start[i] (its release: when the host
+// enqueued it; pass a very negative value for none); a member with prev[i] < 0 at start[i].  Pinned members
+// (pin_end[i] > start[i], prev[i] < 0) are present exactly in [start, pin_end): measured
+// intervals of pods that already ran.  st_out[i] / fin[i] = predicted start / finish (kBig when
+// it never starts, e.g. chained behind a service).
+void sim_chain(int k, const int32_t* w, const double* iters, const double* start, const int32_t* prev,
+               const double* alone, const double* C, int W, double* st_out, double* fin,
+               const double* pin_end = nullptr) {
+  double rem[kMaxK];
+  bool started[kMaxK], done[kMaxK], svc[kMaxK], pin[kMaxK], known[kMaxK];
+  double now = kBig;
+  for (int i = 0; i < k; ++i) {
+    svc[i] = iters[i] <= 0;
+    known[i] = prev[i] < 0;
+    st_out[i] = known[i] ? start[i] : kBig;
+    pin[i] = known[i] && pin_end && pin_end[i] > start[i];
+    rem[i] = (svc[i] || pin[i]) ? kBig : std::max(alone[w[i]] * iters[i], 1e-12);
+    started[i] = done[i] = false;
+    fin[i] = pin[i] ? pin_end[i] : kBig;
+    if (known[i]) now = std::min(now, st_out[i]);
+  }
+  if (now >= kBig) return;
+  for (int step = 0; step < 4 * k + 2; ++step) {
+    bool live = false;
+    for (int i = 0; i < k; ++i) live |= !done[i] && !svc[i] && !pin[i];
+    if (!live) break;
+    for (int i = 0; i < k; ++i) {
+      if (started[i]) continue;
+      if (!known[i] && done[prev[i]]) {
+        known[i] = true;
+        st_out[i] = std::max(fin[prev[i]], start[i]);
+      }
+      if (known[i] && st_out[i] <= now + 1e-12) started[i] = true;
+    }
+    for (int i = 0; i < k; ++i)
+      if (pin[i] && started[i] && !done[i] && fin[i] <= now + 1e-12) done[i] = true;
+    double rate[kMaxK];
+    int am = -1;
+    double am_t = kBig;
+    for (int i = 0; i < k; ++i) {
+      rate[i] = 0.0;
+      if (!started[i] || done[i] || pin[i]) continue;
+      double load = 1.0;
+      const double* ci = C + (size_t)w[i] * W;
+      for (int j = 0; j < k; ++j)
+        if (j != i && started[j] && !done[j]) load += ci[w[j]];
+      rate[i] = 1.0 / load;
+      if (!svc[i]) {
+        const double t = rem[i] / std::max(rate[i], 1e-30);
+        if (t < am_t) am_t = t, am = i;
+      }
+    }
+    double dt = am_t;
+    for (int i = 0; i < k; ++i) {
+      if (!started[i] && known[i]) dt = std::min(dt, st_out[i] - now);
+      else if (pin[i] && started[i] && !done[i]) dt = std::min(dt, fin[i] - now);
+    }
+    if (dt >= kBig) break;          // nothing left that can progress (chained behind a service)
+    dt = std::max(dt, 0.0);
     for (int i = 0; i < k; ++i)
       if (started[i] && !done[i] && !svc[i] && !pin[i]) rem[i] -= rate[i] * dt;
     now += dt;
@@ -300,9 +378,15 @@ py::tuple corun_groups_eval(I64 off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alon
 // tolerance x its longest makespan: a GPU that took extra work for SLOs in one burst gets
 // lighter groups in the next ones, so the per-burst slack does not pile up on one GPU of a
 // pipelined multi-GPU job (the busiest GPU's cumulative work paces it).
+// pipe (optional): each GPU's slot pipelines, for the SLO phase.  A tuple (c_off [NG+1], c_wid,
+// c_start, c_end, f_off [NG+1], f_time): per GPU the in-flight pods of earlier placements with
+// their (measured or predicted) intervals, pinned as co-runners, and the times its free CU slots
+// become free.  With it, phase B counts SLOs met on the pipeline -- the GPU's new pods start at
+// its slot free times (longest first on the earliest slot) next to the in-flight pods -- instead
+// of on the group in isolation; the makespans (phase A, the cap) stay the group's own.
 py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 slo, I32 dev_gpu, I32 dev_free,
                                 I64 res_off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alone, F64 cmat, int sweeps,
-                                double tolerance, int mode, double sigma, py::object base_obj) {
+                                double tolerance, int mode, double sigma, py::object base_obj, py::object pipe_obj) {
   int W;
   check_model(alone, cmat, W);
   const py::ssize_t P = dev_in.shape(0), D = dev_gpu.shape(0), NR = r_wid.shape(0);
@@ -331,6 +415,32 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       if (!std::isfinite(B[g]) || B[g] < 0) throw std::runtime_error("plan_corun: base must be finite and >= 0");
     }
   }
+  // pipeline context (see above)
+  bool pipe = false;
+  I64 p_coff, p_foff;
+  I32 p_cwid;
+  F64 p_cst, p_cend, p_ft;
+  if (!pipe_obj.is_none()) {
+    py::tuple t = pipe_obj.cast<py::tuple>();
+    if (t.size() != 6) throw std::runtime_error("plan_corun: pipe must be (c_off, c_wid, c_start, c_end, f_off, f_time)");
+    p_coff = t[0].cast<I64>();
+    p_cwid = t[1].cast<I32>();
+    p_cst = t[2].cast<F64>();
+    p_cend = t[3].cast<F64>();
+    p_foff = t[4].cast<I64>();
+    p_ft = t[5].cast<F64>();
+    const py::ssize_t NC = p_cwid.shape(0);
+    if (p_coff.shape(0) != NG + 1 || p_foff.shape(0) != NG + 1 || p_cst.shape(0) != NC || p_cend.shape(0) != NC)
+      throw std::runtime_error("plan_corun: pipe array shapes");
+    if (p_coff.data()[0] != 0 || p_coff.data()[NG] != NC || p_foff.data()[0] != 0 ||
+        p_foff.data()[NG] != p_ft.shape(0))
+      throw std::runtime_error("plan_corun: pipe offsets");
+    for (int g = 0; g < NG; ++g)
+      if (p_coff.data()[g + 1] < p_coff.data()[g] || p_foff.data()[g + 1] < p_foff.data()[g])
+        throw std::runtime_error("plan_corun: pipe offsets");
+    check_wids(p_cwid.data(), NC, W, "pipe context");
+    pipe = true;
+  }
   std::vector<int32_t> dev(dev_in.data(), dev_in.data() + P);
   std::vector<int> free(dev_free.data(), dev_free.data() + D);
   const int32_t* U = units.data();
@@ -351,6 +461,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     for (int g = 0; g < NG; ++g)
       for (int64_t r = RO[g]; r < RO[g + 1]; ++r) mem[g].push_back(-1 - (int)r);
     for (py::ssize_t p = 0; p < P; ++p) mem[DG[dev[p]]].push_back((int)p);
+    bool use_pipe = false, phase_b = false;
     auto eval = [&](int g) {
       const auto& v = mem[g];
       const int k = (int)v.size();
@@ -363,10 +474,68 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         it[i] = a >= 0 ? iters.data()[a] : r_iters.data()[-1 - a];
         sl[i] = a >= 0 ? slo.data()[a] : r_slo.data()[-1 - a];
       }
-      return eval_group(k, w, it, sl, A, Cm, W, nullptr, sigma);
+      // phase A needs makespans only: no soft-SLO terms (erfc / log per member)
+      GroupEval e = eval_group(k, w, it, sl, A, Cm, W, nullptr, phase_b ? sigma : 0.0);
+      if (!use_pipe) return e;
+      // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times
+      const int64_t c0 = p_coff.data()[g], c1 = p_coff.data()[g + 1];
+      const int64_t f0 = p_foff.data()[g], f1 = p_foff.data()[g + 1];
+      const int nc = (int)(c1 - c0);
+      if (nc + k > kMaxK) return e;
+      int32_t pw[kMaxK];
+      double pit[kMaxK], pst[kMaxK], pen[kMaxK], pfin[kMaxK];
+      for (int c = 0; c < nc; ++c) {
+        pw[c] = p_cwid.data()[c0 + c];
+        pit[c] = 1.0;
+        pst[c] = p_cst.data()[c0 + c];
+        pen[c] = p_cend.data()[c0 + c];
+      }
+      // new pods longest first onto the earliest free slot; residents already run (first time)
+      int order[kMaxK];
+      for (int i = 0; i < k; ++i) order[i] = i;
+      std::sort(order, order + k, [&](int a, int b) { return A[w[a]] * it[a] > A[w[b]] * it[b]; });
+      const double t0 = f1 > f0 ? p_ft.data()[f0] : 0.0;
+      int nf = 0;
+      for (int q = 0; q < k; ++q) {
+        const int i = order[q];
+        pw[nc + i] = w[i];
+        pit[nc + i] = it[i];
+        pen[nc + i] = 0.0;
+        if (v[i] < 0) {
+          pst[nc + i] = t0;
+        } else {
+          const int64_t fi = std::min<int64_t>(f0 + nf, f1 - 1);
+          pst[nc + i] = f1 > f0 ? p_ft.data()[fi] : 0.0;
+          ++nf;
+        }
+      }
+      // the simulation clock starts at 0: shift the window
+      double lo = kBig;
+      for (int i = 0; i < nc + k; ++i) lo = std::min(lo, pst[i]);
+      for (int i = 0; i < nc + k; ++i) {
+        pst[i] -= lo;
+        if (i < nc) pen[i] -= lo;
+      }
+      sim_group(nc + k, pw, pit, pst, A, Cm, W, pfin, pen);
+      e.ok = e.bad = 0;
+      e.deficit = e.expected = 0.0;
+      for (int i = 0; i < k; ++i) {
+        double tput;
+        if (it[i] <= 0) tput = 1e3 / std::max(steady_ms(k, i, w, A, Cm, W), 1e-12);
+        else tput = it[i] / std::max(pfin[nc + i] - pst[nc + i], 1e-12) * 1e3;
+        e.expected += p_meet(tput, sl[i], sigma);
+        if (sl[i] <= 0 || tput >= sl[i]) ++e.ok;
+        else ++e.bad, e.deficit += 1.0 - tput / sl[i];
+      }
+      return e;
+    };
+    long n_evals = 0;
+    auto meval = [&](int g) {
+      ++n_evals;
+      return eval(g);
     };
     std::vector<GroupEval> ge(NG);
-    for (int g = 0; g < NG; ++g) ge[g] = eval(g);
+    for (int g = 0; g < NG; ++g) ge[g] = meval(g);
     auto replace = [&](int g, int from, int to) {
       for (int& x : mem[g])
         if (x == from) { x = to; return; }
@@ -388,7 +557,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
             if (g1 == g0 || free[d] < U[p]) continue;
             remove(g0, (int)p);
             mem[g1].push_back((int)p);
-            const GroupEval a0 = eval(g0), a1 = eval(g1);
+            const GroupEval a0 = meval(g0), a1 = meval(g1);
             if (accept(g0, g1, ge[g0], ge[g1], a0, a1)) {
               free[d0] += U[p];
               free[d] -= U[p];
@@ -407,9 +576,11 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
           for (py::ssize_t j = i + 1; j < P; ++j) {
             const int di = dev[i], dj = dev[j], gi = DG[di], gj = DG[dj];
             if (gi == gj || U[i] != U[j]) continue;
+            // same workload and length: a no-op for the makespans (phase A)
+            if (!phase_b && wid.data()[i] == wid.data()[j] && iters.data()[i] == iters.data()[j]) continue;
             replace(gi, (int)i, (int)j);
             replace(gj, (int)j, (int)i);
-            const GroupEval ai = eval(gi), aj = eval(gj);
+            const GroupEval ai = meval(gi), aj = meval(gj);
             if (accept(gi, gj, ge[gi], ge[gj], ai, aj)) {
               dev[i] = dj;
               dev[j] = di;
@@ -424,6 +595,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         }
         if (!improved) break;
       }
+      if (std::getenv("GPUSCHED_PLAN_DEBUG")) std::fprintf(stderr, "[plan_corun] phase %d evals %ld\n", phase_b ? 1 : 0, n_evals);
     };
     auto max_mk = [&](bool eff) {
       double m = 0;
@@ -444,6 +616,9 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     if (mode == 0 || mode == 2) {
       // headroom of tolerance x the balanced plan's longest GROUP (not its backlog)
       const double cap = max_mk(true) + std::max(tolerance, 0.0) * max_mk(false);
+      phase_b = true;
+      use_pipe = pipe;
+      for (int g = 0; g < NG; ++g) ge[g] = meval(g);
       run_phase([&](int gi, int gj, const GroupEval& bi, const GroupEval& bj, const GroupEval& ai, const GroupEval& aj) {
         const bool over = (B[gi] + ai.makespan > cap * (1 + eps) && ai.makespan > bi.makespan * (1 + eps)) ||
                           (B[gj] + aj.makespan > cap * (1 + eps) && aj.makespan > bj.makespan * (1 + eps));
@@ -469,9 +644,287 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
   return out;
 }
 
+// One GPU's pipeline as arrays (chain_times / plan_slots): m context members -- pods already
+// placed on the GPU, measured ones pinned to their interval, the rest chained per slot -- and
+// n new pods to place on S CU slots.
+py::tuple chain_times(I32 wid, F64 iters, F64 start, I32 prev, F64 alone, F64 cmat, py::object pin_end) {
+  int W;
+  check_model(alone, cmat, W);
+  const py::ssize_t k = wid.shape(0);
+  if (iters.shape(0) != k || start.shape(0) != k || prev.shape(0) != k)
+    throw std::runtime_error("chain_times: array shapes differ");
+  if (k > kMaxK) throw std::runtime_error("chain_times: more than 64 members");
+  check_wids(wid.data(), k, W, "chain_times");
+  for (py::ssize_t i = 0; i < k; ++i)
+    if (prev.data()[i] >= (int32_t)i) throw std::runtime_error("chain_times: prev must point to an earlier member");
+  F64 pin_a;
+  const double* pp = nullptr;
+  if (!pin_end.is_none()) {
+    pin_a = pin_end.cast<F64>();
+    if (pin_a.shape(0) != k) throw std::runtime_error("chain_times: pin_end must have k entries");
+    pp = pin_a.data();
+  }
+  py::array_t<double> st(k), fin(k);
+  sim_chain((int)k, wid.data(), iters.data(), start.data(), prev.data(), alone.data(), cmat.data(), W,
+            st.mutable_data(), fin.mutable_data(), pp);
+  return py::make_tuple(st, fin);
+}
+
+// Slot assignment of n new pods on one GPU whose CU slots already run a pipeline (context: m
+// members as in chain_times; slot_tail[s] = the context member last on slot s, -1 = the slot is
+// free from slot_free[s]).  New pod j on slot s starts when slot_tail[s] finishes, not before its
+// release n_rel[j].  Every injective assignment (n <= S; enumerated up to max_enum, else a
+// pairwise-swap local search from the longest-first / earliest-free-slot assignment) is
+// simulated as a whole pipeline:
+//   spread = max - min over slots of the predicted end of the slot's last pod -- a slot that
+//            runs ahead of the others idles once the launch-ahead window is exhausted, so a
+//            bounded spread is the throughput side;
+//   expected = members (new pods and unmeasured context pods with an SLO) expected to meet
+//            their SLO under lognormal model error sigma (sigma 0: hard counts).
+// The choice: the most expected SLOs among assignments within spread_tol ms of the least
+// spread any assignment reaches; ties -> the smaller spread.
+// Returns (slot per new pod, start[m+n], fin[m+n], expected, spread, least spread).
+// ph_off [S+1] / ph_wid / ph_iters (optional): per candidate slot, "phantom" pods chained after
+// its last pod -- the slot's future.  Pods placed later co-run with the new pods' tails; without
+// them the pipeline looks emptier than it will be and every prediction is optimistic (measured
+// on MI355X bench traces: -24 % mean log error, ~0 with three phantoms per slot repeating the
+// slot's recent workloads).  Phantoms press on the others; they are never counted.
+py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin, F64 c_slo, I32 slot_tail,
+                     F64 slot_free, I32 n_wid, F64 n_iters, F64 n_slo, F64 n_rel, F64 alone, F64 cmat, double sigma,
+                     double spread_tol, int max_enum, py::object ph_off_o, py::object ph_wid_o, py::object ph_it_o) {
+  int W;
+  check_model(alone, cmat, W);
+  const int m = (int)c_wid.shape(0), S = (int)slot_tail.shape(0), n = (int)n_wid.shape(0);
+  if (c_iters.shape(0) != m || c_start.shape(0) != m || c_prev.shape(0) != m || c_pin.shape(0) != m ||
+      c_slo.shape(0) != m)
+    throw std::runtime_error("plan_slots: context shapes differ");
+  if (slot_free.shape(0) != S || n_iters.shape(0) != n || n_slo.shape(0) != n || n_rel.shape(0) != n)
+    throw std::runtime_error("plan_slots: slot / new-pod shapes differ");
+  if (n > S) throw std::runtime_error("plan_slots: more new pods than slots");
+  if (S > 64) throw std::runtime_error("plan_slots: more than 64 slots");
+  if (m + n > kMaxK) throw std::runtime_error("plan_slots: more than 64 members");
+  check_wids(c_wid.data(), m, W, "plan_slots context");
+  check_wids(n_wid.data(), n, W, "plan_slots new pods");
+  for (int i = 0; i < m; ++i)
+    if (c_prev.data()[i] >= i) throw std::runtime_error("plan_slots: prev must point to an earlier member");
+  for (int s = 0; s < S; ++s)
+    if (slot_tail.data()[s] < -1 || slot_tail.data()[s] >= m) throw std::runtime_error("plan_slots: bad slot tail");
+  std::vector<int64_t> PO(S + 1, 0);
+  std::vector<int32_t> PW;
+  std::vector<double> PI;
+  if (!ph_off_o.is_none()) {
+    I64 po = ph_off_o.cast<I64>();
+    I32 pw = ph_wid_o.cast<I32>();
+    F64 pi = ph_it_o.cast<F64>();
+    if (po.shape(0) != S + 1 || po.data()[0] != 0 || po.data()[S] != pw.shape(0) || pi.shape(0) != pw.shape(0))
+      throw std::runtime_error("plan_slots: phantom arrays");
+    for (int q = 0; q < S; ++q)
+      if (po.data()[q + 1] < po.data()[q]) throw std::runtime_error("plan_slots: phantom offsets");
+    check_wids(pw.data(), pw.shape(0), W, "plan_slots phantoms");
+    PO.assign(po.data(), po.data() + S + 1);
+    PW.assign(pw.data(), pw.data() + pw.shape(0));
+    PI.assign(pi.data(), pi.data() + pi.shape(0));
+  }
+  const int nph = (int)PW.size();
+  if (m + n + nph > kMaxK) throw std::runtime_error("plan_slots: more than 64 members with phantoms");
+  const int k = m + n + nph;
+  int32_t w[kMaxK], pv[kMaxK];
+  double it[kMaxK], s0[kMaxK], pe[kMaxK], sl[kMaxK];
+  for (int i = 0; i < m; ++i) {
+    w[i] = c_wid.data()[i];
+    it[i] = c_iters.data()[i];
+    s0[i] = c_start.data()[i];
+    pv[i] = c_prev.data()[i];
+    pe[i] = c_pin.data()[i];
+    sl[i] = c_slo.data()[i];
+  }
+  for (int j = 0; j < n; ++j) {
+    w[m + j] = n_wid.data()[j];
+    it[m + j] = n_iters.data()[j];
+    sl[m + j] = n_slo.data()[j];
+    pe[m + j] = 0.0;
+  }
+  for (int q = 0; q < nph; ++q) {
+    w[m + n + q] = PW[q];
+    it[m + n + q] = PI[q];
+    sl[m + n + q] = 0.0;
+    pe[m + n + q] = 0.0;
+    s0[m + n + q] = -kBig;
+  }
+  const int32_t* T = slot_tail.data();
+  const double* F = slot_free.data();
+  const double* R = n_rel.data();
+  const double* A = alone.data();
+  const double* Cm = cmat.data();
+  struct Res {
+    double expected = -1.0, spread = kBig;
+  };
+  double st[kMaxK], fin[kMaxK];
+  auto eval = [&](const int* slot, double* st_o, double* fin_o) {
+    int last[64];
+    for (int q = 0; q < S && q < 64; ++q) last[q] = T[q];
+    for (int j = 0; j < n; ++j) {
+      const int s = slot[j], t = T[s];
+      pv[m + j] = t;
+      s0[m + j] = t >= 0 ? R[j] : std::max(F[s], R[j]);
+      if (s < 64) last[s] = m + j;
+    }
+    for (int q = 0; q < S && q < 64; ++q) {
+      int p = last[q];
+      for (int64_t x = PO[q]; x < PO[q + 1]; ++x) {
+        const int i = m + n + (int)x;
+        if (p >= 0) {
+          pv[i] = p;
+          s0[i] = -kBig;
+        } else {
+          pv[i] = -1;
+          s0[i] = F[q];
+        }
+        p = i;
+      }
+    }
+    sim_chain(k, w, it, s0, pv, A, Cm, W, st_o, fin_o, pe);
+    Res r;
+    r.expected = 0.0;
+    for (int i = 0; i < k; ++i) {
+      const bool pinned = i < m && pv[i] < 0 && pe[i] > s0[i];
+      if (pinned || sl[i] <= 0 || it[i] <= 0) continue;
+      const double d = fin_o[i] - st_o[i];
+      r.expected += (fin_o[i] >= kBig) ? 0.0 : p_meet(it[i] / std::max(d, 1e-12) * 1e3, sl[i], sigma);
+    }
+    double lo = kBig, hi = -kBig;
+    for (int s = 0; s < S; ++s) {
+      double e = F[s];
+      if (T[s] >= 0) e = fin_o[T[s]];
+      for (int j = 0; j < n; ++j)
+        if (slot[j] == s) e = fin_o[m + j];
+      lo = std::min(lo, e);
+      hi = std::max(hi, e);
+    }
+    r.spread = hi - lo;
+    return r;
+  };
+  std::vector<int> best(n), cur(n);
+  double best_e = -1.0, best_sp = kBig, min_sp = kBig;
+  {
+    py::gil_scoped_release nogil;
+    // number of injective assignments S! / (S - n)!
+    double count = 1.0;
+    for (int j = 0; j < n; ++j) count *= (double)(S - j);
+    if (n == 0) {
+      best_e = 0.0;
+    } else if (count <= (double)std::max(max_enum, 1)) {
+      std::vector<std::pair<double, double>> all;
+      std::vector<std::vector<int>> asg;
+      std::vector<bool> used(S, false);
+      // depth-first enumeration
+      std::vector<int> pos(n, -1);
+      int j = 0;
+      while (j >= 0) {
+        if (j == n) {
+          const Res r = eval(cur.data(), st, fin);
+          all.emplace_back(r.expected, r.spread);
+          asg.push_back(cur);
+          --j;
+          if (j >= 0) used[cur[j]] = false;
+          continue;
+        }
+        int s = pos[j] + 1;
+        while (s < S && used[s]) ++s;
+        if (s >= S) {
+          pos[j] = -1;
+          --j;
+          if (j >= 0) used[cur[j]] = false;
+          continue;
+        }
+        pos[j] = s;
+        cur[j] = s;
+        used[s] = true;
+        ++j;
+      }
+      for (const auto& x : all) min_sp = std::min(min_sp, x.second);
+      for (size_t a = 0; a < all.size(); ++a) {
+        const double e = all[a].first, sp = all[a].second;
+        if (sp > min_sp + spread_tol + 1e-9) continue;
+        if (e > best_e + 1e-9 || (e > best_e - 1e-9 && sp < best_sp - 1e-9)) {
+          best_e = e;
+          best_sp = sp;
+          best = asg[a];
+        }
+      }
+    } else {
+      // longest work first onto the slot that frees first (from the context alone), then swaps
+      double cst[kMaxK], cfin[kMaxK];
+      if (m > 0) sim_chain(m, w, it, s0, pv, A, Cm, W, cst, cfin, pe);
+      std::vector<double> free_at(S);
+      for (int s = 0; s < S; ++s) free_at[s] = T[s] >= 0 ? cfin[T[s]] : F[s];
+      std::vector<int> order(n);
+      for (int q = 0; q < n; ++q) order[q] = q;
+      std::sort(order.begin(), order.end(),
+                [&](int a, int b) { return A[w[m + a]] * it[m + a] > A[w[m + b]] * it[m + b]; });
+      std::vector<bool> used(S, false);
+      for (int q : order) {
+        int bs = -1;
+        for (int s = 0; s < S; ++s)
+          if (!used[s] && (bs < 0 || free_at[s] < free_at[bs])) bs = s;
+        used[bs] = true;
+        cur[q] = bs;
+      }
+      Res r = eval(cur.data(), st, fin);
+      min_sp = r.spread;
+      const double cap = r.spread + spread_tol;
+      best = cur;
+      best_e = r.expected;
+      best_sp = r.spread;
+      for (int sweep = 0; sweep < 8; ++sweep) {
+        bool improved = false;
+        for (int a = 0; a < n; ++a) {
+          // swap with another new pod, or move to an unused slot
+          for (int b = 0; b < n + S; ++b) {
+            std::vector<int> cand = best;
+            if (b < n) {
+              if (b <= a) continue;
+              std::swap(cand[a], cand[b]);
+            } else {
+              const int s = b - n;
+              if (std::find(cand.begin(), cand.end(), s) != cand.end()) continue;
+              cand[a] = s;
+            }
+            const Res x = eval(cand.data(), st, fin);
+            min_sp = std::min(min_sp, x.spread);
+            if (x.spread > cap + 1e-9) continue;
+            if (x.expected > best_e + 1e-9 || (x.expected > best_e - 1e-9 && x.spread < best_sp - 1e-9)) {
+              best = cand;
+              best_e = x.expected;
+              best_sp = x.spread;
+              improved = true;
+            }
+          }
+        }
+        if (!improved) break;
+      }
+    }
+  }
+  py::array_t<int32_t> out(n);
+  py::array_t<double> st_a(k), fin_a(k);
+  for (int j = 0; j < n; ++j) out.mutable_data()[j] = best[j];
+  {
+    const Res r = eval(best.data(), st_a.mutable_data(), fin_a.mutable_data());
+    if (n == 0) best_sp = min_sp = r.spread;
+  }
+  return py::make_tuple(out, st_a, fin_a, best_e, best_sp, min_sp);
+}
+
 }  // namespace
 
 void register_corun(py::module_& m) {
+  m.def("chain_times", &chain_times, py::arg("wids"), py::arg("iters"), py::arg("starts"), py::arg("prev"),
+        py::arg("alone_ms"), py::arg("cmat"), py::arg("pin_end") = py::none());
+  m.def("plan_slots", &plan_slots, py::arg("c_wid"), py::arg("c_iters"), py::arg("c_start"), py::arg("c_prev"),
+        py::arg("c_pin"), py::arg("c_slo"), py::arg("slot_tail"), py::arg("slot_free"), py::arg("n_wid"),
+        py::arg("n_iters"), py::arg("n_slo"), py::arg("n_release"), py::arg("alone_ms"), py::arg("cmat"),
+        py::arg("sigma") = 0.05, py::arg("spread_tol") = 0.0, py::arg("max_enum") = 720,
+        py::arg("ph_off") = py::none(), py::arg("ph_wid") = py::none(), py::arg("ph_iters") = py::none());
   m.def("corun_times", &corun_times, py::arg("wids"), py::arg("iters"), py::arg("mask"), py::arg("starts"),
         py::arg("alone_ms"), py::arg("cmat"), py::arg("pin_end") = py::none());
   m.def("corun_gpu_eval", &corun_gpu_eval, py::arg("off"), py::arg("r_wid"), py::arg("r_iters"), py::arg("r_slo"),
@@ -482,5 +935,5 @@ void register_corun(py::module_& m) {
   m.def("plan_corun", &plan_corun, py::arg("dev"), py::arg("units"), py::arg("wid"), py::arg("iters"), py::arg("slo"),
         py::arg("dev_gpu"), py::arg("dev_free"), py::arg("res_off"), py::arg("r_wid"), py::arg("r_iters"),
         py::arg("r_slo"), py::arg("alone_ms"), py::arg("cmat"), py::arg("sweeps") = 8, py::arg("tolerance") = 0.03,
-        py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none());
+        py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none(), py::arg("pipe") = py::none());
 }

@@ -312,15 +312,15 @@ def test_plan_feedback_counts_each_gpus_busy_time_once_on_a_pipelined_timeline()
     planner.backlog = {(PB.NODE, 0): 0.0, (PB.NODE, 1): 0.0}
     pods = np.full((2, PB.POD_F * PB.MAX_PODS_GPU), -1.0)
     # GPU 0: pods over [0, 4] and [2, 6] -> 6 ms busy; GPU 1: [10, 13] and [20, 22] -> 5 ms
-    pods[0, :8] = [0, 100.0, 0.0, 4.0, 1, 100.0, 2.0, 6.0]
-    pods[1, :8] = [0, 100.0, 10.0, 13.0, 1, 100.0, 20.0, 22.0]
+    pods[0, :10] = [0, 100.0, 0.0, 4.0, 0, 1, 100.0, 2.0, 6.0, 2]
+    pods[1, :10] = [0, 100.0, 10.0, 13.0, 0, 1, 100.0, 20.0, 22.0, 2]
     cp._plan_feedback(pods)
     assert planner.backlog[(PB.NODE, 0)] == pytest.approx(1.0)
     assert planner.backlog[(PB.NODE, 1)] == pytest.approx(0.0)   # 5 busy vs 5 predicted
     # the next epoch on GPU 0 overlaps the covered [.., 6]: only [6, 9] is new busy time
     cp._carry_pred.append({0: 3.0})
     pods2 = np.full((2, PB.POD_F * PB.MAX_PODS_GPU), -1.0)
-    pods2[0, :4] = [2, 100.0, 5.0, 9.0]
+    pods2[0, :5] = [2, 100.0, 5.0, 9.0, 4]
     cp._plan_feedback(pods2)
     assert planner.backlog[(PB.NODE, 0)] == pytest.approx(1.0)
 
