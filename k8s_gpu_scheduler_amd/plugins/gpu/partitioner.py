@@ -94,6 +94,10 @@ class PartitionController:
         self.decisions: List[Decision] = []
         self._requested: Dict[str, Decision] = {}          # node -> our outstanding request
         self._backoff: Dict[Tuple[str, str], float] = {}    # (node, mode) -> until (wall clock)
+        # partition sizes (CUs) whose pending demand no node can be re-partitioned for (every
+        # node busy, changing, backed off or unable): SLO-sized pods of these sizes may then
+        # take any larger free partition instead of waiting (plugin._whole_choice)
+        self.stuck: set = set()
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
 
@@ -221,6 +225,7 @@ class PartitionController:
     def step(self) -> List[Decision]:
         pending = self.pending_isolated()
         if not pending:
+            self.stuck = set()
             return []
         demand: Counter = Counter()
         for p in pending:
@@ -228,6 +233,7 @@ class PartitionController:
             if size:
                 demand[size] += 1
         if not demand:
+            self.stuck = set()
             return []
         nodes = {O.name(n): n for n in self._nodes()}
         now = time.time()
@@ -251,6 +257,7 @@ class PartitionController:
                 if st.device.healthy and not st.pods:
                     supply[st.device.cus] += 1
         out: List[Decision] = []
+        stuck = set()
         # largest deficit first; one node switches to one mode per step
         for size, need in sorted(demand.items(), key=lambda kv: kv[1] - supply[kv[0]], reverse=True):
             deficit = need - supply[size]
@@ -272,6 +279,7 @@ class PartitionController:
                     cur_size = C.MI355X_CUS // C.COMPUTE_PARTITIONS[self.current_mode(name)]
                     cands.append((demand.get(cur_size, 0) > 0, name))
                 if not cands:
+                    stuck.add(size)
                     break
                 cands.sort()
                 name = cands[0][1]
@@ -291,6 +299,7 @@ class PartitionController:
                 busy_or_changing.add(name)
                 supply[size] += gpus * parts
                 deficit -= gpus * parts
+        self.stuck = stuck
         self.decisions.extend(out)
         return out
 

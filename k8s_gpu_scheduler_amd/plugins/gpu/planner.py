@@ -340,6 +340,9 @@ class BurstPlanner:
         # capacity before the burst (the native planner subtracts the initial assignment)
         cap = np.array(free_units, np.int32)
         np.add.at(cap, dev0, units)
+        hbm = np.array([r.hbm_gib for _, r, _ in assign], np.float64)
+        cap_hbm = np.array(free_hbm, np.float64)
+        np.add.at(cap_hbm, dev0, hbm)
         gkeys = sorted(gkey, key=gkey.get)
         base = None
         if self.carry > 0:
@@ -357,7 +360,7 @@ class BurstPlanner:
                 np.array([r.slo * margin for _, r, _ in assign], np.float64),
                 np.array(dev_group, np.int32), cap, off, r_wid, r_iters, r_slo,
                 model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0,
-                float(plugin.args.corun_sigma), base, pipe)
+                float(plugin.args.corun_sigma), base, pipe, hbm, cap_hbm)
             if self.carry > 0:
                 self._carry(gkeys, per, assign, out, dev_group, model, core, off, r_wid, r_iters, r_slo)
         else:

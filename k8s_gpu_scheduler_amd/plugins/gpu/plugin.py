@@ -71,6 +71,7 @@ class GpuRequest:
     implicit: bool = False  # SLO env only, no amd.com/* request: GPU preferred, not required
     isolated: bool = False  # needs its own compute partition (ANNOT_ISOLATION = "partition")
     part_cus: int = 0       # ... of this many CUs (0 = not sized yet)
+    part_min: bool = False  # part_cus is a floor (SLO-sized): any larger free partition will do
     iters: float = 0.0      # iterations of a batch pod (ITERATIONS env; 0 = long-running service)
 
 
@@ -344,7 +345,9 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             r.implicit = mem <= 0
             size = self.slo_partition_size(pod, slo) if (r.implicit and slo > 0) else None
             if size:
-                r.isolated, r.whole, r.implicit = True, 1, False
+                # a floor, not an exact shape: a busy SPX node's free 256-CU GPU meets the SLO
+                # better than a 128-CU partition the controller may never get to cut
+                r.isolated, r.whole, r.implicit, r.part_min = True, 1, False, True
                 r.part_cus = r.cu = size
                 r.units = 0
                 return r
@@ -520,7 +523,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return None
         req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
         rsig = (req.whole, req.units, req.cu, req.hbm_gib, req.isolated, req.part_cus, req.implicit, req.gpu_pod,
-                req.iters)
+                req.iters, req.part_min and self._larger_ok(req))
         if phase != "score":
             return rsig
         if self.args.pack == "random":
@@ -1294,10 +1297,22 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         return any(c.device.healthy and c.hbm_free + 1e-6 >= req.hbm_gib and c._find_units(req.units) is not None
                    for c in sim)
 
+    def _larger_ok(self, req: GpuRequest) -> bool:
+        """An SLO-sized pod may take a larger free partition when no node can be cut to its
+        size soon: no partition controller, or the controller found no idle node to
+        re-partition for it (every node busy / changing / backed off).  Otherwise it waits
+        for the exact size, so whole GPUs are not spent on half-GPU pods."""
+        if not req.part_min:
+            return False
+        pc = self.partitioner
+        return pc is None or req.part_cus in pc.stuck
+
     def _whole_choice(self, req: GpuRequest, node: str, states: List[DeviceState]) -> Optional[Choice]:
+        larger = req.isolated and self._larger_ok(req)
         free = [st for st in states if st.device.healthy and not st.pods
                 and st.hbm_free + 1e-6 >= req.hbm_gib / max(req.whole, 1)
-                and (not req.isolated or st.device.cus == req.part_cus)]
+                and (not req.isolated or st.device.cus == req.part_cus
+                     or (larger and st.device.cus >= req.part_cus))]
         if len(free) < req.whole:
             return None
         per = req.hbm_gib / max(req.whole, 1)
@@ -1308,7 +1323,9 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             for st in states:
                 if st.pods:
                     used_per_gpu[st.device.gpu] = used_per_gpu.get(st.device.gpu, 0) + 1
-            free.sort(key=lambda s: (-used_per_gpu.get(s.device.gpu, 0), s.device.gpu, s.device.partition))
+            # (an SLO-sized floor: the smallest partition that holds it first)
+            free.sort(key=lambda s: (s.device.cus if req.part_min else 0, -used_per_gpu.get(s.device.gpu, 0),
+                                     s.device.gpu, s.device.partition))
             pick = free[:1]
             return Choice(node, [(s.device.uuid, 0, s.device.units, per, True) for s in pick], 100.0,
                           [s.device for s in pick])

@@ -386,7 +386,8 @@ py::tuple corun_groups_eval(I64 off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alon
 // of on the group in isolation; the makespans (phase A, the cap) stay the group's own.
 py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 slo, I32 dev_gpu, I32 dev_free,
                                 I64 res_off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alone, F64 cmat, int sweeps,
-                                double tolerance, int mode, double sigma, py::object base_obj, py::object pipe_obj) {
+                                double tolerance, int mode, double sigma, py::object base_obj, py::object pipe_obj,
+                                py::object hbm_obj, py::object dev_hbm_obj) {
   int W;
   check_model(alone, cmat, W);
   const py::ssize_t P = dev_in.shape(0), D = dev_gpu.shape(0), NR = r_wid.shape(0);
@@ -441,6 +442,17 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     check_wids(p_cwid.data(), NC, W, "pipe context");
     pipe = true;
   }
+  // optional HBM: per pod GiB (hbm) and per device free GiB before the burst (dev_hbm); moves
+  // and swaps then keep every device within its free HBM, as the initial assignment does
+  std::vector<double> H(P, 0.0), hfree(D, 1e300);
+  if (!hbm_obj.is_none() || !dev_hbm_obj.is_none()) {
+    if (hbm_obj.is_none() || dev_hbm_obj.is_none()) throw std::runtime_error("plan_corun: hbm and dev_hbm go together");
+    F64 hb = hbm_obj.cast<F64>(), dh = dev_hbm_obj.cast<F64>();
+    if (hb.ndim() != 1 || hb.shape(0) != P || dh.ndim() != 1 || dh.shape(0) != D)
+      throw std::runtime_error("plan_corun: hbm must have one entry per pod, dev_hbm one per device");
+    for (py::ssize_t p = 0; p < P; ++p) H[p] = hb.data()[p];
+    for (py::ssize_t d = 0; d < D; ++d) hfree[d] = dh.data()[d];
+  }
   std::vector<int32_t> dev(dev_in.data(), dev_in.data() + P);
   std::vector<int> free(dev_free.data(), dev_free.data() + D);
   const int32_t* U = units.data();
@@ -448,9 +460,10 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
   for (py::ssize_t p = 0; p < P; ++p) {
     if (dev[p] < 0 || dev[p] >= D) throw std::runtime_error("plan_corun: device index out of range");
     free[dev[p]] -= U[p];
+    hfree[dev[p]] -= H[p];
   }
   for (py::ssize_t d = 0; d < D; ++d)
-    if (free[d] < 0) throw std::runtime_error("plan_corun: initial assignment over capacity");
+    if (free[d] < 0 || hfree[d] < -1e-5) throw std::runtime_error("plan_corun: initial assignment over capacity");
   const double* A = alone.data();
   const double* Cm = cmat.data();
   py::array_t<int32_t> out(P);
@@ -554,13 +567,15 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
           const int d0 = dev[p], g0 = DG[d0];
           for (py::ssize_t d = 0; d < D; ++d) {
             const int g1 = DG[d];
-            if (g1 == g0 || free[d] < U[p]) continue;
+            if (g1 == g0 || free[d] < U[p] || hfree[d] + 1e-6 < H[p]) continue;
             remove(g0, (int)p);
             mem[g1].push_back((int)p);
             const GroupEval a0 = meval(g0), a1 = meval(g1);
             if (accept(g0, g1, ge[g0], ge[g1], a0, a1)) {
               free[d0] += U[p];
               free[d] -= U[p];
+              hfree[d0] += H[p];
+              hfree[d] -= H[p];
               dev[p] = (int32_t)d;
               ge[g0] = a0;
               ge[g1] = a1;
@@ -576,6 +591,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
           for (py::ssize_t j = i + 1; j < P; ++j) {
             const int di = dev[i], dj = dev[j], gi = DG[di], gj = DG[dj];
             if (gi == gj || U[i] != U[j]) continue;
+            if (hfree[di] + H[i] - H[j] < -1e-6 || hfree[dj] + H[j] - H[i] < -1e-6) continue;
             // same workload and length: a no-op for the makespans (phase A)
             if (!phase_b && wid.data()[i] == wid.data()[j] && iters.data()[i] == iters.data()[j]) continue;
             replace(gi, (int)i, (int)j);
@@ -584,6 +600,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
             if (accept(gi, gj, ge[gi], ge[gj], ai, aj)) {
               dev[i] = dj;
               dev[j] = di;
+              hfree[di] += H[i] - H[j];
+              hfree[dj] += H[j] - H[i];
               ge[gi] = ai;
               ge[gj] = aj;
               improved = true;
@@ -935,5 +953,6 @@ void register_corun(py::module_& m) {
   m.def("plan_corun", &plan_corun, py::arg("dev"), py::arg("units"), py::arg("wid"), py::arg("iters"), py::arg("slo"),
         py::arg("dev_gpu"), py::arg("dev_free"), py::arg("res_off"), py::arg("r_wid"), py::arg("r_iters"),
         py::arg("r_slo"), py::arg("alone_ms"), py::arg("cmat"), py::arg("sweeps") = 8, py::arg("tolerance") = 0.03,
-        py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none(), py::arg("pipe") = py::none());
+        py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none(), py::arg("pipe") = py::none(),
+        py::arg("hbm") = py::none(), py::arg("dev_hbm") = py::none());
 }

@@ -251,6 +251,29 @@ def test_planner_backlog_steers_long_pod_off_the_backlogged_gpu():
         core.plan_corun(np.array([0, 1], I32), base=np.array([-1.0, 0.0]), **args)
 
 
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_native_burst_planner_respects_free_hbm():
+    """The complementary-pair swap of the test above is blocked when the receiving GPU's free
+    HBM cannot hold the incoming pod (moves/swaps checked units only)."""
+    m = _toy_model()
+    args = dict(units=np.full(4, 2, I32), wid=np.array([0, 0, 1, 1], I32), iters=np.full(4, 10.0),
+                slo=np.full(4, 800.0), dev_gpu=np.array([0, 1], I32), dev_free=np.array([8, 8], I32),
+                res_off=np.zeros(3, I64), r_wid=np.zeros(0, I32), r_iters=np.zeros(0), r_slo=np.zeros(0),
+                alone_ms=m.alone_ms, cmat=m.coupling())
+    # the memory pods need 40 GiB each, the compute pods 10; GPU 1 has 30 GiB: only the
+    # compute pods fit there, so no plan may move a memory pod onto it
+    hbm = np.array([40.0, 40.0, 10.0, 10.0])
+    out = list(core.plan_corun(np.array([0, 0, 1, 1], I32), hbm=hbm, dev_hbm=np.array([100.0, 30.0]), **args))
+    assert out[0] == out[1] == 0
+    for d in (0, 1):
+        assert sum(h for h, o in zip(hbm, out) if o == d) <= (100.0, 30.0)[d]
+    # with room on both, the complementary pairing comes back
+    out = list(core.plan_corun(np.array([0, 0, 1, 1], I32), hbm=hbm, dev_hbm=np.array([100.0, 100.0]), **args))
+    assert out[0] != out[1] and out[2] != out[3]
+    with pytest.raises(RuntimeError):          # the initial assignment must itself fit
+        core.plan_corun(np.array([0, 0, 1, 1], I32), hbm=hbm, dev_hbm=np.array([50.0, 100.0]), **args)
+
+
 def _cumulative_imbalance(carry: float, gpus: int = 4, epochs: int = 24) -> float:
     """Busiest GPU's cumulative predicted work over the mean GPU's, with the bench's control
     plane placing each epoch's burst (the co-run model stands in for the GPUs)."""

@@ -349,3 +349,25 @@ def test_measured_fabric_steers_quad_away_from_degraded_link():
     assert not ag.probe_fabric() and calls == [1]             # the 4-GPU pod runs: not now
     fc.delete("pods", "ring-4", "default")
     assert ag.probe_fabric() and calls == [1, 1]
+
+
+def test_slo_sized_pod_takes_a_larger_gpu_when_no_node_can_be_cut():
+    """Liveness on a busy SPX cluster: the SLO-sized pod needs a 128-CU partition, every node
+    has a resident pod (the controller never re-partitions a busy node), so after one
+    controller step finds no candidate the pod takes a free whole 256-CU GPU instead of
+    staying Pending; an idle node, by contrast, is cut to DPX first (test above)."""
+    fc, r, agents, s, plugin = _cluster(("n1", "n2"))
+    _preds_plugin(plugin, [400.0, 300.0, 200.0, 90.0])
+    for n in ("n1", "n2"):
+        fc.create("pods", O.make_pod(f"resident-{n}", gpu_cu=64, gpu_mem_gib=4,
+                                     node_selector={"kubernetes.io/hostname": n}))
+    assert all(res.node for res in s.schedule_pending())
+    fc.create("pods", O.make_pod("onnx-resnet50-1024-slo", slo=250))
+    (res,) = s.schedule_pending()
+    assert not res.node                                   # a cut might still come: wait for it
+    assert plugin.partitioner.step() == [] and plugin.partitioner.stuck == {128}
+    assert _drain(s, fc, ["onnx-resnet50-1024-slo"])
+    pod = fc.get("pods", "onnx-resnet50-1024-slo", "default")
+    u = O.annotations(pod)[C.ANNOT_DEVICES]
+    devs = {d.device.uuid: d for n in ("n1", "n2") for d in plugin.ledger.devices(n)}
+    assert devs[u].device.cus == 256 and list(devs[u].pods) == ["default/onnx-resnet50-1024-slo"]
