@@ -63,7 +63,8 @@ class NodeAgent:
                  health: Optional[HealthMonitor] = None, evict_unhealthy: bool = False,
                  drain_timeout_s: float = 300.0, evict_hbm_overuse: bool = False, history_every: int = 1,
                  hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc", profile_dir: str = "",
-                 partition_dry_run: bool = False, fabric: Any = None,
+                 partition_dry_run: bool = False, fabric: Any = None, set_checks: Any = None,
+                 background_probes: bool = False,
                  corun_send: Optional[Callable[[List[Dict[str, Any]]], Any]] = None):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
@@ -94,6 +95,13 @@ class NodeAgent:
         # measured per-pair xGMI copy rates (agent.fabric.FabricProber), published with the
         # topology for the multi-GPU placement
         self.fabric = fabric
+        # background_probes: the fabric probe and the RCCL checks of multi-GPU pods' GPU sets
+        # (set_checks, agent.probes.SetChecker) run on their own thread with the node tainted
+        # (agent.probes.ProbeWorker); otherwise the fabric probe runs inside step()
+        self.probes = None
+        if background_probes or set_checks is not None:
+            from .probes import ProbeWorker
+            self.probes = ProbeWorker(self, set_checks)
         self.dry_run_calls: List[Dict[str, Any]] = []
         # per-pod rocprofv3 output the profiling webhook (agent.profile_webhook) routes to a
         # hostPath: finished runs become workload-history samples (pod_profiler.ProfileIngestor)
@@ -155,6 +163,11 @@ class NodeAgent:
         if last and last.get("bw_gbps"):
             topo = dict(topo or {"n": len(last["bw_gbps"])})
             topo["bw_gbps"] = last["bw_gbps"]
+        sets = self.probes.sets if self.probes is not None else None
+        if sets is not None and sets.results:
+            topo = dict(topo or {"n": len(self.source.devices())})
+            topo["set_checks"] = sets.to_json()
+            topo["bad_sets"] = sets.bad_sets()
         if topo:
             self.redis.set(schema.topology_key(self.node), json.dumps(topo, separators=(",", ":")))
 
@@ -544,10 +557,16 @@ class NodeAgent:
         except Exception as e:
             log.warning("partition reconcile failed: %s", e)
         self.publish()
-        try:
-            self.probe_fabric()
-        except Exception as e:
-            log.warning("fabric probe failed: %s", e)
+        if self.probes is None:
+            try:
+                self.probe_fabric()
+            except Exception as e:
+                log.warning("fabric probe failed: %s", e)
+        else:
+            try:
+                self.probes.note_pods()
+            except Exception as e:
+                log.warning("noting multi-GPU pods for set checks failed: %s", e)
         try:
             self.publish_caps()
         except Exception as e:
@@ -596,6 +615,8 @@ class NodeAgent:
         return out
 
     def run(self) -> None:
+        if self.probes is not None:
+            self.probes.start()
         while not self._stop.is_set():
             try:
                 self.step()
@@ -610,6 +631,8 @@ class NodeAgent:
 
     def stop(self) -> None:
         self._stop.set()
+        if self.probes is not None:
+            self.probes.stop()
         if self._thread:
             self._thread.join(timeout=5)
 

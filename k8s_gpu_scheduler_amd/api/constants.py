@@ -51,6 +51,8 @@ LABEL_COMPUTE_PARTITION = "amd.com/compute-partition"
 LABEL_MEMORY_PARTITION = "amd.com/memory-partition"
 LABEL_MIG_CONFIG = "nvidia.com/mig.config"          # parity mode only
 TAINT_PARTITIONING = "amd.com/partitioning"
+# set by the node agent while a fabric / RCCL set probe runs (agent.probes)
+TAINT_PROBING = "amd.com/fabric-probe"
 
 ANNOT_PREFIX = "gpu-scheduler.amd.com/"
 # upstream kube-scheduler NodePreferAvoidPods annotation (JSON AvoidPods)

@@ -246,6 +246,14 @@ def _fabric_prober(args):
     return FabricProber()
 
 
+def _set_checker(args):
+    """RCCL checks of the GPU sets multi-GPU pods ran on (agent.probes): with the fabric probe."""
+    if args.fabric_probe == "off" or args.synthetic or args.set_checks == "off":
+        return None
+    from ..agent.probes import SetChecker
+    return SetChecker()
+
+
 def cmd_agent(args) -> int:
     from ..agent.agent import NodeAgent
     from ..agent.devices import best_source, synthetic_node
@@ -280,6 +288,7 @@ def cmd_agent(args) -> int:
                       hbm_tolerance_gib=args.hbm_tolerance, host_proc=proc_root, profile_dir=args.profile_dir,
                       partition_dry_run=args.partition_dry_run,
                       fabric=_fabric_prober(args), corun_send=_corun_sender(args.corun_recommender),
+                      background_probes=True, set_checks=_set_checker(args),
                       pod_resolver=lambda pid: pod_of_pid(pid, proc_root))
     mgr = None
     if args.device_plugin:
@@ -291,6 +300,8 @@ def cmd_agent(args) -> int:
         threading.Thread(target=mgr.run_forever, name="device-plugin", daemon=True).start()
     if args.once:
         agent.step()
+        if agent.probes is not None:
+            agent.probes.tick()
         if mgr is not None:
             mgr.stop()
         return 0
@@ -442,6 +453,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--evict-hbm-overuse", action="store_true",
                    help="evict (Eviction API, PodDisruptionBudgets apply) pods whose processes hold more VRAM "
                         "than their amd.com/gpu-memory share")
+    s.add_argument("--set-checks", default="auto", choices=["auto", "off"],
+                   help="RCCL all-reduce check of each multi-GPU pod's GPU set once it is idle again "
+                        "(agent.probes); a set below par is published in the topology's bad_sets")
     s.add_argument("--fabric-probe", default="auto", choices=["auto", "off"],
                    help="measure every GPU pair's copy rate (child process, idle GPUs only) at start-up and "
                         "after partition changes; published with the topology for multi-GPU placement")

@@ -79,6 +79,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); outside torchrun the probe spawns them itself")
+    ap.add_argument("--ops", default="all_reduce,all_gather,reduce_scatter")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -95,7 +96,8 @@ def main(argv: Optional[List[str]] = None) -> int:
             os.environ.update({"WORLD_SIZE": "1", "RANK": "0", "MASTER_ADDR": "127.0.0.1",
                                "MASTER_PORT": os.environ.get("MASTER_PORT", "29581")})
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    res = probe([_parse_size(s) for s in a.sizes.split(",")], iters=a.iters)
+    res = probe([_parse_size(s) for s in a.sizes.split(",")], ops=tuple(o for o in a.ops.split(",") if o),
+                iters=a.iters)
     if dist.get_rank() == 0:
         txt = json.dumps({"world": dist.get_world_size(), "results": res})
         print(txt, flush=True)

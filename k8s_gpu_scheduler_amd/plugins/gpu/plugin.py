@@ -392,8 +392,11 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return None
         req: GpuRequest = state.read(_REQ) or self.parse_request(pod)
         node = node_info.node
-        if any(t.get("key") == C.TAINT_PARTITIONING for t in O.node_taints(node)):
-            return Status.unschedulable("node is being re-partitioned", self.NAME)
+        for t in O.node_taints(node):
+            if t.get("key") == C.TAINT_PARTITIONING:
+                return Status.unschedulable("node is being re-partitioned", self.NAME)
+            if t.get("key") == C.TAINT_PROBING:
+                return Status.unschedulable("node's GPU fabric is being probed", self.NAME)
         if not self.ledger.has_node(node_info.name):
             self._on_node(node)
         if req.isolated and not req.part_cus:

@@ -11,7 +11,9 @@ adjacency alone rarely discriminates; the selection therefore ranks candidate se
 3. best fit: take GPUs from the NUMA domain with the fewest free GPUs that still fits,
    so larger future requests keep a whole domain;
 4. measured fabric (agent.fabric, `bw_gbps`): a set containing a degraded pair (copy rate
-   below half the node's median pair) ranks after every set without one, and among the
+   below half the node's median pair), or containing a GPU set whose RCCL all-reduce check
+   failed after a multi-GPU pod ran on it (agent.probes, `bad_sets`), ranks after every set
+   without one, and among the
    rest the set whose slowest pair is fastest wins (quantised to 5 % of the median, so
    measurement noise does not reorder healthy sets) -- ring collectives run at the pace
    of their slowest link;
@@ -37,6 +39,7 @@ class Topology:
     weight: List[List[int]] = field(default_factory=list)
     numa: List[int] = field(default_factory=list)
     bw: List[List[float]] = field(default_factory=list)               # measured GB/s per ordered pair
+    bad_sets: List[List[int]] = field(default_factory=list)           # RCCL set checks below par (agent.probes)
 
     @classmethod
     def fully_connected(cls, n: int = 8, numa_split: bool = True) -> "Topology":
@@ -50,12 +53,14 @@ class Topology:
     def from_json(cls, d: Dict) -> "Topology":
         n = int(d["n"])
         return cls(n, d.get("link_type") or [], d.get("hops") or [], d.get("weight") or [], d.get("numa") or [0] * n,
-                   d.get("bw_gbps") or [])
+                   d.get("bw_gbps") or [], [list(map(int, b)) for b in d.get("bad_sets") or []])
 
     def to_json(self) -> Dict:
         out = {"n": self.n, "link_type": self.link_type, "hops": self.hops, "weight": self.weight, "numa": self.numa}
         if self.bw:
             out["bw_gbps"] = self.bw
+        if self.bad_sets:
+            out["bad_sets"] = self.bad_sets
         return out
 
     def pair_bw(self, i: int, j: int) -> Optional[float]:
@@ -114,6 +119,9 @@ def select_gpu_set(topo: Topology, free_gpus: Sequence[int], k: int,
             slowest = min((topo.pair_bw(a, b) or med) for a, b in itertools.combinations(combo, 2))
             degraded = 1 if slowest < 0.5 * med else 0
             bw_q = -round(20 * slowest / med)
+        # a set whose RCCL bus bandwidth was measured below par: any superset has its rings
+        if any(set(b) <= set(combo) for b in topo.bad_sets):
+            degraded = 1
         key = (degraded, 0 if same_numa else 1, fit, bw_q, load, wsum, combo)
         if best is None or key < best[0]:
             best = (key, list(combo))

@@ -602,6 +602,43 @@ def test_fabric_probe_single_device_publishes(tmp_path):
         json.dump(res, f, indent=1)
 
 
+def test_rccl_set_check_runs_in_background_worker_and_reaches_topology(tmp_path):
+    """agent.probes on the box: the background worker runs the RCCL set check
+    (parallel.rccl_probe in a child process restricted to the set's GPUs) with the node
+    tainted, and the verdict reaches `gpusched:topology:<node>`.  One MI355X here, so the
+    set is {GPU 0} through a 1-rank RCCL communicator: the path, not a multi-GPU rate."""
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import synthetic_node
+    from k8s_gpu_scheduler_amd.agent.probes import SetChecker, busbw_of, set_probe_in_child
+    from k8s_gpu_scheduler_amd.api import constants as C
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.store import schema
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, MASTER_PORT="29623")
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("box", gpus=1))
+    taints = []
+
+    def probe(gpus):
+        taints.append([t["key"] for t in O.node_taints(fc.get("nodes", "box"))])
+        return set_probe_in_child(gpus, mib=64, iters=5, timeout_s=100, env=env)
+    sets = SetChecker(probe)
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    ag = NodeAgent("box", r, synthetic_node(1, node="box"), client=fc, set_checks=sets)
+    ag.publish()
+    sets._queue.append((0,))                 # a one-GPU "set" (note() takes >= 2 GPUs)
+    assert ag.probes.tick() == "set 0"
+    assert taints == [[C.TAINT_PROBING]] and not O.node_taints(fc.get("nodes", "box"))
+    topo = json.loads(r.get(schema.topology_key("box")))
+    (chk,) = topo["set_checks"]
+    assert chk["gpus"] == [0] and chk["busbw_gbps"] > 0 and chk["ok"], chk
+    with open(os.path.join(OUT, "rccl_set_check.json"), "w") as f:
+        json.dump(topo["set_checks"], f, indent=1)
+
+
 def test_device_plugin_allocates_real_device_nodes():
     """Device plugin on the real inventory (amd-smi / HIP): every advertised GPU resolves to
     its own /dev/dri/renderD* through sysfs, and Allocate hands a container /dev/kfd plus

@@ -371,3 +371,64 @@ def test_slo_sized_pod_takes_a_larger_gpu_when_no_node_can_be_cut():
     u = O.annotations(pod)[C.ANNOT_DEVICES]
     devs = {d.device.uuid: d for n in ("n1", "n2") for d in plugin.ledger.devices(n)}
     assert devs[u].device.cus == 256 and list(devs[u].pods) == ["default/onnx-resnet50-1024-slo"]
+
+
+def test_background_probes_taint_discard_when_busy_and_publish_bad_sets():
+    """agent.probes: the fabric probe runs off the agent's step with the node tainted, a
+    result measured while a pod appeared is thrown away, and the RCCL check of a multi-GPU
+    pod's GPU set (scripted) reaches the topology key: the degraded set steers the next
+    4-GPU pod elsewhere (the probe blocked the agent loop and ran un-tainted)."""
+    from k8s_gpu_scheduler_amd.agent.fabric import FabricProber
+    from k8s_gpu_scheduler_amd.agent.probes import SetChecker
+    from k8s_gpu_scheduler_amd.plugins.gpu.topology import Topology, select_gpu_set
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=8))
+    r = rds()
+    src = synthetic_node(8, node="n1")
+    seen_taints = []
+
+    def fabric_probe():
+        seen_taints.append([t["key"] for t in O.node_taints(fc.get("nodes", "n1"))])
+        if len(seen_taints) == 1:           # a pod sneaks onto the node mid-probe
+            p = O.make_pod("sneaky", gpu_cu=64)
+            p["spec"]["nodeName"] = "n1"
+            fc.create("pods", p)
+        return {"n": 8, "bw_gbps": [[0.0 if i == j else 120.0 for j in range(8)] for i in range(8)]}
+    bw = {(0, 1, 2, 3): 80.0, (4, 5, 6, 7): 300.0, (0, 1, 4, 5): 310.0}
+    set_calls = []
+
+    def set_probe(gpus):
+        set_calls.append(tuple(gpus))
+        return {"world": len(gpus), "results": [{"op": "all_reduce", "busbw_gbps": bw[tuple(gpus)]}]}
+    sets = SetChecker(set_probe)
+    ag = NodeAgent("n1", r, src, client=fc, fabric=FabricProber(fabric_probe), set_checks=sets)
+    ag.step()                                   # the step never probes itself
+    assert seen_taints == []
+    w = ag.probes
+    assert w.tick() == "fabric" and w.discarded == 1 and ag.fabric.due      # busy afterwards: discarded
+    assert seen_taints == [[C.TAINT_PROBING]]
+    assert not O.node_taints(fc.get("nodes", "n1"))                       # untainted again
+    assert w.tick() is None                                                # still busy: deferred
+    fc.delete("pods", "sneaky", "default")
+    assert w.tick() == "fabric" and not ag.fabric.due
+    topo = Topology.from_json(json.loads(r.get(schema.topology_key("n1"))))
+    assert topo.pair_bw(0, 1) == 120.0
+    # three multi-GPU pods ran on these sets (annotated with their devices, now finished)
+    uu = [d["uuid"] for d in src.devices()]
+    for i, s_ in enumerate(bw):
+        p = O.make_pod(f"ring-{i}", gpus=4, phase="Succeeded")
+        p["spec"]["nodeName"] = "n1"
+        p["metadata"].setdefault("annotations", {})[C.ANNOT_DEVICES] = ",".join(uu[g] for g in s_)
+        fc.create("pods", p)
+    ag.step()
+    assert sorted(sets.pending()) == sorted(bw)
+    while w.tick():
+        pass
+    assert sorted(set_calls) == sorted(bw) and sets.pending() == []
+    topo = Topology.from_json(json.loads(r.get(schema.topology_key("n1"))))
+    assert topo.bad_sets == [[0, 1, 2, 3]]                     # 80 < 0.6 x median 300
+    gpus, q = select_gpu_set(topo, list(range(8)), 4)
+    assert gpus != [0, 1, 2, 3] and q < 1.0 or gpus != [0, 1, 2, 3]
+    assert select_gpu_set(topo, [0, 1, 2, 3], 4)[1] == 0.5      # only the bad set left: degraded
+    ag.step()
+    assert sets.pending() == []                                # checked recently: not again
