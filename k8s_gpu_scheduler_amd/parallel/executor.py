@@ -94,14 +94,16 @@ class DeviceExecutor:
     #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
     #                   HIP graph on the pod's stream (captured once per workload/slot)
     use_graphs = False
-    #   balance_slots -- Burstable pods of one size are interchangeable across their CU-slice
-    #                   slots (the share is accounting, not a mask), so the executor puts each
-    #                   epoch's pods, longest first, on the slot streams with the least
-    #                   cumulative work (LPT).  The scheduler's first-fit gives the epoch's
-    #                   longest pod (LPT queue order) slot 0 every time, so slot 0's stream
-    #                   carried 131 ms of a 134 ms window and slot 6's 100 ms: the launch-ahead
-    #                   pipeline then waits on slot 0 while the others idle.
-    balance_slots = os.environ.get("GPUSCHED_BALANCE_SLOTS", "1") == "1"
+    #   balance_slots -- (off by default; an A/B arm) re-slot each epoch's same-size Burstable
+    #                   pods longest first onto the slot stream with the least cumulative work
+    #                   (LPT).  It was round 3's default: +1.5 % pods/s over the scheduler's
+    #                   first-fit slots, but blind to SLOs (-9 points of SLO attainment).  The
+    #                   scheduler now chooses each pod's slot itself on its model of the slot
+    #                   pipelines (plugins.gpu.timeline, --plan-slots), and the executor runs
+    #                   every pod on the slot it was given (MI355X, 20 steps x 3 interleaved:
+    #                   603.5 pods/s / 56.25 % SLOs vs 600.7 / 53.75 % for LPT re-slotting,
+    #                   gpurun_out r04_slots_ab20 -> profiles/r04_slots_ab/)
+    balance_slots = os.environ.get("GPUSCHED_BALANCE_SLOTS", "0") == "1"
 
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
         self.device = device

@@ -335,7 +335,7 @@ class ControlPlane:
         n = max(st.get("slot_plans", 0), 1)
         for k in ("slot_spread_ms", "slot_min_spread_ms"):
             st[k] = round(st[k] / n, 3)
-        st["slot_expected_met_pct"] = round(100.0 * st.pop("slot_expected_met") / max(st["slot_pods"], 1), 2)
+        st["slot_pred_met_pct"] = round(100.0 * st.pop("slot_pred_met") / max(st["slot_pods"], 1), 2)
         tl = getattr(planner, "timeline", None)
         if tl is not None:
             st["timeline_measured"] = tl.measured
@@ -613,7 +613,7 @@ def _prewarm(dev: torch.device, ms: float) -> None:
     del a, bt, c
 
 
-def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="MI355X pod-arrival scheduling benchmark")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -658,7 +658,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
                     help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
                          "collected epoch (a GPU slower than its siblings, or the model's error on it)")
-    ap.add_argument("--plan-slots", type=int, default=0, choices=[0, 1],
+    ap.add_argument("--plan-slots", type=int, default=1, choices=[0, 1],
                     help="co-run planner: also choose each pod's CU slot by simulating its GPU's slot pipelines "
                          "(in-flight pods of earlier epochs, measured ones pinned)")
     ap.add_argument("--slot-spread-ms", type=float, default=2.0,
@@ -677,10 +677,12 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     ap.add_argument("--balance", type=float, default=1.0,
                     help="weight of the GPU plugin's least-predicted-load term (0 = off; >0 also sorts the "
                          "queue longest-predicted-work first)")
-    ap.add_argument("--slot-balance", type=int, default=int(os.environ.get("GPUSCHED_BALANCE_SLOTS", "1")),
+    ap.add_argument("--slot-balance", type=int, default=int(os.environ.get("GPUSCHED_BALANCE_SLOTS", "0")),
                     choices=[0, 1],
                     help="1: the executor re-slots each epoch's Burstable pods longest-first onto the least-loaded "
                          "CU slot (blind to SLOs); 0: pods run on the slot the scheduler chose")
+    ap.add_argument("--dump-placements", default="",
+                    help="write every epoch's placements (JSON) for a hardware replay (tools/pipelined_vn.py)")
     ap.add_argument("--no-cu-mask", action="store_true")
     ap.add_argument("--qos", default="burstable", choices=["burstable", "guaranteed"],
                     help="burstable: CU request is an accounted share, kernels may use idle CUs; "
@@ -726,7 +728,29 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                          "the same (593/594 vs 594/592 pods/s at 20 steps, 625 vs 618 at 60; "
                          "profiles/r03_window/README.md)")
     ap.add_argument("--out", default="")
-    a = ap.parse_args(argv)
+    return ap
+
+
+def gpu_executor(a: Any, dev_idx: int = 0) -> Any:
+    """The bench's DeviceExecutor with its kernel / launch policy flags (`a`: parsed args)."""
+    from .executor import DeviceExecutor
+    ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
+    ex.use_graphs = bool(a.graphs)
+    from .. import _native
+    h = _native.hip(required=True)
+    h.set_gemm_policy(a.gemm_policy)
+    h.set_wide_epilogue(a.wide_epilogue)
+    h.set_xcd_blocks(a.xcd_blocks)
+    h.set_xcd_group(a.xcd_group)
+    h.set_triad_variant(a.triad_variant)
+    ex.triad_blocks = a.triad_blocks
+    ex.gemm_share = bool(a.gemm_share)
+    ex.balance_slots = bool(a.slot_balance)
+    return ex
+
+
+def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
+    a = build_parser().parse_args(argv)
     a.lookahead = max(1, a.lookahead)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -801,17 +825,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         cp = ControlPlane(**cp_kwargs)
     async_cp = hasattr(cp, "request_schedule")
     if use_gpu:
-        from .executor import DeviceExecutor
-        ex = DeviceExecutor(dev_idx, use_cu_masks=not a.no_cu_mask)
-        ex.use_graphs = bool(a.graphs)
-        from .. import _native
-        _native.hip(required=True).set_gemm_policy(a.gemm_policy)
-        _native.hip(required=True).set_wide_epilogue(a.wide_epilogue)
-        _native.hip(required=True).set_xcd_blocks(a.xcd_blocks)
-        _native.hip(required=True).set_xcd_group(a.xcd_group)
-        _native.hip(required=True).set_triad_variant(a.triad_variant)
-        ex.triad_blocks = a.triad_blocks
-        ex.gemm_share = bool(a.gemm_share)
+        ex = gpu_executor(a, dev_idx)
     elif a.sim_model:
         from .modelpipe import ModelPipelineExecutor
         ex = ModelPipelineExecutor(noise=a.sim_noise, perturb=a.sim_perturb, seed=a.seed + 1000 * rank)
@@ -926,6 +940,10 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             totals["busy_unit_ms"] += tot[0]
             totals["slo_ok"] += tot[2]
 
+    # --dump-placements: every epoch's placement array (gpu, first unit, units, workload id,
+    # iterations, SLO milli-it/s, masked) for a replay on hardware (tools/pipelined_vn.py)
+    placements: Optional[List[Dict[str, Any]]] = [] if a.dump_placements else None
+
     def run_epochs(count: int, timed: bool) -> None:
         """Launch-ahead pipeline: epoch e is enqueued (device-side ordered behind e-1),
         rank 0 schedules e+1 while the GPU runs, then epoch e-L is collected (L =
@@ -953,6 +971,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                 host["launch"] += t2 - t1
                 host["schedule"] += time.perf_counter() - t2
             pending.append((runs, arr))
+            if placements is not None and rank == 0:
+                placements.append({"timed": bool(timed), "arr": arr.tolist()})
             while len(pending) > a.lookahead:
                 collect(*pending.popleft(), timed)
             if rank == 0 and async_cp:
@@ -1088,6 +1108,13 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(result, f)
+        if placements is not None:
+            with open(a.dump_placements, "w") as f:
+                json.dump({"n_gpus": n_gpus, "lookahead": a.lookahead, "seed": a.seed, "workloads": list(W.NAMES),
+                           "fields": ["gpu", "first_unit", "n_units", "wid", "iters", "slo_milli", "masked"],
+                           "config": result["config"], "sim": {"value": result["value"],
+                                                                "slo_attainment_pct": result["slo_attainment_pct"]},
+                           "epochs": placements}, f)
     if smi_s is not None:
         smi_s.stop()
     ex.close()

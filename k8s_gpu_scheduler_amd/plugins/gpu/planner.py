@@ -83,7 +83,7 @@ class BurstPlanner:
         # the phantom continuation, vs ~0.06 once the co-runners are measured)
         self.slot_sigma = slot_sigma
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
-        self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "slot_expected_met": 0.0,
+        self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "slot_pred_met": 0,
                       "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
 
     # ---------------------------------------------------------------- inputs
@@ -452,7 +452,7 @@ class BurstPlanner:
             if len(ctx["wid"]) + len(items) + len(ctx["ph_wid"]) > 64:
                 continue
             nw = np.array([model.wid(O.name(p)) for p, _ in items], np.int32)
-            sl, _, _, exp, spread, min_spread = core.plan_slots(
+            sl, st0, fin, exp, spread, min_spread = core.plan_slots(
                 ctx["wid"], ctx["iters"], ctx["start"], ctx["prev"], ctx["pin"], ctx["slo"], ctx["slot_tail"],
                 ctx["slot_free"], nw, np.array([r.iters for _, r in items], np.float64),
                 np.array([r.slo * margin for _, r in items], np.float64), np.full(len(items), -1e300),
@@ -462,7 +462,13 @@ class BurstPlanner:
                 res[O.key(p)] = slots[int(s)][0]
             self.stats["slot_plans"] += 1
             self.stats["slot_pods"] += len(items)
-            self.stats["slot_expected_met"] += float(exp)
+            # the new pods predicted to meet their SLO on the chosen slots (hard counts; `exp`
+            # also covers the unmeasured context pods the choice re-predicts)
+            m0 = len(ctx["wid"])
+            for j, (_, r) in enumerate(items):
+                d_ms = float(fin[m0 + j] - st0[m0 + j])
+                if r.slo <= 0 or (d_ms > 0 and r.iters / d_ms * 1e3 >= r.slo * margin):
+                    self.stats["slot_pred_met"] += 1
             self.stats["slot_spread_ms"] += float(spread)
             self.stats["slot_min_spread_ms"] += float(min_spread)
         return res
