@@ -18,6 +18,9 @@ model (models.corun.OnlineCorun, served by the recommender's ObserveCorun) learn
     finished without a trace (not profiled) is dropped -- its pressure would be missing from
     the group and bias the fit.
 
+A pod that ran ALONE on its device becomes a 1-pod group: for a workload the co-run model
+does not know yet, the recommender cold-starts its row from it (models.coldstart).
+
 Observations go to the recommender in batches (`send`, e.g. RecommenderClient.observe_corun);
 its refit worker then serves a new ExportTable("corun") version, which the schedulers'
 CachedPredictions pick up on their next refresh.
@@ -58,7 +61,8 @@ class CorunObserver:
         devs = [d for d in (O.annotations(pod).get(C.ANNOT_DEVICES) or "").split(",") if d]
         return devs[0] if len(devs) == 1 else None
 
-    def add(self, pod: Dict[str, Any], workload: str, iters: float, first_ns: int, last_ns: int) -> bool:
+    def add(self, pod: Dict[str, Any], workload: str, iters: float, first_ns: int, last_ns: int,
+            mfma_share: Optional[float] = None) -> bool:
         uuid = self.device_of(pod)
         if uuid is None or last_ns <= first_ns:
             return False
@@ -69,7 +73,8 @@ class CorunObserver:
         with self._lock:
             self._recs.setdefault(uuid, []).append(
                 {"key": key, "workload": workload, "iters": float(iters), "s": int(first_ns), "e": int(last_ns),
-                 "t": self.clock(), "wait": running, "emitted": False})
+                 "t": self.clock(), "wait": running, "emitted": False,
+                 "mfma": -1.0 if mfma_share is None else float(mfma_share)})
         return True
 
     def _ready(self, uuid: str, r: Dict[str, Any], traced: Set[str]) -> Optional[bool]:
@@ -108,7 +113,10 @@ class CorunObserver:
                             "iters": [x["iters"] if x["iters"] > 0 else 1.0 for x in mem],
                             "ms": [(x["e"] - x["s"]) / 1e6 for x in mem],
                             "start_ms": [(x["s"] - t0) / 1e6 for x in mem],
-                            "target": [x is r for x in mem]})
+                            "target": [x is r for x in mem],
+                            # per member: MFMA share of its kernel time (-1 unknown); a 1-pod
+                            # group of an unseen workload cold-starts its co-run row
+                            "mfma_share": [x.get("mfma", -1.0) for x in mem]})
         sent = 0
         if out:
             try:

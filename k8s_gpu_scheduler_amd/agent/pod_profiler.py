@@ -33,14 +33,32 @@ ROCPROF = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
 log = logging.getLogger(__name__)
 
 
+# kernel-name markers of matrix-core (MFMA) work: this framework's GEMMs (gs::gemm_*),
+# hipBLASLt / Tensile (Cijk_*), rocBLAS, composable_kernel / MIOpen implicit-GEMM convolutions,
+# flash attention
+MFMA_KERNEL_MARKERS = ("gemm", "cijk_", "mfma", "matmul", "igemm", "conv", "fmha", "attn", "xdl", "wmma")
+
+
+def is_mfma_kernel(name: str) -> bool:
+    n = name.lower()
+    return any(m in n for m in MFMA_KERNEL_MARKERS)
+
+
 def summarize_kernel_stats(path: str, top: int = 5) -> Dict[str, Any]:
+    """Busy time, calls, the top kernels and `mfma_share`: the fraction of kernel time in
+    matrix-core kernels (by name) -- the resource shape the co-run model's cold start
+    (models.coldstart) places an unseen workload by."""
     rows = list(csv.DictReader(open(path)))
     tot_ns = sum(float(r.get("TotalDurationNs", 0) or 0) for r in rows)
+    mfma_ns = sum(float(r.get("TotalDurationNs", 0) or 0) for r in rows if is_mfma_kernel(r.get("Name", "")))
     calls = sum(int(float(r.get("Calls", 0) or 0)) for r in rows)
     rows.sort(key=lambda r: -float(r.get("TotalDurationNs", 0) or 0))
-    return {"gpu_busy_ms": tot_ns / 1e6, "kernels": calls,
-            "top": [{"name": r["Name"][:120], "calls": int(float(r["Calls"])),
-                     "ms": float(r["TotalDurationNs"]) / 1e6} for r in rows[:top]]}
+    out = {"gpu_busy_ms": tot_ns / 1e6, "kernels": calls,
+           "top": [{"name": r["Name"][:120], "calls": int(float(r["Calls"])),
+                    "ms": float(r["TotalDurationNs"]) / 1e6} for r in rows[:top]]}
+    if tot_ns > 0:
+        out["mfma_share"] = round(mfma_ns / tot_ns, 4)
+    return out
 
 
 def summarize_counters(path: str) -> Dict[str, float]:
@@ -267,7 +285,8 @@ class ProfileIngestor:
                 continue
             if self.corun is not None and first is not None and last is not None and last > first:
                 try:
-                    self.corun.add(pod, wl, float(req.get("iters", 0.0)), int(first), int(last))
+                    self.corun.add(pod, wl, float(req.get("iters", 0.0)), int(first), int(last),
+                                   mfma_share=sample.get("mfma_share"))
                 except Exception as e:
                     log.warning("profile %s: co-run record failed: %s", d, e)
             self.ingested.append(sample)

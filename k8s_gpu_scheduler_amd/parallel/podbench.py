@@ -152,6 +152,10 @@ class ControlPlane:
         self.sched.keep_results = False
         self.sched.start_informers()
         self.plugin = self.sched.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+        if getattr(self.plugin, "planner", None) is not None:
+            # the bench corrects the backlog per collected epoch (_plan_feedback); its pods are
+            # deleted, never completed, so the deployed completion feedback stays off
+            self.plugin.planner.feedback = None
         self.uuid_to_gpu = {d.device.uuid: d.device.gpu for d in self.ledger.devices(NODE)}
         conf = self.predictions._conf
         self.quarter_tput = {n: conf.by_label[n][f"{C.MI355X_CUS // cu_per_pod}P_{C.MI355X}"] for n in W.NAMES}

@@ -83,6 +83,12 @@ class BurstPlanner:
         # the phantom continuation, vs ~0.06 once the co-runners are measured)
         self.slot_sigma = slot_sigma
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
+        # measured backlog feedback from pod completions (plugins.gpu.feedback; deployed
+        # clusters -- the bench corrects per collected epoch instead)
+        self.feedback = None
+        if carry > 0:
+            from .feedback import CompletionFeedback
+            self.feedback = CompletionFeedback(self)
         self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "slot_pred_met": 0,
                       "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
 
@@ -474,8 +480,9 @@ class BurstPlanner:
         return res
 
     def placed(self, pod: Obj, node: str, choice: Any, req: Any) -> None:
-        """Reserve: the pod took `choice` -- append it to its GPU's slot timeline."""
-        if self.timeline is None or choice is None:
+        """Reserve: the pod took `choice` -- append it to its GPU's slot timeline, and record
+        its predicted duration next to its co-residents for the completion feedback."""
+        if (self.timeline is None and self.feedback is None) or choice is None:
             return
         model = self.plugin.corun_model()
         if model is None:
@@ -487,6 +494,22 @@ class BurstPlanner:
         uuid, u0, n = frac[0][0], frac[0][1], frac[0][2]
         st = next((s for s in self.plugin.ledger.devices(node) if s.device.uuid == uuid), None)
         if st is None:
+            return
+        group = (node,) + self.plugin.corun_group_key(st)
+        if self.feedback is not None and req.iters > 0:
+            mem = [(k, model.wid(u.name), u.iters) for s in self.plugin.ledger.devices(node)
+                   if (node,) + self.plugin.corun_group_key(s) == group for k, u in s.pods.items()]
+            mem = [(k, wi, it) for k, wi, it in mem if wi >= 0 and it > 0]
+            keys = [k for k, _, _ in mem]
+            if O.key(pod) in keys and len(mem) <= 64:
+                # every member's prediction is refreshed with the group as it now stands: a pod
+                # placed earlier co-runs with this one too
+                d = model.group_durations([wi for _, wi, _ in mem], [it for _, _, it in mem])
+                self.feedback.expect(O.key(pod), group, float(d[keys.index(O.key(pod))]))
+                for k, x in zip(keys, d):
+                    if k != O.key(pod):
+                        self.feedback.refresh(k, group, float(x))
+        if self.timeline is None:
             return
         margin = 1.0 + self.plugin.args.corun_margin
         self.timeline.place((node,) + self.plugin.corun_group_key(st), (u0, n), O.key(pod), w, req.iters,

@@ -287,6 +287,9 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         """Rebuild reservations of assigned pods from their annotations (scheduler restart
         recovery) and release finished ones."""
         if O.is_terminal(pod):
+            fb = getattr(self.planner, "feedback", None) if self.planner is not None else None
+            if fb is not None:
+                fb.completed(pod)       # measured vs predicted time -> its GPU's planned backlog
             self.ledger.release(O.key(pod))
             return
         node = O.node_name_of(pod)
@@ -310,6 +313,11 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                                 iters=float(O.pod_iterations(pod)))
 
     def _on_pod_delete(self, pod: Obj) -> None:
+        fb = getattr(self.planner, "feedback", None) if self.planner is not None else None
+        if fb is not None:
+            if O.is_terminal(pod):
+                fb.completed(pod)
+            fb.forget(O.key(pod))
         self.ledger.release(O.key(pod))
         if self.planner is not None:
             self.planner.consume(O.key(pod))

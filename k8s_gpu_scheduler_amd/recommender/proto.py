@@ -87,6 +87,7 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
     _field(cg, "start_ms", 3, _F.TYPE_FLOAT, _F.LABEL_REPEATED)       # start offsets in the group
     _field(cg, "ms", 4, _F.TYPE_FLOAT, _F.LABEL_REPEATED)             # measured wall ms
     _field(cg, "target", 5, _F.TYPE_BOOL, _F.LABEL_REPEATED)          # observation (else co-runner only)
+    _field(cg, "mfma_share", 6, _F.TYPE_FLOAT, _F.LABEL_REPEATED)     # MFMA share of kernel time (-1 unknown)
     ocq = fx.message_type.add(name="ObserveCorunRequest")
     _field(ocq, "groups", 1, _F.TYPE_MESSAGE, _F.LABEL_REPEATED, ".gpusched.recommender.CorunGroup")
     ocp = fx.message_type.add(name="ObserveCorunReply")

@@ -23,7 +23,7 @@ import logging
 import os
 import threading
 from concurrent import futures
-from typing import Any, Callable, Dict, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 import grpc
 import numpy as np
@@ -118,6 +118,11 @@ class CorunSlot:
         self.model: Any = None
         self.version: Optional[str] = None
         self.file_version: Optional[str] = None
+        self.file_label = ""
+
+    def file_version_label(self) -> str:
+        """The version of the file model (what online / cold-start versions extend)."""
+        return self.file_label or (self.version or "").split("+")[0]
 
     def load_if_changed(self) -> bool:
         v = file_version(self.path) if self.path else None
@@ -129,7 +134,7 @@ class CorunSlot:
             return False
         with self._lock:
             self.model, self.file_version = m, v
-            self.version = f"{m.version}@{v[:8]}"
+            self.version = self.file_label = f"{m.version}@{v[:8]}"
         log.info("corun: loaded %s (%d workloads)", self.version, len(m.names))
         return True
 
@@ -154,6 +159,9 @@ class RecommenderService:
         self.corun = CorunSlot(corun_path)
         self._corun_online: Any = None      # models.corun.OnlineCorun on the served file model
         self._corun_online_base: Optional[str] = None
+        # workload -> alone observations (ms per iteration, MFMA share or None) of workloads
+        # the co-run model file does not know (cold start, models.coldstart)
+        self._cold: Dict[str, List[Any]] = {}
         self._corun_refit_mode: Any = "process"
         # OnlineCorun knobs (from_env: CORUN_MIN_OBS, CORUN_MIN_CALIB, CORUN_REFIT_EVERY)
         self.corun_online_kw: Dict[str, int] = {}
@@ -354,7 +362,22 @@ class RecommenderService:
                 self._corun_online = OnlineCorun(fm or base, background=self._corun_refit_mode,
                                                  **self.corun_online_kw)
                 self._corun_online_base = self.corun.file_version
+                reload_cold = bool(self._cold)      # a new model file: cold-start the known rows again
+            else:
+                reload_cold = False
+            # cold start (models.coldstart): a workload the model does not know that ran
+            # ALONE on its device (a 1-pod group) gets a row imputed from its alone profile
+            fresh = reload_cold
+            for g in request.groups:
+                if len(g.workloads) == 1 and len(g.ms) == 1 and len(g.iters) == 1 and g.ms[0] > 0 \
+                        and g.iters[0] > 0 and self._corun_online.base.wid(g.workloads[0]) < 0:
+                    mf = float(g.mfma_share[0]) if len(g.mfma_share) == 1 and g.mfma_share[0] >= 0 else None
+                    self._cold.setdefault(g.workloads[0], []).append((g.ms[0] / g.iters[0], mf))
+                    fresh = True
+            if fresh:
+                self._cold_start_rows()
             on = self._corun_online
+            base = on.base
             for g in request.groups:
                 w = [base.wid(n) for n in g.workloads]
                 k = len(w)
@@ -364,11 +387,39 @@ class RecommenderService:
                 tg = list(g.target) if len(g.target) == k else None
                 on.observe_group(w, list(g.iters), list(g.ms), st, tg)
                 reply.accepted += 1
-            if on.model is not self.corun.get() and on.refits:
-                self.corun.serve(on.model, f"{self.corun.version.split('+')[0]}+online-{on.version}")
+            if on.model is not self.corun.get() and (on.refits or fresh):
+                ver = f"{self.corun.file_version_label()}" + (f"+cold-{len(self._cold)}" if self._cold else "")
+                self.corun.serve(on.model, ver + (f"+online-{on.version}" if on.refits else ""))
             reply.corun = self.corun.version or ""
             reply.observations = int(on.err["n"])
         return reply
+
+    def _cold_start_rows(self) -> None:
+        """Rebuild the online co-run learner on the file model plus every cold-started
+        workload (median alone ms per iteration of its alone observations), carrying the
+        learner's state over: its observation window, error bookkeeping and per-workload
+        refit parameters (new workloads start at 0: the imputed row as is)."""
+        import numpy as np
+        from ..models.coldstart import with_workload
+        from ..models.corun import CorunModel, OnlineCorun
+        old = self._corun_online
+        fm = CorunModel.load(self.corun.path) if self.corun.path else old.base
+        ext = fm
+        for name, obs in sorted(self._cold.items()):
+            a = float(np.median([x[0] for x in obs]))
+            shares = [x[1] for x in obs if x[1] is not None]
+            ext = with_workload(ext, name, a, float(np.median(shares)) if shares else None)
+        on = OnlineCorun(ext, background=self._corun_refit_mode, **self.corun_online_kw)
+        n_old = len(old.base.names)
+        x = np.asarray(old._x)
+        on._x = np.concatenate([x[:n_old], np.zeros(len(ext.names) - n_old), x[n_old:]])
+        on._obs, on.err, on.version, on.refits, on.time_scale = list(old._obs), dict(old.err), old.version, \
+            old.refits, old.time_scale
+        n = len(ext.names)
+        on.model = CorunModel(ext.names, ext.alone_ms * np.exp(on._x[:n]) * on.time_scale,
+                              ext.u * np.exp(on._x[n]), ext.v, dict(ext.meta))
+        self._corun_online = on
+        log.info("corun: cold-started %s", sorted(self._cold))
 
     def Version(self, request: Any, context: Any) -> Any:
         return P.VersionReply(configurations=self.conf.version or "", interference=self.intf.version or "",

@@ -88,7 +88,7 @@ def test_profiled_pods_on_one_gpu_refine_the_served_model_and_the_scheduler_scor
     svc.train()
     srv, port = svc.make_server(0, 2, "127.0.0.1")
     try:
-        cl = RecommenderClient(f"127.0.0.1:{port}")
+        cl = RecommenderClient(f"127.0.0.1:{port}", timeout_s=30.0)   # synchronous refits in the RPC
         v0 = cl.version().corun
         base = CorunModel.load(str(cm))
         slow = CorunModel(base.names, base.alone_ms * 1.3, base.u, base.v)      # this node runs 30 % slower
@@ -120,6 +120,78 @@ def test_profiled_pods_on_one_gpu_refine_the_served_model_and_the_scheduler_scor
         from k8s_gpu_scheduler_amd.plugins.gpu.plugin import GPUPlugin
         plugin = GPUPlugin({"sloObjective": "corun"}, predictions=cache)
         assert plugin.corun_model().version == v1
+    finally:
+        svc.stop()
+        srv.stop(0)
+
+
+def test_cold_start_leave_one_workload_out_on_measured_groups():
+    """models.coldstart: each catalog workload in turn is dropped from the shipped model and
+    re-imputed from its alone profile (alone ms per iteration, MFMA share) and the other 17
+    rows; on its measured MI355X co-run groups (profiles/r03_corun_v2) the imputed row's
+    throughput error stays within 2x the fitted model's held-out error, and
+    far below the roofline prior row's."""
+    import json
+    from k8s_gpu_scheduler_amd.models.coldstart import impute_row, mfma_share
+    from k8s_gpu_scheduler_amd.models.corun import pack_groups
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = json.load(open(os.path.join(root, "profiles", "r03_corun_v2", "groups_2558_hostwait.json")))
+    groups = [g for g in d["groups"] if len(g["w"]) >= 2]
+    m = CorunModel.load()
+    held_out = m.meta["report"]["test"]["mae_pct_of_mean"]
+    prior = CorunModel.prior(m.names)
+
+    def err(model, i):
+        gs = [g for g in groups if m.names[i] in g["w"]]
+        wids, iters, mask, ms, st = pack_groups(gs, m.names, 4)
+        t = model.batch_times(wids, iters, mask, st) - st
+        sel = mask & (wids == i)
+        tp, tm = iters / np.maximum(t, 1e-9) * 1e3, iters / np.maximum(ms, 1e-9) * 1e3
+        return 100 * np.abs(tp - tm)[sel].mean() / tm[sel].mean()
+    imp, pri = [], []
+    for i, n in enumerate(m.names):
+        u, v, nn = impute_row(m, float(m.alone_ms[i]), mfma_share(n), exclude=[i])
+        assert n not in nn
+        U, V = m.u.copy(), m.v.copy()
+        U[i], V[i] = u, v
+        imp.append(err(CorunModel(m.names, m.alone_ms, U, V), i))
+        U[i], V[i] = prior.u[i], prior.v[i]
+        pri.append(err(CorunModel(m.names, m.alone_ms, U, V), i))
+    assert np.mean(imp) <= 2 * held_out, (np.mean(imp), held_out)
+    assert np.median(imp) <= 2 * held_out and np.mean(imp) < 0.5 * np.mean(pri), (imp, pri)
+
+
+def test_unseen_workload_cold_starts_through_observe_corun_and_plans(tmp_path):
+    """An unseen workload profiled alone on its GPU (a 1-pod co-run observation from the node
+    agent) gets a served co-run row: `wid` is no longer -1 and the GPU plugin's model has it;
+    its later co-run groups are then accepted as observations."""
+    cm = tmp_path / "corun.json"
+    shutil.copy(DATA, cm)
+    svc = RecommenderService("", "", corun_path=str(cm))
+    svc._corun_refit_mode = False
+    svc.train()
+    srv, port = svc.make_server(0, 2, "127.0.0.1")
+    try:
+        cl = RecommenderClient(f"127.0.0.1:{port}", timeout_s=30.0)   # synchronous refits in the RPC
+        base = CorunModel.load(str(cm))
+        assert base.wid("llama-prefill-7b-xyz") == -1
+        rep = cl.observe_corun([{"workloads": ["llama_prefill_7b"], "iters": [20], "ms": [3.0],
+                                 "start_ms": [0.0], "target": [True], "mfma_share": [0.9]}])
+        assert rep.accepted == 1 and "+cold-1" in rep.corun
+        cache = CachedPredictions(cl, background=False)
+        cache.refresh(force=True)
+        m = cache.corun()
+        i = m.wid("llama-prefill-7b-xyz")
+        assert i >= 0 and abs(m.alone_ms[i] - 0.15) < 1e-6
+        # a GEMM-heavy newcomer is imputed from the GEMM-heavy catalog rows
+        assert np.allclose(m.u[i], np.exp(np.mean(np.log(m.u[[m.wid(n) for n in svc._corun_online.base.meta[
+            "cold_start"]["llama_prefill_7b"]["neighbours"]]]), axis=0)), rtol=0.5)
+        rep = cl.observe_corun([{"workloads": ["llama_prefill_7b", "onnx_mobilenet_1024"], "iters": [20, 20],
+                                 "ms": [4.0, 2.5], "start_ms": [0.0, 0.0], "target": [True, True]}])
+        assert rep.accepted == 1
+        from k8s_gpu_scheduler_amd.plugins.gpu.plugin import GPUPlugin
+        plugin = GPUPlugin({"sloObjective": "corun"}, predictions=cache)
+        assert plugin.corun_model().wid("llama-prefill-7b-abc") >= 0
     finally:
         svc.stop()
         srv.stop(0)

@@ -435,7 +435,7 @@ def test_observe_corun_rpc_serves_a_refined_model(ref_data, tmp_path):
     svc.train()
     srv, port = svc.make_server(0, 2, "127.0.0.1")
     try:
-        cl = RecommenderClient(f"127.0.0.1:{port}")
+        cl = RecommenderClient(f"127.0.0.1:{port}", timeout_s=30.0)   # synchronous refits in the RPC
         base = CorunModel.load(str(cm))
         slow = CorunModel(base.names, base.alone_ms * 1.25, base.u, base.v)      # the cluster runs 25 % slower
         rng = np.random.default_rng(5)
