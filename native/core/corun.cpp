@@ -40,7 +40,7 @@ constexpr int kMaxK = 64;   // pods per GPU group (CPX: 64 devices of 4 CUs woul
 // own (earlier) co-runners lie outside the observed window.
 void sim_group(int k, const int32_t* w, const double* iters, const double* start, const double* alone,
                const double* C, int W, double* fin, const double* pin_end = nullptr) {
-  double rem[kMaxK], st[kMaxK], pe[kMaxK];
+  double rem[kMaxK], st[kMaxK], pe[kMaxK], load[kMaxK];
   bool started[kMaxK], done[kMaxK], svc[kMaxK], pin[kMaxK];
   for (int i = 0; i < k; ++i) {
     svc[i] = iters[i] <= 0;
@@ -50,16 +50,24 @@ void sim_group(int k, const int32_t* w, const double* iters, const double* start
     rem[i] = (svc[i] || pin[i]) ? kBig : std::max(alone[w[i]] * iters[i], 1e-12);
     started[i] = done[i] = false;
     fin[i] = pin[i] ? pe[i] : svc[i] ? kBig : 0.0;
+    load[i] = 1.0;
   }
+  // load[i] = 1 + sum over ACTIVE j != i of C[w_i][w_j], kept up to date at every start / end
+  // (O(k) per event instead of O(k^2) per step)
+  auto press = [&](int j, double sign) {
+    const double* cj = C + (size_t)w[j];
+    for (int i = 0; i < k; ++i)
+      if (i != j) load[i] += sign * cj[(size_t)w[i] * W];
+  };
   double now = 0.0;
   for (int step = 0; step < 3 * k + 1; ++step) {
     bool live = false;
     for (int i = 0; i < k; ++i) live |= !done[i] && !svc[i] && !pin[i];
     if (!live) break;
     for (int i = 0; i < k; ++i)
-      if (!started[i] && st[i] <= now + 1e-12) started[i] = true;
+      if (!started[i] && st[i] <= now + 1e-12) started[i] = true, press(i, 1.0);
     for (int i = 0; i < k; ++i)
-      if (pin[i] && started[i] && !done[i] && pe[i] <= now + 1e-12) done[i] = true;
+      if (pin[i] && started[i] && !done[i] && pe[i] <= now + 1e-12) done[i] = true, press(i, -1.0);
     double rate[kMaxK];
     double dt = kBig;
     int am = -1;
@@ -67,11 +75,7 @@ void sim_group(int k, const int32_t* w, const double* iters, const double* start
     for (int i = 0; i < k; ++i) {
       rate[i] = 0.0;
       if (!started[i] || done[i] || pin[i]) continue;
-      double load = 1.0;
-      const double* ci = C + (size_t)w[i] * W;
-      for (int j = 0; j < k; ++j)
-        if (j != i && started[j] && !done[j]) load += ci[w[j]];
-      rate[i] = 1.0 / load;
+      rate[i] = 1.0 / load[i];
       if (!svc[i]) {
         const double t = rem[i] / std::max(rate[i], 1e-30);
         if (t < am_t) am_t = t, am = i;
@@ -91,6 +95,7 @@ void sim_group(int k, const int32_t* w, const double* iters, const double* start
       if (rem[i] <= 1e-9 * std::max(wk, 1.0) || (i == am && am_t <= dt + 1e-12)) {
         done[i] = true;
         fin[i] = now;
+        press(i, -1.0);
       }
     }
   }
@@ -106,7 +111,7 @@ void sim_group(int k, const int32_t* w, const double* iters, const double* start
 void sim_chain(int k, const int32_t* w, const double* iters, const double* start, const int32_t* prev,
                const double* alone, const double* C, int W, double* st_out, double* fin,
                const double* pin_end = nullptr) {
-  double rem[kMaxK];
+  double rem[kMaxK], load[kMaxK];
   bool started[kMaxK], done[kMaxK], svc[kMaxK], pin[kMaxK], known[kMaxK];
   double now = kBig;
   for (int i = 0; i < k; ++i) {
@@ -117,9 +122,16 @@ void sim_chain(int k, const int32_t* w, const double* iters, const double* start
     rem[i] = (svc[i] || pin[i]) ? kBig : std::max(alone[w[i]] * iters[i], 1e-12);
     started[i] = done[i] = false;
     fin[i] = pin[i] ? pin_end[i] : kBig;
+    load[i] = 1.0;
     if (known[i]) now = std::min(now, st_out[i]);
   }
   if (now >= kBig) return;
+  // incrementally maintained loads, as sim_group
+  auto press = [&](int j, double sign) {
+    const double* cj = C + (size_t)w[j];
+    for (int i = 0; i < k; ++i)
+      if (i != j) load[i] += sign * cj[(size_t)w[i] * W];
+  };
   for (int step = 0; step < 4 * k + 2; ++step) {
     bool live = false;
     for (int i = 0; i < k; ++i) live |= !done[i] && !svc[i] && !pin[i];
@@ -130,21 +142,17 @@ void sim_chain(int k, const int32_t* w, const double* iters, const double* start
         known[i] = true;
         st_out[i] = std::max(fin[prev[i]], start[i]);
       }
-      if (known[i] && st_out[i] <= now + 1e-12) started[i] = true;
+      if (known[i] && st_out[i] <= now + 1e-12) started[i] = true, press(i, 1.0);
     }
     for (int i = 0; i < k; ++i)
-      if (pin[i] && started[i] && !done[i] && fin[i] <= now + 1e-12) done[i] = true;
+      if (pin[i] && started[i] && !done[i] && fin[i] <= now + 1e-12) done[i] = true, press(i, -1.0);
     double rate[kMaxK];
     int am = -1;
     double am_t = kBig;
     for (int i = 0; i < k; ++i) {
       rate[i] = 0.0;
       if (!started[i] || done[i] || pin[i]) continue;
-      double load = 1.0;
-      const double* ci = C + (size_t)w[i] * W;
-      for (int j = 0; j < k; ++j)
-        if (j != i && started[j] && !done[j]) load += ci[w[j]];
-      rate[i] = 1.0 / load;
+      rate[i] = 1.0 / load[i];
       if (!svc[i]) {
         const double t = rem[i] / std::max(rate[i], 1e-30);
         if (t < am_t) am_t = t, am = i;
@@ -166,6 +174,7 @@ void sim_chain(int k, const int32_t* w, const double* iters, const double* start
       if (rem[i] <= 1e-9 * std::max(wk, 1.0) || (i == am && am_t <= dt + 1e-12)) {
         done[i] = true;
         fin[i] = now;
+        press(i, -1.0);
       }
     }
   }
@@ -475,8 +484,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       for (int64_t r = RO[g]; r < RO[g + 1]; ++r) mem[g].push_back(-1 - (int)r);
     for (py::ssize_t p = 0; p < P; ++p) mem[DG[dev[p]]].push_back((int)p);
     bool use_pipe = false, phase_b = false;
-    auto eval = [&](int g) {
-      const auto& v = mem[g];
+    auto eval_raw = [&](int g, const std::vector<int>& v) {
       const int k = (int)v.size();
       if (k > kMaxK) throw std::runtime_error("plan_corun: GPU group larger than 64 pods");
       int32_t w[kMaxK];
@@ -542,7 +550,31 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       }
       return e;
     };
-    long n_evals = 0;
+    // memo of group evaluations per phase: a sweep re-evaluates mostly the same (GPU, member
+    // set) pairs as the previous one -- only the two groups of an accepted move / swap change.
+    // The members are evaluated in sorted order, so a result is a function of the set.
+    struct KeyHash {
+      size_t operator()(const std::vector<int>& v) const {
+        uint64_t h = 1469598103934665603ull;
+        for (int x : v) h = (h ^ (uint64_t)(uint32_t)x) * 1099511628211ull;
+        return (size_t)h;
+      }
+    };
+    std::unordered_map<std::vector<int>, GroupEval, KeyHash> memo[2];
+    std::vector<int> v;
+    auto eval = [&](int g) {
+      v.assign(mem[g].begin(), mem[g].end());
+      std::sort(v.begin(), v.end());
+      v.push_back(g);
+      auto& M = memo[phase_b ? 1 : 0];
+      auto hit = M.find(v);
+      if (hit != M.end()) return hit->second;
+      const std::vector<int> key = v;
+      v.pop_back();
+      const GroupEval r = eval_raw(g, v);
+      M.emplace(key, r);
+      return r;
+    };    long n_evals = 0;
     auto meval = [&](int g) {
       ++n_evals;
       return eval(g);
@@ -613,7 +645,9 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         }
         if (!improved) break;
       }
-      if (std::getenv("GPUSCHED_PLAN_DEBUG")) std::fprintf(stderr, "[plan_corun] phase %d evals %ld\n", phase_b ? 1 : 0, n_evals);
+      if (std::getenv("GPUSCHED_PLAN_DEBUG"))
+        std::fprintf(stderr, "[plan_corun] phase %d evals %ld simulated %zu\n", phase_b ? 1 : 0, n_evals,
+                     memo[phase_b ? 1 : 0].size());
     };
     auto max_mk = [&](bool eff) {
       double m = 0;

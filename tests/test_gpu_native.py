@@ -283,44 +283,65 @@ def test_executor_epoch_and_bench_smoke():
     assert r["value"] > 0 and not r["simulated"] and r["unscheduled"] == 0
 
 
-def test_planner_backlog_feedback_on_real_timelines():
-    """The N-GPU bench's planner path on real pod timelines: a 2-GPU control plane (co-run
-    planner + backlog carry + measured feedback) plans each epoch; both GPUs' pods run on the
-    one MI355X (GPU 1's on their own slot streams), and each GPU's telemetry rows, with start /
-    end times on the executor clock, feed the backlog as in bench.py."""
+def test_planner_feedback_moves_work_off_a_really_slower_gpu():
+    """The N-GPU bench's planner path on hardware, checked for DIRECTION: a 2-GPU control plane
+    (co-run planner + backlog carry + measured feedback) plans each epoch; each GPU's group runs
+    on the MI355X in turn (isolated, the bench's executor), and GPU 1's pods really run 40 % more
+    iterations than the model is told -- a GPU slower than its sibling.  After 12 epochs the
+    measured feedback must have grown GPU 1's backlog past GPU 0's and moved planned work off
+    it (the planner then keeps balancing, so the relative backlogs need not stay apart); and the
+    co-run model's predicted group times must be within 15 % of the measured ones
+    for >= 80 % of GPU 0's (unslowed) groups."""
     import numpy as np
+    from k8s_gpu_scheduler_amd.models import workloads as W
     from k8s_gpu_scheduler_amd.parallel import podbench as PB
-    from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor
-    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=2, iters=4, seed=5, balance=1.0, plan_bursts=True,
+    from k8s_gpu_scheduler_amd.parallel.executor import PodRun
+    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=2, iters=20, seed=5, balance=1.0, plan_bursts=True,
                          plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0)
     planner = cp.plugin.planner
-    ex = DeviceExecutor(0)
-    corrections = []
+    model = cp.corun.base if cp.corun is not None else planner.plugin.corun_model()
+    ex = PB.gpu_executor(PB.build_parser().parse_args([]), 0)
+    ex.warm([PodRun(0, wl, u, 2, 20, masked=False) for wl in W.NAMES for u in (0, 2)])
+    ex.warm([PodRun(0, wl, u, 2, 28, masked=False) for wl in W.NAMES for u in (0, 2)])
+    share, errs = [], []
+    fed = {}
     orig = planner.correct
 
     def spy(group, delta):
-        corrections.append((group, delta))
+        fed[group] = fed.get(group, 0.0) + delta
         orig(group, delta)
     planner.correct = spy
-    for _ in range(4):
+    for e in range(12):
         cp.finish_live()
         arr = cp.schedule_epoch()
         per_gpu = np.zeros((2, PB.TELE))
         per_gpu[:, PB.SMI0:] = -1.0
         runs = {g: PB._runs_for(arr, g) for g in (0, 1)}
-        for r in runs[1]:                      # GPU 1's pods on the other half of the slots
-            r.first_unit = (r.first_unit + 4) % 8
-        ex.launch_epoch(runs[0] + runs[1])
-        ex.wait_all()
-        for g in (0, 1):
+        assert runs[0] and runs[1], arr
+        work = {g: sum(model.alone_ms[model.wid(r.workload)] * r.iters for r in runs[g]) for g in (0, 1)}
+        if e >= 6:
+            share.append(work[1] / (work[0] + work[1]))
+        for r in runs[1]:
+            r.iters = int(round(r.iters * 1.4))     # the slower GPU: work the model does not see
+        for g in (0, 1):                            # each GPU's group in isolation, in turn
+            ex.launch_epoch(runs[g])
+            ex.wait_all()
             ex.collect(runs[g])
             per_gpu[g, PB.POD0:PB.SMI0] = PB._pod_rows(runs[g], ex.clock)
+            if g == 0 and e >= 1:
+                wall = max(ex.clock.elapsed_time(r.end) for r in runs[g]) - \
+                    min(ex.clock.elapsed_time(r.start) for r in runs[g])
+                pred = float(np.max(model.group_times([model.wid(r.workload) for r in runs[g]],
+                                                      [r.iters for r in runs[g]])))
+                errs.append(abs(pred - wall) / wall)
         cp.update_telemetry(per_gpu, 1.0)
     ex.close()
-    assert planner.planned_bursts == 4 and len(planner.backlog) == 2
-    assert len(corrections) == 8 and all(np.isfinite(d) for _, d in corrections)
-    assert {g for g, _ in corrections} == {(PB.NODE, 0), (PB.NODE, 1)}
-    assert all(np.isfinite(v) for v in planner.backlog.values())
+    g0, g1 = (PB.NODE, 0), (PB.NODE, 1)
+    print("measured feedback", fed, "GPU 1 work share (epochs 6-11)", np.round(share, 3),
+          "group errors", np.round(errs, 3))
+    assert fed[g1] > fed[g0] and fed[g1] > 0, fed          # the feedback grew GPU 1's backlog
+    assert float(np.mean(share)) < 0.5, share
+    assert np.mean(np.asarray(errs) <= 0.15) >= 0.8, errs
 
 
 def test_rccl_probe_single_rank(tmp_path, monkeypatch):

@@ -1,0 +1,139 @@
+"""The slot-pipeline side of the co-run model: the native chained simulation (chain_times),
+the slot planner (plan_slots), the scheduler's slot timelines (plugins.gpu.timeline), the
+model-driven pipeline executor (parallel.modelpipe) and the pipelined virtual node's replay
+(tools/pipelined_vn.py)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from k8s_gpu_scheduler_amd import _native
+from k8s_gpu_scheduler_amd.models import corun as CR
+from k8s_gpu_scheduler_amd.parallel.executor import PodRun
+from k8s_gpu_scheduler_amd.plugins.gpu.timeline import SlotTimeline
+
+core = _native.core()
+has_chain = core is not None and hasattr(core, "chain_times")
+I32 = np.int32
+NEG = -1e300
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _toy():
+    # memwl presses on memwl only, cmpwl on cmpwl only; 1 ms per iteration alone
+    return CR.CorunModel(["memwl", "cmpwl"], [1.0, 1.0], np.array([[0.0, 1.0], [1.0, 0.0]]),
+                         np.array([[0.0, 1.0], [1.0, 0.0]]), {"version": "toy"})
+
+
+@pytest.mark.skipif(not has_chain, reason="_core not built")
+def test_chain_times_chains_a_slot_and_matches_the_group_simulation():
+    m = _toy()
+    # slot A: memwl (10 it) then memwl (5 it); slot B: memwl (10 it) from t=0
+    wid = np.array([0, 0, 0], I32)
+    it = np.array([10.0, 5.0, 10.0])
+    st, fin = core.chain_times(wid, it, np.array([0.0, NEG, 0.0]), np.array([-1, 0, -1], I32), m.alone_ms,
+                               m.coupling())
+    # both first pods share (rate 1/2) until t=20; the chained pod then runs alone 5 ms
+    assert np.allclose(st, [0.0, 20.0, 0.0]) and np.allclose(fin, [20.0, 25.0, 20.0])
+    # without chaining it is the multi-way group simulation with staggered starts
+    rng = np.random.default_rng(1)
+    full = CR.CorunModel.load()
+    for _ in range(20):
+        k = int(rng.integers(2, 7))
+        w = rng.integers(0, len(full.names), k).astype(I32)
+        its = rng.integers(5, 40, k).astype(float)
+        s0 = np.sort(rng.uniform(0, 3, k))
+        _, f1 = core.chain_times(w, its, s0, np.full(k, -1, I32), full.alone_ms, full.coupling())
+        f2 = full.group_times(list(w), list(its), list(s0))
+        assert np.allclose(f1, f2, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.skipif(not has_chain, reason="_core not built")
+def test_plan_slots_puts_the_complementary_pod_next_to_the_inflight_one():
+    """Slot 1 runs a measured memory-bound pod until t=10; slot 0 is free.  A new memory pod
+    on slot 0 would share HBM with it (500 it/s < its 800 SLO); the planner puts the compute
+    pod there and the memory pod on slot 1, after the in-flight one: both meet their SLOs."""
+    m = _toy()
+    sl, st, fin, exp, spread, min_spread = core.plan_slots(
+        np.array([0], I32), np.array([10.0]), np.array([0.0]), np.array([-1], I32), np.array([10.0]),
+        np.array([0.0]), np.array([-1, -1], I32), np.array([0.0, 10.0]),
+        np.array([0, 1], I32), np.array([10.0, 10.0]), np.array([800.0, 800.0]), np.full(2, NEG),
+        m.alone_ms, m.coupling(), 0.0, 100.0, 720)
+    assert list(sl) == [1, 0]
+    assert exp == pytest.approx(2.0)
+    assert np.allclose(fin[1:], [20.0, 10.0])               # memwl after the in-flight pod; cmpwl alongside
+    # the tight spread limit keeps the most even assignment even if it meets fewer SLOs
+    sl2 = core.plan_slots(
+        np.array([0], I32), np.array([10.0]), np.array([0.0]), np.array([-1], I32), np.array([10.0]),
+        np.array([0.0]), np.array([-1, -1], I32), np.array([0.0, 10.0]),
+        np.array([0, 1], I32), np.array([10.0, 10.0]), np.array([800.0, 800.0]), np.full(2, NEG),
+        m.alone_ms, m.coupling(), 0.0, 0.0, 720)[0]
+    assert len(set(sl2)) == 2
+
+
+def test_slot_timeline_chains_unmeasured_pods_and_pins_measured_ones():
+    tl = SlotTimeline(depth=4, phantoms=2)
+    g = ("n0", 0)
+    tl.next_burst()
+    tl.place(g, (0, 2), "a", 0, 10.0, 500.0)
+    tl.place(g, (2, 2), "b", 1, 10.0, 0.0)
+    tl.next_burst()
+    tl.place(g, (0, 2), "c", 1, 5.0, 0.0)
+    assert tl.measure(g, 0, 0.0, 12.0) and tl.measure(g, 2, 0.0, 8.0)
+    assert not tl.measure(g, 6, 0.0, 1.0) and tl.unmatched == 1
+    ctx = tl.context(g, [(0, 2), (2, 2), (4, 2)])
+    keys = ctx["keys"]
+    # the unmeasured "c" starts when slot 0's last measured pod ("a") ended; "b" ended before
+    # that window, so slot 1 is free from its end
+    i_c = keys.index("c")
+    assert ctx["prev"][i_c] == -1 and ctx["start"][i_c] == pytest.approx(12.0)
+    assert list(ctx["slot_tail"]) == [i_c, -1, -1]
+    assert ctx["slot_free"][1] == pytest.approx(8.0)
+    # phantoms: each candidate slot continues with its own recent workloads (2 per slot)
+    assert list(ctx["ph_off"]) == [0, 2, 4, 6]
+
+
+@pytest.mark.skipif(not has_chain, reason="_core not built")
+def test_model_pipeline_executor_runs_slots_back_to_back():
+    from k8s_gpu_scheduler_amd.parallel.modelpipe import ModelPipelineExecutor
+    ex = ModelPipelineExecutor(model=_toy(), noise=0.0, host_ms=0.0)
+    e1 = [PodRun(0, "memwl", 0, 2, 10), PodRun(1, "cmpwl", 2, 2, 10)]
+    e2 = [PodRun(2, "memwl", 0, 2, 5)]
+    # the toy names are not catalog workloads: borrow two catalog entries for the FLOP / byte
+    # accounting the executor keeps
+    import k8s_gpu_scheduler_amd.parallel.modelpipe as MP
+    cat = MP.W.CATALOG
+    MP.W.CATALOG = {"memwl": cat["onnx_mobilenet_1024"], "cmpwl": cat["onnx_resnet50_1024"]}
+    try:
+        ex.launch_epoch(e1)
+        ex.launch_epoch(e2)
+        ex.wait_epoch(e1)
+        ex.wait_epoch(e2)
+    finally:
+        MP.W.CATALOG = cat
+    # memwl and cmpwl do not couple: 10 ms each; the chained memwl then runs 5 ms alone
+    assert e1[0].ms == pytest.approx(10.0) and e1[1].ms == pytest.approx(10.0)
+    assert e2[0].start.t == pytest.approx(10.0) and e2[0].ms == pytest.approx(5.0)
+    assert ex.elapsed_ms == pytest.approx(15.0)
+
+
+def test_pipelined_vn_coupled_release_and_sim_replay():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pipelined_vn as PV
+    # GPU 1 collects epoch 0 at 9 ms, GPU 0 at 5: with lookahead 1, epoch 2's broadcast waits
+    # for both (9), epoch 3's for epoch 1 (max 14, 12)
+    rel = PV.coupled_release([[5.0, 12.0, 20.0, 30.0], [9.0, 14.0, 19.0, 25.0]], 1)
+    assert rel == [0.0, 0.0, 9.0, 14.0]
+    if not has_chain:
+        return
+    from k8s_gpu_scheduler_amd.models import workloads as W
+    from k8s_gpu_scheduler_amd.parallel.modelpipe import ModelPipelineExecutor
+    w = W.INDEX["onnx_mobilenet_1024"]
+    epochs = [{"timed": e > 0, "arr": [[0, 2 * s, 2, w, 20, 1, 0] for s in range(4)] +
+               [[1, 0, 2, w, 20, 1, 0]]} for e in range(4)]
+    out = PV.replay_gpu(ModelPipelineExecutor(noise=0.0), epochs, 0, 2)
+    assert out["pods"] == 12 and out["slo_ok"] == 12 and out["span_ms"] > 0
+    assert len(out["done_ms"]) == 4 and out["done_ms"] == sorted(out["done_ms"])
+    gated = PV.replay_gpu(ModelPipelineExecutor(noise=0.0), epochs, 0, 2, release=[0.0, 0.0, 0.0, 50.0])
+    assert gated["done_ms"][3] > 50.0 > out["done_ms"][3]
