@@ -56,7 +56,7 @@ class BurstPlanner:
     # sweeps: improvement passes of the native planners -- 4 and 8 plan alike (8-GPU pipelined
     # simulation, 3 seeds: 64.8 vs 65.3 % SLOs met, same pods/s) at half the control-plane time
     def __init__(self, plugin: Any, tolerance: float = 0.05, sweeps: int = 4, objective: str = "slo",
-                 carry: float = 0.0, slots: bool = False, spread_ms: float = 2.0, slot_sigma: float = 0.2):
+                 carry: float = 0.0, slots: Any = False, spread_ms: float = 2.0, slot_sigma: float = 0.2):
         if objective not in ("slo", "load"):
             raise ValueError(f"plan objective must be 'slo' or 'load', not {objective!r}")
         if not 0.0 <= carry <= 1.0:
@@ -75,8 +75,18 @@ class BurstPlanner:
         # every planned pod also gets its slot -- the one whose predicted co-runners (the slot
         # pipelines' in-flight pods) let the most pods meet their SLOs, within spread_ms of the
         # most even slot ends (a slot running ahead idles once the pipeline's window is used up)
+        # slots: "" (off: the ledger's best-fit unit range), "lpt" (each GPU's planned pods,
+        # longest predicted work first, onto the CU slot with the least cumulative predicted
+        # work -- the slot streams of a pipelined GPU stay level), "model" (the co-run model's
+        # simulation of the slot pipelines, below); True = "model"
+        self.slot_policy = "model" if slots is True else (slots or "")
+        if self.slot_policy not in ("", "off", "lpt", "model"):
+            raise ValueError(f"slot policy must be off, lpt or model, not {slots!r}")
+        if self.slot_policy == "off":
+            self.slot_policy = ""
+        self._slot_work: Dict[Tuple[str, int, int], float] = {}    # (device, first unit, units) -> ms
         self.timeline = None
-        if slots:
+        if self.slot_policy == "model":
             from .timeline import SlotTimeline
             # 2 phantom pods per slot: 65.6 % SLOs met vs 65.3 with 3 and 64.3 with 1 (8-GPU
             # pipelined simulation, 3 seeds), a smaller pipeline simulation per candidate
@@ -285,7 +295,7 @@ class BurstPlanner:
         for nd, st in placed:
             dev_group.append(gkey.setdefault((nd,) + plugin.corun_group_key(st), len(gkey)))
         n_groups = len(gkey)
-        if n_groups < 2 and self.timeline is None:
+        if n_groups < 2 and not self.slot_policy:
             return None                     # one co-run group (one GPU) and no slots to plan
         free_units = [st.free_units for st in states]
         free_hbm = [st.hbm_free for st in states]
@@ -379,6 +389,8 @@ class BurstPlanner:
         if self.timeline is not None:
             self.timeline.next_burst()
             slot_of = self._plan_slots(assign, out, states, owner, dev_group, model, core, margin)
+        elif self.slot_policy == "lpt":
+            slot_of = self._lpt_slots(assign, out, states, model)
         for (p, _, _), d in zip(assign, out):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid, slot_of.get(O.key(p)))
             plugin._pending_by_key[O.key(p)] = p
@@ -393,6 +405,46 @@ class BurstPlanner:
             align *= 2
         return [(u, n) for u in range(0, st.device.units - n + 1, align)
                 if not any(st.used_units[u:u + n]) and u not in busy]
+
+    def _taken_slots(self) -> Dict[str, set]:
+        """First units of the slots planned for still-pending pods, per device."""
+        taken: Dict[str, set] = {}
+        for k, pl in self.plans.items():
+            if len(pl) > 2 and pl[2] is not None and k in self.plugin._pending_by_key:
+                taken.setdefault(pl[1], set()).add(pl[2])
+        return taken
+
+    def _lpt_slots(self, assign, out, states, model) -> Dict[str, int]:
+        """slot policy "lpt": per device, its planned pods of one size longest predicted work
+        (co-run model alone time x iterations) first, each onto the free slot whose stream has
+        the least cumulative predicted work so far (ties: the lower slot).  On a pipelined GPU
+        the slot streams then stay level over the epochs (a first-fit order gives slot 0 the
+        longest pod of every burst, and the pipeline waits on it); replaces the bench
+        executor's SLO-blind re-slotting, which ran after the scheduler had decided."""
+        by_dev: Dict[int, List[Tuple[Any, Any]]] = {}
+        for (p, r, _), d in zip(assign, out):
+            by_dev.setdefault(int(d), []).append((p, r))
+        taken = self._taken_slots()
+        res: Dict[str, int] = {}
+        for d, items in by_dev.items():
+            st = states[d]
+            uuid = st.device.uuid
+            sizes = {r.units for _, r in items}
+            if len(sizes) != 1:
+                continue
+            n = sizes.pop()
+            slots = [u for u, _ in self._free_slots(st, n, taken.get(uuid, set()))]
+            if len(slots) < len(items):
+                continue
+            work = {O.key(p): float(model.alone_ms[model.wid(O.name(p))]) * max(r.iters, 1.0) for p, r in items}
+            for p, r in sorted(items, key=lambda x: -work[O.key(x[0])]):
+                u = min(slots, key=lambda s: (self._slot_work.get((uuid, s, n), 0.0), s))
+                slots.remove(u)
+                res[O.key(p)] = u
+                self._slot_work[(uuid, u, n)] = self._slot_work.get((uuid, u, n), 0.0) + work[O.key(p)]
+            self.stats["slot_plans"] += 1
+            self.stats["slot_pods"] += len(items)
+        return res
 
     def _pipe_context(self, gkey: Dict[Tuple, int], states, owner, dev_group, model, core) -> Any:
         """plan_corun's `pipe`: per GPU group of one device, its timeline's in-flight pods
@@ -441,10 +493,7 @@ class BurstPlanner:
         by_dev: Dict[int, List[Tuple[Any, Any]]] = {}
         for (p, r, _), d in zip(assign, out):
             by_dev.setdefault(int(d), []).append((p, r))
-        taken: Dict[str, set] = {}
-        for k, pl in self.plans.items():
-            if len(pl) > 2 and pl[2] is not None and k in plugin._pending_by_key:
-                taken.setdefault(pl[1], set()).add(pl[2])
+        taken = self._taken_slots()
         res: Dict[str, int] = {}
         for d, items in by_dev.items():
             st = states[d]

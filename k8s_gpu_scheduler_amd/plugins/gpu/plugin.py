@@ -140,7 +140,7 @@ class GPUArgs:
     # slot pipelines (in-flight pods of earlier placements, measured ones pinned; see
     # plugins.gpu.timeline) -- the most expected SLOs met among slot assignments whose slot
     # ends stay within slotSpreadMs of the most even assignment's
-    plan_slots: bool = False
+    plan_slots: Any = False           # "" / False: off, "lpt", "model" / True (planner.BurstPlanner)
     slot_spread_ms: float = 2.0
     slot_sigma: float = 0.2
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
@@ -227,7 +227,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if self.args.plan_bursts:
             from .planner import BurstPlanner
             self.planner = BurstPlanner(self, self.args.plan_tolerance, objective=self.args.plan_objective,
-                                        carry=self.args.plan_carry, slots=bool(self.args.plan_slots),
+                                        carry=self.args.plan_carry, slots=self.args.plan_slots,
                                         spread_ms=float(self.args.slot_spread_ms),
                                         slot_sigma=float(self.args.slot_sigma))
         self._pred_version: Any = None

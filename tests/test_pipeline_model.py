@@ -137,3 +137,31 @@ def test_pipelined_vn_coupled_release_and_sim_replay():
     assert len(out["done_ms"]) == 4 and out["done_ms"] == sorted(out["done_ms"])
     gated = PV.replay_gpu(ModelPipelineExecutor(noise=0.0), epochs, 0, 2, release=[0.0, 0.0, 0.0, 50.0])
     assert gated["done_ms"][3] > 50.0 > out["done_ms"][3]
+
+
+@pytest.mark.skipif(core is None, reason="_core not built")
+def test_lpt_slot_policy_levels_the_slot_streams_at_one_gpu():
+    """plan_slots='lpt': the scheduler itself puts each epoch's pods, longest predicted work
+    first, on the slot with the least cumulative work -- the longest pod is not always on
+    slot 0 (the first-fit order the executor used to re-slot), and the four slot streams'
+    cumulative work stays within one pod's work of each other."""
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    cp = PB.ControlPlane(n_gpus=1, pods_per_gpu=4, iters=20, seed=3, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
+                         plan_slots="lpt")
+    pl = cp.plugin.planner
+    model = cp.plugin.corun_model()
+    longest_slot = set()
+    max_work = 0.0
+    for _ in range(24):
+        cp.finish_live()
+        arr = cp.schedule_epoch()
+        rows = [r for r in arr if r[0] >= 0]
+        assert sorted(int(r[1]) for r in rows) == [0, 2, 4, 6]
+        work = [float(model.alone_ms[int(r[3])]) * float(r[4]) for r in rows]
+        max_work = max(max_work, max(work))
+        longest_slot.add(int(rows[int(np.argmax(work))][1]))
+    st = cp.planner_stats()
+    assert st["slot_policy"] == "lpt" and st["slot_pods"] == 96
+    assert len(longest_slot) >= 3
+    assert st["slot_work_spread_ms"] <= max_work + 1e-9

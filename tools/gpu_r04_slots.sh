@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 GPU call 3: the GPU test suite at HEAD, then an interleaved N=1 A/B of who picks the
+# CU slot: the scheduler's LPT (default), the executor's LPT re-slotting (round 3), the co-run
+# model's slot plan and the ledger's first fit.
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r04_slots
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/r04_slots/pytest_gpu.log 2>&1 &&
+timeout -k 10 900 python tools/ab.py --rounds 3 --steps 20 --warmup 5 --timeout 150 --out gpurun_out/r04_slots/ab20 \
+  --arm lpt="" --arm executor="--slot-balance 1 --plan-slots off" --arm model="--plan-slots model" \
+  --arm off="--plan-slots off" > gpurun_out/r04_slots/ab20.log 2>&1 &&
+timeout -k 10 600 python tools/ab.py --rounds 2 --steps 60 --warmup 5 --timeout 150 --out gpurun_out/r04_slots/ab60 \
+  --arm lpt="" --arm executor="--slot-balance 1 --plan-slots off" > gpurun_out/r04_slots/ab60.log 2>&1
+rc=$?
+tail -3 gpurun_out/r04_slots/pytest_gpu.log; tail -1 gpurun_out/r04_slots/ab20.log | cut -c1-1200; tail -1 gpurun_out/r04_slots/ab60.log | cut -c1-600
+exit $rc
