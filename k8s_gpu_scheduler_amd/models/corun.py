@@ -131,6 +131,7 @@ class CorunModel:
         self.meta = dict(meta or {})
         self.version = str(self.meta.get("version", "prior"))
         self._cmat = self.u @ self.v.T
+        self._wid_memo: Dict[str, int] = {}
 
     # -- construction
     @classmethod
@@ -201,11 +202,16 @@ class CorunModel:
         i = self.index.get(name)
         if i is not None:
             return i
+        hit = self._wid_memo.get(name)
+        if hit is not None:
+            return hit
         nm = name.replace("-", "_")
         best = -1
         for n, j in self.index.items():
             if n in nm and (best < 0 or len(n) > len(self.names[best])):
                 best = j
+        if len(self._wid_memo) < 65536:         # pod names repeat across Score / plan / Reserve
+            self._wid_memo[name] = best
         return best
 
     def coupling(self) -> np.ndarray:

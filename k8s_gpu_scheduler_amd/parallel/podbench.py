@@ -337,7 +337,7 @@ class ControlPlane:
             return None
         st = dict(planner.stats)
         n = max(st.get("slot_plans", 0), 1)
-        if planner.slot_policy == "model":
+        if planner.slot_policy in ("model", "auto"):
             for k in ("slot_spread_ms", "slot_min_spread_ms"):
                 st[k] = round(st[k] / n, 3)
             st["slot_pred_met_pct"] = round(100.0 * st.pop("slot_pred_met") / max(st["slot_pods"], 1), 2)
@@ -589,7 +589,7 @@ def _effective_config(a: Any) -> Dict[str, Any]:
         if corun:
             out.update(corun_sigma=a.corun_sigma, plan_carry=a.plan_carry,
                        plan_feedback=a.plan_feedback if a.plan_carry > 0 else 0, plan_slots=a.plan_slots)
-            if a.plan_slots == "model":
+            if a.plan_slots in ("model", "auto"):
                 out.update(slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
         else:
             out["plan_objective"] = a.plan_objective
@@ -672,7 +672,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
                     help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
                          "collected epoch (a GPU slower than its siblings, or the model's error on it)")
-    ap.add_argument("--plan-slots", default="lpt", choices=["off", "lpt", "model", "0", "1"],
+    ap.add_argument("--plan-slots", default="lpt", choices=["off", "lpt", "model", "auto", "0", "1"],
                     help="who picks each pod's CU slot on its GPU: 'lpt' (default) the scheduler, longest "
                          "predicted work onto the slot stream with the least cumulative predicted work; 'model' "
                          "the scheduler on the co-run model's simulation of the slot pipelines (in-flight pods "

@@ -79,14 +79,17 @@ class BurstPlanner:
         # longest predicted work first, onto the CU slot with the least cumulative predicted
         # work -- the slot streams of a pipelined GPU stay level), "model" (the co-run model's
         # simulation of the slot pipelines, below); True = "model"
+        # "auto": "model" when the plan spans several GPU groups (the model then also gives the
+        # GPU choice each group's in-flight pipeline), "lpt" on a single GPU, where the slot
+        # permutation is the only freedom and levelling measured better on MI355X
         self.slot_policy = "model" if slots is True else (slots or "")
-        if self.slot_policy not in ("", "off", "lpt", "model"):
-            raise ValueError(f"slot policy must be off, lpt or model, not {slots!r}")
+        if self.slot_policy not in ("", "off", "lpt", "model", "auto"):
+            raise ValueError(f"slot policy must be off, lpt, model or auto, not {slots!r}")
         if self.slot_policy == "off":
             self.slot_policy = ""
         self._slot_work: Dict[Tuple[str, int, int], float] = {}    # (device, first unit, units) -> ms
         self.timeline = None
-        if self.slot_policy == "model":
+        if self.slot_policy in ("model", "auto"):
             from .timeline import SlotTimeline
             # 2 phantom pods per slot: 65.6 % SLOs met vs 65.3 with 3 and 64.3 with 1 (8-GPU
             # pipelined simulation, 3 seeds), a smaller pipeline simulation per candidate
@@ -388,8 +391,9 @@ class BurstPlanner:
         slot_of: Dict[str, int] = {}
         if self.timeline is not None:
             self.timeline.next_burst()
+        if self.slot_policy == "model" or (self.slot_policy == "auto" and n_groups >= 2):
             slot_of = self._plan_slots(assign, out, states, owner, dev_group, model, core, margin)
-        elif self.slot_policy == "lpt":
+        elif self.slot_policy in ("lpt", "auto"):
             slot_of = self._lpt_slots(assign, out, states, model)
         for (p, _, _), d in zip(assign, out):
             self.plans[O.key(p)] = (owner[int(d)], states[int(d)].device.uuid, slot_of.get(O.key(p)))
