@@ -672,13 +672,14 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
                     help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
                          "collected epoch (a GPU slower than its siblings, or the model's error on it)")
-    ap.add_argument("--plan-slots", default="lpt", choices=["off", "lpt", "model", "auto", "0", "1"],
-                    help="who picks each pod's CU slot on its GPU: 'lpt' (default) the scheduler, longest "
-                         "predicted work onto the slot stream with the least cumulative predicted work; 'model' "
-                         "the scheduler on the co-run model's simulation of the slot pipelines (in-flight pods "
-                         "of earlier epochs, measured ones pinned); 'off' the ledger's first fit (1 = model, "
-                         "0 = off).  MI355X N=1, 3 interleaved A/Bs of 20 steps: lpt-style levelling 601 "
-                         "pods/s / 54.6 %% SLOs, model 596 / 53.3 %% (profiles/r04_slot_policy/)")
+    ap.add_argument("--plan-slots", default="auto", choices=["off", "lpt", "model", "auto", "0", "1"],
+                    help="who picks each pod's CU slot on its GPU: 'lpt' the scheduler, longest predicted work "
+                         "onto the slot stream with the least cumulative predicted work; 'model' the scheduler on "
+                         "the co-run model's simulation of the slot pipelines (in-flight pods of earlier epochs, "
+                         "measured ones pinned), which also gives the GPU choice each GPU's pipeline; 'auto' "
+                         "(default) model across GPUs, lpt on one; 'off' the ledger's first fit (1 = model, "
+                         "0 = off).  MI355X N=1, 3 interleaved A/Bs of 20 steps: levelling 601 pods/s / 54.6 %% "
+                         "SLOs, model 596 / 53.3 %% (profiles/r04_slot_policy/)")
     ap.add_argument("--slot-spread-ms", type=float, default=2.0,
                     help="--plan-slots: how far (ms) the slots' predicted ends may spread beyond the most even "
                          "assignment's to meet more SLOs")

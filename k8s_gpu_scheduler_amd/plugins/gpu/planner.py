@@ -100,6 +100,7 @@ class BurstPlanner:
         # the phantom continuation, vs ~0.06 once the co-runners are measured)
         self.slot_sigma = slot_sigma
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
+        self.pipe_phantoms = True    # ... with each slot's next (phantom) pod chained after its new one
         # measured backlog feedback from pod completions (plugins.gpu.feedback; deployed
         # clusters -- the bench corrects per collected epoch instead)
         self.feedback = None
@@ -464,24 +465,31 @@ class BurstPlanner:
         unit = min((r.units for r in (self.plugin.parse_request(p) for p in self._pending_burst) if r.units),
                    default=0) if getattr(self, "_pending_burst", None) else 0
         c_off, f_off = [0], [0]
-        cw, cs, ce, ft = [], [], [], []
+        cw, cs, ce, ft, pw, pi = [], [], [], [], [], []
         for g in range(n_groups):
             d = dev_of[g]
             if ndev[g] == 1 and unit > 0:
                 st = states[d]
                 slots = self._free_slots(st, unit, set())
-                w, s0, s1, fr = self.timeline.pipeline((owner[d],) + self.plugin.corun_group_key(st), slots,
-                                                       model, core)
+                w, s0, s1, fr, phw, phi = self.timeline.pipeline((owner[d],) + self.plugin.corun_group_key(st),
+                                                                 slots, model, core, with_phantoms=True)
                 cw += list(w)
                 cs += list(s0)
                 ce += list(s1)
                 ft += list(fr)
+                pw += list(phw)
+                pi += list(phi)
             c_off.append(len(cw))
             f_off.append(len(ft))
         if not cw and not ft:
             return None
-        return (np.asarray(c_off, np.int64), np.asarray(cw, np.int32), np.asarray(cs, np.float64),
-                np.asarray(ce, np.float64), np.asarray(f_off, np.int64), np.asarray(ft, np.float64))
+        out = (np.asarray(c_off, np.int64), np.asarray(cw, np.int32), np.asarray(cs, np.float64),
+               np.asarray(ce, np.float64), np.asarray(f_off, np.int64), np.asarray(ft, np.float64))
+        if self.pipe_phantoms:
+            # per free slot, the workload its stream runs next (-1: none), chained after the
+            # slot's new pod (native plan_corun)
+            out += (np.asarray(pw, np.int32), np.asarray(pi, np.float64))
+        return out
 
     def _plan_slots(self, assign, out, states, owner, dev_group, model, core, margin: float) -> Dict[str, int]:
         """CU slot of every planned pod on its GPU: the GPU's slot pipelines (the timeline's

@@ -171,8 +171,8 @@ class SlotTimeline:
                 "slot_free": np.asarray([head.get(s, origin) for s in cand], np.float64),
                 "slots": cand}
 
-    def pipeline(self, group: Hashable, slots: Sequence[Slot], model: Any, core: Any
-                 ) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+    def pipeline(self, group: Hashable, slots: Sequence[Slot], model: Any, core: Any, with_phantoms: bool = False
+                 ) -> Tuple[np.ndarray, ...]:
         """The group's in-flight pods as pinned co-runners for the burst planner: (workload
         ids, start, end) -- measured intervals, and predicted ones (the chained pipeline
         simulated with `model`) for pods that have not run yet -- restricted to what is still
@@ -180,14 +180,25 @@ class SlotTimeline:
         ascending (native plan_corun's `pipe`)."""
         ctx = self.context(group, slots)
         k = len(ctx["wid"])
+        # with_phantoms: per free slot (in free-time order) the first phantom of that slot --
+        # the workload its stream most likely runs next (its own most recent one), which the
+        # planner chains after the slot's new pod: a long pod co-runs with the NEXT epoch's
+        # pods too, and without them its predicted co-runners thin out and it looks safe
+        po = ctx["ph_off"]
+        ph_w = np.array([ctx["ph_wid"][po[i]] if po[i + 1] > po[i] else -1 for i in range(len(po) - 1)], np.int32)
+        ph_i = np.array([ctx["ph_iters"][po[i]] if po[i + 1] > po[i] else 0.0 for i in range(len(po) - 1)])
         if k == 0:
-            free = np.sort(ctx["slot_free"])
-            return np.zeros(0, np.int32), np.zeros(0), np.zeros(0), free
+            order = np.argsort(ctx["slot_free"], kind="stable")
+            free = ctx["slot_free"][order]
+            out = (np.zeros(0, np.int32), np.zeros(0), np.zeros(0), free)
+            return out + ((ph_w[order], ph_i[order]) if with_phantoms else ())
         st, fin = core.chain_times(ctx["wid"], ctx["iters"], ctx["start"], ctx["prev"], model.alone_ms,
                                    model.coupling(), ctx["pin"])
         tail = ctx["slot_tail"]
         free = np.where(tail >= 0, fin[np.maximum(tail, 0)], ctx["slot_free"])
-        free = np.sort(free)
+        order = np.argsort(free, kind="stable")
+        free = free[order]
         t0 = float(free[0]) if len(free) else 0.0
         keep = (fin > t0) & (fin < 1e299) & (st < 1e299)
-        return ctx["wid"][keep], st[keep], fin[keep], free
+        out = (ctx["wid"][keep], st[keep], fin[keep], free)
+        return out + ((ph_w[order], ph_i[order]) if with_phantoms else ())

@@ -426,13 +426,14 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     }
   }
   // pipeline context (see above)
-  bool pipe = false;
+  bool pipe = false, phantoms = false;
   I64 p_coff, p_foff;
-  I32 p_cwid;
-  F64 p_cst, p_cend, p_ft;
+  I32 p_cwid, p_hwid;
+  F64 p_cst, p_cend, p_ft, p_hit;
   if (!pipe_obj.is_none()) {
     py::tuple t = pipe_obj.cast<py::tuple>();
-    if (t.size() != 6) throw std::runtime_error("plan_corun: pipe must be (c_off, c_wid, c_start, c_end, f_off, f_time)");
+    if (t.size() != 6 && t.size() != 8)
+      throw std::runtime_error("plan_corun: pipe must be (c_off, c_wid, c_start, c_end, f_off, f_time[, h_wid, h_iters])");
     p_coff = t[0].cast<I64>();
     p_cwid = t[1].cast<I32>();
     p_cst = t[2].cast<F64>();
@@ -449,6 +450,16 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       if (p_coff.data()[g + 1] < p_coff.data()[g] || p_foff.data()[g + 1] < p_foff.data()[g])
         throw std::runtime_error("plan_corun: pipe offsets");
     check_wids(p_cwid.data(), NC, W, "pipe context");
+    if (t.size() == 8) {
+      // per free slot: the pod its stream runs next (-1 none), chained after the slot's new pod
+      p_hwid = t[6].cast<I32>();
+      p_hit = t[7].cast<F64>();
+      if (p_hwid.shape(0) != p_ft.shape(0) || p_hit.shape(0) != p_ft.shape(0))
+        throw std::runtime_error("plan_corun: pipe phantoms must have one entry per free slot");
+      for (py::ssize_t i = 0; i < p_hwid.shape(0); ++i)
+        if (p_hwid.data()[i] >= W) throw std::runtime_error("plan_corun: phantom workload id out of range");
+      phantoms = true;
+    }
     pipe = true;
   }
   // optional HBM: per pod GiB (hbm) and per device free GiB before the burst (dev_hbm); moves
@@ -498,52 +509,85 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       // phase A needs makespans only: no soft-SLO terms (erfc / log per member)
       GroupEval e = eval_group(k, w, it, sl, A, Cm, W, nullptr, phase_b ? sigma : 0.0);
       if (!use_pipe) return e;
-      // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times
+      // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times,
+      // then (phantoms) each slot's next pod chained behind its new one
       const int64_t c0 = p_coff.data()[g], c1 = p_coff.data()[g + 1];
       const int64_t f0 = p_foff.data()[g], f1 = p_foff.data()[g + 1];
       const int nc = (int)(c1 - c0);
+      int nh = 0;
+      if (phantoms)
+        for (int64_t q = f0; q < f1; ++q) nh += p_hwid.data()[q] >= 0;
+      if (nc + k + nh > kMaxK) nh = 0;
       if (nc + k > kMaxK) return e;
-      int32_t pw[kMaxK];
-      double pit[kMaxK], pst[kMaxK], pen[kMaxK], pfin[kMaxK];
+      int32_t pw[kMaxK], pv[kMaxK];
+      double pit[kMaxK], pst[kMaxK], pen[kMaxK], pfin[kMaxK], pso[kMaxK];
       for (int c = 0; c < nc; ++c) {
         pw[c] = p_cwid.data()[c0 + c];
         pit[c] = 1.0;
         pst[c] = p_cst.data()[c0 + c];
         pen[c] = p_cend.data()[c0 + c];
+        pv[c] = -1;
       }
       // new pods longest first onto the earliest free slot; residents already run (first time)
       int order[kMaxK];
       for (int i = 0; i < k; ++i) order[i] = i;
       std::sort(order, order + k, [&](int a, int b) { return A[w[a]] * it[a] > A[w[b]] * it[b]; });
       const double t0 = f1 > f0 ? p_ft.data()[f0] : 0.0;
+      int slot_pod[kMaxK];                       // free slot q -> member index of its new pod
+      for (int64_t q = 0; q < f1 - f0 && q < kMaxK; ++q) slot_pod[q] = -1;
       int nf = 0;
       for (int q = 0; q < k; ++q) {
         const int i = order[q];
         pw[nc + i] = w[i];
         pit[nc + i] = it[i];
         pen[nc + i] = 0.0;
+        pv[nc + i] = -1;
         if (v[i] < 0) {
           pst[nc + i] = t0;
         } else {
           const int64_t fi = std::min<int64_t>(f0 + nf, f1 - 1);
           pst[nc + i] = f1 > f0 ? p_ft.data()[fi] : 0.0;
+          if (f1 > f0 && nf < f1 - f0 && fi - f0 < kMaxK) slot_pod[fi - f0] = nc + i;
           ++nf;
         }
       }
-      // the simulation clock starts at 0: shift the window
+      int m = nc + k;
+      if (nh > 0)
+        for (int64_t q = 0; q < f1 - f0 && q < kMaxK; ++q) {
+          const int32_t hw = p_hwid.data()[f0 + q];
+          if (hw < 0) continue;
+          pw[m] = hw;
+          pit[m] = p_hit.data()[f0 + q];
+          pen[m] = 0.0;
+          if (slot_pod[q] >= 0) {
+            pv[m] = slot_pod[q];
+            pst[m] = -kBig;
+          } else {
+            pv[m] = -1;
+            pst[m] = p_ft.data()[f0 + q];
+          }
+          ++m;
+        }
+      // the simulation clock starts at 0: shift the window (chained members keep -inf)
       double lo = kBig;
-      for (int i = 0; i < nc + k; ++i) lo = std::min(lo, pst[i]);
-      for (int i = 0; i < nc + k; ++i) {
-        pst[i] -= lo;
+      for (int i = 0; i < m; ++i)
+        if (pv[i] < 0) lo = std::min(lo, pst[i]);
+      for (int i = 0; i < m; ++i) {
+        if (pv[i] < 0) pst[i] -= lo;
         if (i < nc) pen[i] -= lo;
       }
-      sim_group(nc + k, pw, pit, pst, A, Cm, W, pfin, pen);
+      if (nh > 0) {
+        sim_chain(m, pw, pit, pst, pv, A, Cm, W, pso, pfin, pen);
+      } else {
+        sim_group(m, pw, pit, pst, A, Cm, W, pfin, pen);
+        for (int i = 0; i < m; ++i) pso[i] = pst[i];
+      }
       e.ok = e.bad = 0;
       e.deficit = e.expected = 0.0;
       for (int i = 0; i < k; ++i) {
         double tput;
         if (it[i] <= 0) tput = 1e3 / std::max(steady_ms(k, i, w, A, Cm, W), 1e-12);
-        else tput = it[i] / std::max(pfin[nc + i] - pst[nc + i], 1e-12) * 1e3;
+        else tput = it[i] / std::max(pfin[nc + i] - pso[nc + i], 1e-12) * 1e3;
         e.expected += p_meet(tput, sl[i], sigma);
         if (sl[i] <= 0 || tput >= sl[i]) ++e.ok;
         else ++e.bad, e.deficit += 1.0 - tput / sl[i];

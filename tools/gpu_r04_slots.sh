@@ -8,10 +8,10 @@ mkdir -p gpurun_out/r04_slots
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/r04_slots/pytest_gpu.log 2>&1 &&
 timeout -k 10 900 python tools/ab.py --rounds 3 --steps 20 --warmup 5 --timeout 150 --out gpurun_out/r04_slots/ab20 \
-  --arm lpt="" --arm executor="--slot-balance 1 --plan-slots off" --arm model="--plan-slots model" \
+  --arm auto="" --arm executor="--slot-balance 1 --plan-slots off" --arm model="--plan-slots model" \
   --arm off="--plan-slots off" > gpurun_out/r04_slots/ab20.log 2>&1 &&
-timeout -k 10 600 python tools/ab.py --rounds 2 --steps 60 --warmup 5 --timeout 150 --out gpurun_out/r04_slots/ab60 \
-  --arm lpt="" --arm executor="--slot-balance 1 --plan-slots off" > gpurun_out/r04_slots/ab60.log 2>&1
+timeout -k 10 900 python -u tools/pipelined_vn.py --gpus 8 --epochs 48 --warmup 5 --seeds 0 1 2 --passes 4 \
+  --policies greedy planner --out gpurun_out/r04_slots/pipelined_vn.json > gpurun_out/r04_slots/pipelined_vn.log 2>&1
 rc=$?
-tail -3 gpurun_out/r04_slots/pytest_gpu.log; tail -1 gpurun_out/r04_slots/ab20.log | cut -c1-1200; tail -1 gpurun_out/r04_slots/ab60.log | cut -c1-600
+tail -3 gpurun_out/r04_slots/pytest_gpu.log; tail -1 gpurun_out/r04_slots/ab20.log | cut -c1-1200; tail -1 gpurun_out/r04_slots/pipelined_vn.log | cut -c1-900
 exit $rc
