@@ -45,7 +45,7 @@ def _targets(asan: bool = False, san_kind: str = "") -> List[Tuple[str, List[str
     smi_src = sorted(glob.glob(os.path.join(NATIVE, "smi", "*.cpp")))
     hip_src = sorted(glob.glob(os.path.join(NATIVE, "hip", "*.hip")) + glob.glob(os.path.join(NATIVE, "hip", "*.cpp")))
     out = [
-        ("_core", core_src, ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", *san, *inc, *core_src]),
+        ("_core", core_src, ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", *san, *inc, *core_src]),
         ("_smi", smi_src, ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *san, *inc, f"-I{ROCM}/include",
                            *smi_src, f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib", "-pthread"]),
         ("_hip", hip_src, [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17",

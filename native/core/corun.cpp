@@ -16,11 +16,17 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <stdexcept>
+#include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -30,6 +36,46 @@ namespace {
 
 constexpr double kBig = 1e300;
 constexpr int kMaxK = 64;   // pods per GPU group (CPX: 64 devices of 4 CUs would be the extreme)
+
+// A tiny fork-join pool for the planner's candidate batches (tens of microseconds each, a few
+// hundred per plan): T-1 workers spin on a generation counter for the duration of one plan
+// call (no sleeping: a futex wake-up costs more than a batch), the caller takes share 0.
+class SpinPool {
+ public:
+  explicit SpinPool(int t) : T_(t) {
+    for (int k = 1; k < T_; ++k)
+      th_.emplace_back([this, k] {
+        int seen = 0;
+        for (;;) {
+          int e;
+          while ((e = gen_.load(std::memory_order_acquire)) == seen) __builtin_ia32_pause();
+          seen = e;
+          if (quit_.load(std::memory_order_acquire)) return;
+          (*fn_)(k);
+          left_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+      });
+  }
+  void run(const std::function<void(int)>& f) {
+    fn_ = &f;
+    left_.store(T_ - 1, std::memory_order_relaxed);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
+    f(0);
+    while (left_.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+  }
+  ~SpinPool() {
+    quit_.store(true, std::memory_order_release);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  int T_;
+  std::vector<std::thread> th_;
+  std::atomic<int> gen_{0}, left_{0};
+  std::atomic<bool> quit_{false};
+  const std::function<void(int)>* fn_ = nullptr;
+};
 
 // fin[i] = wall ms at which pod i finishes (kBig for a service pod); tput_ms[i] = ms per
 // iteration achieved (fin / iters, or the steady-state ms/iter of a service pod).
@@ -594,9 +640,10 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       }
       return e;
     };
-    // memo of group evaluations per phase: a sweep re-evaluates mostly the same (GPU, member
-    // set) pairs as the previous one -- only the two groups of an accepted move / swap change.
-    // The members are evaluated in sorted order, so a result is a function of the set.
+    // memo of group evaluations per phase and thread: a sweep re-evaluates mostly the same
+    // (GPU, member set) pairs as the previous one -- only the two groups of an accepted move /
+    // swap change.  The members are evaluated in sorted order, so a result is a function of
+    // the set.
     struct KeyHash {
       size_t operator()(const std::vector<int>& v) const {
         uint64_t h = 1469598103934665603ull;
@@ -604,94 +651,162 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         return (size_t)h;
       }
     };
-    std::unordered_map<std::vector<int>, GroupEval, KeyHash> memo[2];
-    std::vector<int> v;
-    auto eval = [&](int g) {
-      v.assign(mem[g].begin(), mem[g].end());
+    using Memo = std::unordered_map<std::vector<int>, GroupEval, KeyHash>;
+    // candidate evaluation runs on T threads (GPUSCHED_PLAN_THREADS, default 4): each batch
+    // -- every move of one pod, or every swap partner of one pod -- is evaluated in parallel on
+    // the current state, then the FIRST accepted candidate in the sequential order is applied,
+    // so the plan is exactly the one-thread plan
+    int T = 4;
+    if (const char* e = std::getenv("GPUSCHED_PLAN_THREADS")) T = std::max(1, std::atoi(e));
+    T = std::max(1, std::min({T, (int)std::max(1u, std::thread::hardware_concurrency()), 16}));
+    std::vector<std::array<Memo, 2>> memo(T);
+    std::atomic<long> n_evals{0};
+    auto eval_set = [&](int g, std::vector<int>& v, int tid) {
       std::sort(v.begin(), v.end());
       v.push_back(g);
-      auto& M = memo[phase_b ? 1 : 0];
+      auto& M = memo[tid][phase_b ? 1 : 0];
       auto hit = M.find(v);
+      n_evals.fetch_add(1, std::memory_order_relaxed);
       if (hit != M.end()) return hit->second;
       const std::vector<int> key = v;
       v.pop_back();
       const GroupEval r = eval_raw(g, v);
       M.emplace(key, r);
       return r;
-    };    long n_evals = 0;
-    auto meval = [&](int g) {
-      ++n_evals;
-      return eval(g);
     };
     std::vector<GroupEval> ge(NG);
-    for (int g = 0; g < NG; ++g) ge[g] = meval(g);
-    auto replace = [&](int g, int from, int to) {
-      for (int& x : mem[g])
-        if (x == from) { x = to; return; }
+    auto eval_all = [&] {
+      for (int g = 0; g < NG; ++g) {
+        std::vector<int> v(mem[g].begin(), mem[g].end());
+        ge[g] = eval_set(g, v, 0);
+      }
     };
-    auto remove = [&](int g, int x) {
-      auto& v = mem[g];
-      v.erase(std::find(v.begin(), v.end(), x));
-    };
+    eval_all();
+    SpinPool pool(T);
     const double eps = 1e-9;
+    // candidate c: a move (pod a -> device b) or a swap (pods a, b); its two changed groups
+    struct Cand {
+      int a, b, ga, gb;
+    };
+    struct Out {
+      GroupEval ea, eb;
+    };
+    std::vector<Cand> cand;
+    std::vector<Out> res;
+    std::atomic<bool> failed{false};
+    std::string err;
+    std::mutex err_mu;
+    auto evaluate = [&](bool swap) {
+      res.resize(cand.size());
+      const int n = (int)cand.size();
+      auto job = [&](int tid) {
+        std::vector<int> va, vb;
+        for (int c = tid; c < n; c += T) {
+          const Cand& x = cand[c];
+          try {
+            va.assign(mem[x.ga].begin(), mem[x.ga].end());
+            vb.assign(mem[x.gb].begin(), mem[x.gb].end());
+            if (swap) {
+              *std::find(va.begin(), va.end(), x.a) = x.b;
+              *std::find(vb.begin(), vb.end(), x.b) = x.a;
+            } else {
+              va.erase(std::find(va.begin(), va.end(), x.a));
+              vb.push_back(x.a);
+            }
+            res[c].ea = eval_set(x.ga, va, tid);
+            res[c].eb = eval_set(x.gb, vb, tid);
+          } catch (const std::exception& ex) {
+            std::lock_guard<std::mutex> lk(err_mu);
+            failed = true;
+            err = ex.what();
+          }
+        }
+      };
+      if (T > 1 && n > 1) pool.run(job);
+      else job(0);
+      if (failed) throw std::runtime_error(err);
+    };
+    // SLO phase pruning: a move / swap between two GPUs whose members all meet their SLOs
+    // with near certainty cannot raise the expected count -- skip it (it could only trim a
+    // makespan, phase A's job).
+    auto saturated = [&](const GroupEval& x) { return x.bad == 0 && x.expected >= x.ok - 0.02; };
     // phase runner: crit(before_i, before_j, after_i, after_j) -> accept
     auto run_phase = [&](auto&& accept) {
       for (int sw = 0; sw < sweeps; ++sw) {
         bool improved = false;
-        // moves into free capacity on another GPU
+        // moves into free capacity on another GPU (the first accepted device per pod)
         for (py::ssize_t p = 0; p < P; ++p) {
           const int d0 = dev[p], g0 = DG[d0];
+          cand.clear();
           for (py::ssize_t d = 0; d < D; ++d) {
             const int g1 = DG[d];
             if (g1 == g0 || free[d] < U[p] || hfree[d] + 1e-6 < H[p]) continue;
-            remove(g0, (int)p);
+            if (phase_b && saturated(ge[g0]) && saturated(ge[g1])) continue;
+            cand.push_back({(int)p, (int)d, g0, g1});
+          }
+          if (cand.empty()) continue;
+          evaluate(false);
+          for (size_t c = 0; c < cand.size(); ++c) {
+            const int d = cand[c].b, g1 = cand[c].gb;
+            if (!accept(g0, g1, ge[g0], ge[g1], res[c].ea, res[c].eb)) continue;
+            mem[g0].erase(std::find(mem[g0].begin(), mem[g0].end(), (int)p));
             mem[g1].push_back((int)p);
-            const GroupEval a0 = meval(g0), a1 = meval(g1);
-            if (accept(g0, g1, ge[g0], ge[g1], a0, a1)) {
-              free[d0] += U[p];
-              free[d] -= U[p];
-              hfree[d0] += H[p];
-              hfree[d] -= H[p];
-              dev[p] = (int32_t)d;
-              ge[g0] = a0;
-              ge[g1] = a1;
-              improved = true;
-              break;
-            }
-            remove(g1, (int)p);
-            mem[g0].push_back((int)p);
+            free[d0] += U[p];
+            free[d] -= U[p];
+            hfree[d0] += H[p];
+            hfree[d] -= H[p];
+            dev[p] = (int32_t)d;
+            ge[g0] = res[c].ea;
+            ge[g1] = res[c].eb;
+            improved = true;
+            break;
           }
         }
-        // swaps of equal-size pods across GPUs
+        // swaps of equal-size pods across GPUs: partners of pod i in order; after an accepted
+        // swap the remaining partners are re-evaluated against pod i's new GPU
         for (py::ssize_t i = 0; i < P; ++i) {
-          for (py::ssize_t j = i + 1; j < P; ++j) {
-            const int di = dev[i], dj = dev[j], gi = DG[di], gj = DG[dj];
-            if (gi == gj || U[i] != U[j]) continue;
-            if (hfree[di] + H[i] - H[j] < -1e-6 || hfree[dj] + H[j] - H[i] < -1e-6) continue;
-            // same workload and length: a no-op for the makespans (phase A)
-            if (!phase_b && wid.data()[i] == wid.data()[j] && iters.data()[i] == iters.data()[j]) continue;
-            replace(gi, (int)i, (int)j);
-            replace(gj, (int)j, (int)i);
-            const GroupEval ai = meval(gi), aj = meval(gj);
-            if (accept(gi, gj, ge[gi], ge[gj], ai, aj)) {
+          py::ssize_t j0 = i + 1;
+          while (j0 < P) {
+            cand.clear();
+            const int di = dev[i], gi = DG[di];
+            for (py::ssize_t j = j0; j < P; ++j) {
+              const int dj = dev[j], gj = DG[dj];
+              if (gi == gj || U[i] != U[j]) continue;
+              if (hfree[di] + H[i] - H[j] < -1e-6 || hfree[dj] + H[j] - H[i] < -1e-6) continue;
+              if (phase_b && saturated(ge[gi]) && saturated(ge[gj])) continue;
+              // same workload and length: a no-op for the makespans (phase A)
+              if (!phase_b && wid.data()[i] == wid.data()[j] && iters.data()[i] == iters.data()[j]) continue;
+              cand.push_back({(int)i, (int)j, gi, gj});
+            }
+            if (cand.empty()) break;
+            evaluate(true);
+            py::ssize_t next = P;
+            for (size_t c = 0; c < cand.size(); ++c) {
+              const int j = cand[c].b, gj = cand[c].gb, dj = dev[j];
+              if (!accept(gi, gj, ge[gi], ge[gj], res[c].ea, res[c].eb)) continue;
+              *std::find(mem[gi].begin(), mem[gi].end(), (int)i) = j;
+              *std::find(mem[gj].begin(), mem[gj].end(), j) = (int)i;
               dev[i] = dj;
               dev[j] = di;
               hfree[di] += H[i] - H[j];
               hfree[dj] += H[j] - H[i];
-              ge[gi] = ai;
-              ge[gj] = aj;
+              ge[gi] = res[c].ea;
+              ge[gj] = res[c].eb;
               improved = true;
-            } else {
-              replace(gi, (int)j, (int)i);
-              replace(gj, (int)i, (int)j);
+              next = j + 1;
+              break;
             }
+            j0 = next;
           }
         }
         if (!improved) break;
       }
-      if (std::getenv("GPUSCHED_PLAN_DEBUG"))
-        std::fprintf(stderr, "[plan_corun] phase %d evals %ld simulated %zu\n", phase_b ? 1 : 0, n_evals,
-                     memo[phase_b ? 1 : 0].size());
+      if (std::getenv("GPUSCHED_PLAN_DEBUG")) {
+        size_t sims = 0;
+        for (int t = 0; t < T; ++t) sims += memo[t][phase_b ? 1 : 0].size();
+        std::fprintf(stderr, "[plan_corun] phase %d evals %ld simulated %zu threads %d\n", phase_b ? 1 : 0,
+                     n_evals.load(), sims, T);
+      }
     };
     auto max_mk = [&](bool eff) {
       double m = 0;
@@ -714,7 +829,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       const double cap = max_mk(true) + std::max(tolerance, 0.0) * max_mk(false);
       phase_b = true;
       use_pipe = pipe;
-      for (int g = 0; g < NG; ++g) ge[g] = meval(g);
+      eval_all();
       run_phase([&](int gi, int gj, const GroupEval& bi, const GroupEval& bj, const GroupEval& ai, const GroupEval& aj) {
         const bool over = (B[gi] + ai.makespan > cap * (1 + eps) && ai.makespan > bi.makespan * (1 + eps)) ||
                           (B[gj] + aj.makespan > cap * (1 + eps) && aj.makespan > bj.makespan * (1 + eps));

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from k8s_gpu_scheduler_amd.parallel.podbench import ControlPlane  # noqa: E402
 
 BENCH = dict(balance=1.0, plan_bursts=True, plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05,
-             plan_carry=1.0, plan_feedback=True, plan_slots="lpt")
+             plan_carry=1.0, plan_feedback=True, plan_slots="auto")
 
 
 def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
