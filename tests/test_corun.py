@@ -380,3 +380,26 @@ def test_planner_realign_keeps_only_the_burst_not_yet_run():
     p.last_increments = {("n", 0): 1.0, ("n", 1): 3.0}
     p.realign()
     assert p.backlog == {("n", 0): 0.0, ("n", 1): 2.0}
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_native_planner_threads_give_the_one_thread_plan(monkeypatch):
+    """plan_corun evaluates each candidate batch on GPUSCHED_PLAN_THREADS threads and applies
+    the first accepted candidate in sequential order: the plan must not depend on the count."""
+    m = CR.CorunModel.load()
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        ng, per = 8, 4
+        P = ng * per
+        wid = rng.integers(0, len(m.names), P).astype(I32)
+        args = dict(units=np.full(P, 2, I32), wid=wid, iters=np.full(P, 20.0),
+                    slo=rng.uniform(500, 9000, P), dev_gpu=np.arange(ng, dtype=I32),
+                    dev_free=np.full(ng, 8, I32), res_off=np.zeros(ng + 1, I64), r_wid=np.zeros(0, I32),
+                    r_iters=np.zeros(0), r_slo=np.zeros(0), alone_ms=m.alone_ms, cmat=m.coupling(),
+                    tolerance=0.3, sigma=0.05 * (trial % 2), base=rng.uniform(0, 2, ng))
+        dev0 = np.repeat(np.arange(ng, dtype=I32), per)
+        outs = []
+        for t in ("1", "3", "4"):
+            monkeypatch.setenv("GPUSCHED_PLAN_THREADS", t)
+            outs.append(list(core.plan_corun(dev0, **args)))
+        assert outs[0] == outs[1] == outs[2]
