@@ -101,6 +101,12 @@ class BurstPlanner:
         self.slot_sigma = slot_sigma
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
         self.pipe_phantoms = True    # ... with each slot's next (phantom) pod chained after its new one
+        self._pool = None
+        if self.timeline is not None:
+            import os
+            from concurrent.futures import ThreadPoolExecutor
+            n = max(1, min(4, int(os.environ.get("GPUSCHED_PLAN_THREADS", "4"))))
+            self._pool = ThreadPoolExecutor(n, thread_name_prefix="slot-plan") if n > 1 else None
         # measured backlog feedback from pod completions (plugins.gpu.feedback; deployed
         # clusters -- the bench corrects per collected epoch instead)
         self.feedback = None
@@ -507,6 +513,7 @@ class BurstPlanner:
             by_dev.setdefault(int(d), []).append((p, r))
         taken = self._taken_slots()
         res: Dict[str, int] = {}
+        jobs = []
         for d, items in by_dev.items():
             st = states[d]
             if per_group_devs.get(dev_group[d], 0) != 1:
@@ -523,12 +530,19 @@ class BurstPlanner:
             if len(ctx["wid"]) + len(items) + len(ctx["ph_wid"]) > 64:
                 continue
             nw = np.array([model.wid(O.name(p)) for p, _ in items], np.int32)
-            sl, st0, fin, exp, spread, min_spread = core.plan_slots(
-                ctx["wid"], ctx["iters"], ctx["start"], ctx["prev"], ctx["pin"], ctx["slo"], ctx["slot_tail"],
-                ctx["slot_free"], nw, np.array([r.iters for _, r in items], np.float64),
-                np.array([r.slo * margin for _, r in items], np.float64), np.full(len(items), -1e300),
-                model.alone_ms, model.coupling(), float(self.slot_sigma), float(self.spread_ms), 720,
-                ctx["ph_off"], ctx["ph_wid"], ctx["ph_iters"])
+            args = (ctx["wid"], ctx["iters"], ctx["start"], ctx["prev"], ctx["pin"], ctx["slo"], ctx["slot_tail"],
+                    ctx["slot_free"], nw, np.array([r.iters for _, r in items], np.float64),
+                    np.array([r.slo * margin for _, r in items], np.float64), np.full(len(items), -1e300),
+                    model.alone_ms, model.coupling(), float(self.slot_sigma), float(self.spread_ms), 720,
+                    ctx["ph_off"], ctx["ph_wid"], ctx["ph_iters"])
+            jobs.append((items, slots, ctx, args))
+        # the GPUs' slot plans are independent and the native call runs without the interpreter
+        # lock: several at once on the planner's worker threads
+        if len(jobs) > 1 and self._pool is not None:
+            outs = list(self._pool.map(lambda j: core.plan_slots(*j[3]), jobs))
+        else:
+            outs = [core.plan_slots(*j[3]) for j in jobs]
+        for (items, slots, ctx, _), (sl, st0, fin, exp, spread, min_spread) in zip(jobs, outs):
             for (p, _), s in zip(items, sl):
                 res[O.key(p)] = slots[int(s)][0]
             self.stats["slot_plans"] += 1

@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <functional>
 #include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -644,34 +645,56 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     // (GPU, member set) pairs as the previous one -- only the two groups of an accepted move /
     // swap change.  The members are evaluated in sorted order, so a result is a function of
     // the set.
-    struct KeyHash {
-      size_t operator()(const std::vector<int>& v) const {
-        uint64_t h = 1469598103934665603ull;
-        for (int x : v) h = (h ^ (uint64_t)(uint32_t)x) * 1099511628211ull;
-        return (size_t)h;
+    // key: a 64-bit mix of the sorted member codes and the GPU (no allocation per lookup; a
+    // collision among the few thousand sets of one plan is ~1e-12 likely)
+    using Memo = std::unordered_map<uint64_t, GroupEval>;
+    auto key_of = [](const std::vector<int>& v) {
+      uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)v.size();
+      for (int x : v) {
+        uint64_t z = h + 0x9e3779b97f4a7c15ull + (uint64_t)(uint32_t)x;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        h = z ^ (z >> 31);
       }
+      return h;
     };
-    using Memo = std::unordered_map<std::vector<int>, GroupEval, KeyHash>;
     // candidate evaluation runs on T threads (GPUSCHED_PLAN_THREADS, default 4): each batch
     // -- every move of one pod, or every swap partner of one pod -- is evaluated in parallel on
     // the current state, then the FIRST accepted candidate in the sequential order is applied,
     // so the plan is exactly the one-thread plan
-    int T = 4;
+    // (default 1: at 8 GPUs a batch is 10-30 candidates, mostly memo hits, and the fork-join
+    // cost more than it saved -- 21.9 vs 10.1 ms per plan with 4 threads in this container)
+    int T = 1;
     if (const char* e = std::getenv("GPUSCHED_PLAN_THREADS")) T = std::max(1, std::atoi(e));
     T = std::max(1, std::min({T, (int)std::max(1u, std::thread::hardware_concurrency()), 16}));
-    std::vector<std::array<Memo, 2>> memo(T);
+    // one memo per phase shared by the threads (a reader-writer lock: lookups far outnumber
+    // inserts once the first sweep has run)
+    std::array<Memo, 2> memo;
+    std::shared_mutex memo_mu;
     std::atomic<long> n_evals{0};
     auto eval_set = [&](int g, std::vector<int>& v, int tid) {
+      (void)tid;
       std::sort(v.begin(), v.end());
       v.push_back(g);
-      auto& M = memo[tid][phase_b ? 1 : 0];
-      auto hit = M.find(v);
-      n_evals.fetch_add(1, std::memory_order_relaxed);
-      if (hit != M.end()) return hit->second;
-      const std::vector<int> key = v;
+      const uint64_t key = key_of(v);
       v.pop_back();
+      auto& M = memo[phase_b ? 1 : 0];
+      n_evals.fetch_add(1, std::memory_order_relaxed);
+      if (T > 1) {
+        std::shared_lock<std::shared_mutex> lk(memo_mu);
+        auto hit = M.find(key);
+        if (hit != M.end()) return hit->second;
+      } else {
+        auto hit = M.find(key);
+        if (hit != M.end()) return hit->second;
+      }
       const GroupEval r = eval_raw(g, v);
-      M.emplace(key, r);
+      if (T > 1) {
+        std::unique_lock<std::shared_mutex> lk(memo_mu);
+        M.emplace(key, r);
+      } else {
+        M.emplace(key, r);
+      }
       return r;
     };
     std::vector<GroupEval> ge(NG);
@@ -726,10 +749,11 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       else job(0);
       if (failed) throw std::runtime_error(err);
     };
-    // SLO phase pruning: a move / swap between two GPUs whose members all meet their SLOs
-    // with near certainty cannot raise the expected count -- skip it (it could only trim a
-    // makespan, phase A's job).
-    auto saturated = [&](const GroupEval& x) { return x.bad == 0 && x.expected >= x.ok - 0.02; };
+    // SLO phase pruning: a move / swap between two GPUs on which every member is predicted to
+    // meet its SLO is skipped -- it could only widen margins (the soft objective) or trim a
+    // makespan (phase A's job).  8-GPU pipelined simulation, 4 seeds: 68.9 % SLOs met at 4,631
+    // pods/s vs 69.3 % at 4,542 without the pruning, for 40 % less planning time.
+    auto saturated = [&](const GroupEval& x) { return x.bad == 0; };
     // phase runner: crit(before_i, before_j, after_i, after_j) -> accept
     auto run_phase = [&](auto&& accept) {
       for (int sw = 0; sw < sweeps; ++sw) {
@@ -802,8 +826,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         if (!improved) break;
       }
       if (std::getenv("GPUSCHED_PLAN_DEBUG")) {
-        size_t sims = 0;
-        for (int t = 0; t < T; ++t) sims += memo[t][phase_b ? 1 : 0].size();
+        const size_t sims = memo[phase_b ? 1 : 0].size();
         std::fprintf(stderr, "[plan_corun] phase %d evals %ld simulated %zu threads %d\n", phase_b ? 1 : 0,
                      n_evals.load(), sims, T);
       }
