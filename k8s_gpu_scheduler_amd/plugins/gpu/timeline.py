@@ -48,6 +48,8 @@ class SlotTimeline:
         self.burst = 0
         self.measured = 0
         self.unmatched = 0
+        self._ver = 0                   # bumped by every change: context() results are memoised on it
+        self._ctx_memo: Dict[Any, Dict[str, Any]] = {}
 
     # ------------------------------------------------------------------ updates
     def next_burst(self) -> int:
@@ -56,6 +58,7 @@ class SlotTimeline:
 
     def place(self, group: Hashable, slot: Slot, key: str, wid: int, iters: float, slo: float) -> None:
         """A pod was placed on `slot` of `group` (after every pod placed there before)."""
+        self._ver += 1
         with self._lock:
             chain = self._g.setdefault(group, {}).setdefault(tuple(slot), [])
             chain.append(_Entry(key, int(wid), float(iters), float(slo), self.burst))
@@ -66,6 +69,7 @@ class SlotTimeline:
     def measure(self, group: Hashable, first_unit: int, start: float, end: float) -> bool:
         """The oldest unmeasured pod on the slot starting at `first_unit` ran [start, end)
         (times on the group's executor clock; a slot's pods run in placement order)."""
+        self._ver += 1
         with self._lock:
             slots = self._g.get(group)
             if not slots:
@@ -85,6 +89,7 @@ class SlotTimeline:
     def realign(self) -> None:
         """Every group drained (e.g. a pipelined job synchronised its GPUs): only each group's
         latest burst -- placed, not run yet -- remains, starting from an idle GPU."""
+        self._ver += 1
         with self._lock:
             for g, slots in self._g.items():
                 last = max((e.burst for ch in slots.values() for e in ch), default=None)
@@ -95,6 +100,7 @@ class SlotTimeline:
                     slots[s] = keep
 
     def forget(self, group: Hashable) -> None:
+        self._ver += 1
         with self._lock:
             self._g.pop(group, None)
 
@@ -104,6 +110,17 @@ class SlotTimeline:
             return {s: [(e.key, e.start, e.end) for e in ch] for s, ch in self._g.get(group, {}).items()}
 
     def context(self, group: Hashable, slots: Sequence[Slot]) -> Dict[str, Any]:
+        """Memoised `_context` (the planner asks twice per burst and GPU: for plan_corun's
+        pipeline evaluation and for the slot plan)."""
+        key = (group, tuple(tuple(x) for x in slots), self._ver)
+        hit = self._ctx_memo.get(key)
+        if hit is None:
+            if len(self._ctx_memo) > 256:
+                self._ctx_memo.clear()
+            hit = self._ctx_memo[key] = self._context(group, slots)
+        return hit
+
+    def _context(self, group: Hashable, slots: Sequence[Slot]) -> Dict[str, Any]:
         """The group's pipeline as plan_slots arrays: pinned measured pods that overlap the
         unmeasured ones, then every slot's unmeasured pods chained; slot_tail / slot_free for
         the candidate `slots`.  Times are relative to the group's clock: measured ends where
