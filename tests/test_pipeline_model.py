@@ -165,3 +165,30 @@ def test_lpt_slot_policy_levels_the_slot_streams_at_one_gpu():
     assert st["slot_policy"] == "lpt" and st["slot_pods"] == 96
     assert len(longest_slot) >= 3
     assert st["slot_work_spread_ms"] <= max_work + 1e-9
+
+
+@pytest.mark.skipif(not has_chain, reason="_core not built")
+def test_plan_corun_pipeline_phantoms_shape_and_no_op():
+    """plan_corun's pipeline context may carry one phantom (the slot's likely next pod) per
+    free slot; with every phantom absent (-1) the plan equals the phantom-free plan, and a
+    phantom that presses on the burst's memory pods changes the predicted SLOs it plans on."""
+    m = _toy()
+    args = dict(units=np.full(4, 2, I32), wid=np.array([0, 0, 1, 1], I32), iters=np.array([20.0, 20.0, 5.0, 5.0]),
+                slo=np.array([900.0, 900.0, 0.0, 0.0]), dev_gpu=np.array([0, 1], I32), dev_free=np.array([4, 4], I32),
+                res_off=np.zeros(3, np.int64), r_wid=np.zeros(0, I32), r_iters=np.zeros(0), r_slo=np.zeros(0),
+                alone_ms=m.alone_ms, cmat=m.coupling(), tolerance=1.0)
+    six = (np.array([0, 0, 0], np.int64), np.zeros(0, I32), np.zeros(0), np.zeros(0),
+           np.array([0, 2, 4], np.int64), np.zeros(4))
+    dev0 = np.array([0, 0, 1, 1], I32)
+    base = list(core.plan_corun(dev0, pipe=six, **args))
+    none = six + (np.full(4, -1, I32), np.zeros(4))
+    assert list(core.plan_corun(dev0, pipe=none, **args)) == base
+    # each memory pod beside a compute pod is the only plan meeting both 900 it/s SLOs
+    assert base[0] != base[1] and base[2] != base[3]
+    with pytest.raises(RuntimeError):
+        core.plan_corun(dev0, pipe=six + (np.full(3, -1, I32), np.zeros(3)), **args)
+    # memory-pressing phantoms behind every slot: the short compute pods' slots continue with
+    # memory pods, which co-run with the long memory pods -- still a valid full plan
+    mem = six + (np.zeros(4, I32), np.full(4, 20.0))
+    out = list(core.plan_corun(dev0, pipe=mem, **args))
+    assert sorted(out) == [0, 0, 1, 1]
