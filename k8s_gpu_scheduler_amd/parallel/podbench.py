@@ -107,7 +107,7 @@ class ControlPlane:
                  online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
-                 slot_sigma: float = 0.2):
+                 slot_sigma: float = 0.2, adaptive: bool = False):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -184,6 +184,15 @@ class ControlPlane:
         self._carry_pred: "collections.deque[Dict[int, float]]" = collections.deque()
         self._covered: Dict[int, float] = {}
         self.epoch = 0
+        # adaptive planning effort (GPU runs): the control plane must schedule an epoch within
+        # the pipeline's period (the interval between consecutive schedule requests) or it
+        # paces the GPUs; when the planner's share of that period runs high it drops to a
+        # cheaper effort level (planner.set_effort), and climbs back when there is room
+        self.adaptive = adaptive
+        self._last_start: Optional[float] = None
+        self._period_ema: Optional[float] = None
+        self._cost_ema: Optional[float] = None
+        self.effort_epochs: Dict[int, int] = {}
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
         self.unscheduled = 0
@@ -207,9 +216,32 @@ class ControlPlane:
                 pass
         self.live = []
 
+    # effort thresholds: share of the pipeline period the scheduling of one epoch may take
+    EFFORT_DOWN = 0.6
+    EFFORT_UP = 0.3
+
+    def _adapt_effort(self, t0: float) -> None:
+        planner = getattr(self.plugin, "planner", None)
+        if planner is None:
+            return
+        if self._last_start is not None:
+            per = t0 - self._last_start
+            self._period_ema = per if self._period_ema is None else 0.8 * self._period_ema + 0.2 * per
+        self._last_start = t0
+        if self.adaptive and self._period_ema and self._cost_ema is not None and self.epoch >= 4:
+            share = self._cost_ema / self._period_ema
+            if share > self.EFFORT_DOWN and planner.effort < 2:
+                planner.set_effort(planner.effort + 1)
+                self._cost_ema = None             # re-measure at the new level
+            elif share < self.EFFORT_UP and planner.effort > 0:
+                planner.set_effort(planner.effort - 1)
+                self._cost_ema = None
+        self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
+
     def schedule_epoch(self) -> np.ndarray:
         """Create this epoch's pods, run them through the scheduler, return placements."""
         t0 = time.perf_counter()
+        self._adapt_effort(t0)
         pods = self.arrivals()
         for p in pods:
             w = W.CATALOG[p["workload"]]
@@ -244,7 +276,9 @@ class ControlPlane:
             self.live.append((ns, name))
         self.queue_drop(dropped)
         self.epoch += 1
-        self.sched_s += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self.sched_s += dt
+        self._cost_ema = dt if self._cost_ema is None else 0.8 * self._cost_ema + 0.2 * dt
         return arr
 
     def queue_drop(self, dropped: List[Tuple[str, str]]) -> None:
@@ -352,6 +386,8 @@ class ControlPlane:
             b = list(planner.backlog.values())
             st["backlog_spread_ms"] = round(max(b) - min(b), 3)
         st["slot_policy"] = planner.slot_policy or "off"
+        if self.effort_epochs:
+            st["effort_epochs"] = {str(k): v for k, v in sorted(self.effort_epochs.items())}
         if planner._slot_work:          # lpt: how level the slot streams' cumulative work is
             by: Dict[Any, List[float]] = {}
             for (dev, _, _), w in planner._slot_work.items():
@@ -700,6 +736,10 @@ def build_parser() -> argparse.ArgumentParser:
                     choices=[0, 1],
                     help="1: the executor re-slots each epoch's Burstable pods longest-first onto the least-loaded "
                          "CU slot (blind to SLOs); 0: pods run on the slot the scheduler chose")
+    ap.add_argument("--cp-adaptive", type=int, default=1, choices=[0, 1],
+                    help="GPU runs: the control plane lowers the planner's effort (phantoms, sweeps, then "
+                         "model slot plans) while scheduling an epoch takes > 60 %% of the pipeline period, "
+                         "and raises it again below 30 %% (planner.set_effort)")
     ap.add_argument("--dump-placements", default="",
                     help="write every epoch's placements (JSON) for a hardware replay (tools/pipelined_vn.py)")
     ap.add_argument("--no-cu-mask", action="store_true")
@@ -804,7 +844,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      plan_tolerance=a.plan_tolerance, plan_objective=a.plan_objective,
                      online_scale=bool(a.online_scale), slo_objective=a.slo_objective, corun_sigma=a.corun_sigma,
                      plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=a.plan_slots,
-                     slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
+                     slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
+                     adaptive=bool(a.cp_adaptive) and not a.sim)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc

@@ -101,6 +101,11 @@ class BurstPlanner:
         self.slot_sigma = slot_sigma
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
         self.pipe_phantoms = True    # ... with each slot's next (phantom) pod chained after its new one
+        # effort level (set_effort): 0 = as configured, 1 = no pipeline phantoms and half the
+        # sweeps, 2 = also slot levelling instead of the model's slot plans and no pipeline
+        # evaluation -- a control plane that falls behind its GPUs trades plan quality for time
+        self.effort = 0
+        self._configured = (self.sweeps, self.slot_policy)
         self._pool = None
         if self.timeline is not None:
             import os
@@ -115,6 +120,17 @@ class BurstPlanner:
             self.feedback = CompletionFeedback(self)
         self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "slot_pred_met": 0,
                       "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
+
+    def set_effort(self, level: int) -> None:
+        level = max(0, min(2, int(level)))
+        sweeps, slots = self._configured
+        self.effort = level
+        self.sweeps = sweeps if level == 0 else max(1, sweeps // 2)
+        self.pipe_phantoms = level == 0
+        self.pipe_eval = level < 2
+        if slots in ("model", "auto"):
+            self.slot_policy = slots if level < 2 else "lpt"
+        self.stats["effort_changes"] = self.stats.get("effort_changes", 0) + 1
 
     # ---------------------------------------------------------------- inputs
     def _matrix(self) -> Optional[Tuple[List[str], List[str], np.ndarray]]:

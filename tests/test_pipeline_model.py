@@ -192,3 +192,28 @@ def test_plan_corun_pipeline_phantoms_shape_and_no_op():
     mem = six + (np.zeros(4, I32), np.full(4, 20.0))
     out = list(core.plan_corun(dev0, pipe=mem, **args))
     assert sorted(out) == [0, 0, 1, 1]
+
+
+@pytest.mark.skipif(core is None, reason="_core not built")
+def test_control_plane_lowers_planning_effort_when_it_paces_the_gpus():
+    """ControlPlane(adaptive=True): scheduling back to back (the pipeline period is the
+    scheduling time itself) drives the planner to its cheapest effort level; with ample time
+    between requests it climbs back to the configured plan."""
+    import time as _t
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=4, iters=20, seed=1, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
+                         plan_slots="auto", adaptive=True)
+    pl = cp.plugin.planner
+    assert pl.effort == 0 and pl.pipe_phantoms and pl.slot_policy == "auto"
+    for _ in range(16):
+        cp.finish_live()
+        cp.schedule_epoch()
+    assert pl.effort == 2 and pl.slot_policy == "lpt" and not pl.pipe_eval
+    for _ in range(40):
+        cp.finish_live()
+        _t.sleep(0.08)
+        cp.schedule_epoch()
+    assert pl.effort == 0 and pl.slot_policy == "auto" and pl.pipe_phantoms
+    st = cp.planner_stats()
+    assert set(st["effort_epochs"]) == {"0", "1", "2"}
