@@ -230,7 +230,7 @@ class ControlPlane:
         self._last_start = t0
         if self.adaptive and self._period_ema and self._cost_ema is not None and self.epoch >= 4:
             share = self._cost_ema / self._period_ema
-            if share > self.EFFORT_DOWN and planner.effort < 2:
+            if share > self.EFFORT_DOWN and planner.effort < planner.MAX_EFFORT:
                 planner.set_effort(planner.effort + 1)
                 self._cost_ema = None             # re-measure at the new level
             elif share < self.EFFORT_UP and planner.effort > 0:
@@ -737,8 +737,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="1: the executor re-slots each epoch's Burstable pods longest-first onto the least-loaded "
                          "CU slot (blind to SLOs); 0: pods run on the slot the scheduler chose")
     ap.add_argument("--cp-adaptive", type=int, default=1, choices=[0, 1],
-                    help="GPU runs: the control plane lowers the planner's effort (phantoms, sweeps, then "
-                         "model slot plans) while scheduling an epoch takes > 60 %% of the pipeline period, "
+                    help="GPU runs: the control plane lowers the planner's effort (phantoms and sweeps, model slot "
+                         "plans, then burst plans) while scheduling an epoch takes > 60 %% of the pipeline period, "
                          "and raises it again below 30 %% (planner.set_effort)")
     ap.add_argument("--dump-placements", default="",
                     help="write every epoch's placements (JSON) for a hardware replay (tools/pipelined_vn.py)")

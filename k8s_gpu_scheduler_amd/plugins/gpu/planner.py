@@ -103,7 +103,8 @@ class BurstPlanner:
         self.pipe_phantoms = True    # ... with each slot's next (phantom) pod chained after its new one
         # effort level (set_effort): 0 = as configured, 1 = no pipeline phantoms and half the
         # sweeps, 2 = also slot levelling instead of the model's slot plans and no pipeline
-        # evaluation -- a control plane that falls behind its GPUs trades plan quality for time
+        # evaluation, 3 = no burst plans at all (Score alone places every pod) -- a control
+        # plane that falls behind its GPUs trades plan quality for time
         self.effort = 0
         self._configured = (self.sweeps, self.slot_policy)
         self._pool = None
@@ -121,8 +122,10 @@ class BurstPlanner:
         self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "slot_pred_met": 0,
                       "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
 
+    MAX_EFFORT = 3
+
     def set_effort(self, level: int) -> None:
-        level = max(0, min(2, int(level)))
+        level = max(0, min(self.MAX_EFFORT, int(level)))
         sweeps, slots = self._configured
         self.effort = level
         self.sweeps = sweeps if level == 0 else max(1, sweeps // 2)
@@ -170,6 +173,8 @@ class BurstPlanner:
         hit = self.plans.get(key)
         if hit is not None:
             return hit
+        if self.effort >= 3:
+            return None                     # effort 3: Score places every pod on its own
         from ... import _native
         core = _native.core()
         model = self.plugin.corun_model()

@@ -206,14 +206,14 @@ def test_control_plane_lowers_planning_effort_when_it_paces_the_gpus():
                          plan_slots="auto", adaptive=True)
     pl = cp.plugin.planner
     assert pl.effort == 0 and pl.pipe_phantoms and pl.slot_policy == "auto"
-    for _ in range(16):
+    for _ in range(24):
         cp.finish_live()
         cp.schedule_epoch()
-    assert pl.effort == 2 and pl.slot_policy == "lpt" and not pl.pipe_eval
-    for _ in range(40):
+    assert pl.effort == 3 and pl.slot_policy == "lpt" and not pl.pipe_eval
+    for _ in range(60):
         cp.finish_live()
         _t.sleep(0.08)
         cp.schedule_epoch()
     assert pl.effort == 0 and pl.slot_policy == "auto" and pl.pipe_phantoms
     st = cp.planner_stats()
-    assert set(st["effort_epochs"]) == {"0", "1", "2"}
+    assert set(st["effort_epochs"]) == {"0", "1", "2", "3"}
