@@ -101,6 +101,7 @@ class BurstPlanner:
         self.slot_sigma = slot_sigma
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
         self.pipe_phantoms = True    # ... with each slot's next (phantom) pod chained after its new one
+        self.sweeps_b: Optional[int] = None     # SLO-phase sweeps (None: `sweeps`)
         # effort level (set_effort): 0 = as configured, 1 = no pipeline phantoms and half the
         # sweeps, 2 = also slot levelling instead of the model's slot plans and no pipeline
         # evaluation, 3 = no burst plans at all (Score alone places every pod) -- a control
@@ -411,7 +412,8 @@ class BurstPlanner:
                 np.array([r.slo * margin for _, r, _ in assign], np.float64),
                 np.array(dev_group, np.int32), cap, off, r_wid, r_iters, r_slo,
                 model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0,
-                float(plugin.args.corun_sigma), base, pipe, hbm, cap_hbm)
+                float(plugin.args.corun_sigma), base, pipe, hbm, cap_hbm,
+                -1 if self.sweeps_b is None else int(self.sweeps_b))
             if self.carry > 0:
                 self._carry(gkeys, per, assign, out, dev_group, model, core, off, r_wid, r_iters, r_slo)
         else:

@@ -443,7 +443,7 @@ py::tuple corun_groups_eval(I64 off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alon
 py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 slo, I32 dev_gpu, I32 dev_free,
                                 I64 res_off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alone, F64 cmat, int sweeps,
                                 double tolerance, int mode, double sigma, py::object base_obj, py::object pipe_obj,
-                                py::object hbm_obj, py::object dev_hbm_obj) {
+                                py::object hbm_obj, py::object dev_hbm_obj, int sweeps_b) {
   int W;
   check_model(alone, cmat, W);
   const py::ssize_t P = dev_in.shape(0), D = dev_gpu.shape(0), NR = r_wid.shape(0);
@@ -756,7 +756,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     auto saturated = [&](const GroupEval& x) { return x.bad == 0; };
     // phase runner: crit(before_i, before_j, after_i, after_j) -> accept
     auto run_phase = [&](auto&& accept) {
-      for (int sw = 0; sw < sweeps; ++sw) {
+      const int nsw = (phase_b && sweeps_b >= 0) ? sweeps_b : sweeps;
+      for (int sw = 0; sw < nsw; ++sw) {
         bool improved = false;
         // moves into free capacity on another GPU (the first accepted device per pod)
         for (py::ssize_t p = 0; p < P; ++p) {
@@ -1170,5 +1171,5 @@ void register_corun(py::module_& m) {
         py::arg("dev_gpu"), py::arg("dev_free"), py::arg("res_off"), py::arg("r_wid"), py::arg("r_iters"),
         py::arg("r_slo"), py::arg("alone_ms"), py::arg("cmat"), py::arg("sweeps") = 8, py::arg("tolerance") = 0.03,
         py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none(), py::arg("pipe") = py::none(),
-        py::arg("hbm") = py::none(), py::arg("dev_hbm") = py::none());
+        py::arg("hbm") = py::none(), py::arg("dev_hbm") = py::none(), py::arg("sweeps_b") = -1);
 }
