@@ -129,8 +129,11 @@ class ControlPlane:
                 self.predictions.install_corun(base)
                 # refits run in a worker process (a refit in a thread stalled this control plane
                 # by ~50 ms per 8-GPU epoch through the interpreter lock), about every 8 epochs
+                # (GPUSCHED_CORUN_REFIT=sync: refits inline, so simulated studies and tests do not
+                # depend on when a worker's result arrives)
+                mode = os.environ.get("GPUSCHED_CORUN_REFIT", "process")
                 self.corun = OnlineCorun(base, refit_every=max(128, 8 * n_gpus * pods_per_gpu),
-                                         background="process")
+                                         background=False if mode == "sync" else mode)
         args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.5, "w_balance": balance, "pack": "binpack",
                 "compat_env": False, "plan_bursts": bool(plan_bursts) and policy != "random",
                 "plan_tolerance": plan_tolerance, "plan_objective": plan_objective, "w_complement": complement,

@@ -305,21 +305,28 @@ def test_planner_backlog_carry_evens_out_cumulative_gpu_work():
 def test_planner_feedback_moves_work_off_a_slow_gpu(tmp_path):
     """Virtual node in --simulate mode (co-run model +-5 % stands in for the GPUs), GPU 0
     running 8 % slower than the model says: with measured busy-time feedback into the backlog
-    the pipelined node epoch (the busiest GPU's cumulative time) is shorter than without."""
+    the pipelined node epoch (the busiest GPU's cumulative time) is shorter than without --
+    on average over three arrival seeds, and on most of them (refits inline: deterministic)."""
     import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = tmp_path / "vn.json"
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "virtual_node_bench.py"), "--simulate",
-                        "--gpus", "4", "--epochs", "32", "--seed", "1", "--sim-speed", "1.08",
-                        "--policies", "corun_plan_t30_s05_c100", "corun_plan_t30_s05_c100_nofb", "--out", str(out)],
-                       capture_output=True, text=True, timeout=300, env=dict(os.environ, PYTHONPATH=root))
-    assert r.returncode == 0, r.stderr[-2000:]
-    res = json.loads(out.read_text())["results"]
-    fb, nofb = res["corun_plan_t30_s05_c100"], res["corun_plan_t30_s05_c100_nofb"]
-    assert fb["epoch_ms_pipelined_l2"] < nofb["epoch_ms_pipelined_l2"], (fb, nofb)
+    fb_ms, nofb_ms = [], []
+    for seed in (1, 2, 3):
+        out = tmp_path / f"vn{seed}.json"
+        r = subprocess.run([sys.executable, os.path.join(root, "tools", "virtual_node_bench.py"), "--simulate",
+                            "--gpus", "4", "--epochs", "32", "--seed", str(seed), "--sim-speed", "1.08",
+                            "--policies", "corun_plan_t30_s05_c100", "corun_plan_t30_s05_c100_nofb",
+                            "--out", str(out)],
+                           capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, PYTHONPATH=root, GPUSCHED_CORUN_REFIT="sync"))
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(out.read_text())["results"]
+        fb_ms.append(res["corun_plan_t30_s05_c100"]["epoch_ms_pipelined_l2"])
+        nofb_ms.append(res["corun_plan_t30_s05_c100_nofb"]["epoch_ms_pipelined_l2"])
+    assert sum(fb_ms) < sum(nofb_ms), (fb_ms, nofb_ms)
+    assert sum(a < b for a, b in zip(fb_ms, nofb_ms)) >= 2, (fb_ms, nofb_ms)
 
 
 @pytest.mark.skipif(not has_core, reason="_core not built")
