@@ -107,7 +107,7 @@ class ControlPlane:
                  online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
-                 slot_sigma: float = 0.2, adaptive: bool = False):
+                 slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -159,6 +159,8 @@ class ControlPlane:
             # the bench corrects the backlog per collected epoch (_plan_feedback); its pods are
             # deleted, never completed, so the deployed completion feedback stays off
             self.plugin.planner.feedback = None
+            if effort:
+                self.plugin.planner.set_effort(effort)     # the starting level (fixed without adaptive)
         self.uuid_to_gpu = {d.device.uuid: d.device.gpu for d in self.ledger.devices(NODE)}
         conf = self.predictions._conf
         self.quarter_tput = {n: conf.by_label[n][f"{C.MI355X_CUS // cu_per_pod}P_{C.MI355X}"] for n in W.NAMES}
@@ -632,6 +634,7 @@ def _effective_config(a: Any) -> Dict[str, Any]:
                        plan_feedback=a.plan_feedback if a.plan_carry > 0 else 0, plan_slots=a.plan_slots)
             if a.plan_slots in ("model", "auto"):
                 out.update(slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
+            out.update(plan_effort=a.plan_effort, cp_adaptive=int(bool(a.cp_adaptive) and not a.sim))
         else:
             out["plan_objective"] = a.plan_objective
     elif corun:
@@ -743,8 +746,12 @@ def build_parser() -> argparse.ArgumentParser:
                          "CU slot (blind to SLOs); 0: pods run on the slot the scheduler chose")
     ap.add_argument("--cp-adaptive", type=int, default=1, choices=[0, 1],
                     help="GPU runs: the control plane lowers the planner's effort (phantoms and sweeps, model slot "
-                         "plans, then burst plans) while scheduling an epoch takes > 85 %% of the pipeline period, "
+                         "plans, then sweeps) while scheduling an epoch takes > 85 %% of the pipeline period, "
                          "and raises it again below 50 %% (planner.set_effort)")
+    ap.add_argument("--plan-effort", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="the planner's starting effort level (0 = full; 1 = no phantoms, half the sweeps; 2 = "
+                         "also lpt slots and no pipeline evaluation; 3 = also one sweep per planning phase); with --cp-adaptive 0 or "
+                         "--sim it stays fixed")
     ap.add_argument("--dump-placements", default="",
                     help="write every epoch's placements (JSON) for a hardware replay (tools/pipelined_vn.py)")
     ap.add_argument("--no-cu-mask", action="store_true")
@@ -850,7 +857,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      online_scale=bool(a.online_scale), slo_objective=a.slo_objective, corun_sigma=a.corun_sigma,
                      plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=a.plan_slots,
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
-                     adaptive=bool(a.cp_adaptive) and not a.sim)
+                     adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc

@@ -104,8 +104,10 @@ class BurstPlanner:
         self.sweeps_b: Optional[int] = None     # SLO-phase sweeps (None: `sweeps`)
         # effort level (set_effort): 0 = as configured, 1 = no pipeline phantoms and half the
         # sweeps, 2 = also slot levelling instead of the model's slot plans and no pipeline
-        # evaluation, 3 = no burst plans at all (Score alone places every pod) -- a control
-        # plane that falls behind its GPUs trades plan quality for time
+        # evaluation, 3 = also one sweep per phase -- a control plane that falls behind its GPUs
+        # trades plan quality for time.  (Dropping burst plans altogether is NOT cheaper at 8
+        # GPUs: Score then evaluates the co-run groups of every candidate GPU per pod, 22.6 vs
+        # 17.0 ms per epoch for level 2 in tools/cp_timing.py, at greedy's SLOs.)
         self.effort = 0
         self._configured = (self.sweeps, self.slot_policy)
         self._pool = None
@@ -129,7 +131,7 @@ class BurstPlanner:
         level = max(0, min(self.MAX_EFFORT, int(level)))
         sweeps, slots = self._configured
         self.effort = level
-        self.sweeps = sweeps if level == 0 else max(1, sweeps // 2)
+        self.sweeps = sweeps if level == 0 else 1 if level >= 3 else max(1, sweeps // 2)
         self.pipe_phantoms = level == 0
         self.pipe_eval = level < 2
         if slots in ("model", "auto"):
@@ -174,8 +176,6 @@ class BurstPlanner:
         hit = self.plans.get(key)
         if hit is not None:
             return hit
-        if self.effort >= 3:
-            return None                     # effort 3: Score places every pod on its own
         from ... import _native
         core = _native.core()
         model = self.plugin.corun_model()

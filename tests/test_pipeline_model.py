@@ -209,7 +209,8 @@ def test_control_plane_lowers_planning_effort_when_it_paces_the_gpus():
     for _ in range(24):
         cp.finish_live()
         cp.schedule_epoch()
-    assert pl.effort == 3 and pl.slot_policy == "lpt" and not pl.pipe_eval
+    assert pl.effort == 3 and pl.slot_policy == "lpt" and not pl.pipe_eval and pl.sweeps == 1
+    assert pl.stats["bursts"] > 0           # level 3 still plans bursts (one sweep per phase)
     for _ in range(60):
         cp.finish_live()
         _t.sleep(0.08)

@@ -37,8 +37,12 @@ def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
     return float(np.median(ts))
 
 
-for name, kw in (("plain", {}), ("bench-defaults", BENCH)):
-    for n in (1, 2, 4, 8):
+CONFIGS = [("plain", {}), ("bench-defaults", BENCH)]
+# the adaptive control plane's cheaper levels (planner.set_effort; bench --plan-effort)
+CONFIGS += [(f"bench-effort{k}", dict(BENCH, effort=k)) for k in (1, 2, 3)]
+only = os.environ.get("CP_TIMING_GPUS")
+for name, kw in CONFIGS:
+    for n in ((int(only),) if only else (1, 2, 4, 8)):
         dt = run(n, kw)
         print(f"{name} gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}",
               flush=True)
