@@ -41,7 +41,8 @@ MODULES = (
     "framework.interface", "framework.runtime", "framework.scheduler", "framework.queue",
     "framework.cache", "framework.changes", "framework.default_plugins", "framework.placement_plugins",
     "kube.client", "kube.informer",
-    "plugins.gpu.plugin", "plugins.gpu.devices", "plugins.gpu.scoring",
+    "plugins.gpu.plugin", "plugins.gpu.devices", "plugins.gpu.scoring", "plugins.gpu.planner",
+    "plugins.gpu.timeline",
     "telemetry.cache", "telemetry.workcost",
     "parallel.podbench",
 )
@@ -120,9 +121,10 @@ class _Finder(importlib.abc.MetaPathFinder):
     """For compiled modules: the extension when its recorded source hash matches the
     current source, else the .py (never a stale extension)."""
 
-    def __init__(self, manifest: Dict[str, str], pure: bool = False):
+    def __init__(self, manifest: Dict[str, str], pure: bool = False, skip: frozenset = frozenset()):
         self.manifest = manifest
         self.pure = pure
+        self.skip = skip
         self.compiled: Dict[str, bool] = {}
 
     def find_spec(self, fullname: str, path=None, target=None) -> Optional[importlib.machinery.ModuleSpec]:
@@ -132,7 +134,7 @@ class _Finder(importlib.abc.MetaPathFinder):
         if mod not in MODULES:
             return None
         src, ext = _source(mod), _ext_path(mod)
-        use_ext = (not self.pure and os.path.exists(ext) and os.path.exists(src)
+        use_ext = (not self.pure and mod not in self.skip and os.path.exists(ext) and os.path.exists(src)
                    and self.manifest.get(mod) == _sha(src))
         self.compiled[fullname] = use_ext
         if use_ext:
@@ -147,10 +149,14 @@ _finder: Optional[_Finder] = None
 
 def install() -> Optional[_Finder]:
     """Idempotent.  With GPUSCHED_PURE_PYTHON=1 the finder still runs -- and imports every
-    listed module from its .py, which an extension next to it would otherwise shadow."""
+    listed module from its .py, which an extension next to it would otherwise shadow;
+    GPUSCHED_CY_SKIP=mod[,mod] (dotted names below the package) does so for those modules
+    only (A/Bs of one module's compilation)."""
     global _finder
     if _finder is None:
-        _finder = _Finder(_read_manifest(), pure=os.environ.get("GPUSCHED_PURE_PYTHON", "") not in ("", "0"))
+        skip = frozenset(x.strip() for x in os.environ.get("GPUSCHED_CY_SKIP", "").split(",") if x.strip())
+        _finder = _Finder(_read_manifest(), pure=os.environ.get("GPUSCHED_PURE_PYTHON", "") not in ("", "0"),
+                          skip=skip)
         sys.meta_path.insert(0, _finder)
     return _finder
 
