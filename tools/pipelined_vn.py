@@ -50,6 +50,12 @@ POLICIES = {
     "greedy": ["--plan-bursts", "0"],
     # the bench default: burst planner on the co-run model, backlog carry, slot planning
     "planner": [],
+    # the cheaper planning levels the adaptive control plane falls back to at 8 GPUs
+    # (planner.set_effort: 1 = no phantoms, half the sweeps; 2 = also lpt slots, no pipeline
+    # evaluation; 3 = also one sweep per phase)
+    "planner-e1": ["--plan-effort", "1"],
+    "planner-e2": ["--plan-effort", "2"],
+    "planner-e3": ["--plan-effort", "3"],
     "random": ["--policy", "random"],
 }
 
@@ -132,7 +138,7 @@ def main() -> None:
     ap.add_argument("--epochs", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seeds", type=int, nargs="+", default=[0])
-    ap.add_argument("--policies", nargs="+", default=list(POLICIES), choices=list(POLICIES))
+    ap.add_argument("--policies", nargs="+", default=["greedy", "planner", "random"], choices=list(POLICIES))
     ap.add_argument("--replay", default="gpu", choices=["gpu", "sim"])
     ap.add_argument("--passes", type=int, default=3,
                     help="replay passes: 1 = free-running virtual GPUs; more = launches gated by the coupled "
