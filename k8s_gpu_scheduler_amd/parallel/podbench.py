@@ -107,7 +107,8 @@ class ControlPlane:
                  online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
-                 slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0):
+                 slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0,
+                 effort_down: Optional[float] = None):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -194,6 +195,8 @@ class ControlPlane:
         # paces the GPUs; when the planner's share of that period runs high it drops to a
         # cheaper effort level (planner.set_effort), and climbs back when there is room
         self.adaptive = adaptive
+        if effort_down is not None:
+            self.EFFORT_DOWN = float(effort_down)
         self._last_start: Optional[float] = None
         self._period_ema: Optional[float] = None
         self._cost_ema: Optional[float] = None
@@ -635,6 +638,8 @@ def _effective_config(a: Any) -> Dict[str, Any]:
             if a.plan_slots in ("model", "auto"):
                 out.update(slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
             out.update(plan_effort=a.plan_effort, cp_adaptive=int(bool(a.cp_adaptive) and not a.sim))
+            if a.cp_adaptive and not a.sim:
+                out["cp_effort_down"] = a.cp_effort_down
         else:
             out["plan_objective"] = a.plan_objective
     elif corun:
@@ -748,6 +753,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="GPU runs: the control plane lowers the planner's effort (phantoms and sweeps, model slot "
                          "plans, then sweeps) while scheduling an epoch takes > 85 %% of the pipeline period, "
                          "and raises it again below 50 %% (planner.set_effort)")
+    ap.add_argument("--cp-effort-down", type=float, default=ControlPlane.EFFORT_DOWN,
+                    help="--cp-adaptive: the share of the pipeline period above which the planner's effort drops")
     ap.add_argument("--plan-effort", type=int, default=0, choices=[0, 1, 2, 3],
                     help="the planner's starting effort level (0 = full; 1 = no phantoms, half the sweeps; 2 = "
                          "also lpt slots and no pipeline evaluation; 3 = also one sweep per planning phase); with --cp-adaptive 0 or "
@@ -857,7 +864,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      online_scale=bool(a.online_scale), slo_objective=a.slo_objective, corun_sigma=a.corun_sigma,
                      plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=a.plan_slots,
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
-                     adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort)
+                     adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort,
+                     effort_down=a.cp_effort_down)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
