@@ -381,7 +381,7 @@ class BurstPlanner:
             assign.append((p, r, d))
         if len(assign) < 2:
             return None
-        self._pending_burst = [p for p, _, _ in assign]
+        self._burst_unit = min((r.units for _, r, _ in assign if r.units), default=0)
         if max((len(m) for m in per), default=0) + len(assign) > 64:
             return None
         off = np.zeros(n_groups + 1, np.int64)
@@ -491,8 +491,7 @@ class BurstPlanner:
         for d, g in enumerate(dev_group):
             ndev[g] += 1
             dev_of[g] = d
-        unit = min((r.units for r in (self.plugin.parse_request(p) for p in self._pending_burst) if r.units),
-                   default=0) if getattr(self, "_pending_burst", None) else 0
+        unit = getattr(self, "_burst_unit", 0)       # the burst's smallest slot size (_plan_corun)
         c_off, f_off = [0], [0]
         cw, cs, ce, ft, pw, pi = [], [], [], [], [], []
         for g in range(n_groups):
