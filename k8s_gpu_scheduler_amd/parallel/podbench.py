@@ -229,6 +229,12 @@ class ControlPlane:
     # ~100 %; the margin covers the placement broadcast and timing noise)
     EFFORT_DOWN = 0.85
     EFFORT_UP = 0.5
+    EFFORT_TARGET = 0.7
+    # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py:
+    # 8.1 / 6.3 / 4.5 / 4.1 ms, profiles/r04_cp2/): a control plane that paces its GPUs jumps
+    # straight to the level predicted to fit, instead of one level per re-measurement (8-rank
+    # box rehearsal: stepping spent ~20 of 65 epochs above the level it settled at)
+    LEVEL_COST = (1.0, 0.78, 0.56, 0.5)
 
     def _adapt_effort(self, t0: float) -> None:
         planner = getattr(self.plugin, "planner", None)
@@ -238,14 +244,24 @@ class ControlPlane:
             per = t0 - self._last_start
             self._period_ema = per if self._period_ema is None else 0.8 * self._period_ema + 0.2 * per
         self._last_start = t0
-        if self.adaptive and self._period_ema and self._cost_ema is not None and self.epoch >= 4:
+        if self.adaptive and self._period_ema and self._cost_ema is not None and self.epoch >= 3:
+            cur = planner.effort
             share = self._cost_ema / self._period_ema
-            if share > self.EFFORT_DOWN and planner.effort < planner.MAX_EFFORT:
-                planner.set_effort(planner.effort + 1)
+            base = self._cost_ema / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]
+
+            def fits(level: int, frac: float) -> bool:
+                return base * self.LEVEL_COST[min(level, len(self.LEVEL_COST) - 1)] <= frac * self._period_ema
+
+            new = cur
+            if share > self.EFFORT_DOWN and cur < planner.MAX_EFFORT:
+                # the cheapest-first search from the next level: the first predicted to fit
+                new = next((lv for lv in range(cur + 1, planner.MAX_EFFORT + 1) if fits(lv, self.EFFORT_TARGET)),
+                           planner.MAX_EFFORT)
+            elif share < self.EFFORT_UP and cur > 0 and fits(cur - 1, self.EFFORT_TARGET):
+                new = cur - 1
+            if new != cur:
+                planner.set_effort(new)
                 self._cost_ema = None             # re-measure at the new level
-            elif share < self.EFFORT_UP and planner.effort > 0:
-                planner.set_effort(planner.effort - 1)
-                self._cost_ema = None
         self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
 
     def schedule_epoch(self) -> np.ndarray:
@@ -288,7 +304,8 @@ class ControlPlane:
         self.epoch += 1
         dt = time.perf_counter() - t0
         self.sched_s += dt
-        self._cost_ema = dt if self._cost_ema is None else 0.8 * self._cost_ema + 0.2 * dt
+        if self.epoch > 1:                # the first epoch pays one-time costs (caches, imports)
+            self._cost_ema = dt if self._cost_ema is None else 0.8 * self._cost_ema + 0.2 * dt
         return arr
 
     def queue_drop(self, dropped: List[Tuple[str, str]]) -> None:
