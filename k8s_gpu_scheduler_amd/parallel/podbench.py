@@ -198,8 +198,8 @@ class ControlPlane:
         if effort_down is not None:
             self.EFFORT_DOWN = float(effort_down)
         self._last_start: Optional[float] = None
-        self._period_ema: Optional[float] = None
-        self._cost_ema: Optional[float] = None
+        self._periods: "collections.deque[float]" = collections.deque(maxlen=4)
+        self._costs: "collections.deque[float]" = collections.deque(maxlen=4)
         self.effort_epochs: Dict[int, int] = {}
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -240,17 +240,21 @@ class ControlPlane:
         planner = getattr(self.plugin, "planner", None)
         if planner is None:
             return
-        if self._last_start is not None:
-            per = t0 - self._last_start
-            self._period_ema = per if self._period_ema is None else 0.8 * self._period_ema + 0.2 * per
+        if self._last_start is not None and self.epoch >= 2:
+            # (the first intervals include the ranks' start-up and pipeline fill)
+            self._periods.append(t0 - self._last_start)
         self._last_start = t0
-        if self.adaptive and self._period_ema and self._cost_ema is not None and self.epoch >= 3:
+        if self.adaptive and len(self._periods) >= 2 and len(self._costs) >= 2:
+            # medians of the last few epochs: one slow epoch (or a start-up gap) must not move
+            # the level, and a decision rests on costs measured at the current level only
+            period = float(np.median(self._periods))
+            cost = float(np.median(self._costs))
             cur = planner.effort
-            share = self._cost_ema / self._period_ema
-            base = self._cost_ema / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]
+            share = cost / period
+            base = cost / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]
 
             def fits(level: int, frac: float) -> bool:
-                return base * self.LEVEL_COST[min(level, len(self.LEVEL_COST) - 1)] <= frac * self._period_ema
+                return base * self.LEVEL_COST[min(level, len(self.LEVEL_COST) - 1)] <= frac * period
 
             new = cur
             if share > self.EFFORT_DOWN and cur < planner.MAX_EFFORT:
@@ -261,7 +265,8 @@ class ControlPlane:
                 new = cur - 1
             if new != cur:
                 planner.set_effort(new)
-                self._cost_ema = None             # re-measure at the new level
+                self._costs.clear()               # re-measure at the new level (the period too:
+                self._periods.clear()             # the GPUs were paced, or are now)
         self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
 
     def schedule_epoch(self) -> np.ndarray:
@@ -305,7 +310,7 @@ class ControlPlane:
         dt = time.perf_counter() - t0
         self.sched_s += dt
         if self.epoch > 1:                # the first epoch pays one-time costs (caches, imports)
-            self._cost_ema = dt if self._cost_ema is None else 0.8 * self._cost_ema + 0.2 * dt
+            self._costs.append(dt)
         return arr
 
     def queue_drop(self, dropped: List[Tuple[str, str]]) -> None:
