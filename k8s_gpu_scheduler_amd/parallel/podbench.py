@@ -200,6 +200,7 @@ class ControlPlane:
         self._last_start: Optional[float] = None
         self._periods: "collections.deque[float]" = collections.deque(maxlen=4)
         self._costs: "collections.deque[float]" = collections.deque(maxlen=4)
+        self._settle = 0
         self.effort_epochs: Dict[int, int] = {}
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -235,13 +236,17 @@ class ControlPlane:
     # straight to the level predicted to fit, instead of one level per re-measurement (8-rank
     # box rehearsal: stepping spent ~20 of 65 epochs above the level it settled at)
     LEVEL_COST = (1.0, 0.78, 0.56, 0.5)
+    EFFORT_SETTLE = 3        # epochs after a level change whose request intervals are not sampled
 
     def _adapt_effort(self, t0: float) -> None:
         planner = getattr(self.plugin, "planner", None)
         if planner is None:
             return
-        if self._last_start is not None and self.epoch >= 2:
-            # (the first intervals include the ranks' start-up and pipeline fill)
+        if self._settle > 0:
+            self._settle -= 1
+        elif self._last_start is not None and self.epoch >= 2:
+            # (the first intervals include the ranks' start-up and pipeline fill; right after a
+            # level change, the requests queued while the GPUs were paced arrive back to back)
             self._periods.append(t0 - self._last_start)
         self._last_start = t0
         if self.adaptive and len(self._periods) >= 2 and len(self._costs) >= 2:
@@ -267,6 +272,7 @@ class ControlPlane:
                 planner.set_effort(new)
                 self._costs.clear()               # re-measure at the new level (the period too:
                 self._periods.clear()             # the GPUs were paced, or are now)
+                self._settle = self.EFFORT_SETTLE
         self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
 
     def schedule_epoch(self) -> np.ndarray:
