@@ -201,6 +201,7 @@ class ControlPlane:
         self._periods: "collections.deque[float]" = collections.deque(maxlen=4)
         self._costs: "collections.deque[float]" = collections.deque(maxlen=4)
         self._settle = 0
+        self._over = 0
         self.effort_epochs: Dict[int, int] = {}
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -234,7 +235,8 @@ class ControlPlane:
     # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py:
     # 8.1 / 6.3 / 4.5 / 4.1 ms, profiles/r04_cp2/): a control plane that paces its GPUs jumps
     # straight to the level predicted to fit, instead of one level per re-measurement (8-rank
-    # box rehearsal: stepping spent ~20 of 65 epochs above the level it settled at)
+    # box rehearsal, profiles/r04_cp_rehearsal/: stepping spent ~20 of 65 epochs above the level
+    # it settled at)
     LEVEL_COST = (1.0, 0.78, 0.56, 0.5)
     EFFORT_SETTLE = 3        # epochs after a level change whose request intervals are not sampled
 
@@ -262,7 +264,10 @@ class ControlPlane:
                 return base * self.LEVEL_COST[min(level, len(self.LEVEL_COST) - 1)] <= frac * period
 
             new = cur
-            if share > self.EFFORT_DOWN and cur < planner.MAX_EFFORT:
+            # two consecutive checks over the threshold before a step down (one noisy window of
+            # a busy host CPU must not cost plan quality for the rest of the run)
+            self._over = self._over + 1 if share > self.EFFORT_DOWN else 0
+            if self._over >= 2 and cur < planner.MAX_EFFORT:
                 # the cheapest-first search from the next level: the first predicted to fit
                 new = next((lv for lv in range(cur + 1, planner.MAX_EFFORT + 1) if fits(lv, self.EFFORT_TARGET)),
                            planner.MAX_EFFORT)
@@ -273,6 +278,7 @@ class ControlPlane:
                 self._costs.clear()               # re-measure at the new level (the period too:
                 self._periods.clear()             # the GPUs were paced, or are now)
                 self._settle = self.EFFORT_SETTLE
+                self._over = 0
         self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
 
     def schedule_epoch(self) -> np.ndarray:
