@@ -273,6 +273,10 @@ class ControlPlane:
                            planner.MAX_EFFORT)
             elif share < self.EFFORT_UP and cur > 0 and fits(cur - 1, self.EFFORT_TARGET):
                 new = cur - 1
+            if os.environ.get("GPUSCHED_EFFORT_DEBUG"):
+                print(f"[effort] epoch {self.epoch} level {cur}->{new} share {share:.2f} period "
+                      f"{[round(x * 1e3, 2) for x in self._periods]} cost {[round(x * 1e3, 2) for x in self._costs]}",
+                      file=sys.stderr, flush=True)
             if new != cur:
                 planner.set_effort(new)
                 self._costs.clear()               # re-measure at the new level (the period too:
