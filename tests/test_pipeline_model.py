@@ -218,3 +218,39 @@ def test_control_plane_lowers_planning_effort_when_it_paces_the_gpus():
     assert pl.effort == 0 and pl.slot_policy == "auto" and pl.pipe_phantoms
     st = cp.planner_stats()
     assert set(st["effort_epochs"]) == {"0", "1", "2", "3"}
+
+
+@pytest.mark.skipif(core is None, reason="_core not built")
+def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
+    """A control plane whose scheduling takes the whole period (it paces the GPUs) jumps from
+    level 0 straight to the first level whose predicted cost fits 70 % of the period (level 2:
+    0.56 of level 0's cost), after two consecutive over-threshold checks; the request intervals
+    right after the change are not sampled; with room again it climbs back one level."""
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=4, iters=20, seed=1, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
+                         plan_slots="auto", adaptive=True)
+    pl = cp.plugin.planner
+    cp.epoch = 10
+    t = [0.0]
+
+    def step(period_ms, cost_ms):
+        t[0] += period_ms / 1e3
+        cp._adapt_effort(t[0])
+        cp._costs.append(cost_ms / 1e3)
+
+    step(10, 10)
+    for _ in range(2):
+        step(10, 10)
+    assert pl.effort == 0                     # first over-threshold check: patience
+    step(10, 10)
+    assert pl.effort == 2 and not cp._periods and cp._settle == cp.EFFORT_SETTLE
+    for _ in range(cp.EFFORT_SETTLE):
+        step(2, 5.6)                          # queued requests arrive back to back: not sampled
+    assert not cp._periods and pl.effort == 2
+    for _ in range(4):
+        step(10, 5.6)                         # 56 % of the period: stays
+    assert pl.effort == 2
+    for _ in range(4):
+        step(20, 5.6)                         # 28 %: level 1 (78 / 56 x 5.6 = 7.8 ms) fits 70 % of 20
+    assert pl.effort == 1
