@@ -198,8 +198,8 @@ class ControlPlane:
         if effort_down is not None:
             self.EFFORT_DOWN = float(effort_down)
         self._last_start: Optional[float] = None
-        self._periods: "collections.deque[float]" = collections.deque(maxlen=4)
-        self._costs: "collections.deque[float]" = collections.deque(maxlen=4)
+        self._periods: "collections.deque[float]" = collections.deque(maxlen=6)
+        self._costs: "collections.deque[float]" = collections.deque(maxlen=6)
         self._settle = 0
         self._over = 0
         self.effort_epochs: Dict[int, int] = {}
@@ -251,11 +251,13 @@ class ControlPlane:
             # level change, the requests queued while the GPUs were paced arrive back to back)
             self._periods.append(t0 - self._last_start)
         self._last_start = t0
-        if self.adaptive and len(self._periods) >= 2 and len(self._costs) >= 2:
-            # medians of the last few epochs: one slow epoch (or a start-up gap) must not move
-            # the level, and a decision rests on costs measured at the current level only
-            period = float(np.median(self._periods))
-            cost = float(np.median(self._costs))
+        if self.adaptive and len(self._periods) >= 3 and len(self._costs) >= 3:
+            # means over the last few epochs (rates: requests can arrive in pairs, so single
+            # intervals alternate short / long and a median of an odd window reads the short one),
+            # with start-up gaps and post-change intervals kept out of the window; a decision rests
+            # on costs measured at the current level only
+            period = float(np.mean(self._periods))
+            cost = float(np.mean(self._costs))
             cur = planner.effort
             share = cost / period
             base = cost / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]

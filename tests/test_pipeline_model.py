@@ -239,18 +239,21 @@ def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
         cp._adapt_effort(t[0])
         cp._costs.append(cost_ms / 1e3)
 
-    step(10, 10)
-    for _ in range(2):
+    levels = []
+    for _ in range(8):
         step(10, 10)
-    assert pl.effort == 0                     # first over-threshold check: patience
-    step(10, 10)
-    assert pl.effort == 2 and not cp._periods and cp._settle == cp.EFFORT_SETTLE
+        levels.append(pl.effort)
+        if pl.effort:
+            break
+    # the windows fill (3 samples), the first over-threshold check waits (patience), then one jump
+    assert levels[:4] == [0, 0, 0, 0] and levels[-1] == 2 and 1 not in levels
+    assert not cp._periods and cp._settle == cp.EFFORT_SETTLE
     for _ in range(cp.EFFORT_SETTLE):
         step(2, 5.6)                          # queued requests arrive back to back: not sampled
     assert not cp._periods and pl.effort == 2
-    for _ in range(4):
+    for _ in range(6):
         step(10, 5.6)                         # 56 % of the period: stays
     assert pl.effort == 2
-    for _ in range(4):
+    for _ in range(6):
         step(20, 5.6)                         # 28 %: level 1 (78 / 56 x 5.6 = 7.8 ms) fits 70 % of 20
     assert pl.effort == 1
