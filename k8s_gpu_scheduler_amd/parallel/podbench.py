@@ -202,6 +202,7 @@ class ControlPlane:
         self._costs: "collections.deque[float]" = collections.deque(maxlen=6)
         self._settle = 0
         self._over = 0
+        self._changed = False
         self.effort_epochs: Dict[int, int] = {}
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -251,7 +252,12 @@ class ControlPlane:
             # level change, the requests queued while the GPUs were paced arrive back to back)
             self._periods.append(t0 - self._last_start)
         self._last_start = t0
-        if self.adaptive and len(self._periods) >= 3 and len(self._costs) >= 3:
+        # the first decision (no level change yet) acts on two samples without patience: the
+        # warm-up epochs are few, and a control plane that paces its GPUs from the start would
+        # carry that backlog into the timed region
+        first = not self._changed
+        need = 2 if first else 3
+        if self.adaptive and len(self._periods) >= need and len(self._costs) >= need:
             # means over the last few epochs (rates: requests can arrive in pairs, so single
             # intervals alternate short / long and a median of an odd window reads the short one),
             # with start-up gaps and post-change intervals kept out of the window; a decision rests
@@ -269,7 +275,7 @@ class ControlPlane:
             # two consecutive checks over the threshold before a step down (one noisy window of
             # a busy host CPU must not cost plan quality for the rest of the run)
             self._over = self._over + 1 if share > self.EFFORT_DOWN else 0
-            if self._over >= 2 and cur < planner.MAX_EFFORT:
+            if self._over >= (1 if first else 2) and cur < planner.MAX_EFFORT:
                 # the cheapest-first search from the next level: the first predicted to fit
                 new = next((lv for lv in range(cur + 1, planner.MAX_EFFORT + 1) if fits(lv, self.EFFORT_TARGET)),
                            planner.MAX_EFFORT)
@@ -285,6 +291,7 @@ class ControlPlane:
                 self._periods.clear()             # the GPUs were paced, or are now)
                 self._settle = self.EFFORT_SETTLE
                 self._over = 0
+                self._changed = True
         self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
 
     def schedule_epoch(self) -> np.ndarray:

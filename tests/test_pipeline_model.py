@@ -245,8 +245,9 @@ def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
         levels.append(pl.effort)
         if pl.effort:
             break
-    # the windows fill (3 samples), the first over-threshold check waits (patience), then one jump
-    assert levels[:4] == [0, 0, 0, 0] and levels[-1] == 2 and 1 not in levels
+    # the first decision: as soon as two samples are in, one jump (later ones wait for three
+    # samples and two over-threshold checks)
+    assert levels[:2] == [0, 0] and levels[-1] == 2 and 1 not in levels
     assert not cp._periods and cp._settle == cp.EFFORT_SETTLE
     for _ in range(cp.EFFORT_SETTLE):
         step(2, 5.6)                          # queued requests arrive back to back: not sampled
