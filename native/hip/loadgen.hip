@@ -907,9 +907,7 @@ static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 2
 // landed and every pod stream got its own HW queue (interleaved A/B, profiles/r02_gemm_share_ab.txt;
 // in round 1, with the older kernels, it had been even: profiles/r01_gemm_policy_ab.txt).
 // 0 = co-running pods always take the 128x128 / 2-per-CU picker.  2 = tile 4 instead of tile
-// 10 for lone GEMMs.  3 = as 1, but co-running pods take the 256x256 tile already when it gives
-// half of their CU share a workgroup (the 8-phase kernel keeps the MFMAs ~68 % busy on its CUs,
-// the 128x128 tile ~29 % on the small catalog GEMMs: profiles/r03_pmc_bench_kernels.json).
+// 10 for lone GEMMs.
 static int g_gemm_policy = 1;
 // split-K for lone GEMMs whose 256x256 tiles leave CUs idle: -1 = auto (up to 8 slices), 0 = off,
 // 2..8 = at most that many slices.  Off by default: on the tall-K 2048x4096x8192 the split
@@ -920,7 +918,7 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 3) throw std::runtime_error("gemm policy must be 0..3");
+  if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");
   g_gemm_policy = p;
 }
 
@@ -944,8 +942,6 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
   if (alone && fits256) return g_gemm_policy == 2 ? 4 : 10;
   if (!alone && fits256 && g_gemm_policy >= 1) return 10;
-  if (!alone && g_gemm_policy == 3 && (M % 256 == 0) && (N % 256 == 0) && 2 * (M / 256) * (N / 256) >= budget)
-    return 10;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
