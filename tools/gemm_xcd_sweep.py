@@ -14,7 +14,8 @@ from k8s_gpu_scheduler_amd import _native  # noqa: E402
 from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
 
 SHAPES = [(4096, 4096, 4096), (8192, 8192, 8192), (8192, 8192, 2048), (4096, 8192, 4096), (2048, 4096, 8192)]
-ARMS = ["torch", "g2", "g4", "g8", "g16", "plain"]
+ARMS = os.environ.get("XCD_SWEEP_ARMS", "torch,g2,g4,g8,g16,plain").split(",")
+ROUNDS = int(os.environ.get("XCD_SWEEP_ROUNDS", "3"))
 
 
 def t_ms(fn, iters=20, warm=3):
@@ -39,7 +40,7 @@ def main():
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         ref = (a.float() @ bt.float().T)
         res = {x: [] for x in ARMS}
-        for _ in range(3):
+        for _ in range(ROUNDS):
             for arm in ARMS:
                 if arm == "torch":
                     fn = lambda: torch.matmul(a, bt.T, out=c)  # noqa: E731
@@ -56,15 +57,15 @@ def main():
         h.set_gemm_tile(0)
         h.set_xcd_blocks(1)
         h.set_xcd_group(4)
-        med = {k: sorted(v)[1] for k, v in res.items()}
+        med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
         row = {"shape": [M, N, K], "median_tflops": med,
                "vs_hipblaslt": {k: round(v / med["torch"], 3) for k, v in med.items() if k != "torch"}}
         out.append(row)
         print(json.dumps(row), flush=True)
         del a, bt, c, ref
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/gemm_xcd_sweep.json", "w") as f:
-        json.dump({"note": "uniform [-1,1) bf16, bf16 out, no bias/act; median TF/s of 3 interleaved rounds x 20 "
+    with open(os.environ.get("XCD_SWEEP_OUT", "gpurun_out/gemm_xcd_sweep.json"), "w") as f:
+        json.dump({"rounds": ROUNDS, "note": "uniform [-1,1) bf16, bf16 out, no bias/act; median TF/s of interleaved rounds x 20 "
                            "iters; g<k> = XCD-block order with k tile rows per group (default 4), plain = GROUP_M "
                            "order", "results": out}, f, indent=1)
 
