@@ -35,6 +35,7 @@ void set_gemm_tile(int t);
 void set_gemm_policy(int p);
 void set_wide_epilogue(int on);
 void set_xcd_blocks(int on);
+void set_lone_plain_order(int on);
 void set_xcd_group(int rows);
 void xcd_probe(uintptr_t out, int blocks, uintptr_t stream);
 int pick_xcd_map(int tiles_m, int tiles_n);

@@ -66,6 +66,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_gemm_policy", &gs::set_gemm_policy, py::arg("policy"));
   m.def("set_wide_epilogue", &gs::set_wide_epilogue, py::arg("on"));
   m.def("set_xcd_blocks", &gs::set_xcd_blocks, py::arg("on"));
+  m.def("set_lone_plain_order", &gs::set_lone_plain_order, py::arg("on"));
   m.def("set_xcd_group", &gs::set_xcd_group, py::arg("rows"));
   m.def("xcd_probe", &gs::xcd_probe, py::arg("out"), py::arg("blocks"), py::arg("stream"));
   m.def("pick_xcd_map", &gs::pick_xcd_map, py::arg("tiles_m"), py::arg("tiles_n"));

@@ -809,6 +809,10 @@ static void launch_gemm_v(const __bf16* A, const __bf16* B, __bf16* Cp, const fl
 static int g_xcd_blocks = 1;
 static int g_xcd_group = 4;         // tile rows per group inside an XCD block
 void set_xcd_blocks(int on) { g_xcd_blocks = on ? 1 : 0; }
+// lone 8-phase GEMMs (whole-chip budget) in the plain GROUP_M order (1, default) or the same
+// order as co-running pods (0, A/B knob)
+static int g_lone_plain_order = 1;
+void set_lone_plain_order(int on) { g_lone_plain_order = on ? 1 : 0; }
 
 void set_xcd_group(int rows) {
   if (rows < 1 || rows > 64) throw std::runtime_error("xcd group rows must be 1..64");
@@ -850,8 +854,12 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
 
 template <bool PEEL, bool WIDE>
 static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
-                         int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
-  const int xmap = pick_xcd_map(M / 256, N / 256);
+                         int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block, bool lone) {
+  // a lone GEMM (the whole chip) takes the plain GROUP_M order: 0.936 vs 0.913 of hipBLASLt at
+  // 4096^3, 0.94 vs 0.916 at 4096x8192x4096, 0.935 vs 0.918 at 8192^2x2048, 0.914 vs 0.92 at 8192^3
+  // (7 interleaved rounds, profiles/r04_gemm_xcd/); co-running pods keep the XCD-block order
+  // (+2.6 % bench pods/s, profiles/r02_xcd_block_order_ab.txt)
+  const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / 256);
   if (relu && bp)
     hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
   else if (relu)
@@ -866,12 +874,12 @@ static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const flo
 // epilogue (when C rows are 16-B aligned, else the 8-B epilogue)
 template <bool PEEL>
 static void launch_8ph(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
-                       int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block) {
+                       int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block, bool lone) {
   const bool wide = PEEL && wide_ok(Cp, ldc);
   if (wide)
-    launch_8ph_v<PEEL, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
+    launch_8ph_v<PEEL, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
   else
-    launch_8ph_v<PEEL, false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
+    launch_8ph_v<PEEL, false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
 }
 
 // 0 = auto, 1 = 128x128 (4 waves, 2/CU), 2 = 64x128, 3 = 64x64,
@@ -1023,10 +1031,11 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 9:
     case 10: {
       const dim3 grid((M / 256) * (N / 256)), block(512);
+      const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
       if (t == 10)
-        launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
+        launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
       else
-        launch_8ph<false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block);
+        launch_8ph<false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
       break;
     }
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;

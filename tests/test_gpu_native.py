@@ -738,12 +738,18 @@ def test_xcd_dispatch_and_tile_orders_bit_exact():
     y, z = torch.rand(1 << 20, device="cuda"), torch.rand(1 << 20, device="cuda")
     try:
         h.set_gemm_tile(10)
-        ref = loadgen.gemm(a, bt, bias=bias, relu=True)
+        # a co-running pod's GEMM (CU budget 64) takes the XCD-block order, a lone one the plain
+        # GROUP_M order (set_lone_plain_order); every order computes the same bits
+        ref = loadgen.gemm(a, bt, bias=bias, relu=True, cu_budget=64)
         tref = torch.empty_like(y)
         loadgen.triad(tref, y, z, 1.5)
         torch.testing.assert_close(ref.float(), torch.relu(a.float() @ bt.float().T + bias), atol=0.1, rtol=0.02)
-        h.set_xcd_blocks(0)
         assert torch.equal(loadgen.gemm(a, bt, bias=bias, relu=True), ref)
+        h.set_lone_plain_order(0)
+        assert torch.equal(loadgen.gemm(a, bt, bias=bias, relu=True), ref)
+        h.set_lone_plain_order(1)
+        h.set_xcd_blocks(0)
+        assert torch.equal(loadgen.gemm(a, bt, bias=bias, relu=True, cu_budget=64), ref)
         h.set_xcd_blocks(1)
         torch.testing.assert_close(tref, y + 1.5 * z)
         for gone in ("set_xcd_mask", "set_c_nontemporal", "set_triad_aux"):
@@ -753,4 +759,5 @@ def test_xcd_dispatch_and_tile_orders_bit_exact():
                 h.set_gemm_tile(bad)
     finally:
         h.set_xcd_blocks(1)
+        h.set_lone_plain_order(1)
         h.set_gemm_tile(0)

@@ -1,5 +1,6 @@
 """Lone large GEMMs: the 8-phase 256x256 kernel under each XCD tile-order setting (XCD-block
-order with 2 / 4 / 8 / 16 tile rows per group, and the plain GROUP_M order) against hipBLASLt
+order with 2 / 4 / 8 / 16 tile rows per group, and the plain GROUP_M order -- the lone-GEMM
+default since round 4, set_lone_plain_order) against hipBLASLt
 (torch), interleaved rounds in one process on uniform [-1, 1) operands.
 Writes gpurun_out/gemm_xcd_sweep.json."""
 import json
@@ -46,8 +47,9 @@ def main():
                     fn = lambda: torch.matmul(a, bt.T, out=c)  # noqa: E731
                 else:
                     h.set_gemm_tile(10)
-                    h.set_xcd_blocks(0 if arm == "plain" else 1)
+                    h.set_lone_plain_order(1 if arm == "plain" else 0)
                     if arm != "plain":
+                        h.set_xcd_blocks(1)
                         h.set_xcd_group(int(arm[1:]))
                     fn = lambda: loadgen.gemm(a, bt, out=c)  # noqa: E731
                 res[arm].append(round(2 * M * N * K / t_ms(fn) / 1e9, 1))
@@ -57,6 +59,7 @@ def main():
         h.set_gemm_tile(0)
         h.set_xcd_blocks(1)
         h.set_xcd_group(4)
+        h.set_lone_plain_order(1)
         med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
         row = {"shape": [M, N, K], "median_tflops": med,
                "vs_hipblaslt": {k: round(v / med["torch"], 3) for k, v in med.items() if k != "torch"}}
