@@ -56,6 +56,9 @@ POLICIES = {
     "planner-e1": ["--plan-effort", "1"],
     "planner-e2": ["--plan-effort", "2"],
     "planner-e3": ["--plan-effort", "3"],
+    # how far a GPU's predicted time may exceed the balanced plan's slowest GPU to meet more SLOs
+    "planner-tol05": ["--plan-tolerance", "0.5"],
+    "planner-tol08": ["--plan-tolerance", "0.8"],
     "random": ["--policy", "random"],
 }
 
