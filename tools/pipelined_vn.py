@@ -59,6 +59,10 @@ POLICIES = {
     # how far a GPU's predicted time may exceed the balanced plan's slowest GPU to meet more SLOs
     "planner-tol05": ["--plan-tolerance", "0.5"],
     "planner-tol08": ["--plan-tolerance", "0.8"],
+    # the model error the planner's expected-SLO objective assumes (default 0.05, the held-out
+    # error of isolated groups; pipelined predictions are looser)
+    "planner-sig10": ["--corun-sigma", "0.1"],
+    "planner-sig20": ["--corun-sigma", "0.2"],
     "random": ["--policy", "random"],
 }
 
