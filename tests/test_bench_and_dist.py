@@ -29,6 +29,16 @@ def test_bench_sim_single_process():
     assert r["sol_pct"]["peak"] <= r["sol_pct"]["achievable"] and r["achieved_hbm_tbps_per_gpu"] > 0
 
 
+def test_bench_pinned_effort_level_is_recorded_and_held():
+    """--plan-effort pins the planner's level (the simulated bench never adapts): the JSON's
+    config records the level and that adaptation was off, and every epoch ran at that level."""
+    from k8s_gpu_scheduler_amd.parallel.podbench import main
+    r = main(["--sim", "--gpus", "2", "--steps", "3", "--warmup", "1", "--plan-effort", "2"])
+    assert r["config"]["plan_effort"] == 2 and r["config"]["cp_adaptive"] == 0
+    assert "cp_effort_down" not in r["config"]
+    assert set(r["planner"]["effort_epochs"]) == {"2"} and r["planner"]["slot_policy"] == "lpt"
+
+
 def test_bench_random_policy_runs():
     from k8s_gpu_scheduler_amd.parallel.podbench import main
     r = main(["--sim", "--gpus", "2", "--steps", "2", "--warmup", "1", "--policy", "random"])
