@@ -41,8 +41,6 @@ random-walking onto one GPU, whose cumulative work paces a pipelined multi-GPU j
 """
 from __future__ import annotations
 
-import collections
-
 from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -90,9 +88,6 @@ class BurstPlanner:
         if self.slot_policy == "off":
             self.slot_policy = ""
         self._slot_work: Dict[Tuple[str, int, int], float] = {}    # (device, first unit, units) -> ms
-        import os as _os
-        self.lpt_xtol = float(_os.environ.get("GPUSCHED_LPT_XTOL", "0"))    # A/B knob, 0 = plain levelling
-        self._slot_hist: Dict[Tuple[str, int, int], Any] = {}
         self.timeline = None
         if self.slot_policy in ("model", "auto"):
             from .timeline import SlotTimeline
@@ -476,35 +471,11 @@ class BurstPlanner:
             if len(slots) < len(items):
                 continue
             work = {O.key(p): float(model.alone_ms[model.wid(O.name(p))]) * max(r.iters, 1.0) for p, r in items}
-            cm = model.coupling() if self.lpt_xtol > 0 else None
             for p, r in sorted(items, key=lambda x: -work[O.key(x[0])]):
-                wk = work[O.key(p)]
                 u = min(slots, key=lambda s: (self._slot_work.get((uuid, s, n), 0.0), s))
-                if cm is not None:
-                    # interference-aware (A/B): among the slots whose stream is within xtol x this
-                    # pod's work of the least loaded one, the one where the pod overlaps (in
-                    # predicted work time) the least coupling with the other slots' recent pods
-                    wi = model.wid(O.name(p))
-                    lo = self._slot_work.get((uuid, u, n), 0.0)
-                    near = [x for x in slots if self._slot_work.get((uuid, x, n), 0.0) <= lo + self.lpt_xtol * wk]
-
-                    def cost(x):
-                        a = self._slot_work.get((uuid, x, n), 0.0)
-                        c = 0.0
-                        for (dv, s2, _), hist in self._slot_hist.items():
-                            if dv != uuid or s2 == x:
-                                continue
-                            for (x0, x1, wj) in hist:
-                                ov = min(a + wk, x1) - max(a, x0)
-                                if ov > 0:
-                                    c += ov * (cm[wi, wj] + cm[wj, wi])
-                        return (c, a, x)
-                    u = min(near, key=cost)
-                    a0 = self._slot_work.get((uuid, u, n), 0.0)
-                    self._slot_hist.setdefault((uuid, u, n), collections.deque(maxlen=8)).append((a0, a0 + wk, wi))
                 slots.remove(u)
                 res[O.key(p)] = u
-                self._slot_work[(uuid, u, n)] = self._slot_work.get((uuid, u, n), 0.0) + wk
+                self._slot_work[(uuid, u, n)] = self._slot_work.get((uuid, u, n), 0.0) + work[O.key(p)]
             self.stats["slot_plans"] += 1
             self.stats["slot_pods"] += len(items)
         return res
