@@ -88,11 +88,19 @@ class SetChecker:
     (k - 1) x this per-link rate (a k-GPU ring crosses k - 1 links per GPU; 20 GB/s is far
     below a healthy MI355X xGMI link, ~153 GB/s, and catches a link down to PCIe rates)."""
 
+    # a probe that ran on idle GPUs but produced no result (child crash, RCCL hang until the
+    # timeout, no JSON) is not retried at once: after the first failure the set waits
+    # retry_s (doubling per failure); after max_failures it is published as bad -- a set on
+    # which RCCL cannot complete an all-reduce is not a set to place a ring on
     def __init__(self, probe: Callable[[Sequence[int]], Optional[Dict[str, Any]]] = set_probe_in_child,
                  recheck_s: float = 3600.0, frac: float = 0.6, floor_link_gbps: float = 20.0, keep: int = 64,
-                 clock: Callable[[], float] = time.time):
+                 clock: Callable[[], float] = time.time, retry_s: float = 300.0, max_failures: int = 2):
         self.probe = probe
         self.recheck_s = recheck_s
+        self.retry_s = retry_s
+        self.max_failures = max_failures
+        self.failures: Dict[GpuSet, int] = {}
+        self._retry_at: Dict[GpuSet, float] = {}
         self.frac = frac
         self.floor_link_gbps = floor_link_gbps
         self.keep = keep
@@ -110,6 +118,8 @@ class SetChecker:
             r = self.results.get(s)
             if s in self._queue or (r is not None and self.clock() - r["ts"] < self.recheck_s):
                 return False
+            if self.clock() < self._retry_at.get(s, 0.0):
+                return False
             self._queue.append(s)
             return True
 
@@ -123,7 +133,9 @@ class SetChecker:
                 self._queue.remove(gpus)
             bw = busbw_of(res)
             if bw is None:
-                return None
+                return self._failed(gpus)
+            self.failures.pop(gpus, None)
+            self._retry_at.pop(gpus, None)
             self.results[gpus] = {"gpus": list(gpus), "busbw_gbps": round(bw, 1), "ts": self.clock()}
             if len(self.results) > self.keep:
                 oldest = min(self.results, key=lambda s: self.results[s]["ts"])
@@ -131,19 +143,35 @@ class SetChecker:
             self._judge()
             return dict(self.results.get(gpus, {})) or None
 
+    def _failed(self, gpus: GpuSet) -> Optional[Dict[str, Any]]:
+        """(lock held) A probe of `gpus` ran and failed: back off, or after max_failures
+        publish the set as bad."""
+        n = self.failures.get(gpus, 0) + 1
+        self.failures[gpus] = n
+        if n < self.max_failures:
+            self._retry_at[gpus] = self.clock() + self.retry_s * 2 ** (n - 1)
+            return None
+        self._retry_at.pop(gpus, None)
+        self.failures.pop(gpus, None)
+        self.results[gpus] = {"gpus": list(gpus), "busbw_gbps": 0.0, "ts": self.clock(), "failed": True}
+        self._judge()
+        return dict(self.results[gpus])
+
     def _judge(self) -> None:
         """(Re)judge every set against its size's median: a set checked before its peers
         existed is re-judged as they arrive."""
         by_k: Dict[int, List[float]] = {}
         for s, r in self.results.items():
-            by_k.setdefault(len(s), []).append(r["busbw_gbps"])
+            if not r.get("failed"):
+                by_k.setdefault(len(s), []).append(r["busbw_gbps"])
         for s, r in self.results.items():
-            vals = sorted(by_k[len(s)])
+            vals = sorted(by_k.get(len(s), []))
             med = vals[len(vals) // 2] if len(vals) >= 3 else None
             floor = (len(s) - 1) * self.floor_link_gbps
             r["floor_gbps"] = floor
             r["median_gbps"] = med
-            r["ok"] = bool(r["busbw_gbps"] >= floor and (med is None or r["busbw_gbps"] >= self.frac * med))
+            r["ok"] = bool(not r.get("failed") and r["busbw_gbps"] >= floor and
+                           (med is None or r["busbw_gbps"] >= self.frac * med))
 
     def bad_sets(self) -> List[List[int]]:
         with self._lock:
@@ -164,6 +192,10 @@ class ProbeWorker:
         self.taint = taint
         self.discarded = 0
         self.ran: List[str] = []
+        self.failed: List[str] = []
+        self.retry_s = 300.0             # fabric probe back-off after a failed run (doubling)
+        self._fabric_failures = 0
+        self._fabric_retry_at = 0.0
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
 
@@ -215,13 +247,17 @@ class ProbeWorker:
         return n
 
     # ---------------------------------------------------------------- one probe
-    def _exclusive(self, what: str, gpus: Optional[Sequence[int]], fn: Callable[[], Any]) -> Tuple[bool, Any]:
-        """(ran, result): fn() with the node tainted, only from idle GPUs and only kept when
-        they are still idle afterwards."""
+    DEFERRED, DISCARDED, RAN = "deferred", "discarded", "ran"
+
+    def _exclusive(self, what: str, gpus: Optional[Sequence[int]], fn: Callable[[], Any]) -> Tuple[str, Any]:
+        """(outcome, result): fn() with the node tainted, only from idle GPUs and only kept when
+        they are still idle afterwards.  outcome: DEFERRED (busy before: not run), DISCARDED
+        (busy afterwards: result thrown away, the probe is still due) or RAN (result = fn()'s,
+        None when the probe itself failed)."""
         reasons = self.busy(gpus)
         if reasons:
             log.info("%s deferred: GPUs busy (%s)", what, "; ".join(reasons[:3]))
-            return False, None
+            return self.DEFERRED, None
         res_api = None
         if self.taint and self.agent.client is not None:
             from ..kube.resources import Resources
@@ -230,7 +266,7 @@ class ProbeWorker:
                 res_api.taint_node(self.agent.node, C.TAINT_PROBING, what.split()[0], "NoSchedule")
             except Exception as e:
                 log.warning("%s: tainting %s failed (%s): not probing", what, self.agent.node, e)
-                return False, None
+                return self.DEFERRED, None
         try:
             out = fn()
         finally:
@@ -243,37 +279,53 @@ class ProbeWorker:
         if after:
             self.discarded += 1
             log.warning("%s: GPUs became busy during the probe (%s): result discarded", what, "; ".join(after[:3]))
-            return True, None
+            return self.DISCARDED, None
         self.ran.append(what)
-        return True, out
+        return self.RAN, out
 
     def tick(self) -> Optional[str]:
         """Run at most one due probe; returns what ran ('fabric' / 'set 0,1,2,3') or None."""
         ag = self.agent
         fab = getattr(ag, "fabric", None)
-        if fab is not None and fab.due:
-            ran, res = self._exclusive("fabric", None, fab.probe)
-            if ran:
-                if res is not None:
+        if fab is not None and fab.due and time.time() >= self._fabric_retry_at:
+            how, res = self._exclusive("fabric", None, fab.probe)
+            if how != self.DEFERRED:
+                if how == self.RAN:
+                    # done either way: a failed probe (child crash / timeout / no JSON) must
+                    # not re-taint the node and re-run every period_s forever -- it is retried
+                    # after a doubling back-off (the last good topology stays published)
                     fab.due = False
-                    fab.last = res
-                    from .fabric import degraded_pairs
-                    bad = degraded_pairs(res.get("bw_gbps") or [])
-                    if bad:
-                        log.warning("fabric on %s: degraded GPU pairs %s", ag.node, bad)
-                    ag.publish_topology()
+                    if res is not None:
+                        self._fabric_failures = 0
+                        fab.last = res
+                        from .fabric import degraded_pairs
+                        bad = degraded_pairs(res.get("bw_gbps") or [])
+                        if bad:
+                            log.warning("fabric on %s: degraded GPU pairs %s", ag.node, bad)
+                        ag.publish_topology()
+                    else:
+                        self._fabric_failures += 1
+                        self.failed.append("fabric")
+                        self._fabric_retry_at = time.time() + self.retry_s * 2 ** min(self._fabric_failures - 1, 6)
+                        fab.due = True
+                        log.warning("fabric probe on %s failed (%d in a row): retry in %.0f s", ag.node,
+                                    self._fabric_failures, self._fabric_retry_at - time.time())
                 return "fabric"
         if self.sets is not None:
             for s in self.sets.pending():
-                ran, res = self._exclusive(f"set {','.join(map(str, s))}", s, lambda s=s: self.sets.probe(s))
-                if not ran:
+                how, res = self._exclusive(f"set {','.join(map(str, s))}", s, lambda s=s: self.sets.probe(s))
+                if how == self.DEFERRED:
                     continue
-                if res is not None:
+                if how == self.RAN:
+                    # a failed probe is recorded too (back-off, then a bad set): it leaves the queue
                     doc = self.sets.record(s, res)
+                    if res is None:
+                        self.failed.append(f"set {','.join(map(str, s))}")
                     if doc is not None and not doc["ok"]:
-                        log.warning("RCCL set check on %s: GPUs %s at %.1f GB/s busbw: degraded", ag.node,
-                                    doc["gpus"], doc["busbw_gbps"])
-                    ag.publish_topology()
+                        log.warning("RCCL set check on %s: GPUs %s at %.1f GB/s busbw%s: degraded", ag.node,
+                                    doc["gpus"], doc["busbw_gbps"], " (probe failed)" if doc.get("failed") else "")
+                    if doc is not None:
+                        ag.publish_topology()
                 return f"set {','.join(map(str, s))}"
         return None
 

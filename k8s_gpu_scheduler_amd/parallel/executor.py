@@ -116,6 +116,7 @@ class DeviceExecutor:
         self._unit_last: Dict[int, Tuple[Tuple[int, int], torch.cuda.Event]] = {}
         self.epoch_runs: List[List[PodRun]] = []
         self._graphs: Dict[Tuple, "torch.cuda.CUDAGraph"] = {}
+        self.lazy_captures = 0           # graphs captured by launch_epoch (not warm()): outside pod timing
         self.flops_done = 0.0
         self.bytes_done = 0.0
         self._slot_work: Dict[Tuple[int, int], float] = {}     # (first unit, units) -> cumulative work
@@ -198,11 +199,24 @@ class DeviceExecutor:
         same CUs -- exactly the ledger's capacity model."""
         if self.balance_slots:
             self._balance(runs)
+        # buffers, streams and (with use_graphs) graphs of every pod are made BEFORE any pod's
+        # start event is recorded: a lazy capture synchronises the device and captures on the
+        # host, and inside a pod's [start, end) it would be measured as that pod's run time --
+        # an outlier the planner's feedback would read as a slow GPU (GPUTEST_r04.json)
+        prep = []
         for r in runs:
-            key = (r.first_unit, r.n_units, r.masked)
             w = CATALOG[r.workload]
             bufs = self.buffers(w, r.first_unit, r.n_units)
             budget = self._budget(r)
+            st = self.stream_for(r.first_unit, r.n_units, r.masked).stream
+            g = None
+            if self.use_graphs:
+                n0 = len(self._graphs)
+                g = self._graph_for(r, bufs, st, budget)
+                self.lazy_captures += len(self._graphs) - n0
+            prep.append((w, bufs, budget, g))
+        for r, (w, bufs, budget, g) in zip(runs, prep):
+            key = (r.first_unit, r.n_units, r.masked)
             r.start = torch.cuda.Event(enable_timing=True)
             r.end = torch.cuda.Event(enable_timing=True)
             st = self.stream_for(*key).stream
@@ -217,8 +231,7 @@ class DeviceExecutor:
                         st.wait_event(last[1])
                     waited.add(id(last[1]))
             r.start.record(st)
-            if self.use_graphs:
-                g = self._graph_for(r, bufs, st, budget)
+            if g is not None:
                 with torch.cuda.stream(st):
                     g.replay()
             else:

@@ -160,6 +160,9 @@ class ControlPlane:
             # the bench corrects the backlog per collected epoch (_plan_feedback); its pods are
             # deleted, never completed, so the deployed completion feedback stays off
             self.plugin.planner.feedback = None
+            # ... and deletes them while they still run on the executor, whose measured
+            # intervals keep the slot timelines (not the deletions)
+            self.plugin.planner.drop_on_delete = False
             if effort:
                 self.plugin.planner.set_effort(effort)     # the starting level (fixed without adaptive)
         self.uuid_to_gpu = {d.device.uuid: d.device.gpu for d in self.ledger.devices(NODE)}
@@ -383,8 +386,9 @@ class ControlPlane:
             planner.realign()
 
     def _plan_feedback(self, pods: np.ndarray) -> None:
-        """Fold each GPU's measured busy time for the collected epoch, minus what the planner
-        predicted for it, into the planner's backlog.  With a timeline the busy time is the
+        """Report each GPU's measured busy time for the collected epoch next to what the planner
+        predicted for it (planner.observe_time: the GPU's measured speed, which scales its
+        future backlog increments).  With a timeline the busy time is the
         union of the epoch's pod intervals past what earlier epochs already covered (the
         launch-ahead pipeline overlaps neighbouring epochs); without one (isolated groups) the
         slowest pod's wall time."""
@@ -408,7 +412,7 @@ class ControlPlane:
             else:
                 busy = max(self.iters / float(r[1]) * 1e3 for r in rec)
             if g in pred:
-                planner.correct((NODE, g), busy - pred[g])
+                planner.observe_time((NODE, g), pred[g], busy)
 
     def _feed_timeline(self, pods: np.ndarray) -> None:
         """Measured pod intervals (executor clock) into the planner's slot timelines: each

@@ -16,8 +16,10 @@ completions:
 
     delta_ms(pod) = measured_ms / median_ratio  -  predicted_ms
 
-and the GPU's co-run group gets `planner.correct(group, sum of its pods' deltas)`.  A uniform
-slowdown of every GPU moves the median, not the backlogs; one slow GPU's pods come out above
+and the GPU's co-run group gets `planner.observe_time(group, predicted, measured / median)`:
+the planner keeps a window median of those ratios per GPU as its measured speed and scales the
+GPU's future backlog increments by it (bounded -- see BurstPlanner.observe_time).  A uniform
+slowdown of every GPU moves the median, not the speeds; one slow GPU's pods come out above
 the median and shift the next plans off it.
 
 Predicted durations are recorded at Reserve (the pod's group on the co-run model, with the
@@ -67,6 +69,12 @@ def measured_ms(pod: Obj) -> Optional[float]:
                 return v
         except ValueError:
             pass
+    span = container_span(pod)
+    return None if span is None else (span[1] - span[0]) * 1e3
+
+
+def container_span(pod: Obj) -> Optional[Tuple[float, float]]:
+    """(earliest startedAt, latest finishedAt) of the pod's terminated containers, epoch s."""
     t0, t1 = None, None
     for cs in (pod.get("status") or {}).get("containerStatuses") or []:
         term = (cs.get("state") or {}).get("terminated") or {}
@@ -77,7 +85,7 @@ def measured_ms(pod: Obj) -> Optional[float]:
         t1 = b if t1 is None else max(t1, b)
     if t0 is None or t1 is None or t1 <= t0:
         return None
-    return (t1 - t0) * 1e3
+    return t0, t1
 
 
 class CompletionFeedback:
@@ -130,12 +138,14 @@ class CompletionFeedback:
             if len(self._ratios) < self.min_n:
                 return True
             med = statistics.median(self._ratios)
-            by: Dict[Hashable, float] = collections.defaultdict(float)
-            for g, p, m in self._held:
-                by[g] += m / med - p
-            self._held = []
+            held, self._held = self._held, []
+        by: Dict[Hashable, float] = collections.defaultdict(float)
+        for g, p, m in held:
+            # the planner bounds what one completion can do (planner.observe_time: clipped
+            # ratios, a window median per GPU, a clipped relative backlog)
+            self.planner.observe_time(g, p, m / med)
+            by[g] += m / med - p
         for g, d in by.items():
-            self.planner.correct(g, d)
             self.corrections[g] += d
         self.applied += len(by)
         return True

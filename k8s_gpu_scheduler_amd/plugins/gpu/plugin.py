@@ -289,7 +289,9 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if O.is_terminal(pod):
             fb = getattr(self.planner, "feedback", None) if self.planner is not None else None
             if fb is not None:
-                fb.completed(pod)       # measured vs predicted time -> its GPU's planned backlog
+                fb.completed(pod)       # measured vs predicted time -> its GPU's measured speed
+            if self.planner is not None:
+                self.planner.released(pod, "terminal")
             self.ledger.release(O.key(pod))
             return
         node = O.node_name_of(pod)
@@ -314,12 +316,14 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
 
     def _on_pod_delete(self, pod: Obj) -> None:
         fb = getattr(self.planner, "feedback", None) if self.planner is not None else None
+        terminal = O.is_terminal(pod)
         if fb is not None:
-            if O.is_terminal(pod):
+            if terminal:
                 fb.completed(pod)
             fb.forget(O.key(pod))
         self.ledger.release(O.key(pod))
         if self.planner is not None:
+            self.planner.released(pod, "terminal" if terminal else "delete")
             self.planner.consume(O.key(pod))
 
     # ------------------------------------------------------------------ request
@@ -616,6 +620,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
             return
         self.ledger.release(O.key(pod))
         if self.planner is not None:
+            self.planner.released(pod, "unreserve")
             self.planner.consume(O.key(pod))
 
     def pre_bind(self, state: CycleState, pod: Obj, node_name: str) -> Optional[Status]:

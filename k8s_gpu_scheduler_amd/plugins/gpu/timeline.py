@@ -86,6 +86,33 @@ class SlotTimeline:
             self.unmatched += 1
             return False
 
+    def drop(self, key: str) -> bool:
+        """Remove a pod that will not run on its slot (unreserved, or deleted before it ran):
+        left in its chain it would be simulated as phantom work forever."""
+        self._ver += 1
+        with self._lock:
+            for slots in self._g.values():
+                for chain in slots.values():
+                    for i, e in enumerate(chain):
+                        if e.key == key:
+                            del chain[i]
+                            return True
+        return False
+
+    def measure_key(self, key: str, start: float, end: float) -> bool:
+        """A pod identified by key ran [start, end) (a cluster's producer: the pod's container
+        startedAt / finishedAt on the wall clock, instead of the executor's per-slot order)."""
+        self._ver += 1
+        with self._lock:
+            for slots in self._g.values():
+                for chain in slots.values():
+                    for e in chain:
+                        if e.key == key:
+                            e.start, e.end = float(start), float(end)
+                            self.measured += 1
+                            return True
+        return False
+
     def realign(self) -> None:
         """Every group drained (e.g. a pipelined job synchronised its GPUs): only each group's
         latest burst -- placed, not run yet -- remains, starting from an idle GPU."""

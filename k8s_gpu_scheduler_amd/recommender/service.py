@@ -405,21 +405,39 @@ class RecommenderService:
         old = self._corun_online
         fm = CorunModel.load(self.corun.path) if self.corun.path else old.base
         ext = fm
-        for name, obs in sorted(self._cold.items()):
+        # arrival order (dicts keep insertion order), never re-sorted: a new workload's row is
+        # appended after every earlier cold-started one
+        for name, obs in self._cold.items():
+            if fm.wid(name) >= 0:
+                continue
             a = float(np.median([x[0] for x in obs]))
             shares = [x[1] for x in obs if x[1] is not None]
             ext = with_workload(ext, name, a, float(np.median(shares)) if shares else None)
         on = OnlineCorun(ext, background=self._corun_refit_mode, **self.corun_online_kw)
-        n_old = len(old.base.names)
+        # carry the learner's state over BY NAME (copying by position shifted an
+        # earlier cold row's refit parameters and observations onto another workload)
+        old_names = list(old.base.names)
+        n_old = len(old_names)
         x = np.asarray(old._x)
-        on._x = np.concatenate([x[:n_old], np.zeros(len(ext.names) - n_old), x[n_old:]])
-        on._obs, on.err, on.version, on.refits, on.time_scale = list(old._obs), dict(old.err), old.version, \
+        new_of_old = [ext.names.index(nm) if nm in ext.names else -1 for nm in old_names]
+        nx = np.zeros(len(ext.names) + (len(x) - n_old))
+        for i, j in enumerate(new_of_old):
+            if j >= 0:
+                nx[j] = x[i]
+        nx[len(ext.names):] = x[n_old:]
+        on._x = nx
+        obs = []
+        for o in old._obs:
+            w = [new_of_old[i] if 0 <= i < n_old else -1 for i in o[0]]
+            if min(w, default=-1) >= 0:
+                obs.append((tuple(w),) + tuple(o[1:]))
+        on._obs, on.err, on.version, on.refits, on.time_scale = obs, dict(old.err), old.version, \
             old.refits, old.time_scale
         n = len(ext.names)
         on.model = CorunModel(ext.names, ext.alone_ms * np.exp(on._x[:n]) * on.time_scale,
                               ext.u * np.exp(on._x[n]), ext.v, dict(ext.meta))
         self._corun_online = on
-        log.info("corun: cold-started %s", sorted(self._cold))
+        log.info("corun: cold-started %s", list(self._cold))
 
     def Version(self, request: Any, context: Any) -> Any:
         return P.VersionReply(configurations=self.conf.version or "", interference=self.intf.version or "",

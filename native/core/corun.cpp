@@ -540,7 +540,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     std::vector<std::vector<int>> mem(NG);
     for (int g = 0; g < NG; ++g)
       for (int64_t r = RO[g]; r < RO[g + 1]; ++r) mem[g].push_back(-1 - (int)r);
-    for (py::ssize_t p = 0; p < P; ++p) mem[DG[dev[p]]].push_back((int)p);
+    std::vector<int> nburst(NG, 0);                  // burst pods per GPU
+    for (py::ssize_t p = 0; p < P; ++p) mem[DG[dev[p]]].push_back((int)p), ++nburst[DG[dev[p]]];
     bool use_pipe = false, phase_b = false;
     auto eval_raw = [&](int g, const std::vector<int>& v) {
       const int k = (int)v.size();
@@ -762,6 +763,10 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         // moves into free capacity on another GPU (the first accepted device per pod)
         for (py::ssize_t p = 0; p < P; ++p) {
           const int d0 = dev[p], g0 = DG[d0];
+          // never empty a GPU of its burst pods while the burst has a pod for every GPU: a GPU
+          // with free units left idle for a whole burst is a starved pipeline (round 4's driver
+          // box put a 4-pod burst on one GPU of two, GPUTEST_r04.json)
+          if (P >= NG && nburst[g0] <= 1) continue;
           cand.clear();
           for (py::ssize_t d = 0; d < D; ++d) {
             const int g1 = DG[d];
@@ -776,6 +781,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
             if (!accept(g0, g1, ge[g0], ge[g1], res[c].ea, res[c].eb)) continue;
             mem[g0].erase(std::find(mem[g0].begin(), mem[g0].end(), (int)p));
             mem[g1].push_back((int)p);
+            --nburst[g0];
+            ++nburst[g1];
             free[d0] += U[p];
             free[d] -= U[p];
             hfree[d0] += H[p];

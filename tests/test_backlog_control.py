@@ -1,0 +1,137 @@
+"""The burst planner's backlog control is a bounded state (plugins.gpu.planner.observe_time):
+measured feedback sets each GPU's relative speed (a window median of measured / predicted
+ratios), speeds scale the carried predicted increments, and the relative backlog is clipped --
+so one outlier is absorbed, a persistently slow GPU converges to a steady smaller share, and
+no GPU with free units ever receives zero pods of a burst because of carried backlog.
+
+This is the CPU counterpart of the hardware direction test
+(tests/test_gpu_native.py::test_planner_feedback_moves_work_off_a_really_slower_gpu, which
+failed on the round-4 driver box with an undamped integrator, GPUTEST_r04.json)."""
+import numpy as np
+import pytest
+
+from k8s_gpu_scheduler_amd import _native
+from k8s_gpu_scheduler_amd.models import workloads as W
+from k8s_gpu_scheduler_amd.parallel import podbench as PB
+
+has_core = _native.core() is not None
+pytestmark = pytest.mark.skipif(not has_core, reason="_core not built")
+
+
+def _run(epochs: int, slow=(1.0, 1.0), outlier=None, seed: int = 5, noise: float = 0.03):
+    """2-GPU control plane (2 pods per GPU per burst: the planner may put 0-4 pods on a GPU),
+    each GPU's group "runs" for its co-run model duration x slow[g] x (1 +- noise); outlier =
+    (epoch, gpu, extra ms) added to one measured busy time.  Returns per-epoch (pods per GPU,
+    GPU 1 work share, backlog spread, plan-visible spread)."""
+    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=2, iters=20, seed=seed, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0)
+    planner = cp.plugin.planner
+    model = cp.corun.base
+    rng = np.random.default_rng(seed)
+    keys = [(PB.NODE, 0), (PB.NODE, 1)]
+    out = []
+    for e in range(epochs):
+        cp.finish_live()
+        arr = cp.schedule_epoch()
+        runs = {g: PB._runs_for(arr, g) for g in (0, 1)}
+        work = {g: sum(model.alone_ms[model.wid(r.workload)] * r.iters for r in runs[g]) for g in (0, 1)}
+        pods = np.full((2, PB.POD_F * PB.MAX_PODS_GPU), -1.0)
+        for g in (0, 1):
+            rs = runs[g]
+            if not rs:
+                continue
+            d = model.group_durations([model.wid(r.workload) for r in rs], [r.iters for r in rs])
+            d = np.asarray(d) * slow[g] * (1.0 + noise * rng.uniform(-1, 1, len(rs)))
+            if outlier is not None and outlier[0] == e and outlier[1] == g:
+                d = d + outlier[2]
+            for i, (r, ms) in enumerate(zip(rs, d)):
+                pods[g, i * PB.POD_F:(i + 1) * PB.POD_F] = [W.INDEX[r.workload], r.iters / (ms / 1e3), -1, -1, -1]
+        cp._plan_feedback(pods)
+        bl = [planner.backlog.get(k, 0.0) for k in keys]
+        base = planner.plan_base(keys)
+        out.append(((len(runs[0]), len(runs[1])), work[1] / max(work[0] + work[1], 1e-9),
+                    max(bl) - min(bl), float(base.max() - base.min())))
+    return out, planner
+
+
+def test_single_outlier_is_absorbed_without_a_zero_pod_burst():
+    base, _ = _run(24)
+    hit, planner = _run(24, outlier=(10, 1, 50.0))
+    assert all(min(n) > 0 for n, _, _, _ in hit), [n for n, *_ in hit]
+    # a +50 ms outlier (~10 bursts of work) on one epoch: the window median ignores it, so
+    # within 3 bursts the plans are back to the undisturbed run's
+    assert [n for n, *_ in hit[14:]] == [n for n, *_ in base[14:]]
+    assert max(s for *_, s in hit) <= planner.SPREAD_CLIP * planner._burst_ms * 1.5 + 1e-6
+
+
+def test_persistent_slowdown_converges_to_a_steady_share():
+    res, planner = _run(200, slow=(1.0, 1.1))
+    assert all(min(n) > 0 for n, _, _, _ in res)
+    share = np.array([s for _, s, _, _ in res])
+    spread = np.array([b for _, _, b, _ in res])
+    # bounded state: the stored relative backlog never exceeds its clip
+    assert spread.max() <= planner.STORE_CLIP * planner._burst_ms * 1.5 + 1e-6, spread.max()
+    # steady: the slow GPU's mean share over the last 100 bursts is below half and the two
+    # 50-burst halves agree (no drift, no divergence)
+    a, b = share[100:150].mean(), share[150:].mean()
+    assert share[100:].mean() < 0.49, share[100:].mean()
+    assert abs(a - b) < 0.03, (a, b)
+    assert planner.rel_speeds([(PB.NODE, 0), (PB.NODE, 1)])[1] > 1.03
+
+
+def test_uniform_slowdown_changes_no_plan():
+    base, _ = _run(30)
+    slow, _ = _run(30, slow=(1.15, 1.15))
+    assert [n for n, *_ in slow] == [n for n, *_ in base]
+
+
+def test_speed_is_a_clipped_window_median():
+    from k8s_gpu_scheduler_amd.plugins.gpu.planner import BurstPlanner
+    p = BurstPlanner.__new__(BurstPlanner)
+    p.carry, p._speed_obs, p.stats = 1.0, {}, {}
+    g = ("n", 0)
+    p.observe_time(g, 10.0, 11.0)
+    p.observe_time(g, 10.0, 500.0)          # outlier, clipped to SPEED_CLIP[1]
+    assert p.speed(g) == 1.0                # fewer than SPEED_MIN_OBS observations
+    p.observe_time(g, 10.0, 11.0)
+    assert p.speed(g) == pytest.approx(1.1)
+    p.observe_time(g, 0.0, 5.0)             # no prediction: ignored
+    assert len(p._speed_obs[g]) == 3
+
+
+def test_released_pods_leave_the_slot_timeline_and_the_feedback():
+    """unreserved / deleted pods were never removed from the slot chains (phantom
+    work forever) and their predicted durations outlived them in the completion feedback."""
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.plugins.gpu.planner import BurstPlanner
+    from k8s_gpu_scheduler_amd.plugins.gpu.timeline import SlotTimeline
+
+    class _FB:
+        def __init__(self):
+            self.forgot = []
+
+        def forget(self, k):
+            self.forgot.append(k)
+    p = BurstPlanner.__new__(BurstPlanner)
+    p.timeline, p.feedback, p.drop_on_delete = SlotTimeline(depth=6, phantoms=2), _FB(), True
+    g = ("n", 0)
+    pods = {n: O.make_pod(n, gpu_cu=64) for n in ("a", "b", "c")}
+    for i, n in enumerate(pods):
+        p.timeline.place(g, (2 * i, 2), O.key(pods[n]), 0, 20.0, 1.0)
+    p.released(pods["a"], "unreserve")
+    p.released(pods["b"], "delete")
+    fin = pods["c"]
+    fin["status"] = {"phase": "Succeeded", "containerStatuses": [{"state": {"terminated": {
+        "startedAt": "2026-01-01T00:00:01Z", "finishedAt": "2026-01-01T00:00:03Z"}}}]}
+    p.released(fin, "terminal")
+    ch = p.timeline.chains(g)
+    keys = [k for c in ch.values() for k, _, _ in c]
+    assert keys == [O.key(fin)]
+    (_, s, e), = [x for c in ch.values() for x in c]
+    assert e - s == pytest.approx(2000.0)                  # measured from its container times (ms)
+    assert p.feedback.forgot == [O.key(pods["a"]), O.key(pods["b"])]
+    # the pipelined bench keeps deleted in-flight pods (its executor measures them)
+    p.drop_on_delete = False
+    p.timeline.place(g, (0, 2), "default/d", 0, 20.0, 1.0)
+    p.released(O.make_pod("d", gpu_cu=64), "delete")
+    assert "default/d" in [k for c in p.timeline.chains(g).values() for k, _, _ in c]

@@ -95,7 +95,11 @@ def test_slow_gpu_sheds_planned_work_uniform_slowdown_changes_nothing():
     assert pl1 == pl0                                      # uniform: the median absorbs it
     assert uni_bl == pytest.approx(base_bl, rel=1e-5, abs=1e-2)     # (timestamps carry microseconds)
     slow_share, slow_bl, fb, _ = _run((1.0, 1.1))
+    pl = fb.planner
     g0, g1 = ("n0", 0), ("n0", 1)
     assert fb.corrections[g1] > fb.corrections[g0]
-    assert slow_share < base_share - 0.01, (slow_share, base_share)
-    assert slow_share < 0.5
+    assert pl.speed(g1) > pl.speed(g0)
+    # the share that levels the MEASURED work is 1 / 2.1 = 0.476 for a GPU 10 % slower: the
+    # planner moves toward it and no further (round 4's unbounded integrator overshot to 0.44;
+    # each GPU is full every burst here, so only long / short swaps can move work)
+    assert 0.46 < slow_share < base_share - 0.005, (slow_share, base_share)

@@ -333,26 +333,26 @@ def test_planner_feedback_moves_work_off_a_slow_gpu(tmp_path):
 def test_plan_feedback_counts_each_gpus_busy_time_once_on_a_pipelined_timeline():
     """The bench's feedback: a GPU's busy time for a collected epoch is the union of its pods'
     intervals past what earlier epochs covered (neighbouring epochs overlap in the pipeline);
-    measured minus predicted goes into that GPU's planner backlog."""
+    (predicted, measured) goes to the planner's per-GPU speed estimate."""
     from k8s_gpu_scheduler_amd.parallel import podbench as PB
     cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=4, iters=20, seed=0, balance=1.0, plan_bursts=True,
                          plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0)
     planner = cp.plugin.planner
+    seen = []
+    planner.observe_time = lambda g, p, m: seen.append((g[1], p, m))
     cp._carry_pred.append({0: 5.0, 1: 5.0})
-    planner.backlog = {(PB.NODE, 0): 0.0, (PB.NODE, 1): 0.0}
     pods = np.full((2, PB.POD_F * PB.MAX_PODS_GPU), -1.0)
     # GPU 0: pods over [0, 4] and [2, 6] -> 6 ms busy; GPU 1: [10, 13] and [20, 22] -> 5 ms
     pods[0, :10] = [0, 100.0, 0.0, 4.0, 0, 1, 100.0, 2.0, 6.0, 2]
     pods[1, :10] = [0, 100.0, 10.0, 13.0, 0, 1, 100.0, 20.0, 22.0, 2]
     cp._plan_feedback(pods)
-    assert planner.backlog[(PB.NODE, 0)] == pytest.approx(1.0)
-    assert planner.backlog[(PB.NODE, 1)] == pytest.approx(0.0)   # 5 busy vs 5 predicted
+    assert seen == [(0, 5.0, pytest.approx(6.0)), (1, 5.0, pytest.approx(5.0))]
     # the next epoch on GPU 0 overlaps the covered [.., 6]: only [6, 9] is new busy time
     cp._carry_pred.append({0: 3.0})
     pods2 = np.full((2, PB.POD_F * PB.MAX_PODS_GPU), -1.0)
     pods2[0, :5] = [2, 100.0, 5.0, 9.0, 4]
     cp._plan_feedback(pods2)
-    assert planner.backlog[(PB.NODE, 0)] == pytest.approx(1.0)
+    assert seen[-1] == (0, 3.0, pytest.approx(3.0))
 
 
 @pytest.mark.skipif(not has_core, reason="_core not built")

@@ -195,3 +195,35 @@ def test_unseen_workload_cold_starts_through_observe_corun_and_plans(tmp_path):
     finally:
         svc.stop()
         srv.stop(0)
+
+
+def test_cold_start_rows_keep_their_state_when_a_later_name_sorts_first(tmp_path):
+    """rebuilding the learner with cold rows in sorted order shifted an earlier cold
+    row's refit parameter and stored observations onto another workload when a later
+    newcomer's name sorted before it.  Rows now append in arrival order and state moves by name."""
+    cm = tmp_path / "corun.json"
+    shutil.copy(DATA, cm)
+    svc = RecommenderService("", "", corun_path=str(cm))
+    svc._corun_refit_mode = False
+    svc.train()
+    srv, port = svc.make_server(0, 2, "127.0.0.1")
+    try:
+        cl = RecommenderClient(f"127.0.0.1:{port}", timeout_s=30.0)
+        cl.observe_corun([{"workloads": ["zz_newcomer_b"], "iters": [20], "ms": [3.0], "start_ms": [0.0],
+                           "target": [True], "mfma_share": [0.9]}])
+        cl.observe_corun([{"workloads": ["zz_newcomer_b", "onnx_mobilenet_1024"], "iters": [20, 20],
+                           "ms": [4.0, 2.5], "start_ms": [0.0, 0.0], "target": [True, True]}])
+        on = svc._corun_online
+        ib = on.base.wid("zz_newcomer_b")
+        on._x[ib] = 0.25                                   # a refit parameter of the cold row
+        cl.observe_corun([{"workloads": ["aa_newcomer_a"], "iters": [20], "ms": [1.0], "start_ms": [0.0],
+                           "target": [True], "mfma_share": [0.1]}])
+        on2 = svc._corun_online
+        ib2, ia2 = on2.base.wid("zz_newcomer_b"), on2.base.wid("aa_newcomer_a")
+        assert ia2 > ib2 >= 0                              # arrival order
+        assert on2._x[ib2] == 0.25 and on2._x[ia2] == 0.0
+        names = [[on2.base.names[w] for w in o[0]] for o in on2._obs]
+        assert ["zz_newcomer_b", "onnx_mobilenet_1024"] in names
+    finally:
+        svc.stop()
+        srv.stop(0)

@@ -432,3 +432,51 @@ def test_background_probes_taint_discard_when_busy_and_publish_bad_sets():
     assert select_gpu_set(topo, [0, 1, 2, 3], 4)[1] == 0.5      # only the bad set left: degraded
     ag.step()
     assert sets.pending() == []                                # checked recently: not again
+
+
+def test_failed_probes_back_off_and_a_failing_set_is_published_bad():
+    """a probe that ran on idle GPUs and produced nothing (child crash, RCCL
+    timeout, no JSON) stayed due, so the worker re-tainted the node and re-ran it every
+    period forever, and a set that hangs RCCL was never marked bad."""
+    from k8s_gpu_scheduler_amd.agent.fabric import FabricProber
+    from k8s_gpu_scheduler_amd.agent.probes import SetChecker
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=8))
+    r = rds()
+    src = synthetic_node(8, node="n1")
+    calls = {"fabric": 0, "set": 0}
+
+    def fabric_probe():
+        calls["fabric"] += 1
+        return None
+
+    def set_probe(gpus):
+        calls["set"] += 1
+        return None
+    now = [1000.0]
+    sets = SetChecker(set_probe, clock=lambda: now[0], retry_s=300.0, max_failures=2)
+    ag = NodeAgent("n1", r, src, client=fc, fabric=FabricProber(fabric_probe), set_checks=sets)
+    w = ag.probes
+    assert w.tick() == "fabric" and calls["fabric"] == 1 and w.failed == ["fabric"]
+    assert not O.node_taints(fc.get("nodes", "n1"))            # untainted after the failed run
+    assert w.tick() is None and calls["fabric"] == 1           # backing off: not re-run at once
+    # a 4-GPU pod ran on GPUs 0-3; its set check fails twice -> published as a bad set
+    uu = [d["uuid"] for d in src.devices()]
+    p = O.make_pod("ring", gpus=4, phase="Succeeded")
+    p["spec"]["nodeName"] = "n1"
+    p["metadata"].setdefault("annotations", {})[C.ANNOT_DEVICES] = ",".join(uu[:4])
+    fc.create("pods", p)
+    ag.step()
+    assert sets.pending() == [(0, 1, 2, 3)]
+    assert w.tick() == "set 0,1,2,3" and calls["set"] == 1 and sets.pending() == []
+    assert w.tick() is None and calls["set"] == 1              # out of the queue
+    ag.step()
+    assert sets.pending() == []                                # re-noted only after the back-off
+    now[0] += 301.0
+    ag.step()
+    assert sets.pending() == [(0, 1, 2, 3)]
+    assert w.tick() == "set 0,1,2,3" and calls["set"] == 2
+    assert sets.bad_sets() == [[0, 1, 2, 3]]
+    topo = json.loads(r.get(schema.topology_key("n1")))
+    assert [0, 1, 2, 3] in topo["bad_sets"]
+    assert not O.node_taints(fc.get("nodes", "n1"))
