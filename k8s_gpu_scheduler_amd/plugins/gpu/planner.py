@@ -415,7 +415,8 @@ class BurstPlanner:
                 np.array(dev_group, np.int32), cap, off, r_wid, r_iters, r_slo,
                 model.alone_ms, model.coupling(), self.sweeps, float(self.tolerance), 0,
                 float(plugin.args.corun_sigma), base, pipe, hbm, cap_hbm,
-                -1 if self.sweeps_b is None else int(self.sweeps_b))
+                -1 if self.sweeps_b is None else int(self.sweeps_b),
+                np.array(self.rel_speeds(gkeys), np.float64) if self._speed_obs else None)
             if self.carry > 0:
                 self._carry(gkeys, per, assign, out, dev_group, model, core, off, r_wid, r_iters, r_slo)
         else:

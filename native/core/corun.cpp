@@ -443,7 +443,7 @@ py::tuple corun_groups_eval(I64 off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alon
 py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 slo, I32 dev_gpu, I32 dev_free,
                                 I64 res_off, I32 r_wid, F64 r_iters, F64 r_slo, F64 alone, F64 cmat, int sweeps,
                                 double tolerance, int mode, double sigma, py::object base_obj, py::object pipe_obj,
-                                py::object hbm_obj, py::object dev_hbm_obj, int sweeps_b) {
+                                py::object hbm_obj, py::object dev_hbm_obj, int sweeps_b, py::object speed_obj) {
   int W;
   check_model(alone, cmat, W);
   const py::ssize_t P = dev_in.shape(0), D = dev_gpu.shape(0), NR = r_wid.shape(0);
@@ -470,6 +470,20 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     for (int g = 0; g < NG; ++g) {
       B[g] = base.data()[g];
       if (!std::isfinite(B[g]) || B[g] < 0) throw std::runtime_error("plan_corun: base must be finite and >= 0");
+    }
+  }
+  // speed[g] (optional): GPU g's measured time / predicted time relative to its siblings
+  // (planner.observe_time).  Its group makespans are scaled by it in both phases, so a burst is
+  // balanced in MEASURED time -- without it a 40 %-slow GPU got balanced (model) work every
+  // burst and only the carried backlog pulled it back, one burst late (shares oscillating
+  // 0.34 / 0.48 / 0.57 on MI355X); the SLO counts stay the model's
+  std::vector<double> S(NG, 1.0);
+  if (!speed_obj.is_none()) {
+    F64 sp = speed_obj.cast<F64>();
+    if (sp.ndim() != 1 || sp.shape(0) != NG) throw std::runtime_error("plan_corun: speed must have n_gpu entries");
+    for (int g = 0; g < NG; ++g) {
+      S[g] = sp.data()[g];
+      if (!std::isfinite(S[g]) || S[g] <= 0) throw std::runtime_error("plan_corun: speed must be finite and > 0");
     }
   }
   // pipeline context (see above)
@@ -556,6 +570,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       }
       // phase A needs makespans only: no soft-SLO terms (erfc / log per member)
       GroupEval e = eval_group(k, w, it, sl, A, Cm, W, nullptr, phase_b ? sigma : 0.0);
+      e.makespan *= S[g];
       if (!use_pipe) return e;
       // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times,
       // then (phantoms) each slot's next pod chained behind its new one
@@ -1178,5 +1193,6 @@ void register_corun(py::module_& m) {
         py::arg("dev_gpu"), py::arg("dev_free"), py::arg("res_off"), py::arg("r_wid"), py::arg("r_iters"),
         py::arg("r_slo"), py::arg("alone_ms"), py::arg("cmat"), py::arg("sweeps") = 8, py::arg("tolerance") = 0.03,
         py::arg("mode") = 0, py::arg("sigma") = 0.0, py::arg("base") = py::none(), py::arg("pipe") = py::none(),
-        py::arg("hbm") = py::none(), py::arg("dev_hbm") = py::none(), py::arg("sweeps_b") = -1);
+        py::arg("hbm") = py::none(), py::arg("dev_hbm") = py::none(), py::arg("sweeps_b") = -1,
+        py::arg("speed") = py::none());
 }

@@ -135,3 +135,16 @@ def test_released_pods_leave_the_slot_timeline_and_the_feedback():
     p.timeline.place(g, (0, 2), "default/d", 0, 20.0, 1.0)
     p.released(O.make_pod("d", gpu_cu=64), "delete")
     assert "default/d" in [k for c in p.timeline.chains(g).values() for k, _, _ in c]
+
+
+def test_direction_arrivals_stay_in_band_with_a_40pct_slower_gpu():
+    """The hardware direction test's arrivals (seed 5) with GPU 1 running 1.4x the model's
+    time: with measured speeds scaling the plan's makespans (native plan_corun `speed`) each
+    burst is balanced in measured time, so GPU 1's share of epochs 6-11 stays within
+    [0.15, 0.5] (target 1 / 2.4 = 0.42) -- without it the carried backlog pulled work back one
+    burst late (0.34 / 0.48 / 0.57 on MI355X)."""
+    res, planner = _run(12, slow=(1.0, 1.4), seed=5)
+    share = np.array([s for _, s, _, _ in res])[6:]
+    assert share.min() >= 0.15 and share.max() <= 0.5, share
+    assert abs(share.mean() - 1 / 2.4) < 0.05, share
+    assert all(min(n) > 0 for n, *_ in res)
