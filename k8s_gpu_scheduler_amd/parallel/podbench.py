@@ -108,7 +108,7 @@ class ControlPlane:
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
                  slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0,
-                 effort_down: Optional[float] = None):
+                 effort_down: Optional[float] = None, learn_corun: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -128,6 +128,7 @@ class ControlPlane:
             base = corun_model or CorunModel.load()
             if base is not None:
                 self.predictions.install_corun(base)
+            if base is not None and learn_corun:
                 # refits run in a worker process (a refit in a thread stalled this control plane
                 # by ~50 ms per 8-GPU epoch through the interpreter lock), about every 8 epochs
                 # (GPUSCHED_CORUN_REFIT=sync: refits inline, so simulated studies and tests do not
@@ -431,13 +432,13 @@ class ControlPlane:
         if planner is None:
             return None
         st = dict(planner.stats)
-        n = max(st.get("slot_plans", 0), 1)
-        if planner.slot_policy in ("model", "auto"):
+        n = st.get("model_slot_plans", 0)
+        if n > 0:       # only when the co-run model's slot plans ran ("auto" at N=1 resolves to lpt)
             for k in ("slot_spread_ms", "slot_min_spread_ms"):
                 st[k] = round(st[k] / n, 3)
-            st["slot_pred_met_pct"] = round(100.0 * st.pop("slot_pred_met") / max(st["slot_pods"], 1), 2)
+            st["slot_pred_met_pct"] = round(100.0 * st.pop("slot_pred_met") / max(st["model_slot_pods"], 1), 2)
         else:
-            for k in ("slot_spread_ms", "slot_min_spread_ms", "slot_pred_met"):
+            for k in ("slot_spread_ms", "slot_min_spread_ms", "slot_pred_met", "model_slot_plans", "model_slot_pods"):
                 st.pop(k, None)
         tl = getattr(planner, "timeline", None)
         if tl is not None:
@@ -684,7 +685,7 @@ def _effective_config(a: Any) -> Dict[str, Any]:
     if planned:
         out["plan_tolerance"] = a.plan_tolerance
         if corun:
-            out.update(corun_sigma=a.corun_sigma, plan_carry=a.plan_carry,
+            out.update(corun_sigma=a.corun_sigma, corun_learn=a.corun_learn, plan_carry=a.plan_carry,
                        plan_feedback=a.plan_feedback if a.plan_carry > 0 else 0, plan_slots=a.plan_slots)
             if a.plan_slots in ("model", "auto"):
                 out.update(slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
@@ -694,7 +695,7 @@ def _effective_config(a: Any) -> Dict[str, Any]:
         else:
             out["plan_objective"] = a.plan_objective
     elif corun:
-        out["corun_sigma"] = a.corun_sigma
+        out.update(corun_sigma=a.corun_sigma, corun_learn=a.corun_learn)
     if not corun:
         out["online_scale"] = a.online_scale          # the pairwise table's online learner
     return out
@@ -760,6 +761,11 @@ def build_parser() -> argparse.ArgumentParser:
                     help="GPU plugin SLO objective: 'corun' = the multi-way co-run model (data/corun_mi355x.json, "
                          "refined online) as a constraint on Score and in the burst planner; 'terms' = the "
                          "reference's pairwise interference terms")
+    ap.add_argument("--corun-learn", type=int, default=0, choices=[0, 1],
+                    help="refine the co-run model online from the pods' measured times (models.corun.OnlineCorun). "
+                         "Off by default: its first refit needs 256 observed pods (a refit on fewer made the model "
+                         "worse on replayed bench timelines), which a 20-step N=1 run (80 pods) never reaches -- "
+                         "the deployed recommender learns through ObserveCorun instead (agent/corun_observer.py)")
     ap.add_argument("--corun-sigma", type=float, default=0.05,
                     help="co-run burst planner: expected SLOs met under the model's log error of this sigma "
                          "(held-out ~0.05, profiles/r03_corun_v2/); 0 = hard predicted counts")
@@ -824,7 +830,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
-    ap.add_argument("--gemm-policy", type=int, default=1, choices=[0, 1, 2],
+    ap.add_argument("--gemm-policy", type=int, default=1, choices=[0, 1, 2, 3, 4],
                     help="GEMM tile policy: 1 (default) 8-phase 256x256 also for co-running pods it fills, 0 128x128 for co-running pods")
     ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],
                     help="GEMM epilogue (A/B knob): 1 LDS-staged 16-B row stores, 0 scattered 8-B stores")
@@ -916,7 +922,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=a.plan_slots,
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
                      adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort,
-                     effort_down=a.cp_effort_down)
+                     effort_down=a.cp_effort_down, learn_corun=bool(a.corun_learn))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -1120,6 +1126,20 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         dist.barrier()
     if use_gpu:
         torch.cuda.synchronize()
+    # GPUSCHED_PROFILE_MARKERS=<file>: a tiny marker kernel (xcd_probe_kernel) right before and
+    # right after the timed region, so a counter profile can keep exactly the timed dispatches
+    # (tools/pmc_bench_summary.py), and the timed pods written to <file> for compulsory bytes
+    marker_path = os.environ.get("GPUSCHED_PROFILE_MARKERS") if use_gpu else None
+    marker = None
+    if marker_path:
+        from .. import _native as _nat
+        _mk_buf = torch.zeros(8, dtype=torch.int32, device=dev)
+
+        def marker() -> None:
+            _nat.hip(required=True).xcd_probe(_mk_buf.data_ptr(), 8, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        marker()
+        n_runs0 = sum(len(r) for r in ex.epoch_runs)
     t_start = time.perf_counter()
     wall0 = time.time()
     if use_gpu:
@@ -1138,6 +1158,11 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    if marker is not None:
+        marker()
+        timed_pods = [(r.workload, r.n_units, r.iters) for ep in ex.epoch_runs for r in ep][n_runs0:]
+        with open(marker_path, "w") as f:
+            json.dump({"pods": timed_pods, "gemm_share": bool(ex.gemm_share)}, f)
     wall1 = time.time()
     if use_gpu and trace is not None:
         fin = torch.cuda.Event(enable_timing=True)
@@ -1223,7 +1248,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "smi": _smi_report(smi_rows, a.smi_period_ms),
             "slo_attainment_pct": round(100.0 * totals["slo_ok"] / max(totals["pods"], 1), 2),
             "sched_ms_per_pod": round(cp.sched_s / max(totals["pods"], 1) * 1e3, 4),
-            "interference_mae": cp.interference_mae(),
+            **({"interference_mae": mae} if (mae := cp.interference_mae()) else {}),
             "planner": cp.planner_stats(),
             "unscheduled": cp.unscheduled,
             "host_ms_per_step_rank0": {k: round(v / a.steps * 1e3, 3) for k, v in host.items()},

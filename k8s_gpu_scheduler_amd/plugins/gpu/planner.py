@@ -128,8 +128,10 @@ class BurstPlanner:
         if carry > 0:
             from .feedback import CompletionFeedback
             self.feedback = CompletionFeedback(self)
-        self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "slot_pred_met": 0,
-                      "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
+        # slot_plans / slot_pods: every slot plan (lpt or model); the model_* fields and the spread
+        # / predicted-met sums only for the co-run model's slot plans (_plan_slots)
+        self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "model_slot_plans": 0, "model_slot_pods": 0,
+                      "slot_pred_met": 0, "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
 
     MAX_EFFORT = 3
 
@@ -572,6 +574,8 @@ class BurstPlanner:
                 res[O.key(p)] = slots[int(s)][0]
             self.stats["slot_plans"] += 1
             self.stats["slot_pods"] += len(items)
+            self.stats["model_slot_plans"] += 1
+            self.stats["model_slot_pods"] += len(items)
             # the new pods predicted to meet their SLO on the chosen slots (hard counts; `exp`
             # also covers the unmeasured context pods the choice re-predicts)
             m0 = len(ctx["wid"])

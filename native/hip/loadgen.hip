@@ -926,7 +926,7 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 2) throw std::runtime_error("gemm policy must be 0..2");
+  if (p < 0 || p > 4) throw std::runtime_error("gemm policy must be 0..4");
   g_gemm_policy = p;
 }
 
@@ -950,6 +950,11 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
   if (alone && fits256) return g_gemm_policy == 2 ? 4 : 10;
   if (!alone && fits256 && g_gemm_policy >= 1) return 10;
+  // 3 / 4 (A/B arms): a co-running GEMM too small for one 256x256 tile per CU of its share
+  // takes 256x128 (8 waves, 2 / 3 LDS stages) when that still gives every CU of the share a
+  // block -- twice the arithmetic intensity per staged byte of 128x128 (85 vs 64 FLOP/B)
+  if (!alone && g_gemm_policy >= 3 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget)
+    return g_gemm_policy == 3 ? 5 : 8;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
