@@ -199,14 +199,17 @@ class ControlPlane:
         # paces the GPUs; when the planner's share of that period runs high it drops to a
         # cheaper effort level (planner.set_effort), and climbs back when there is room
         self.adaptive = adaptive
-        if effort_down is not None:
-            self.EFFORT_DOWN = float(effort_down)
         self._last_start: Optional[float] = None
-        self._periods: "collections.deque[float]" = collections.deque(maxlen=6)
-        self._costs: "collections.deque[float]" = collections.deque(maxlen=6)
-        self._settle = 0
-        self._over = 0
-        self._changed = False
+        # the effort rule itself is the planner's (plugins.gpu.planner.EffortController): here
+        # the time a plan may take is the pipeline period (the interval between schedule requests)
+        self._effort = None
+        planner = getattr(self.plugin, "planner", None)
+        if planner is not None:
+            from ..plugins.gpu.planner import EffortController
+            self._effort = EffortController(planner, down=float(effort_down) if effort_down is not None else self.EFFORT_DOWN,
+                                            up=0.5, target=0.7, settle=3)
+            if os.environ.get("GPUSCHED_EFFORT_DEBUG"):
+                self._effort.debug = lambda msg: print(f"[effort] epoch {self.epoch} {msg}", file=sys.stderr, flush=True)
         self.effort_epochs: Dict[int, int] = {}
         self.live: List[Tuple[str, str]] = []
         self.sched_s = 0.0
@@ -231,71 +234,22 @@ class ControlPlane:
                 pass
         self.live = []
 
-    # effort thresholds: share of the pipeline period the scheduling of one epoch may take (the
-    # control plane runs in its own process, overlapped with the GPUs: it paces them only past
-    # ~100 %; the margin covers the placement broadcast and timing noise)
-    EFFORT_DOWN = 0.85
-    EFFORT_UP = 0.5
-    EFFORT_TARGET = 0.7
-    # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py:
-    # 8.1 / 6.3 / 4.5 / 4.1 ms, profiles/r04_cp2/): a control plane that paces its GPUs jumps
-    # straight to the level predicted to fit, instead of one level per re-measurement (8-rank
-    # box rehearsal, profiles/r04_cp_rehearsal/: stepping spent ~20 of 65 epochs above the level
-    # it settled at)
-    LEVEL_COST = (1.0, 0.78, 0.56, 0.5)
-    EFFORT_SETTLE = 3        # epochs after a level change whose request intervals are not sampled
+    EFFORT_DOWN = 0.85       # share of the pipeline period over which the planner steps down
 
     def _adapt_effort(self, t0: float) -> None:
+        """Adaptive planning effort (GPU runs): the control plane must schedule an epoch within
+        the pipeline's period or it paces the GPUs (EffortController, the allowed time being the
+        interval between consecutive schedule requests; thresholds 85 % down / 50 % up, jump
+        target 70 %, the control plane runs in its own process, overlapped with the GPUs)."""
         planner = getattr(self.plugin, "planner", None)
-        if planner is None:
+        if planner is None or self._effort is None:
             return
-        if self._settle > 0:
-            self._settle -= 1
-        elif self._last_start is not None and self.epoch >= 2:
-            # (the first intervals include the ranks' start-up and pipeline fill; right after a
-            # level change, the requests queued while the GPUs were paced arrive back to back)
-            self._periods.append(t0 - self._last_start)
+        if self._last_start is not None and self.epoch >= 2:
+            # (the first intervals include the ranks' start-up and pipeline fill)
+            self._effort.add_allowed(t0 - self._last_start)
         self._last_start = t0
-        # the first decision (no level change yet) acts on two samples without patience: the
-        # warm-up epochs are few, and a control plane that paces its GPUs from the start would
-        # carry that backlog into the timed region
-        first = not self._changed
-        need = 2 if first else 3
-        if self.adaptive and len(self._periods) >= need and len(self._costs) >= need:
-            # means over the last few epochs (rates: requests can arrive in pairs, so single
-            # intervals alternate short / long and a median of an odd window reads the short one),
-            # with start-up gaps and post-change intervals kept out of the window; a decision rests
-            # on costs measured at the current level only
-            period = float(np.mean(self._periods))
-            cost = float(np.mean(self._costs))
-            cur = planner.effort
-            share = cost / period
-            base = cost / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]
-
-            def fits(level: int, frac: float) -> bool:
-                return base * self.LEVEL_COST[min(level, len(self.LEVEL_COST) - 1)] <= frac * period
-
-            new = cur
-            # two consecutive checks over the threshold before a step down (one noisy window of
-            # a busy host CPU must not cost plan quality for the rest of the run)
-            self._over = self._over + 1 if share > self.EFFORT_DOWN else 0
-            if self._over >= (1 if first else 2) and cur < planner.MAX_EFFORT:
-                # the cheapest-first search from the next level: the first predicted to fit
-                new = next((lv for lv in range(cur + 1, planner.MAX_EFFORT + 1) if fits(lv, self.EFFORT_TARGET)),
-                           planner.MAX_EFFORT)
-            elif share < self.EFFORT_UP and cur > 0 and fits(cur - 1, self.EFFORT_TARGET):
-                new = cur - 1
-            if os.environ.get("GPUSCHED_EFFORT_DEBUG"):
-                print(f"[effort] epoch {self.epoch} level {cur}->{new} share {share:.2f} period "
-                      f"{[round(x * 1e3, 2) for x in self._periods]} cost {[round(x * 1e3, 2) for x in self._costs]}",
-                      file=sys.stderr, flush=True)
-            if new != cur:
-                planner.set_effort(new)
-                self._costs.clear()               # re-measure at the new level (the period too:
-                self._periods.clear()             # the GPUs were paced, or are now)
-                self._settle = self.EFFORT_SETTLE
-                self._over = 0
-                self._changed = True
+        if self.adaptive:
+            self._effort.decide()
         self.effort_epochs[planner.effort] = self.effort_epochs.get(planner.effort, 0) + 1
 
     def schedule_epoch(self) -> np.ndarray:
@@ -338,8 +292,8 @@ class ControlPlane:
         self.epoch += 1
         dt = time.perf_counter() - t0
         self.sched_s += dt
-        if self.epoch > 1:                # the first epoch pays one-time costs (caches, imports)
-            self._costs.append(dt)
+        if self.epoch > 1 and self._effort is not None:   # the first epoch pays one-time costs
+            self._effort.add_cost(dt)
         return arr
 
     def queue_drop(self, dropped: List[Tuple[str, str]]) -> None:

@@ -55,6 +55,84 @@ from .scoring import workload_column
 Obj = Dict[str, Any]
 
 
+class EffortController:
+    """Planning-effort control: keeps the burst planner's cost inside what it may take.
+
+    Each decision compares the mean cost of the last plans at the current level with the mean
+    time they were ALLOWED -- in the bench the interval between schedule requests (the GPUs'
+    pipeline period: a control plane slower than that paces its GPUs), in a cluster the
+    configured per-burst budget (`planBudgetMs`).  Over `down` x the allowed time on `patience`
+    consecutive checks it jumps to the cheapest level predicted to fit `target` x (LEVEL_COST:
+    measured relative cost per level), below `up` x it steps back one level if that level is
+    predicted to fit; right after a change it re-measures (costs at the new level only; the
+    first `settle` allowed-time samples, which still carry the old pace, are not taken).  The
+    first decision acts on two samples without patience: a control plane that paces its GPUs
+    from the start would carry that backlog into a timed region (rehearsed at 8 GPUs on the box
+    CPU: profiles/r04_cp_rehearsal/jump_first/)."""
+
+    # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py:
+    # 8.1 / 6.3 / 4.5 / 4.1 ms, profiles/r04_cp2/)
+    LEVEL_COST = (1.0, 0.78, 0.56, 0.5)
+
+    def __init__(self, planner: "BurstPlanner", down: float = 0.85, up: float = 0.5, target: float = 0.7,
+                 settle: int = 3, window: int = 6):
+        import collections
+        self.planner = planner
+        self.down, self.up, self.target, self.settle_n = down, up, target, settle
+        self._allowed: "collections.deque[float]" = collections.deque(maxlen=window)
+        self._costs: "collections.deque[float]" = collections.deque(maxlen=window)
+        self._settle = 0
+        self._over = 0
+        self._changed = False
+        self.level_samples: Dict[int, int] = {}
+        self.changes = 0
+        self.debug = None            # callable(str) for a decision trace
+
+    def add_cost(self, cost_s: float) -> None:
+        self._costs.append(float(cost_s))
+
+    def add_allowed(self, allowed_s: float) -> None:
+        """One sample of the time a plan may take (skipped while settling after a change)."""
+        if self._settle > 0:
+            self._settle -= 1
+            return
+        self._allowed.append(float(allowed_s))
+
+    def decide(self) -> int:
+        """Act on the windows; returns the (possibly new) level."""
+        pl = self.planner
+        cur = pl.effort
+        first = not self._changed
+        need = 2 if first else 3
+        if len(self._allowed) >= need and len(self._costs) >= need:
+            allowed = float(np.mean(self._allowed))
+            cost = float(np.mean(self._costs))
+            share = cost / max(allowed, 1e-12)
+            base = cost / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]
+
+            def fits(level: int) -> bool:
+                return base * self.LEVEL_COST[min(level, len(self.LEVEL_COST) - 1)] <= self.target * allowed
+            new = cur
+            self._over = self._over + 1 if share > self.down else 0
+            if self._over >= (1 if first else 2) and cur < pl.MAX_EFFORT:
+                new = next((lv for lv in range(cur + 1, pl.MAX_EFFORT + 1) if fits(lv)), pl.MAX_EFFORT)
+            elif share < self.up and cur > 0 and fits(cur - 1):
+                new = cur - 1
+            if self.debug is not None:
+                self.debug(f"level {cur}->{new} share {share:.2f} allowed {[round(x * 1e3, 2) for x in self._allowed]} "
+                           f"cost {[round(x * 1e3, 2) for x in self._costs]}")
+            if new != cur:
+                pl.set_effort(new)
+                self._costs.clear()
+                self._allowed.clear()
+                self._settle = self.settle_n
+                self._over = 0
+                self._changed = True
+                self.changes += 1
+        self.level_samples[pl.effort] = self.level_samples.get(pl.effort, 0) + 1
+        return pl.effort
+
+
 class BurstPlanner:
     # sweeps: improvement passes of the native planners -- 4 and 8 plan alike (8-GPU pipelined
     # simulation, 3 seeds: 64.8 vs 65.3 % SLOs met, same pods/s) at half the control-plane time
@@ -132,8 +210,37 @@ class BurstPlanner:
         # / predicted-met sums only for the co-run model's slot plans (_plan_slots)
         self.stats = {"bursts": 0, "slot_plans": 0, "slot_pods": 0, "model_slot_plans": 0, "model_slot_pods": 0,
                       "slot_pred_met": 0, "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
+        self.budget_ms = 0.0
+        self.budget: Optional[EffortController] = None
+        import time
+        self.clock = time.perf_counter          # plan timing (a test may script it)
 
     MAX_EFFORT = 3
+
+    def set_budget(self, budget_ms: float) -> None:
+        """A deployed scheduler's per-burst planning budget (planBudgetMs; 0 = none): every burst
+        plan's own wall time is measured and the effort level follows EffortController against
+        the budget (over it: down to the level predicted to fit 80 % of it; under half of it:
+        back up)."""
+        self.budget_ms = float(budget_ms)
+        self.budget = EffortController(self, down=1.0, up=0.5, target=0.8, settle=0) if budget_ms > 0 else None
+
+    def _timed_plan(self, fn, *args) -> Any:
+        """Run one burst plan; with a budget, feed its wall time to the effort controller."""
+        n0 = self.stats["bursts"]
+        t0 = self.clock()
+        out = fn(*args)
+        dt = self.clock() - t0
+        if self.stats["bursts"] == n0:
+            return out                   # nothing was planned (no burst): not a plan sample
+        self.stats["plan_ms_last"] = round(dt * 1e3, 3)
+        self.stats["plan_ms_sum"] = self.stats.get("plan_ms_sum", 0.0) + dt * 1e3
+        self.stats["plans_timed"] = self.stats.get("plans_timed", 0) + 1
+        if self.budget is not None:
+            self.budget.add_cost(dt)
+            self.budget.add_allowed(self.budget_ms / 1e3)
+            self.budget.decide()
+        return out
 
     def set_effort(self, level: int) -> None:
         level = max(0, min(self.MAX_EFFORT, int(level)))
@@ -188,7 +295,7 @@ class BurstPlanner:
         core = _native.core()
         model = self.plugin.corun_model()
         if model is not None and core is not None and hasattr(core, "plan_corun"):
-            return self._plan_corun(pod, nodes, model, core)
+            return self._timed_plan(self._plan_corun, pod, nodes, model, core)
         mat = self._matrix()
         if core is None or mat is None or not hasattr(core, "plan_assignment"):
             return None

@@ -141,6 +141,11 @@ class GPUArgs:
     # plugins.gpu.timeline) -- the most expected SLOs met among slot assignments whose slot
     # ends stay within slotSpreadMs of the most even assignment's
     plan_slots: Any = False           # "" / False: off, "lpt", "model" / True (planner.BurstPlanner)
+    # per-burst planning budget (ms; 0 = none): each burst plan's wall time is measured and the
+    # planner's effort level follows it (planner.EffortController: a burst over budget -> the
+    # cheapest level predicted to fit, under half of it -> one level back up); exported as
+    # gpusched_plan_effort_level / gpusched_plan_ms
+    plan_budget_ms: float = 0.0
     slot_spread_ms: float = 2.0
     slot_sigma: float = 0.2
     pack: str = "binpack"             # binpack (MostAllocated) | spread (LeastAllocated) | random
@@ -176,7 +181,7 @@ class GPUArgs:
                  "lptWindowSeconds": "lpt_window_s",
                  "planBursts": "plan_bursts", "planTolerance": "plan_tolerance",
                  "planObjective": "plan_objective", "sloObjective": "slo_objective", "corunMargin": "corun_margin", "corunSigma": "corun_sigma",
-                 "planCarry": "plan_carry", "planSlots": "plan_slots", "slotSpreadMs": "slot_spread_ms", "slotSigma": "slot_sigma",
+                 "planCarry": "plan_carry", "planSlots": "plan_slots", "planBudgetMs": "plan_budget_ms", "slotSpreadMs": "slot_spread_ms", "slotSigma": "slot_sigma",
                  "defaultCU": "default_cu", "compatEnv": "compat_env", "redisPassword": "redis_password",
                  "parityMaster": "parity_master", "parityReconfigure": "parity_reconfigure",
                  "reconfigureTimeoutSeconds": "reconfigure_timeout_s", "parityShuffle": "parity_shuffle",
@@ -230,6 +235,7 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                                         carry=self.args.plan_carry, slots=self.args.plan_slots,
                                         spread_ms=float(self.args.slot_spread_ms),
                                         slot_sigma=float(self.args.slot_sigma))
+            self.planner.set_budget(float(self.args.plan_budget_ms or 0.0))
         self._pred_version: Any = None
         self._lock = threading.RLock()
         self._rng = random.Random(self.args.seed)

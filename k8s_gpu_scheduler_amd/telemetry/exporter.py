@@ -47,6 +47,10 @@ class GpuExporter:
         self.slo = Gauge("gpusched_slo_attainment", "fraction of pods meeting their SLO", registry=self.registry)
         self.ext = Gauge("gpusched_extension_point_mean_us", "mean latency per extension point", ["point"],
                          registry=self.registry)
+        self.plan_level = Gauge("gpusched_plan_effort_level", "burst planner effort level (0 = full)", ["profile"],
+                                registry=self.registry)
+        self.plan_ms = Gauge("gpusched_plan_ms", "wall time of the last burst plan", ["profile"],
+                             registry=self.registry)
         self.ecc = {k: Gauge(f"amd_gpu_ecc_{k}_total", f"accumulated {k} ECC errors", lab, registry=self.registry)
                     for k in ("uncorrectable", "correctable")}
         self.healthy = Gauge("amd_gpu_healthy", "1 if the node agent considers the device healthy", lab,
@@ -105,11 +109,27 @@ class GpuExporter:
         for p, d in (ext or {}).items():
             self.ext.labels(p).set(d.get("mean_us", 0.0))
 
+    def observe_planner(self, profile: str, level: int, plan_ms: Optional[float]) -> None:
+        self.plan_level.labels(profile).set(level)
+        if plan_ms is not None:
+            self.plan_ms.labels(profile).set(plan_ms)
+
     def render(self) -> bytes:
         return generate_latest(self.registry)
 
     def serve(self, port: int = 9400, addr: str = "0.0.0.0") -> None:
         start_http_server(port, addr, registry=self.registry)
+
+
+def observe_planner(exporter: "GpuExporter", profile: str, fw) -> None:
+    """The GPU plugin's burst-planner effort level and last plan time (if it has a planner)."""
+    try:
+        plugin = fw.plugin(C.PLUGIN_NAME)
+    except Exception:
+        return
+    pl = getattr(plugin, "planner", None)
+    if pl is not None:
+        exporter.observe_planner(profile, pl.effort, pl.stats.get("plan_ms_last"))
 
 
 def attach_scheduler_metrics(exporter: "GpuExporter", sched, period_s: float = 5.0):
@@ -132,8 +152,9 @@ def attach_scheduler_metrics(exporter: "GpuExporter", sched, period_s: float = 5
     def loop():
         while not stop.wait(period_s):
             ext = {}
-            for fw in sched.frameworks.values():
+            for name, fw in sched.frameworks.items():
                 ext.update(fw.metrics.summary())
+                observe_planner(exporter, name, fw)
             exporter.observe_scheduler(ext=ext)
     threading.Thread(target=loop, daemon=True, name="sched-metrics").start()
     return stop.set

@@ -66,6 +66,7 @@ def test_scheduler_profile_loads_and_instantiates():
     assert gpu.args.w_balance == 0.5 and gpu.args.model == "MI355X"
     # the deployed burst planner: co-run model, 30 % tolerance, backlog carried between bursts
     assert gpu.args.plan_bursts and gpu.args.plan_tolerance == 0.3 and gpu.args.plan_carry == 1.0
+    assert gpu.args.plan_budget_ms == 20 and gpu.planner.budget is not None
     assert gpu.planner is not None and gpu.planner.carry == 1.0
     dep = _find("Deployment", "gpu-scheduler", "kube-system")
     spec = dep["spec"]["template"]["spec"]
