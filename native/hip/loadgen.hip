@@ -904,8 +904,11 @@ static int g_gemm_tile = 0;
 // steady-state K loop peeled (constant vmcnt, no per-phase stage conditions).
 // (Measured and removed: a 256x256 kernel with 4 waves of 128x128 wave tiles, 3-4 LDS stages --
 // slower than the 8-phase kernel at every catalog shape, profiles/r02_gemm_4wave_study.json.)
-static const int kTileBM[11] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256};
-static const int kTileBN[11] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256};
+// 11 / 12 = 128x128 with 3 / 4 LDS stages (counted vmcnt, glds issued 2 / 3 K-tiles ahead): a
+// co-running pod's small GEMM gets ~1 block per CU of its share, so its 4 waves (one per SIMD)
+// must hide the MALL / HBM latency of the next tiles by depth, not by a second resident block.
+static const int kTileBM[13] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128};
+static const int kTileBN[13] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -926,12 +929,12 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 4) throw std::runtime_error("gemm policy must be 0..4");
+  if (p < 0 || p > 6) throw std::runtime_error("gemm policy must be 0..6");
   g_gemm_policy = p;
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 10) throw std::runtime_error("gemm tile must be 0..10");
+  if (t < 0 || t > 12) throw std::runtime_error("gemm tile must be 0..12");
   g_gemm_tile = t;
 }
 
@@ -955,6 +958,9 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // block -- twice the arithmetic intensity per staged byte of 128x128 (85 vs 64 FLOP/B)
   if (!alone && g_gemm_policy >= 3 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget)
     return g_gemm_policy == 3 ? 5 : 8;
+  // 5 / 6 (A/B arms): the co-running small GEMM's 128x128 tile with 3 / 4 LDS stages
+  if (!alone && g_gemm_policy >= 5 && M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= budget)
+    return g_gemm_policy == 5 ? 11 : 12;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
@@ -1033,6 +1039,8 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 6: launch_gemm<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 7: launch_gemm<64, 128, 2, 2, 2, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 8: launch_gemm<256, 128, 4, 2, 1, 3>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 11: launch_gemm<128, 128, 2, 2, 1, 3, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
+    case 12: launch_gemm<128, 128, 2, 2, 1, 4, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 9:
     case 10: {
       const dim3 grid((M / 256) * (N / 256)), block(512);
