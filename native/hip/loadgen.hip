@@ -455,10 +455,13 @@ gemm_fp8_nt_kernel(const uint8_t* __restrict__ A8, const uint8_t* __restrict__ B
 // group, so on every SIMD (one wave of each group) one wave issues its reads and glds
 // while the other runs MFMAs.
 __device__ __forceinline__ void wait_vmcnt_rt(int n) {
-  // s_waitcnt takes an immediate: n (loads allowed in flight) is 0, 2, 4 or 6
+  // s_waitcnt takes an immediate: n (loads allowed in flight) is 0 .. 6
   if (n >= 6) wait_vmcnt<6>();
-  else if (n >= 4) wait_vmcnt<4>();
-  else if (n >= 2) wait_vmcnt<2>();
+  else if (n == 5) wait_vmcnt<5>();
+  else if (n == 4) wait_vmcnt<4>();
+  else if (n == 3) wait_vmcnt<3>();
+  else if (n == 2) wait_vmcnt<2>();
+  else if (n == 1) wait_vmcnt<1>();
   else wait_vmcnt<0>();
 }
 
@@ -466,36 +469,72 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 // the grid is tiles x S; block (s, tile) multiplies the K slice [s*K, (s+1)*K) (K = the slice
 // length here) and stores its fp32 partial tile to ws[s] (row-major, ld = N) instead of C;
 // splitk_reduce then sums the S partials, adds bias, applies the activation and writes bf16.
-template <bool RELU, bool BIAS, bool PEEL = false, bool WIDE = false, bool SPLIT = false>
+//
+// BN = 128: the same 8-phase schedule on a 256 x 128 block tile (tile 13) for the GEMMs of a
+// co-running pod that are too small to give every CU of its share a 256 x 256 tile (the
+// catalog's M = 1024 layers at a 64-CU share): B half-tiles are 64 rows (one glds per thread
+// instead of two), each wave owns 128 x 32 outputs (one 16-column fragment per B half), and the
+// counted waits follow the unequal half-tile sizes (inflight_8ph).  Half the blocks of the
+// 128 x 128 tile, each staging 85 FLOP per byte instead of 64, with the two staggered wave groups
+// of the 8-phase kernel instead of one lock-step group.
+template <int BN>
+struct Tile8ph {
+  static constexpr int HALF_A = 128 * 64 * 2;          // bytes of an A half-tile image (128 rows x 64 k)
+  static constexpr int HALF_B = (BN / 2) * 64 * 2;     // a B half-tile (BN/2 rows x 64 k)
+  static constexpr int BUF = 2 * HALF_A + 2 * HALF_B;  // one K-tile: A0 A1 B0 B1
+  static constexpr int OA0 = 0, OA1 = HALF_A, OB0 = 2 * HALF_A, OB1 = 2 * HALF_A + HALF_B;
+  static constexpr int NJ = BN / 128;                  // 16-column fragments per wave per B half
+  static constexpr int WCOLS = BN / 8;                 // columns per wave per B half
+  static constexpr int GA = 2, GB = BN / 128;          // glds per thread for an A / B half-tile
+};
+
+// glds (per thread) allowed in flight at the counted wait of global phase p: those of phases
+// p-2 .. p that exist (phase q stages half-tile j = (q + 5) mod 4 -- A0, B0, B1, A1 for j = 0..3
+// -- and nothing after last_stage)
+template <int BN>
+__device__ __forceinline__ int inflight_8ph(int p, int last_stage) {
+  int n = 0;
+#pragma unroll
+  for (int q = p - 2; q <= p; ++q) {
+    if (q > last_stage) continue;
+    const int j = ((q + 5) % 4 + 4) % 4;
+    n += (j == 0 || j == 3) ? Tile8ph<BN>::GA : Tile8ph<BN>::GB;
+  }
+  return n;
+}
+
+template <bool RELU, bool BIAS, bool PEEL = false, bool WIDE = false, bool SPLIT = false, int BN = 256>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                      const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap,
                      float* __restrict__ ws = nullptr) {
-  constexpr int HALF = 128 * 64 * 2;               // bytes of one half-tile image
-  constexpr int BUF = 4 * HALF;                    // one K-tile: A0 A1 B0 B1
-  constexpr int OA0 = 0, OA1 = HALF, OB0 = 2 * HALF, OB1 = 3 * HALF;
+  static_assert(BN == 256 || BN == 128, "8-phase block tile is 256 x 256 or 256 x 128");
+  using TL = Tile8ph<BN>;
+  constexpr int BUF = TL::BUF;
+  constexpr int OA0 = TL::OA0, OA1 = TL::OA1, OB0 = TL::OB0, OB1 = TL::OB1;
+  constexpr int NJ = TL::NJ;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   int nwg = gridDim.x;
   int b = blockIdx.x;
   int split = 0;
   if constexpr (SPLIT) {
-    nwg = (M / 256) * (N / 256);                   // tiles; the S slices of one tile are nwg apart
+    nwg = (M / 256) * (N / BN);                    // tiles; the S slices of one tile are nwg apart
     split = b / nwg;
     b -= split * nwg;
     A += (size_t)split * K;
     Bt += (size_t)split * K;
   }
   int tm, tn;
-  tile_coords(b, nwg, M / 256, N / 256, xmap, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
+  tile_coords(b, nwg, M / 256, N / BN, xmap, tm, tn);
+  const int m0 = tm * 256, n0 = tn * BN;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x & (kWave - 1);
   const int wr = wave >> 2, wc = wave & 3;
   const int frow = lane & 15, fk = lane >> 4;
 
-  f32x4 acc[2][4][2][2];                           // [h][mi][g][nj]
+  f32x4 acc[2][4][2][NJ];                          // [h][mi][g][nj]
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -503,8 +542,8 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[h][i][g][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ar[2][4], b0r[2][2], b1r[2][2];            // [kk][mi], [kk][nj]
+        for (int j = 0; j < NJ; ++j) acc[h][i][g][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ar[2][4], b0r[2][NJ], b1r[2][NJ];          // [kk][mi], [kk][nj]
 
   const int T = K / 64;
   const int last_stage = 4 * T - 6;                // global phase of the last glds
@@ -514,7 +553,7 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     if (j == 0 || j == 3)
       stage_tile<128, 512, 64>(A, lda, m0 + (j == 3 ? 128 : 0), u * 64, dst, wave, lane);
     else
-      stage_tile<128, 512, 64>(Bt, ldb, n0 + (j == 2 ? 128 : 0), u * 64, dst, wave, lane);
+      stage_tile<BN / 2, 512, 64>(Bt, ldb, n0 + (j == 2 ? BN / 2 : 0), u * 64, dst, wave, lane);
   };
   auto read_a = [&](const char* half) {
 #pragma unroll
@@ -522,46 +561,49 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
       for (int i = 0; i < 4; ++i) ar[kk][i] = lds_frag<64>(half, wr * 64 + i * 16 + frow, kk * 4 + fk);
   };
-  auto read_b = [&](const char* half, bf16x8 (&br)[2][2]) {
+  auto read_b = [&](const char* half, bf16x8 (&br)[2][NJ]) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) br[kk][j] = lds_frag<64>(half, wc * 32 + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < NJ; ++j) br[kk][j] = lds_frag<64>(half, wc * TL::WCOLS + j * 16 + frow, kk * 4 + fk);
   };
   auto barrier = [] {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto mfma_quadrant = [&](int h, int g, bf16x8 (&br)[2][2]) {
+  auto mfma_quadrant = [&](int h, int g, bf16x8 (&br)[2][NJ]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[h][i][g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(br[kk][j], ar[kk][i], acc[h][i][g][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  // loads allowed in flight at the wait of global phase p: the glds of phases p-2 .. p
-  // that exist (2 per phase)
-  auto inflight = [&](int p) { return 2 * max(0, min(3, last_stage - p + 3)); };
+  // loads allowed in flight at the wait of global phase p: the glds of phases p-2 .. p that
+  // exist (BN = 256: 2 per phase; BN = 128: 2 for an A half, 1 for a B half)
+  auto inflight = [&](int p) { return inflight_8ph<BN>(p, last_stage); };
+  // steady state: phase 2 of a K-tile waits with B0, B1, A1 in flight; phase 4 with A1, A0, B0
+  constexpr int STEADY2 = 2 * TL::GB + TL::GA;
+  constexpr int STEADY4 = 2 * TL::GA + TL::GB;
 
   // prologue: K-tile 0 and half-tiles A0, B0 of K-tile 1 (phases -5 .. 0)
 #pragma unroll
   for (int j = 0; j < 4; ++j) stage(0, j);
   stage(1, 0);
   stage(1, 1);
-  wait_vmcnt<4>();                                 // K-tile 0 landed; K-tile 1's A0/B0 in flight
+  wait_vmcnt<TL::GA + TL::GB>();                   // K-tile 0 landed; K-tile 1's A0/B0 in flight
   barrier();
   if (wr == 1) barrier();                          // group 1 runs one barrier behind
 
   int t0 = 0;
   if constexpr (PEEL) {
     // Steady state (t <= T-3): every phase stages its half-tile and three half-tiles stay in
-    // flight, so the waits are the constant vmcnt(6) and nothing branches -- the generic
-    // loop below only runs the last two K-tiles, where the pipeline drains.
+    // flight, so the waits are constant counts and nothing branches -- the generic loop below
+    // only runs the last two K-tiles, where the pipeline drains.
     for (; t0 + 2 < T; ++t0) {
       const char* cur = smem + (t0 & 1) * BUF;
       read_b(cur + OB0, b0r);
@@ -573,7 +615,7 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
       barrier();
       read_b(cur + OB1, b1r);
       stage(t0 + 1, 3);
-      wait_vmcnt<6>();
+      wait_vmcnt<STEADY2>();
       barrier();
       mfma_quadrant(0, 1, b1r);
       barrier();
@@ -583,7 +625,7 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
       mfma_quadrant(1, 1, b1r);
       barrier();
       stage(t0 + 2, 1);
-      wait_vmcnt<6>();
+      wait_vmcnt<STEADY4>();
       barrier();
       mfma_quadrant(1, 0, b0r);
       barrier();
@@ -628,8 +670,8 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = n0 + g * 128 + wc * 32 + j * 16 + fk * 4;
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + g * (BN / 2) + wc * TL::WCOLS + j * 16 + fk * 4;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -642,18 +684,19 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   }
 
   if constexpr (WIDE) {
-    // Wide epilogue (wide_put / wide_store): the whole 256x256 bf16 block tile is assembled in
-    // LDS (exactly the 128 KiB the K loop used; every wave is past its last LDS read and every
+    // Wide epilogue (wide_put / wide_store): the whole 256 x BN bf16 block tile is assembled in
+    // LDS (at most the LDS the K loop used; every wave is past its last LDS read and every
     // LDS-DMA has retired -- the drained pipeline's vmcnt(0) -- once the now-aligned wave
-    // groups meet at one more barrier), then whole 512-B rows go out with 16-B stores: 16
-    // coalesced stores per lane instead of 32 scattered 8-B ones (the scattered tail cost
-    // 7-20 % of the kernel at K = 8192 .. 2048).
+    // groups meet at one more barrier), then whole rows go out with 16-B stores: coalesced
+    // stores instead of scattered 8-B ones (the scattered tail cost 7-20 % of the 256 x 256
+    // kernel at K = 8192 .. 2048).
+    static_assert(256 * BN * 2 <= 2 * BUF, "wide epilogue image exceeds the staging LDS");
     barrier();
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = g * 128 + wc * 32 + j * 16 + fk * 4;
+      for (int j = 0; j < NJ; ++j) {
+        const int col = g * (BN / 2) + wc * TL::WCOLS + j * 16 + fk * 4;
         f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
         if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
 #pragma unroll
@@ -664,11 +707,11 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
             bf16x4 o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
-            wide_put<256>(smem, h * 128 + wr * 64 + i * 16 + frow, col, o);
+            wide_put<BN>(smem, h * 128 + wr * 64 + i * 16 + frow, col, o);
           }
       }
     __syncthreads();
-    wide_store<256, 256, 512>(smem, C, ldc, m0, n0);
+    wide_store<256, BN, 512>(smem, C, ldc, m0, n0);
     return;
   }
 
@@ -676,8 +719,8 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
   for (int g = 0; g < 2; ++g)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + g * 128 + wc * 32 + j * 16 + fk * 4;
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + g * (BN / 2) + wc * TL::WCOLS + j * 16 + fk * 4;
       f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
       if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + col);
 #pragma unroll
@@ -852,34 +895,35 @@ static void launch_gemm(const __bf16* A, const __bf16* B, __bf16* Cp, const floa
     launch_gemm_v<BM, BN, WGM, WGN, OCC, STAGES, KT, HOIST, false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
 }
 
-template <bool PEEL, bool WIDE>
+template <bool PEEL, bool WIDE, int BN = 256>
 static void launch_8ph_v(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                          int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block, bool lone) {
   // a lone GEMM (the whole chip) takes the plain GROUP_M order: 0.936 vs 0.913 of hipBLASLt at
   // 4096^3, 0.94 vs 0.916 at 4096x8192x4096, 0.935 vs 0.918 at 8192^2x2048, 0.914 vs 0.92 at 8192^3
   // (7 interleaved rounds, profiles/r04_gemm_xcd/); co-running pods keep the XCD-block order
   // (+2.6 % bench pods/s, profiles/r02_xcd_block_order_ab.txt)
-  const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / 256);
+  const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / BN);
   if (relu && bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, true, PEEL, WIDE, false, BN>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap, nullptr);
   else if (relu)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<true, false, PEEL, WIDE, false, BN>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap, nullptr);
   else if (bp)
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, true, PEEL, WIDE, false, BN>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap, nullptr);
   else
-    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL, WIDE>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
+    hipLaunchKernelGGL((gemm_bf16_nt_256_8ph<false, false, PEEL, WIDE, false, BN>), grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap, nullptr);
 }
 
 // tile 9 = the original 8-phase kernel; 10 = peeled steady-state loop + wide LDS-staged
-// epilogue (when C rows are 16-B aligned, else the 8-B epilogue)
-template <bool PEEL>
+// epilogue (when C rows are 16-B aligned, else the 8-B epilogue); 13 = tile 10's schedule on a
+// 256 x 128 block tile
+template <bool PEEL, int BN = 256>
 static void launch_8ph(const __bf16* A, const __bf16* B, __bf16* Cp, const float* bp, int M, int N, int K, int lda,
                        int ldb, int ldc, bool relu, hipStream_t s, dim3 grid, dim3 block, bool lone) {
   const bool wide = PEEL && wide_ok(Cp, ldc);
   if (wide)
-    launch_8ph_v<PEEL, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
+    launch_8ph_v<PEEL, true, BN>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
   else
-    launch_8ph_v<PEEL, false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
+    launch_8ph_v<PEEL, false, BN>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
 }
 
 // 0 = auto, 1 = 128x128 (4 waves, 2/CU), 2 = 64x128, 3 = 64x64,
@@ -907,8 +951,9 @@ static int g_gemm_tile = 0;
 // 11 / 12 = 128x128 with 3 / 4 LDS stages (counted vmcnt, glds issued 2 / 3 K-tiles ahead): a
 // co-running pod's small GEMM gets ~1 block per CU of its share, so its 4 waves (one per SIMD)
 // must hide the MALL / HBM latency of the next tiles by depth, not by a second resident block.
-static const int kTileBM[13] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128};
-static const int kTileBN[13] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128};
+// 13 = 256x128 8-phase (gemm_bf16_nt_256_8ph<..., BN = 128>, peeled + wide epilogue; K >= 128)
+static const int kTileBM[14] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256};
+static const int kTileBN[14] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -929,12 +974,12 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 6) throw std::runtime_error("gemm policy must be 0..6");
+  if (p < 0 || p > 7) throw std::runtime_error("gemm policy must be 0..7");
   g_gemm_policy = p;
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 12) throw std::runtime_error("gemm tile must be 0..12");
+  if (t < 0 || t > 13) throw std::runtime_error("gemm tile must be 0..13");
   g_gemm_tile = t;
 }
 
@@ -958,6 +1003,9 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // block -- twice the arithmetic intensity per staged byte of 128x128 (85 vs 64 FLOP/B)
   if (!alone && g_gemm_policy >= 3 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget)
     return g_gemm_policy == 3 ? 5 : 8;
+  // 7: the co-running small GEMM on the 256x128 8-phase kernel when that gives every CU of the
+  // share a block
+  if (!alone && g_gemm_policy == 7 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget) return 13;
   // 5 / 6 (A/B arms): the co-running small GEMM's 128x128 tile with 3 / 4 LDS stages
   if (!alone && g_gemm_policy >= 5 && M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= budget)
     return g_gemm_policy == 5 ? 11 : 12;
@@ -1030,6 +1078,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
   }
   int t = pick_gemm_tile(M, N, cu_budget);
   if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
+  if (t == 13 && K < 128) t = 5;
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
   switch (t) {
     case 1: launch_gemm<128, 128, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
@@ -1049,6 +1098,12 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
         launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
       else
         launch_8ph<false>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
+      break;
+    }
+    case 13: {
+      const dim3 grid((M / 256) * (N / 128)), block(512);
+      const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
+      launch_8ph<true, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
       break;
     }
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;

@@ -42,7 +42,7 @@ def test_gemm_matches_fp32_reference(M, N, K, relu, bias):
     assert err <= 0.01 * ref.abs().max().item() + 1e-2, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 11, 12])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 11, 12, 13])
 def test_gemm_every_tile_variant(tile):
     from k8s_gpu_scheduler_amd import _native
     from k8s_gpu_scheduler_amd.ops import loadgen
@@ -60,10 +60,11 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-@pytest.mark.parametrize("tile", [9, 10, 11, 12])
+@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13])
 def test_gemm_256_8phase_numerics_and_race_screen(tile):
     """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled), and the
-    128x128 multi-stage kernels (11, 12: 3 / 4 LDS stages, counted vmcnt): every
+    128x128 multi-stage kernels (11, 12: 3 / 4 LDS stages, counted vmcnt), and the 8-phase
+    schedule on a 256x128 block (13: unequal half-tile glds counts in the waits): every
     K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles

@@ -24,7 +24,7 @@ from k8s_gpu_scheduler_amd.ops.cumask import MaskedStream  # noqa: E402
 from k8s_gpu_scheduler_amd.plugins.gpu.devices import cu_slice_mask  # noqa: E402
 
 PEAK_TF = 2500.0
-TILES = [int(t) for t in os.environ.get("SMALL_GEMM_TILES", "1,11,12,5,10").split(",")]
+TILES = [int(t) for t in os.environ.get("SMALL_GEMM_TILES", "1,13,10").split(",")]
 REPS = 8
 
 
