@@ -16,6 +16,7 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <cstring>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -557,23 +558,101 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     std::vector<int> nburst(NG, 0);                  // burst pods per GPU
     for (py::ssize_t p = 0; p < P; ++p) mem[DG[dev[p]]].push_back((int)p), ++nburst[DG[dev[p]]];
     bool use_pipe = false, phase_b = false;
+    // Simulation memos keyed by a group's WORKLOAD multiset, not by its pod indices: pods of one
+    // workload and length are interchangeable in a simulation and a burst repeats workloads, so
+    // most candidate moves / swaps re-evaluate a multiset that was already simulated (8-GPU bench
+    // epochs: ~2.5k simulations per phase collapse to a few hundred).  A plain group simulation
+    // (every member starts at once) depends on nothing else and is shared by both phases and
+    // every GPU; a pipeline simulation also depends on the GPU (its in-flight context and free
+    // slots) and on which members are residents.  SLO verdicts are evaluated per member on top.
+    auto mix = [](uint64_t h, uint64_t x) {
+      uint64_t z = h + 0x9e3779b97f4a7c15ull + x;
+      z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+      z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+      return z ^ (z >> 31);
+    };
+    auto dbits = [](double d) {
+      uint64_t u;
+      std::memcpy(&u, &d, sizeof u);
+      return u;
+    };
+    struct PlainSim {
+      double makespan;
+      double tput[kMaxK];          // iterations/s per member, in the canonical (w, it) order
+    };
+    std::unordered_map<uint64_t, PlainSim> plain_memo;
+    std::unordered_map<uint64_t, std::array<double, kMaxK>> pipe_memo;
+    std::shared_mutex sim_mu;
+    std::atomic<long> n_plain{0}, n_pipe{0};
+    const bool threaded = std::getenv("GPUSCHED_PLAN_THREADS") && std::atoi(std::getenv("GPUSCHED_PLAN_THREADS")) > 1;
     auto eval_raw = [&](int g, const std::vector<int>& v) {
       const int k = (int)v.size();
       if (k > kMaxK) throw std::runtime_error("plan_corun: GPU group larger than 64 pods");
       int32_t w[kMaxK];
       double it[kMaxK], sl[kMaxK];
+      bool res[kMaxK];
       for (int i = 0; i < k; ++i) {
         const int a = v[i];
         w[i] = a >= 0 ? wid.data()[a] : r_wid.data()[-1 - a];
         it[i] = a >= 0 ? iters.data()[a] : r_iters.data()[-1 - a];
         sl[i] = a >= 0 ? slo.data()[a] : r_slo.data()[-1 - a];
+        res[i] = a < 0;
       }
-      // phase A needs makespans only: no soft-SLO terms (erfc / log per member)
-      GroupEval e = eval_group(k, w, it, sl, A, Cm, W, nullptr, phase_b ? sigma : 0.0);
-      e.makespan *= S[g];
-      if (!use_pipe) return e;
-      // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times,
-      // then (phantoms) each slot's next pod chained behind its new one
+      // plain simulation on the canonical (w, it) order
+      int ord[kMaxK];
+      for (int i = 0; i < k; ++i) ord[i] = i;
+      std::sort(ord, ord + k, [&](int a, int b) { return w[a] != w[b] ? w[a] < w[b] : it[a] < it[b]; });
+      uint64_t hk = mix(0x5bd1e995ull, (uint64_t)k);
+      for (int q = 0; q < k; ++q) hk = mix(mix(hk, (uint64_t)(uint32_t)w[ord[q]]), dbits(it[ord[q]]));
+      PlainSim ps;
+      bool hit = false;
+      {
+        std::shared_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
+        if (threaded) lk.lock();
+        auto f = plain_memo.find(hk);
+        if (f != plain_memo.end()) ps = f->second, hit = true;
+      }
+      if (!hit) {
+        int32_t cw[kMaxK];
+        double cit[kMaxK], fin[kMaxK];
+        for (int q = 0; q < k; ++q) cw[q] = w[ord[q]], cit[q] = it[ord[q]];
+        sim_group(k, cw, cit, nullptr, A, Cm, W, fin);
+        ps.makespan = 0.0;
+        for (int q = 0; q < k; ++q) {
+          if (cit[q] <= 0) {
+            ps.tput[q] = 1e3 / std::max(steady_ms(k, q, cw, A, Cm, W), 1e-12);
+          } else {
+            ps.tput[q] = cit[q] / std::max(fin[q], 1e-12) * 1e3;
+            ps.makespan = std::max(ps.makespan, fin[q]);
+          }
+        }
+        n_plain.fetch_add(1, std::memory_order_relaxed);
+        std::unique_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
+        if (threaded) lk.lock();
+        plain_memo.emplace(hk, ps);
+      }
+      GroupEval e;
+      e.makespan = ps.makespan * S[g];
+      const double sg = phase_b ? sigma : 0.0;      // phase A needs makespans only
+      auto verdicts = [&](const double* tput, const int* perm) {
+        e.ok = e.bad = 0;
+        e.deficit = e.expected = 0.0;
+        for (int q = 0; q < k; ++q) {
+          const int i = perm[q];
+          e.expected += p_meet(tput[q], sl[i], sg);
+          if (sl[i] <= 0 || tput[q] >= sl[i]) ++e.ok;
+          else ++e.bad, e.deficit += 1.0 - tput[q] / sl[i];
+        }
+      };
+      if (!use_pipe) {
+        verdicts(ps.tput, ord);
+        return e;
+      }
+      // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times
+      // (longest first onto the earliest free slot; residents already run), then (phantoms)
+      // each slot's next pod chained behind its new one.  Canonical order: residents first, then
+      // new pods longest first (ties by workload and length), so the result is a function of
+      // the multiset
       const int64_t c0 = p_coff.data()[g], c1 = p_coff.data()[g + 1];
       const int64_t f0 = p_foff.data()[g], f1 = p_foff.data()[g + 1];
       const int nc = (int)(c1 - c0);
@@ -581,80 +660,101 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       if (phantoms)
         for (int64_t q = f0; q < f1; ++q) nh += p_hwid.data()[q] >= 0;
       if (nc + k + nh > kMaxK) nh = 0;
-      if (nc + k > kMaxK) return e;
-      int32_t pw[kMaxK], pv[kMaxK];
-      double pit[kMaxK], pst[kMaxK], pen[kMaxK], pfin[kMaxK], pso[kMaxK];
-      for (int c = 0; c < nc; ++c) {
-        pw[c] = p_cwid.data()[c0 + c];
-        pit[c] = 1.0;
-        pst[c] = p_cst.data()[c0 + c];
-        pen[c] = p_cend.data()[c0 + c];
-        pv[c] = -1;
+      if (nc + k > kMaxK) {
+        verdicts(ps.tput, ord);
+        return e;
       }
-      // new pods longest first onto the earliest free slot; residents already run (first time)
-      int order[kMaxK];
-      for (int i = 0; i < k; ++i) order[i] = i;
-      std::sort(order, order + k, [&](int a, int b) { return A[w[a]] * it[a] > A[w[b]] * it[b]; });
-      const double t0 = f1 > f0 ? p_ft.data()[f0] : 0.0;
-      int slot_pod[kMaxK];                       // free slot q -> member index of its new pod
-      for (int64_t q = 0; q < f1 - f0 && q < kMaxK; ++q) slot_pod[q] = -1;
-      int nf = 0;
-      for (int q = 0; q < k; ++q) {
-        const int i = order[q];
-        pw[nc + i] = w[i];
-        pit[nc + i] = it[i];
-        pen[nc + i] = 0.0;
-        pv[nc + i] = -1;
-        if (v[i] < 0) {
-          pst[nc + i] = t0;
-        } else {
-          const int64_t fi = std::min<int64_t>(f0 + nf, f1 - 1);
-          pst[nc + i] = f1 > f0 ? p_ft.data()[fi] : 0.0;
-          if (f1 > f0 && nf < f1 - f0 && fi - f0 < kMaxK) slot_pod[fi - f0] = nc + i;
-          ++nf;
+      int po[kMaxK];
+      for (int i = 0; i < k; ++i) po[i] = i;
+      std::sort(po, po + k, [&](int a, int b) {
+        if (res[a] != res[b]) return res[a];
+        const double wa = A[w[a]] * it[a], wb = A[w[b]] * it[b];
+        if (wa != wb) return wa > wb;
+        return w[a] != w[b] ? w[a] < w[b] : it[a] < it[b];
+      });
+      uint64_t hp = mix(mix(0x27d4eb2fULL, (uint64_t)g), (uint64_t)k);
+      for (int q = 0; q < k; ++q)
+        hp = mix(mix(mix(hp, (uint64_t)res[po[q]]), (uint64_t)(uint32_t)w[po[q]]), dbits(it[po[q]]));
+      std::array<double, kMaxK> pt;
+      bool phit = false;
+      {
+        std::shared_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
+        if (threaded) lk.lock();
+        auto f = pipe_memo.find(hp);
+        if (f != pipe_memo.end()) pt = f->second, phit = true;
+      }
+      if (!phit) {
+        int32_t pw[kMaxK], pv[kMaxK];
+        double pit[kMaxK], pst[kMaxK], pen[kMaxK], pfin[kMaxK], pso[kMaxK];
+        for (int c = 0; c < nc; ++c) {
+          pw[c] = p_cwid.data()[c0 + c];
+          pit[c] = 1.0;
+          pst[c] = p_cst.data()[c0 + c];
+          pen[c] = p_cend.data()[c0 + c];
+          pv[c] = -1;
         }
-      }
-      int m = nc + k;
-      if (nh > 0)
-        for (int64_t q = 0; q < f1 - f0 && q < kMaxK; ++q) {
-          const int32_t hw = p_hwid.data()[f0 + q];
-          if (hw < 0) continue;
-          pw[m] = hw;
-          pit[m] = p_hit.data()[f0 + q];
-          pen[m] = 0.0;
-          if (slot_pod[q] >= 0) {
-            pv[m] = slot_pod[q];
-            pst[m] = -kBig;
+        const double t0 = f1 > f0 ? p_ft.data()[f0] : 0.0;
+        int slot_pod[kMaxK];                       // free slot q -> simulation index of its new pod
+        for (int64_t q = 0; q < f1 - f0 && q < kMaxK; ++q) slot_pod[q] = -1;
+        int nf = 0;
+        for (int q = 0; q < k; ++q) {
+          const int i = po[q];
+          pw[nc + q] = w[i];
+          pit[nc + q] = it[i];
+          pen[nc + q] = 0.0;
+          pv[nc + q] = -1;
+          if (res[i]) {
+            pst[nc + q] = t0;
           } else {
-            pv[m] = -1;
-            pst[m] = p_ft.data()[f0 + q];
+            const int64_t fi = std::min<int64_t>(f0 + nf, f1 - 1);
+            pst[nc + q] = f1 > f0 ? p_ft.data()[fi] : 0.0;
+            if (f1 > f0 && nf < f1 - f0 && fi - f0 < kMaxK) slot_pod[fi - f0] = nc + q;
+            ++nf;
           }
-          ++m;
         }
-      // the simulation clock starts at 0: shift the window (chained members keep -inf)
-      double lo = kBig;
-      for (int i = 0; i < m; ++i)
-        if (pv[i] < 0) lo = std::min(lo, pst[i]);
-      for (int i = 0; i < m; ++i) {
-        if (pv[i] < 0) pst[i] -= lo;
-        if (i < nc) pen[i] -= lo;
+        int m = nc + k;
+        if (nh > 0)
+          for (int64_t q = 0; q < f1 - f0 && q < kMaxK; ++q) {
+            const int32_t hw = p_hwid.data()[f0 + q];
+            if (hw < 0) continue;
+            pw[m] = hw;
+            pit[m] = p_hit.data()[f0 + q];
+            pen[m] = 0.0;
+            if (slot_pod[q] >= 0) {
+              pv[m] = slot_pod[q];
+              pst[m] = -kBig;
+            } else {
+              pv[m] = -1;
+              pst[m] = p_ft.data()[f0 + q];
+            }
+            ++m;
+          }
+        // the simulation clock starts at 0: shift the window (chained members keep -inf)
+        double lo = kBig;
+        for (int i = 0; i < m; ++i)
+          if (pv[i] < 0) lo = std::min(lo, pst[i]);
+        for (int i = 0; i < m; ++i) {
+          if (pv[i] < 0) pst[i] -= lo;
+          if (i < nc) pen[i] -= lo;
+        }
+        if (nh > 0) {
+          sim_chain(m, pw, pit, pst, pv, A, Cm, W, pso, pfin, pen);
+        } else {
+          sim_group(m, pw, pit, pst, A, Cm, W, pfin, pen);
+          for (int i = 0; i < m; ++i) pso[i] = pst[i];
+        }
+        int32_t cw[kMaxK];
+        for (int q = 0; q < k; ++q) cw[q] = w[po[q]];
+        for (int q = 0; q < k; ++q) {
+          if (pit[nc + q] <= 0) pt[q] = 1e3 / std::max(steady_ms(k, q, cw, A, Cm, W), 1e-12);
+          else pt[q] = pit[nc + q] / std::max(pfin[nc + q] - pso[nc + q], 1e-12) * 1e3;
+        }
+        n_pipe.fetch_add(1, std::memory_order_relaxed);
+        std::unique_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
+        if (threaded) lk.lock();
+        pipe_memo.emplace(hp, pt);
       }
-      if (nh > 0) {
-        sim_chain(m, pw, pit, pst, pv, A, Cm, W, pso, pfin, pen);
-      } else {
-        sim_group(m, pw, pit, pst, A, Cm, W, pfin, pen);
-        for (int i = 0; i < m; ++i) pso[i] = pst[i];
-      }
-      e.ok = e.bad = 0;
-      e.deficit = e.expected = 0.0;
-      for (int i = 0; i < k; ++i) {
-        double tput;
-        if (it[i] <= 0) tput = 1e3 / std::max(steady_ms(k, i, w, A, Cm, W), 1e-12);
-        else tput = it[i] / std::max(pfin[nc + i] - pso[nc + i], 1e-12) * 1e3;
-        e.expected += p_meet(tput, sl[i], sigma);
-        if (sl[i] <= 0 || tput >= sl[i]) ++e.ok;
-        else ++e.bad, e.deficit += 1.0 - tput / sl[i];
-      }
+      verdicts(pt.data(), po);
       return e;
     };
     // memo of group evaluations per phase and thread: a sweep re-evaluates mostly the same
@@ -850,8 +950,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       }
       if (std::getenv("GPUSCHED_PLAN_DEBUG")) {
         const size_t sims = memo[phase_b ? 1 : 0].size();
-        std::fprintf(stderr, "[plan_corun] phase %d evals %ld simulated %zu threads %d\n", phase_b ? 1 : 0,
-                     n_evals.load(), sims, T);
+        std::fprintf(stderr, "[plan_corun] phase %d evals %ld sets %zu plain sims %ld pipe sims %ld threads %d\n",
+                     phase_b ? 1 : 0, n_evals.load(), sims, n_plain.load(), n_pipe.load(), T);
       }
     };
     auto max_mk = [&](bool eff) {

@@ -231,13 +231,14 @@ def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
                          plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
                          plan_slots="auto", adaptive=True)
     pl = cp.plugin.planner
+    ctl = cp._effort                          # the planner's EffortController, fed with periods
     cp.epoch = 10
     t = [0.0]
 
     def step(period_ms, cost_ms):
         t[0] += period_ms / 1e3
         cp._adapt_effort(t[0])
-        cp._costs.append(cost_ms / 1e3)
+        ctl.add_cost(cost_ms / 1e3)
 
     levels = []
     for _ in range(8):
@@ -248,10 +249,10 @@ def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
     # the first decision: as soon as two samples are in, one jump (later ones wait for three
     # samples and two over-threshold checks)
     assert levels[:2] == [0, 0] and levels[-1] == 2 and 1 not in levels
-    assert not cp._periods and cp._settle == cp.EFFORT_SETTLE
-    for _ in range(cp.EFFORT_SETTLE):
+    assert not ctl._allowed and ctl._settle == ctl.settle_n == 3
+    for _ in range(ctl.settle_n):
         step(2, 5.6)                          # queued requests arrive back to back: not sampled
-    assert not cp._periods and pl.effort == 2
+    assert not ctl._allowed and pl.effort == 2
     for _ in range(6):
         step(10, 5.6)                         # 56 % of the period: stays
     assert pl.effort == 2

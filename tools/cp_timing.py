@@ -41,8 +41,16 @@ CONFIGS = [("plain", {}), ("bench-defaults", BENCH)]
 # the adaptive control plane's cheaper levels (planner.set_effort; bench --plan-effort)
 CONFIGS += [(f"bench-effort{k}", dict(BENCH, effort=k)) for k in (1, 2, 3)]
 only = os.environ.get("CP_TIMING_GPUS")
-for name, kw in CONFIGS:
-    for n in ((int(only),) if only else (1, 2, 4, 8)):
-        dt = run(n, kw)
-        print(f"{name} gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}",
-              flush=True)
+pick = os.environ.get("CP_TIMING_CONFIGS")          # comma-separated config names (default: all)
+rounds = int(os.environ.get("CP_TIMING_ROUNDS", "1"))  # interleaved rounds: the median is printed
+if pick:
+    CONFIGS = [c for c in CONFIGS if c[0] in pick.split(",")]
+res = {}
+for r in range(rounds):
+    for name, kw in CONFIGS:
+        for n in ((int(only),) if only else (1, 2, 4, 8)):
+            res.setdefault((name, n), []).append(run(n, kw))
+for (name, n), v in res.items():
+    dt = float(np.median(v))
+    print(f"{name} gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}"
+          + (f" rounds={[round(x * 1e3, 2) for x in v]}" if rounds > 1 else ""), flush=True)
