@@ -8,6 +8,8 @@ reverse order, Permit, PreBind, the first non-Skip Bind plugin, PostBind.
 """
 from __future__ import annotations
 
+from ..api import constants as C
+
 import logging
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -78,6 +80,18 @@ class Framework:
             self.points[point] = lst
         self._pool: Optional[ThreadPoolExecutor] = None
         self.score_in_parallel = any(getattr(p, "SCORE_DOES_IO", False) for p in self.points["score"])
+        # plan hints: a score plugin that may already have decided a pod's node (the GPU plugin's
+        # burst plan, `planned_node`) short-cuts the cycle -- Filter on that node only, no Score --
+        # but only when its weight makes one point of its score outweigh every other score
+        # plugin's whole range, i.e. when Score could not pick another feasible node anyway
+        # (the deployed profile: GPU 10100 vs the in-tree plugins' 1-2 each x 100)
+        self._hinters: List[Any] = []
+        for p in self.points["score"]:
+            if not hasattr(p, "planned_node"):
+                continue
+            others = sum(self.weights.get(q.name(), 1) for q in self.points["score"] if q is not p)
+            if self.weights.get(p.name(), 1) > others * C.MAX_NODE_SCORE:
+                self._hinters.append(p)
 
     @property
     def scheduler_name(self) -> str:
@@ -97,6 +111,14 @@ class Framework:
             return fn()
         finally:
             self.metrics.add(point, time.perf_counter_ns() - t0)
+
+    def plan_hint(self, state: CycleState, pod: Obj) -> Optional[str]:
+        """The node a dominant score plugin has already planned for `pod` (None: none)."""
+        for p in self._hinters:
+            n = p.planned_node(state, pod)
+            if n:
+                return n
+        return None
 
     # ---------------------------------------------------------------- queue sort
     def queue_sort_less(self) -> Optional[Callable[[Any, Any], bool]]:

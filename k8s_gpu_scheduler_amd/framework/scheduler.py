@@ -159,6 +159,8 @@ class Scheduler:
         self.extenders = [HTTPExtender(c) for c in getattr(config, "extenders", None) or []]
         self.fast_path = not self.extenders     # the node-result cache cannot see extender verdicts
         self.fast_min_nodes = 16      # below this the per-cycle signature work costs more than it saves
+        self.plan_hints = True        # planned pods skip Score (Framework.plan_hint)
+        self.plan_hint_hits = 0
         self._fast: Dict[str, NodeResultCache] = {}
         for name, fw in self.frameworks.items():
             for inst in fw._instances.values():
@@ -271,6 +273,21 @@ class Scheduler:
         st = fw.run_pre_filter(state, pod)
         if not st.ok:
             return self._fail(pi, fw, state, res, st, t0)
+        # a planned pod (framework.plan_hint: the GPU plugin's burst plan, whose weight decides
+        # Score): Filter on the planned node only and no Score; a stale plan (node gone or no
+        # longer feasible) falls through to the full cycle
+        hint = fw.plan_hint(state, pod) if (self.plan_hints and not self.extenders) else None
+        if hint is not None:
+            ni = self._snapshot.get(hint)
+            if ni is not None:
+                feasible, _ = fw.find_feasible(state, pod, [ni], 0)
+                if feasible:
+                    st = fw.run_pre_score(state, pod, feasible)
+                    if not st.ok:
+                        return self._fail(pi, fw, state, res, st, t0)
+                    res.evaluated, res.feasible = 1, 1
+                    self.plan_hint_hits += 1
+                    return self._assume_and_bind(fw, state, pi, pod, hint, res, t0)
         limit = self.num_feasible_nodes_to_find(len(nodes))
         sampled = limit < len(nodes)
         got = fast.schedule(state, pod, self._snapshot, self._next_start % len(nodes) if sampled else 0,

@@ -801,7 +801,10 @@ class BurstPlanner:
         its measured relative speed, is added to its backlog; backlogs decay by `carry` per
         burst, are kept relative to the least loaded group (only differences steer the plan)
         and clipped (anti-windup, above)."""
-        _, mk0 = core.corun_groups_eval(off, r_wid, r_iters, r_slo, model.alone_ms, model.coupling())
+        if len(r_wid):
+            _, mk0 = core.corun_groups_eval(off, r_wid, r_iters, r_slo, model.alone_ms, model.coupling())
+        else:                               # no residents anywhere (e.g. every GPU drained)
+            mk0 = np.zeros(len(gkeys))
         groups = [list(m) for m in per]
         for (p, r, _), d in zip(assign, out):
             groups[dev_group[int(d)]].append((model.wid(O.name(p)), r.iters, r.slo))

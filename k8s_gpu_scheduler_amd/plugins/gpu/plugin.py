@@ -465,6 +465,14 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
                        Status.unschedulable("insufficient free GPU units/HBM or no xGMI clique", self.NAME))
         return out
 
+    def planned_node(self, state: CycleState, pod: Obj) -> Optional[str]:
+        """The node of this pod's burst plan, if one was made (the framework then filters only
+        that node and skips Score: with this plugin's weight the plan decides anyway)."""
+        if self.planner is None or self.parity is not None:
+            return None
+        hit = self.planner.plans.get(O.key(pod))
+        return hit[0] if hit is not None else None
+
     def pre_score(self, state: CycleState, pod: Obj, nodes: List[Any]) -> Optional[Status]:
         if self.parity is not None:
             return None
@@ -604,6 +612,10 @@ class GPUPlugin(QueueSortPlugin, PreFilterPlugin, FilterPlugin, PreScorePlugin, 
         if req is None or not req.gpu_pod:
             return None
         choice = (state.read(_CHOICE) or {}).get(node_name)
+        if choice is None:
+            plan = state.read(_PLAN)
+            if plan is not None:            # a planned pod that skipped Score (planned_node)
+                choice = self._planned_choice(state, req, node_name, plan)
         if choice is None:
             choice = self._best_choice(state, pod, req, node_name, scoring=True)
         if choice is not None:

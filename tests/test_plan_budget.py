@@ -81,3 +81,51 @@ def test_burst_over_budget_drops_effort_and_recovers_with_the_level_exported():
     assert levels[-1] == 0, levels
     assert pl.budget.changes >= 2 and pl.stats["plans_timed"] == 16
     assert f'gpusched_plan_effort_level{{profile="{C.SCHEDULER_NAME}"}} 0.0' in exp.render().decode()
+
+
+def _place_bursts(plan_hints: bool, disable_defaults: bool):
+    fc = FakeCluster()
+    for n in ("n0", "n1", "n2"):
+        fc.create("nodes", O.make_node(n, gpus=8))
+    args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.0, "w_balance": 1.0, "slo_objective": "corun",
+            "plan_bursts": True, "plan_tolerance": 0.3, "plan_carry": 1.0}
+    s = Scheduler(fc, default_gpu_config(args, disable_defaults=disable_defaults), full_registry(),
+                  bind_async=False, seed=0,
+                  extras={"ledger": DeviceLedger(), "telemetry": TelemetryCache(stale_s=0),
+                          "predictions": CachedPredictions(corun=CorunModel.load())})
+    s.plan_hints = plan_hints
+    s.start_informers()
+    rng = np.random.default_rng(3)
+    out = []
+    for b in range(4):
+        names = []
+        for i in range(24):
+            wl = W.NAMES[int(rng.integers(len(W.NAMES)))]
+            nm = f"{wl.replace('_', '-')}-b{b}-{i}"
+            fc.create("pods", O.make_pod(nm, gpu_cu=64, env={C.ENV_ITERATIONS: "20"}))
+            names.append(nm)
+        assert all(r.node for r in s.schedule_pending())
+        for nm in names:
+            p = fc.get("pods", nm, "default")
+            out.append((nm, O.node_name_of(p), O.annotations(p)[C.ANNOT_DEVICE_INDICES]))
+        if b % 2:                      # half the bursts finish: residents for the next plans
+            for nm in names:
+                fc.delete("pods", nm, "default")
+    return out, s.plan_hint_hits
+
+
+@pytest.mark.parametrize("disable_defaults", [True, False])
+def test_planned_pods_skip_score_with_identical_placements(disable_defaults):
+    """Framework.plan_hint: a pod the GPU plugin's burst plan has already placed is filtered on
+    its planned node only and skips Score when the GPU weight (10100) decides Score anyway -- the
+    placements, node AND CU slot, are exactly those of the full cycle.  With the in-tree score
+    plugins enabled beside it the hint stays off: NodePreferAvoidPods (weight 10000) can outvote
+    one GPU point, so Score must run."""
+    fast, hits = _place_bursts(True, disable_defaults)
+    full, hits0 = _place_bursts(False, disable_defaults)
+    assert hits0 == 0
+    if disable_defaults:
+        assert hits >= 4 * 23 - 4                   # every pod after the first of each burst
+    else:
+        assert hits == 0
+    assert fast == full
