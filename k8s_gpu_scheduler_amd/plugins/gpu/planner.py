@@ -55,6 +55,13 @@ from .scoring import workload_column
 Obj = Dict[str, Any]
 
 
+def _median(xs) -> float:
+    """Median of a short sequence (np.median costs ~100 us a call: 8 groups per burst)."""
+    v = sorted(xs)
+    n = len(v)
+    return float(v[n // 2]) if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
+
+
 class EffortController:
     """Planning-effort control: keeps the burst planner's cost inside what it may take.
 
@@ -105,8 +112,8 @@ class EffortController:
         first = not self._changed
         need = 2 if first else 3
         if len(self._allowed) >= need and len(self._costs) >= need:
-            allowed = float(np.mean(self._allowed))
-            cost = float(np.mean(self._costs))
+            allowed = sum(self._allowed) / len(self._allowed)
+            cost = sum(self._costs) / len(self._costs)
             share = cost / max(allowed, 1e-12)
             base = cost / self.LEVEL_COST[min(cur, len(self.LEVEL_COST) - 1)]
 
@@ -198,7 +205,9 @@ class BurstPlanner:
         if self.timeline is not None:
             import os
             from concurrent.futures import ThreadPoolExecutor
-            n = max(1, min(4, int(os.environ.get("GPUSCHED_PLAN_THREADS", "4"))))
+            # the GPUs' slot plans run side by side (native, without the interpreter lock):
+            # one thread per GPU of an 8-GPU node where the host has the cores
+            n = max(1, min(8, int(os.environ.get("GPUSCHED_SLOT_THREADS", str(min(8, os.cpu_count() or 1))))))
             self._pool = ThreadPoolExecutor(n, thread_name_prefix="slot-plan") if n > 1 else None
         # measured backlog feedback from pod completions (plugins.gpu.feedback; deployed
         # clusters -- the bench corrects per collected epoch instead)
@@ -774,13 +783,13 @@ class BurstPlanner:
         q = self._speed_obs.get(group)
         if not q or len(q) < self.SPEED_MIN_OBS:
             return 1.0
-        return float(np.median(q))
+        return _median(q)
 
     def rel_speeds(self, gkeys: List[Tuple]) -> List[float]:
         """Each group's speed over the median group's (a uniform slowdown changes nothing),
         1.0 inside the dead band."""
         s = [self.speed(k) for k in gkeys]
-        med = float(np.median(s)) if s else 1.0
+        med = _median(s) if s else 1.0
         out = []
         for x in s:
             r = x / med if med > 0 else 1.0
@@ -824,7 +833,7 @@ class BurstPlanner:
             self.last_increments[k] = inc
             self._last_scaled[k] = inc * speeds[g]
             self.backlog[k] = self.carry * self.backlog.get(k, 0.0) + inc * speeds[g]
-        mean_inc = float(np.mean(incs)) if incs else 0.0
+        mean_inc = sum(incs) / len(incs) if incs else 0.0
         if mean_inc > 0:
             self._burst_ms = mean_inc if self._burst_ms <= 0 else 0.5 * (self._burst_ms + mean_inc)
         lo = min(self.backlog[k] for k in gkeys)
