@@ -37,6 +37,7 @@ class PodRun:
     end: Optional[torch.cuda.Event] = None
     ms: float = 0.0
     gpu: int = 0                 # the node's GPU index (simulated executors keep one pipeline per GPU)
+    policy: int = 0              # kernel policy from the scheduler: 1 = wide GEMM tiles (whole-chip budget)
 
     @property
     def throughput(self) -> float:
@@ -161,6 +162,8 @@ class DeviceExecutor:
         torch.cuda.synchronize(self.device)
 
     def _budget(self, r: PodRun) -> int:
+        if r.policy == 1:
+            return 0                     # wide: tiles for the whole chip (more, smaller workgroups)
         return r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
 
     def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:

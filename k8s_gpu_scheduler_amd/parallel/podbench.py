@@ -54,7 +54,7 @@ from ..telemetry.cache import DeviceSample, TelemetryCache
 from ..telemetry.workcost import WorkCostModel
 
 NODE = "mi355x-node-0"
-FIELDS = 7    # gpu, first_unit, n_units, workload_id, iters, slo_milli, masked
+FIELDS = 8    # gpu, first_unit, n_units, workload_id, iters, slo_milli, masked, kernel_policy
 UNITS_PER_GPU = 8
 MAX_PODS_GPU = 8              # per-pod co-run records per GPU and epoch
 COST0 = 4
@@ -108,7 +108,7 @@ class ControlPlane:
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
                  slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0,
-                 effort_down: Optional[float] = None, learn_corun: bool = True):
+                 effort_down: Optional[float] = None, learn_corun: bool = True, kernel_policy: str = "off"):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.cu_per_pod = cu_per_pod
         self.qos = qos
@@ -193,6 +193,15 @@ class ControlPlane:
         self.plan_feedback = plan_feedback and plan_carry > 0
         self._carry_pred: "collections.deque[Dict[int, float]]" = collections.deque()
         self._covered: Dict[int, float] = {}
+        self.epoch = 0
+        # per-pod kernel policy ("risk"): a GEMM-heavy pod the co-run model predicts to miss its
+        # SLO next to its GPU's other new pods gets the wide GEMM tiling (the whole chip as its
+        # tile budget: more, smaller workgroups that spread over the CUs its Burstable share may
+        # borrow) -- the scheduler's annotation gpu-scheduler.amd.com/kernel-policy=wide
+        if kernel_policy not in ("off", "risk"):
+            raise ValueError(f"kernel policy must be off or risk, not {kernel_policy!r}")
+        self.kernel_policy = kernel_policy
+        self.policy_pods = 0
         self.epoch = 0
         # adaptive planning effort (GPU runs): the control plane must schedule an epoch within
         # the pipeline's period (the interval between consecutive schedule requests) or it
@@ -286,15 +295,44 @@ class ControlPlane:
             u0, n = st.pods[r.pod_key].units
             p = byname[name]
             arr[i] = (self.uuid_to_gpu[uuid], u0, n, W.INDEX[p["workload"]], self.iters, int(p["slo"] * 1000),
-                      1 if self.qos == "guaranteed" else 0)
+                      1 if self.qos == "guaranteed" else 0, 0)
             self.live.append((ns, name))
         self.queue_drop(dropped)
+        if self.kernel_policy == "risk":
+            self._kernel_policies(arr)
         self.epoch += 1
         dt = time.perf_counter() - t0
         self.sched_s += dt
         if self.epoch > 1 and self._effort is not None:   # the first epoch pays one-time costs
             self._effort.add_cost(dt)
         return arr
+
+    # GEMM-heavy: at least this share of the pod's alone roofline time is MFMA work
+    POLICY_GEMM_SHARE = 0.6
+
+    def _kernel_policies(self, arr: np.ndarray) -> None:
+        """Kernel policy per placed pod (column 7): 1 (wide GEMM tiles) for a GEMM-heavy pod
+        whose throughput the co-run model predicts below its SLO next to its GPU's other new
+        pods of this epoch."""
+        model = self.predictions.corun() if hasattr(self.predictions, "corun") else None
+        if model is None:
+            return
+        by_gpu: Dict[int, List[int]] = {}
+        for i, row in enumerate(arr):
+            if row[0] >= 0:
+                by_gpu.setdefault(int(row[0]), []).append(i)
+        for g, idx in by_gpu.items():
+            wids = [model.wid(W.NAMES[int(arr[i][3])]) for i in idx]
+            if min(wids) < 0:
+                continue
+            its = [float(arr[i][4]) for i in idx]
+            dur = model.group_durations(wids, its)
+            for i, w_i, it, d in zip(idx, wids, its, dur):
+                slo = arr[i][5] / 1000.0
+                mfma, hbm = W.roofline_split(W.NAMES[int(arr[i][3])]) or (0.0, 1.0)
+                if slo > 0 and d > 0 and it / d * 1e3 < slo and mfma >= self.POLICY_GEMM_SHARE * (mfma + hbm):
+                    arr[i][7] = 1
+                    self.policy_pods += 1
 
     def queue_drop(self, dropped: List[Tuple[str, str]]) -> None:
         # pods that did not fit are dropped at the end of the epoch (arrivals are
@@ -402,6 +440,8 @@ class ControlPlane:
             b = list(planner.backlog.values())
             st["backlog_spread_ms"] = round(max(b) - min(b), 3)
         st["slot_policy"] = planner.slot_policy or "off"
+        if self.kernel_policy != "off":
+            st["kernel_policy_pods"] = self.policy_pods
         if self.effort_epochs:
             st["effort_epochs"] = {str(k): v for k, v in sorted(self.effort_epochs.items())}
         if planner._slot_work:          # lpt: how level the slot streams' cumulative work is
@@ -635,7 +675,7 @@ def _effective_config(a: Any) -> Dict[str, Any]:
     corun = a.slo_objective == "corun"
     planned = bool(a.plan_bursts) and a.policy != "random"
     out: Dict[str, Any] = {"balance": a.balance, "slo_objective": a.slo_objective, "plan_bursts": int(planned),
-                           "slot_balance": a.slot_balance}
+                           "slot_balance": a.slot_balance, "kernel_policy": a.kernel_policy}
     if planned:
         out["plan_tolerance"] = a.plan_tolerance
         if corun:
@@ -659,10 +699,11 @@ def _runs_for(arr: np.ndarray, gpu: int):
     from .executor import PodRun
     out = []
     for i, row in enumerate(arr):
-        g, u0, n, wid, iters, slo_m, masked = (int(x) for x in row)
+        g, u0, n, wid, iters, slo_m, masked = (int(x) for x in row[:7])
         if g != gpu or g < 0:
             continue
-        out.append(PodRun(i, W.NAMES[wid], u0, n, iters, slo_m / 1000.0, masked=bool(masked), gpu=g))
+        pol = int(row[7]) if len(row) > 7 and row[7] > 0 else 0
+        out.append(PodRun(i, W.NAMES[wid], u0, n, iters, slo_m / 1000.0, masked=bool(masked), gpu=g, policy=pol))
     return out
 
 
@@ -715,6 +756,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="GPU plugin SLO objective: 'corun' = the multi-way co-run model (data/corun_mi355x.json, "
                          "refined online) as a constraint on Score and in the burst planner; 'terms' = the "
                          "reference's pairwise interference terms")
+    ap.add_argument("--kernel-policy", default="off", choices=["off", "risk"],
+                    help="per-pod kernel policy from the scheduler: 'risk' = a GEMM-heavy pod the co-run model "
+                         "predicts below its SLO runs its GEMMs on whole-chip tiles (more, smaller workgroups)")
     ap.add_argument("--corun-learn", type=int, default=0, choices=[0, 1],
                     help="refine the co-run model online from the pods' measured times (models.corun.OnlineCorun). "
                          "Off by default: its first refit needs 256 observed pods (a refit on fewer made the model "
@@ -876,7 +920,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=a.plan_slots,
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
                      adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort,
-                     effort_down=a.cp_effort_down, learn_corun=bool(a.corun_learn))
+                     effort_down=a.cp_effort_down, learn_corun=bool(a.corun_learn),
+                     kernel_policy=a.kernel_policy)
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc
@@ -966,6 +1011,9 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     if use_gpu:
         from .executor import PodRun
         ex.warm([PodRun(0, wl, u, 2, a.iters, masked=a.qos == "guaranteed") for wl in W.NAMES for u in (0, 2, 4, 6)])
+        if a.kernel_policy != "off":        # the wide-tile graphs too (no capture inside the run)
+            ex.warm([PodRun(0, wl, u, 2, a.iters, masked=a.qos == "guaranteed", policy=1) for wl in W.NAMES
+                     for u in (0, 2, 4, 6)])
 
     if use_gpu and a.prewarm_ms > 0:
         _prewarm(dev, a.prewarm_ms)

@@ -80,7 +80,7 @@ def test_dead_control_plane_raises_instead_of_hanging():
     from k8s_gpu_scheduler_amd.parallel.controlplane_proc import ControlPlaneProc
     cp = ControlPlaneProc(n_gpus=1, pods_per_gpu=2, iters=2, seed=0)
     try:
-        assert cp.schedule_epoch().shape == (2, 7)
+        assert cp.schedule_epoch().shape == (2, 8)
         cp.request_schedule()
         cp._p.kill()
         cp._p.join()
