@@ -115,7 +115,8 @@ class NodeAgent:
             self.corun = None
             if corun_send is not None:
                 from .corun_observer import CorunObserver
-                self.corun = CorunObserver(corun_send, running_on=self._running_on if client is not None else None)
+                self.corun = CorunObserver(corun_send, running_on=self._running_on if client is not None else None,
+                                           finished_on=self._finished_on if client is not None else None)
             self.profiles = ProfileIngestor(profile_dir, RedisHistory(redis), node=node, corun=self.corun,
                                             pod_lookup=self._pod_lookup if client is not None else None)
         self.history_every = max(1, history_every)
@@ -611,6 +612,20 @@ class NodeAgent:
             if O.is_terminal(p):
                 continue
             if uuid in (O.annotations(p).get(C.ANNOT_DEVICES) or "").split(","):
+                out.add(O.key(p))
+        return out
+
+    def _finished_on(self, uuid: str, span: Tuple[float, float]) -> set:
+        """Keys of this node's terminal pods on device `uuid` whose containers ran during
+        `span` (epoch s: another pod's container startedAt .. finishedAt)."""
+        from ..plugins.gpu.feedback import container_span
+        pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        out = set()
+        for p in pods:
+            if not O.is_terminal(p) or uuid not in (O.annotations(p).get(C.ANNOT_DEVICES) or "").split(","):
+                continue
+            sp = container_span(p)
+            if sp is not None and sp[1] > span[0] and sp[0] < span[1]:
                 out.add(O.key(p))
         return out
 

@@ -16,7 +16,11 @@ model (models.corun.OnlineCorun, served by the recommender's ObserveCorun) learn
   * co-runners still running when the target is ingested are waited for: the pods running on
     the device then (`running_on`) must all have finished, and a target whose co-runner
     finished without a trace (not profiled) is dropped -- its pressure would be missing from
-    the group and bias the fit.
+    the group and bias the fit;
+  * co-runners that had ALREADY finished when the target was ingested are found by their
+    container times (`finished_on`: terminal pods on the device whose container
+    startedAt .. finishedAt overlaps the target's own container span); any of them without a
+    trace drops the target for the same reason.
 
 A pod that ran ALONE on its device becomes a 1-pod group: for a workload the co-run model
 does not know yet, the recommender cold-starts its row from it (models.coldstart).
@@ -30,7 +34,7 @@ from __future__ import annotations
 import logging
 import threading
 import time
-from typing import Any, Callable, Dict, List, Optional, Set
+from typing import Any, Callable, Dict, List, Optional, Set, Tuple
 
 from ..api import constants as C
 from ..api import objects as O
@@ -41,9 +45,11 @@ log = logging.getLogger(__name__)
 class CorunObserver:
     def __init__(self, send: Callable[[List[Dict[str, Any]]], Any],
                  running_on: Optional[Callable[[str], Set[str]]] = None, settle_s: float = 5.0,
-                 clock: Callable[[], float] = time.monotonic, keep_s: float = 900.0, max_group: int = 16):
+                 clock: Callable[[], float] = time.monotonic, keep_s: float = 900.0, max_group: int = 16,
+                 finished_on: Optional[Callable[[str, Tuple[float, float]], Set[str]]] = None):
         self.send = send
         self.running_on = running_on
+        self.finished_on = finished_on
         self.settle_s = settle_s
         self.clock = clock
         self.keep_s = keep_s
@@ -70,6 +76,12 @@ class CorunObserver:
         running = None
         if self.running_on is not None:
             running = set(self.running_on(uuid)) - {key}
+        if self.finished_on is not None:
+            from ..plugins.gpu.feedback import container_span
+            span = container_span(pod)
+            if span is not None:
+                # (never running any more: _ready then only asks that each left a trace)
+                running = (running or set()) | (set(self.finished_on(uuid, span)) - {key})
         with self._lock:
             self._recs.setdefault(uuid, []).append(
                 {"key": key, "workload": workload, "iters": float(iters), "s": int(first_ns), "e": int(last_ns),
@@ -83,7 +95,7 @@ class CorunObserver:
             return None
         if r["wait"] is None:
             return True
-        if r["wait"] & set(self.running_on(uuid)):
+        if self.running_on is not None and r["wait"] & set(self.running_on(uuid)):
             return None                     # a co-runner of it is still running
         return r["wait"] <= traced          # every one of them left a trace
 

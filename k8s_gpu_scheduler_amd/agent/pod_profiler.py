@@ -175,16 +175,24 @@ class ProfileIngestor:
     stats (kernel_stats.csv, or counter_collection.csv for a PMC pass); ingested ones are
     removed, so each run is counted once.
 
-    `pod_lookup(ns, name)` (the agent's API client): a directory is ingested only for a pod
-    that exists with that UID on this node -- defence in depth behind the webhook's per-
-    container subPathExpr mount; the pod's own workload annotation names the history it goes
-    to.  Files over `max_file_bytes` are not read.  With a `corun` observer
+    `pod_lookup(ns, name)` (the agent's API client): a directory is ingested for a pod that
+    exists with that UID on this node -- defence in depth behind the webhook's per-container
+    subPathExpr mount; the pod's own workload annotation names the history it goes to.  A pod
+    that no longer exists (deleted after it ran) keeps its run: its directory is ingested under
+    the name rule's workload while younger than `orphan_grace_s`.  Files over `max_file_bytes` are not read.  With a `corun` observer
     (agent.corun_observer.CorunObserver) each traced pod's kernel interval on its device is
     also recorded, so pods that overlapped on one GPU become co-run observations."""
 
     def __init__(self, root: str, history: RedisHistory, keep_dir: str = "",
                  pod_lookup: Optional[Callable[[str, str], Optional[Dict[str, Any]]]] = None,
-                 node: str = "", corun: Any = None, max_file_bytes: int = 64 << 20):
+                 node: str = "", corun: Any = None, max_file_bytes: int = 64 << 20,
+                 orphan_grace_s: float = 3600.0):
+        # a directory whose pod object is already gone (a Job pod garbage-collected or
+        # TTL-deleted before this pass) is still that pod's: only its own container could write
+        # there (the webhook's per-container subPathExpr mount names it by namespace, name and
+        # UID).  It is ingested under the name rule's workload while younger than
+        # orphan_grace_s; older orphans are dropped
+        self.orphan_grace_s = orphan_grace_s
         self.root = root
         self.history = history
         self.keep_dir = keep_dir
@@ -207,7 +215,7 @@ class ProfileIngestor:
                 out.append((dirpath, rel))
         return out
 
-    def _owner(self, ns: str, name: str, uid: str) -> Tuple[bool, Optional[Dict[str, Any]]]:
+    def _owner(self, ns: str, name: str, uid: str, d: str = "") -> Tuple[bool, Optional[Dict[str, Any]]]:
         """(accept, pod object or None)."""
         if self.pod_lookup is None:
             return True, None
@@ -215,7 +223,13 @@ class ProfileIngestor:
             pod = self.pod_lookup(ns, name)
         except Exception as e:          # apiserver blip: keep the directory for the next pass
             raise RuntimeError(f"pod lookup failed: {e}") from e
-        if pod is None or O.uid(pod) != uid:
+        if pod is None:                 # gone (deleted after it ran): an orphan within its grace
+            try:
+                age = time.time() - os.path.getmtime(d) if d else float("inf")
+            except OSError:
+                age = float("inf")
+            return age <= self.orphan_grace_s, None
+        if O.uid(pod) != uid:           # a different pod of that name: never this directory's
             return False, None
         if self.node and O.node_name_of(pod) not in ("", self.node):
             return False, None
@@ -235,7 +249,7 @@ class ProfileIngestor:
         n = 0
         for d, (ns, name, uid, container, tag) in self._finished():
             try:
-                ok, owner = self._owner(ns, name, uid)
+                ok, owner = self._owner(ns, name, uid, d)
             except RuntimeError as e:
                 log.warning("profile %s: %s", d, e)
                 continue

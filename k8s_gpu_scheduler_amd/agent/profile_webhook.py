@@ -17,7 +17,9 @@ the kubelet starts, but admission can rewrite what the kubelet will start:
     the downward API: a controller's pod may get its generated name after admission), so a
     container sees only its own directory -- it cannot read, overwrite or forge another pod's
     profiles; <tag> records the request the pod was admitted with (CU share, HBM, iterations:
-    `cu64-hbm8-it20`), so the agent can attribute a profile even after the pod object is gone;
+    `cu64-hbm8-it20`), so the agent can attribute a profile even after the pod object is gone
+    (a pod deleted after it ran is ingested under its name's workload within the ingestor's
+    orphan grace period, pod_profiler.ProfileIngestor);
   the container exits --> rocprofv3 writes run_kernel_stats.csv / run_kernel_trace.csv
     into the hostPath --> the node agent (pod_profiler.ProfileIngestor, NodeAgent.step)
     summarises each finished directory into the pod's WORKLOAD history in Redis

@@ -227,3 +227,29 @@ def test_cold_start_rows_keep_their_state_when_a_later_name_sorts_first(tmp_path
     finally:
         svc.stop()
         srv.stop(0)
+
+
+def test_observer_drops_a_target_whose_finished_corunner_left_no_trace():
+    """an unprofiled pod that overlapped the target on its device and had ALREADY
+    finished when the target's trace was ingested was neither waited for nor detected.  Its
+    container span (startedAt .. finishedAt) overlapping the target's now drops the target; a
+    traced one or one that ran at another time does not."""
+    def term(name, t0, t1):
+        return {"metadata": {"name": name, "namespace": "default", "annotations": {C.ANNOT_DEVICES: UUID}},
+                "status": {"phase": "Succeeded", "containerStatuses": [{"state": {"terminated": {
+                    "startedAt": f"2026-01-01T00:00:{t0:02d}Z", "finishedAt": f"2026-01-01T00:00:{t1:02d}Z"}}}]}}
+    pods = {"default/ghost": term("ghost", 1, 4), "default/late": term("late", 30, 40),
+            "default/b": term("b", 2, 6)}
+
+    def finished_on(uuid, span):
+        from k8s_gpu_scheduler_amd.plugins.gpu.feedback import container_span
+        return {k for k, p in pods.items() if (s := container_span(p)) and s[1] > span[0] and s[0] < span[1]}
+    ob = CorunObserver(lambda g: None, running_on=lambda u: set(), settle_s=0.0, finished_on=finished_on)
+    ob.add(term("a", 0, 5), "onnx_resnet50_1024", 20, 0, 10_000_000)     # ghost (untraced) overlapped
+    assert ob.step() == 0 and ob.dropped == 1
+    del pods["default/ghost"]
+    sent = []
+    ob2 = CorunObserver(sent.append, running_on=lambda u: set(), settle_s=0.0, finished_on=finished_on)
+    ob2.add(term("b", 2, 6), "onnx_mobilenet_1024", 20, 2_000_000, 6_000_000)
+    ob2.add(term("a", 0, 5), "onnx_resnet50_1024", 20, 0, 10_000_000)    # b overlapped and is traced
+    assert ob2.step() == 2 and ob2.dropped == 0

@@ -199,3 +199,25 @@ def test_webhook_handler_fails_open():
             raise RuntimeError("redis down")
     out = webhook_handler(Boom(), {"request": {"uid": "x", "kind": {"kind": "Pod"}, "object": {}}})
     assert out["response"]["allowed"] and "patch" not in out["response"]
+
+
+def test_ingestor_keeps_runs_of_deleted_pods_within_the_grace_and_rejects_foreign_uids(tmp_path):
+    """a Job pod deleted before the agent's pass lost its profile.  Its directory is
+    authentic by construction (only its own container could write under <ns>/<pod>/<uid>), so it
+    is ingested under the name's workload while younger than the orphan grace; a pod of the same
+    name with ANOTHER uid still rejects it, and stale orphans are dropped."""
+    r = Redis(FakeRedisBackend(FakeRedisEngine()))
+    root = str(tmp_path / "prof")
+    kern = [("gs::stream_triad_u<4, true>", 20, 2_000_000)]
+    gone = _write_profile(root, "default", "onnx-mobilenet-1024-job1", "uid-a", "main", "cu64-hbm4-it20", kern)
+    other = _write_profile(root, "default", "onnx-resnet50-2048-j", "uid-b", "main", "cu64-hbm8-it20", kern)
+    old = _write_profile(root, "default", "onnx-ssd-mobilenet-1024-z", "uid-c", "main", "cu64-hbm4-it20", kern)
+    os.utime(old, (1.0, 1.0))                                             # an orphan from long ago
+    live = {("default", "onnx-resnet50-2048-j"): {"metadata": {"name": "onnx-resnet50-2048-j",
+                                                               "namespace": "default", "uid": "uid-NEW"}}}
+    ing = ProfileIngestor(root, RedisHistory(r), pod_lookup=lambda ns, n: live.get((ns, n)), orphan_grace_s=600.0)
+    assert ing.step() == 1
+    assert RedisHistory(r).read("onnx_mobilenet_1024")                    # the deleted pod's run kept
+    assert not RedisHistory(r).read("onnx_resnet50_2048")                 # uid mismatch: rejected
+    assert not RedisHistory(r).read("onnx_ssd_mobilenet_1024")            # stale orphan: dropped
+    assert not os.path.exists(gone) and not os.path.exists(other) and not os.path.exists(old)
