@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Tuple
 
 @dataclass(frozen=True)
 class Op:
-    kind: str              # "gemm" | "triad"
+    kind: str              # "gemm" (bf16) | "gemm8" (fp8 e4m3, bf16 out) | "triad"
     M: int = 0
     N: int = 0
     K: int = 0
@@ -34,14 +34,24 @@ class Op:
     n_floats: int = 0      # triad
 
     @property
+    def is_gemm(self) -> bool:
+        return self.kind in ("gemm", "gemm8")
+
+    @property
     def flops(self) -> float:
-        return 2.0 * self.M * self.N * self.K if self.kind == "gemm" else 2.0 * self.n_floats
+        return 2.0 * self.M * self.N * self.K if self.is_gemm else 2.0 * self.n_floats
 
     @property
     def bytes(self) -> float:
         if self.kind == "gemm":
             return 2.0 * (self.M * self.K + self.N * self.K + self.M * self.N)
+        if self.kind == "gemm8":
+            return 1.0 * (self.M * self.K + self.N * self.K) + 2.0 * self.M * self.N
         return 12.0 * self.n_floats
+
+    def mfma_rate(self) -> float:
+        """MFMA throughput relative to bf16 (the fp8 MFMA does twice the work per clock)."""
+        return 2.0 if self.kind == "gemm8" else 1.0
 
 
 @dataclass(frozen=True)
@@ -96,14 +106,39 @@ for _fw in FRAMEWORKS:
 NAMES: List[str] = sorted(CATALOG)
 INDEX: Dict[str, int] = {n: i for i, n in enumerate(NAMES)}
 
+# Workloads OUTSIDE the reference's 18 (no configuration / interference rows, no co-run rows
+# in data/corun_mi355x.json): kernel mixes the catalog does not have, runnable by the executor
+# and the pod entrypoint, and what the co-run model's cold start is checked on
+# (models.coldstart, tools/corun_extra_groups.py -> profiles/r05_coldstart/):
+#   fp8_llm_2048     three fp8 GEMMs 2048 x 4096 x 4096 (LLM-projection-like, MFMA-bound on
+#                    the block-scaled fp8 MFMA the catalog never uses)
+#   triad_only_2048  three HBM stream passes, no GEMM at all
+EXTRA: Dict[str, Workload] = {
+    "fp8_llm_2048": Workload("fp8_llm_2048", "llm_fp8", "hip", 2048, (Op("gemm8", 2048, 4096, 4096),) * 3, 1.0),
+    "triad_only_2048": Workload("triad_only_2048", "stream", "hip", 2048,
+                                (Op("triad", n_floats=2048 * 16384),) * 3, 1.0),
+}
+
+
+def get(name: str) -> Workload:
+    """A catalog or extra workload by exact name."""
+    w = CATALOG.get(name)
+    if w is None:
+        w = EXTRA.get(name)
+    if w is None:
+        raise KeyError(name)
+    return w
+
 
 def workload_for_pod(pod_name: str) -> Workload:
     """Same matching rule as the recommender: first catalog name that is a substring of
-    the pod name with '-' -> '_' (reference recom_server.py:67-71)."""
+    the pod name with '-' -> '_' (reference recom_server.py:67-71); the extra workloads after
+    the catalog."""
     nm = pod_name.replace("-", "_")
-    for n in sorted(CATALOG, key=len, reverse=True):
-        if n in nm:
-            return CATALOG[n]
+    for table in (CATALOG, EXTRA):
+        for n in sorted(table, key=len, reverse=True):
+            if n in nm:
+                return table[n]
     raise KeyError(pod_name)
 
 
@@ -115,8 +150,8 @@ def roofline_split(pod_name: str, tflops: float = 1.0e3, tbps: float = 6.0) -> O
         w = workload_for_pod(pod_name)
     except KeyError:
         return None
-    m = sum(o.flops for o in w.ops if o.kind == "gemm") / (tflops * 1e12)
-    h = sum(o.bytes for o in w.ops if o.kind != "gemm") / (tbps * 1e12)
+    m = sum(o.flops / o.mfma_rate() for o in w.ops if o.is_gemm) / (tflops * 1e12)
+    h = sum(o.bytes for o in w.ops if not o.is_gemm) / (tbps * 1e12)
     return m, h
 
 
@@ -130,8 +165,9 @@ def roofline_seconds(w: Workload, share: float, peak_tflops: float = 1100.0, hbm
     with measurements."""
     t = 0.0
     for o in w.ops:
-        if o.kind == "gemm":
-            t += max(o.flops / (peak_tflops * 1e12 * share), o.bytes / (hbm_tbps * 1e12 * share ** share_bw_exp))
+        if o.is_gemm:
+            t += max(o.flops / (peak_tflops * o.mfma_rate() * 1e12 * share),
+                     o.bytes / (hbm_tbps * 1e12 * share ** share_bw_exp))
         else:
             t += o.bytes / (hbm_tbps * 1e12 * share ** share_bw_exp)
     return t

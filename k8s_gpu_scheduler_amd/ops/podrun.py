@@ -1,4 +1,4 @@
-"""Container entrypoint of a synthetic pod: run one catalog workload on the GPU the pod got.
+"""Container entrypoint of a synthetic pod: run one catalog (or extra) workload on the GPU the pod got.
 
     python -m k8s_gpu_scheduler_amd.ops.podrun --workload onnx_resnet50_1024 [--iters N]
 
@@ -27,27 +27,20 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     import torch
     from ..models import workloads as W
-    from . import loadgen
-    from ..parallel.executor import _Buffers
-    if a.workload not in W.CATALOG:
+    from ..parallel.executor import _Buffers, enqueue_ops
+    try:
+        w = W.get(a.workload)
+    except KeyError:
         print(f"unknown workload {a.workload!r}", file=sys.stderr)
         return 2
     iters = a.iters or int(float(os.environ.get("ITERATIONS", "0") or 0)) or 20
     budget = a.cu_budget or int(os.environ.get("GPU_SCHED_CU", "0") or 0)
     torch.cuda.set_device(0)
-    w = W.CATALOG[a.workload]
     bufs = _Buffers(w, torch.device("cuda", 0))
     st = torch.cuda.current_stream()
 
     def run(n: int) -> None:
-        for _ in range(n):
-            for o, t in bufs.ops:
-                if o.kind == "gemm":
-                    x, bt, bias, c = t
-                    loadgen.gemm(x, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
-                else:
-                    x, y, z = t
-                    loadgen.triad(x, y, z, 1.0001, stream=st)
+        enqueue_ops(bufs, n, st, budget)
 
     run(1)                                   # first launch: code objects, allocations
     torch.cuda.synchronize()

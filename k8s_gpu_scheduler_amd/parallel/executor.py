@@ -19,7 +19,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from ..models.workloads import CATALOG, Op, Workload
+from ..models.workloads import Op, Workload, get as workload_by_name
 from ..ops import loadgen
 from ..plugins.gpu.devices import CUS_PER_XCD as CUS_PER_UNIT, cu_slice_mask
 
@@ -49,9 +49,11 @@ class _Buffers:
         self.ops: List[Tuple[Op, tuple]] = []
         g = torch.Generator(device="cpu").manual_seed(hash(w.name) & 0xFFFF)
         for o in w.ops:
-            if o.kind == "gemm":
+            if o.is_gemm:
                 a = ((torch.rand(o.M, o.K, generator=g) * 2 - 1).to(torch.bfloat16)).to(device)
                 bt = ((torch.rand(o.N, o.K, generator=g) * 2 - 1).to(torch.bfloat16) * 0.05).to(device)
+                if o.kind == "gemm8":                   # e4m3 operands (weights scaled into range)
+                    a, bt = a.to(loadgen.FP8), (bt * 16).to(loadgen.FP8)
                 bias = torch.zeros(o.N, dtype=torch.float32, device=device)
                 c = torch.empty(o.M, o.N, dtype=torch.bfloat16, device=device)
                 self.ops.append((o, (a, bt, bias, c)))
@@ -60,6 +62,22 @@ class _Buffers:
                 y = torch.ones(o.n_floats, dtype=torch.float32, device=device)
                 z = torch.ones(o.n_floats, dtype=torch.float32, device=device)
                 self.ops.append((o, (x, y, z)))
+
+
+def enqueue_ops(bufs: _Buffers, iters: int, st, budget: int, blocks: int = 0) -> None:
+    """`iters` iterations of a workload's op list on stream `st` (GEMM tiles sized for `budget`
+    CUs, 0 = the whole chip)."""
+    for _ in range(iters):
+        for o, t in bufs.ops:
+            if o.kind == "gemm":
+                a, bt, bias, c = t
+                loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+            elif o.kind == "gemm8":
+                a, bt, bias, c = t
+                loadgen.gemm_fp8(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+            else:
+                x, y, z = t
+                loadgen.triad(x, y, z, 1.0001, blocks=blocks, stream=st)
 
 
 def lpt_balance(runs: List[PodRun], slot_work: Dict[Tuple[int, int], float], work=None) -> None:
@@ -156,7 +174,7 @@ class DeviceExecutor:
         outside any timed region."""
         for p in placements:
             st = self.stream_for(p.first_unit, p.n_units, p.masked)
-            bufs = self.buffers(CATALOG[p.workload], p.first_unit, p.n_units)
+            bufs = self.buffers(workload_by_name(p.workload), p.first_unit, p.n_units)
             if self.use_graphs:
                 self._graph_for(p, bufs, st.stream, self._budget(p))
         torch.cuda.synchronize(self.device)
@@ -167,15 +185,7 @@ class DeviceExecutor:
         return r.n_units * CUS_PER_UNIT if self.gemm_share else 0   # the pod's CU share
 
     def _enqueue_ops(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> None:
-        blocks = self.triad_blocks
-        for _ in range(r.iters):
-            for o, t in bufs.ops:
-                if o.kind == "gemm":
-                    a, bt, bias, c = t
-                    loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
-                else:
-                    x, y, z = t
-                    loadgen.triad(x, y, z, 1.0001, blocks=blocks, stream=st)
+        enqueue_ops(bufs, r.iters, st, budget, self.triad_blocks)
 
     def _graph_for(self, r: PodRun, bufs: "_Buffers", st, budget: int) -> "torch.cuda.CUDAGraph":
         """One HIP graph per (workload, unit slot, QoS, iters): captured on the pod's own
@@ -208,7 +218,7 @@ class DeviceExecutor:
         # an outlier the planner's feedback would read as a slow GPU (GPUTEST_r04.json)
         prep = []
         for r in runs:
-            w = CATALOG[r.workload]
+            w = workload_by_name(r.workload)
             bufs = self.buffers(w, r.first_unit, r.n_units)
             budget = self._budget(r)
             st = self.stream_for(r.first_unit, r.n_units, r.masked).stream
@@ -251,7 +261,7 @@ class DeviceExecutor:
     def pod_work(r: PodRun) -> float:
         """Relative work of a pod (its kernels' roofline time alone on the GPU x iterations)."""
         from ..models.workloads import roofline_seconds
-        return roofline_seconds(CATALOG[r.workload], 1.0) * max(r.iters, 1)
+        return roofline_seconds(workload_by_name(r.workload), 1.0) * max(r.iters, 1)
 
     def _balance(self, runs: List[PodRun]) -> None:
         lpt_balance(runs, self._slot_work, self.pod_work)
