@@ -68,7 +68,7 @@ class CorunObserver:
         return devs[0] if len(devs) == 1 else None
 
     def add(self, pod: Dict[str, Any], workload: str, iters: float, first_ns: int, last_ns: int,
-            mfma_share: Optional[float] = None) -> bool:
+            mfma_share: Optional[float] = None, cu_fill: Optional[float] = None) -> bool:
         uuid = self.device_of(pod)
         if uuid is None or last_ns <= first_ns:
             return False
@@ -86,7 +86,8 @@ class CorunObserver:
             self._recs.setdefault(uuid, []).append(
                 {"key": key, "workload": workload, "iters": float(iters), "s": int(first_ns), "e": int(last_ns),
                  "t": self.clock(), "wait": running, "emitted": False,
-                 "mfma": -1.0 if mfma_share is None else float(mfma_share)})
+                 "mfma": -1.0 if mfma_share is None else float(mfma_share),
+                 "fill": -1.0 if cu_fill is None else float(cu_fill)})
         return True
 
     def _ready(self, uuid: str, r: Dict[str, Any], traced: Set[str]) -> Optional[bool]:
@@ -128,7 +129,9 @@ class CorunObserver:
                             "target": [x is r for x in mem],
                             # per member: MFMA share of its kernel time (-1 unknown); a 1-pod
                             # group of an unseen workload cold-starts its co-run row
-                            "mfma_share": [x.get("mfma", -1.0) for x in mem]})
+                            "mfma_share": [x.get("mfma", -1.0) for x in mem],
+                            # ... and the CU fill of its kernels (-1 unknown)
+                            "cu_fill": [x.get("fill", -1.0) for x in mem]})
         sent = 0
         if out:
             try:

@@ -138,15 +138,41 @@ class ProfiledLauncher(PodLauncher):
         return res
 
 
-def summarize_kernel_trace(path: str) -> Dict[str, Any]:
+def _workgroups(r: Dict[str, str]) -> Optional[int]:
+    """Workgroups of one kernel-trace dispatch (rocprofv3 grid and workgroup sizes are in
+    work-items per dimension); None when the row has no sizes."""
+    n = 1
+    for d in ("X", "Y", "Z"):
+        g, w = r.get(f"Grid_Size_{d}"), r.get(f"Workgroup_Size_{d}")
+        if g in (None, "") or w in (None, ""):
+            if d == "X":
+                return None
+            continue
+        g, w = int(float(g)), max(1, int(float(w)))
+        n *= max(1, -(-g // w))
+    return n
+
+
+def summarize_kernel_trace(path: str, cus: int = C.MI355X_CUS) -> Dict[str, Any]:
     """Span (first kernel start .. last kernel end) and busy time (union of kernel intervals)
-    of a rocprofv3 kernel_trace.csv, in ms."""
+    of a rocprofv3 kernel_trace.csv, in ms; `cu_fill`: the kernel-time-weighted fraction of
+    the chip's CUs the dispatches occupy (min(1, workgroups / CUs)) -- the co-run cold start's
+    footprint feature (models.coldstart)."""
     iv = []
+    fw = ft = 0.0
     for r in csv.DictReader(open(path)):
         try:
-            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         except (KeyError, ValueError):
             continue
+        iv.append((a, b))
+        try:
+            wg = _workgroups(r)
+        except ValueError:
+            wg = None
+        if wg is not None and b > a:
+            fw += (b - a) * min(1.0, wg / cus)
+            ft += b - a
     if not iv:
         return {}
     iv.sort()
@@ -160,7 +186,10 @@ def summarize_kernel_trace(path: str) -> Dict[str, Any]:
             ce = max(ce, b)
     busy += ce - cs
     span = last_ns - first_ns
-    return {"span_ms": span / 1e6, "busy_union_ms": busy / 1e6, "first_ns": first_ns, "last_ns": last_ns}
+    out = {"span_ms": span / 1e6, "busy_union_ms": busy / 1e6, "first_ns": first_ns, "last_ns": last_ns}
+    if ft > 0:
+        out["cu_fill"] = round(fw / ft, 4)
+    return out
 
 
 class ProfileIngestor:
@@ -300,7 +329,7 @@ class ProfileIngestor:
             if self.corun is not None and first is not None and last is not None and last > first:
                 try:
                     self.corun.add(pod, wl, float(req.get("iters", 0.0)), int(first), int(last),
-                                   mfma_share=sample.get("mfma_share"))
+                                   mfma_share=sample.get("mfma_share"), cu_fill=sample.get("cu_fill"))
                 except Exception as e:
                     log.warning("profile %s: co-run record failed: %s", d, e)
             self.ingested.append(sample)

@@ -156,6 +156,33 @@ def roofline_split(pod_name: str, tflops: float = 1.0e3, tbps: float = 6.0) -> O
 
 
 # ---------------------------------------------------------------- analytic predictions
+CUS = 256                          # MI355X compute units
+POD_CU_BUDGET = 64                 # a bench pod's GEMM tile budget (2 CU-slice units x 32 CUs)
+
+
+def cu_fill(w: Workload, cu_budget: int = POD_CU_BUDGET) -> Optional[float]:
+    """Fraction of the chip's CUs the workload's kernels occupy, weighted by their (roofline)
+    time: min(1, workgroups / CUs) per kernel -- GEMM workgroups as the native tile picker
+    launches them for `cu_budget` (`_hip.gemm_workgroups`), the stream kernels' 8192 blocks
+    fill the chip.  A pod that leaves CUs idle alone leaves co-runners room; one that fills
+    the chip alone presses on and suffers from every co-runner (models.coldstart).  None when
+    the HIP extension is not built."""
+    from .. import _native
+    h = _native.hip(required=False)
+    if h is None:
+        return None
+    t = f = 0.0
+    for o in w.ops:
+        dt = roofline_seconds(Workload(w.name, w.family, w.framework, w.batch, (o,), 0.0), 1.0)
+        if o.is_gemm:
+            fo = min(1.0, h.gemm_workgroups(o.M, o.N, o.K, cu_budget, o.kind == "gemm8") / CUS)
+        else:
+            fo = 1.0
+        t += dt
+        f += dt * fo
+    return f / t if t > 0 else None
+
+
 def roofline_seconds(w: Workload, share: float, peak_tflops: float = 1100.0, hbm_tbps: float = 5.5,
                      share_bw_exp: float = 0.6) -> float:
     """Per-iteration time on a `share` of the GPU's XCDs.  Compute scales linearly with

@@ -64,7 +64,8 @@ class RecommenderClient:
         return self._call(f"/{P.EXT_SERVICE}/Version", P.Empty())
 
     def observe_corun(self, groups: List[Dict[str, Any]]) -> Any:
-        """Send co-run groups (dicts: workloads, iters, ms[, start_ms, target, mfma_share]) for the
+        """Send co-run groups (dicts: workloads, iters, ms[, start_ms, target, mfma_share,
+        cu_fill]) for the
         recommender's online co-run model (ExportTable("corun") then serves the refined one)."""
         req = P.ObserveCorunRequest()
         for g in groups:
@@ -78,6 +79,8 @@ class RecommenderClient:
                 x.target.extend(bool(v) for v in g["target"])
             if g.get("mfma_share") is not None:
                 x.mfma_share.extend(float(v) for v in g["mfma_share"])
+            if g.get("cu_fill") is not None:
+                x.cu_fill.extend(float(v) for v in g["cu_fill"])
         return self._call(f"/{P.EXT_SERVICE}/ObserveCorun", req)
 
     def observe_interference(self, observations: List[Tuple[str, List[str], float]]) -> Any:

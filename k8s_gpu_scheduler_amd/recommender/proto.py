@@ -88,6 +88,7 @@ def _build_pool() -> descriptor_pool.DescriptorPool:
     _field(cg, "ms", 4, _F.TYPE_FLOAT, _F.LABEL_REPEATED)             # measured wall ms
     _field(cg, "target", 5, _F.TYPE_BOOL, _F.LABEL_REPEATED)          # observation (else co-runner only)
     _field(cg, "mfma_share", 6, _F.TYPE_FLOAT, _F.LABEL_REPEATED)     # MFMA share of kernel time (-1 unknown)
+    _field(cg, "cu_fill", 7, _F.TYPE_FLOAT, _F.LABEL_REPEATED)        # CU fill of its kernels (-1 unknown)
     ocq = fx.message_type.add(name="ObserveCorunRequest")
     _field(ocq, "groups", 1, _F.TYPE_MESSAGE, _F.LABEL_REPEATED, ".gpusched.recommender.CorunGroup")
     ocp = fx.message_type.add(name="ObserveCorunReply")

@@ -372,7 +372,8 @@ class RecommenderService:
                 if len(g.workloads) == 1 and len(g.ms) == 1 and len(g.iters) == 1 and g.ms[0] > 0 \
                         and g.iters[0] > 0 and self._corun_online.base.wid(g.workloads[0]) < 0:
                     mf = float(g.mfma_share[0]) if len(g.mfma_share) == 1 and g.mfma_share[0] >= 0 else None
-                    self._cold.setdefault(g.workloads[0], []).append((g.ms[0] / g.iters[0], mf))
+                    cf = float(g.cu_fill[0]) if len(g.cu_fill) == 1 and g.cu_fill[0] > 0 else None
+                    self._cold.setdefault(g.workloads[0], []).append((g.ms[0] / g.iters[0], mf, cf))
                     fresh = True
             if fresh:
                 self._cold_start_rows()
@@ -412,7 +413,9 @@ class RecommenderService:
                 continue
             a = float(np.median([x[0] for x in obs]))
             shares = [x[1] for x in obs if x[1] is not None]
-            ext = with_workload(ext, name, a, float(np.median(shares)) if shares else None)
+            fills = [x[2] for x in obs if len(x) > 2 and x[2] is not None]
+            ext = with_workload(ext, name, a, float(np.median(shares)) if shares else None,
+                                fill=float(np.median(fills)) if fills else None)
         on = OnlineCorun(ext, background=self._corun_refit_mode, **self.corun_online_kw)
         # carry the learner's state over BY NAME (copying by position shifted an
         # earlier cold row's refit parameters and observations onto another workload)

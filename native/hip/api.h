@@ -40,6 +40,8 @@ void set_xcd_group(int rows);
 void xcd_probe(uintptr_t out, int blocks, uintptr_t stream);
 int pick_xcd_map(int tiles_m, int tiles_n);
 int pick_gemm_tile(int M, int N, int cu_budget);
+// workgroups of the GEMM launch this shape / CU budget gets (the kernel's CU footprint)
+int gemm_workgroups(int M, int N, int K, int cu_budget, bool fp8, bool split_workspace);
 std::vector<int> peer_access_matrix();
 double peer_copy_gbps(int src, int dst, size_t bytes, int iters);
 }  // namespace gs

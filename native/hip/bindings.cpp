@@ -71,6 +71,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("xcd_probe", &gs::xcd_probe, py::arg("out"), py::arg("blocks"), py::arg("stream"));
   m.def("pick_xcd_map", &gs::pick_xcd_map, py::arg("tiles_m"), py::arg("tiles_n"));
   m.def("pick_gemm_tile", &gs::pick_gemm_tile, py::arg("M"), py::arg("N"), py::arg("cu_budget") = 0);
+  m.def("gemm_workgroups", &gs::gemm_workgroups, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("cu_budget") = 0,
+        py::arg("fp8") = false, py::arg("split_workspace") = false);
   m.def("peer_access_matrix", &gs::peer_access_matrix);
   m.def("peer_copy_gbps", &gs::peer_copy_gbps, py::arg("src"), py::arg("dst"), py::arg("bytes"),
         py::arg("iters") = 10, py::call_guard<py::gil_scoped_release>());

@@ -1049,6 +1049,32 @@ static void launch_splitk(const __bf16* A, const __bf16* B, __bf16* Cp, const fl
   hipLaunchKernelGGL((splitk_reduce<RELU, BIAS>), dim3(rblocks), dim3(256), 0, s, ws, S, M, N, bp, Cp, ldc);
 }
 
+// the tile gemm_bf16_nt launches for this shape (pick_gemm_tile + the kernels' shape limits)
+static int resolve_gemm_tile(int M, int N, int K, int cu_budget) {
+  int t = pick_gemm_tile(M, N, cu_budget);
+  if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
+  if (t == 13 && K < 128) t = 5;
+  if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked by the caller)
+  return t;
+}
+
+// fp8 fill rule, as the bf16 picker: 128x128 when it gives every CU of the budget a block (two
+// for a lone kernel), else 64x64
+static bool fp8_tile_128(int M, int N, int cu_budget) {
+  const bool alone = cu_budget <= 0 || cu_budget >= kCus;
+  const int need = alone ? 2 * kCus : cu_budget;
+  return M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= need;
+}
+
+int gemm_workgroups(int M, int N, int K, int cu_budget, bool fp8, bool split_workspace) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % 64 || N % 64) throw std::runtime_error("gemm_workgroups: bad shape");
+  if (fp8) return fp8_tile_128(M, N, cu_budget) ? (M / 128) * (N / 128) : (M / 64) * (N / 64);
+  const int S = split_workspace ? pick_split_k(M, N, K, cu_budget) : 1;
+  if (S > 1) return (M / 256) * (N / 256) * S;
+  const int t = resolve_gemm_tile(M, N, K, cu_budget);
+  return (M / kTileBM[t]) * (N / kTileBN[t]);
+}
+
 void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, int N, int K, int lda, int ldb,
                   int ldc, bool relu, uintptr_t stream, int cu_budget, uintptr_t workspace, size_t workspace_floats) {
   // Host-side shape checks: the kernel has no bounds checks by design.
@@ -1076,10 +1102,7 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     HIP_CHECK(hipGetLastError());
     return;
   }
-  int t = pick_gemm_tile(M, N, cu_budget);
-  if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
-  if (t == 13 && K < 128) t = 5;
-  if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked above)
+  const int t = resolve_gemm_tile(M, N, K, cu_budget);
   switch (t) {
     case 1: launch_gemm<128, 128, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 2: launch_gemm<64, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
@@ -1143,11 +1166,7 @@ void gemm_fp8_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, 
   auto B = reinterpret_cast<const uint8_t*>(bt);
   auto Cp = reinterpret_cast<__bf16*>(c);
   auto bp = reinterpret_cast<const float*>(bias);
-  // same fill rule as the bf16 picker: 128x128 when it gives every CU of the budget a
-  // block (two for a lone kernel), else 64x64
-  const bool alone = cu_budget <= 0 || cu_budget >= kCus;
-  const int need = alone ? 2 * kCus : cu_budget;
-  if (M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= need)
+  if (fp8_tile_128(M, N, cu_budget))
     launch_gemm_fp8<128, 128, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
   else
     launch_gemm_fp8<64, 64, 2, 2, 2>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);

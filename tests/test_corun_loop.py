@@ -253,3 +253,76 @@ def test_observer_drops_a_target_whose_finished_corunner_left_no_trace():
     ob2.add(term("b", 2, 6), "onnx_mobilenet_1024", 20, 2_000_000, 6_000_000)
     ob2.add(term("a", 0, 5), "onnx_resnet50_1024", 20, 0, 10_000_000)    # b overlapped and is traced
     assert ob2.step() == 2 and ob2.dropped == 0
+
+
+def test_cold_start_transfers_to_other_kernel_mixes_with_cu_fill():
+    """two workloads outside the catalog's kernel mix (models.workloads.EXTRA:
+    fp8-GEMM LLM-like, triad-only), measured in co-run groups with catalog pods on MI355X
+    (profiles/r05_coldstart/groups.json, tools/corun_extra_groups.py), cold-started from their
+    alone groups only.  With the CU-fill scaling (betas fitted on the catalog rows alone) both
+    stay within 2x the fitted model's held-out MAE; without it the chip-filling fp8 workload is
+    ~3x off -- the catalog has no GEMM row that fills the chip at a pod's tile budget."""
+    import json
+    from k8s_gpu_scheduler_amd.models.coldstart import cu_fill, fill_betas, mfma_share, with_workload
+    from k8s_gpu_scheduler_amd.models.corun import pack_groups
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = json.load(open(os.path.join(root, "profiles", "r05_coldstart", "groups.json")))
+    groups = d["groups"]
+    base = CorunModel.load()
+    held_out = base.meta["report"]["test"]["mae_pct_of_mean"]
+    bs, bp = fill_betas(base)
+    assert 0.0 < bs < bp < 1.5                       # pressure scales with footprint more than sensitivity
+
+    def alone(n):
+        return float(np.median([g["ms"][0] / g["iters"] for g in groups if g["w"] == [n]]))
+
+    def err(use_fill):
+        m = base
+        for x in d["extra"]:
+            m = with_workload(m, x, alone(x), mfma_share(x), fill=cu_fill(x) if use_fill else None)
+        out = {}
+        for x in d["extra"]:
+            gs = [g for g in groups if x in g["w"] and len(g["w"]) >= 2]
+            wids, iters, mask, ms, st = pack_groups(gs, m.names, 4)
+            t = m.batch_times(wids, iters, mask, st) - st
+            sel = mask & (wids == m.index[x])
+            tp, tm = iters / np.maximum(t, 1e-9) * 1e3, iters / np.maximum(ms, 1e-9) * 1e3
+            out[x] = 100 * np.abs(tp - tm)[sel].mean() / tm[sel].mean()
+        return out
+    with_fill, without = err(True), err(False)
+    assert all(v <= 2 * held_out for v in with_fill.values()), (with_fill, held_out)
+    assert without["fp8_llm_2048"] > 2 * held_out > with_fill["fp8_llm_2048"], (without, with_fill)
+    assert cu_fill("fp8_llm_2048") == 1.0 and cu_fill("onnx_resnet50_2048") == 0.25
+
+
+def test_kernel_trace_cu_fill_reaches_the_cold_row(tmp_path):
+    """The pod profiler's kernel trace gives a pod's CU fill (time-weighted workgroups / CUs);
+    the co-run observer sends it with the alone group and the recommender's cold row uses it."""
+    from k8s_gpu_scheduler_amd.agent.pod_profiler import summarize_kernel_trace
+    tr = tmp_path / "kernel_trace.csv"
+    tr.write_text("Kernel_Name,Start_Timestamp,End_Timestamp,Workgroup_Size_X,Workgroup_Size_Y,Workgroup_Size_Z,"
+                  "Grid_Size_X,Grid_Size_Y,Grid_Size_Z\n"
+                  "gemm_fp8,0,300,256,1,1,131072,1,1\n"            # 512 workgroups: fills 256 CUs
+                  "small,300,400,256,1,1,16384,1,1\n")             # 64 workgroups: a quarter
+    s = summarize_kernel_trace(str(tr))
+    assert abs(s["cu_fill"] - (300 * 1.0 + 100 * 0.25) / 400) < 1e-4
+    cm = tmp_path / "corun.json"
+    shutil.copy(DATA, cm)
+    svc = RecommenderService("", "", corun_path=str(cm))
+    svc._corun_refit_mode = False
+    svc.train()
+    srv, port = svc.make_server(0, 2, "127.0.0.1")
+    try:
+        cl = RecommenderClient(f"127.0.0.1:{port}", timeout_s=30.0)
+        rep = cl.observe_corun([{"workloads": ["llm_fp8_serving"], "iters": [20], "ms": [2.2], "start_ms": [0.0],
+                                 "target": [True], "mfma_share": [1.0], "cu_fill": [1.0]}])
+        assert rep.accepted == 1
+        on = svc._corun_online
+        assert on.base.meta["cold_start"]["llm_fp8_serving"]["cu_fill"] == 1.0
+        i = on.base.wid("llm_fp8_serving")
+        nn = [on.base.wid(n) for n in on.base.meta["cold_start"]["llm_fp8_serving"]["neighbours"]]
+        # a chip-filling newcomer presses harder than the (partly idle) GEMM rows it was imputed from
+        assert (on.base.u @ on.base.v[i]).mean() > max((on.base.u @ on.base.v[j]).mean() for j in nn)
+    finally:
+        svc.stop()
+        srv.stop(0)

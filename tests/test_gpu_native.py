@@ -495,6 +495,30 @@ def test_executor_graph_replay_matches_eager():
         assert torch.equal(a, b)
 
 
+def test_executor_runs_extra_workloads_fp8_and_triad_only():
+    """The workloads outside the catalog (models.workloads.EXTRA) run through the executor's
+    captured graphs: the fp8 GEMMs' output equals the eager fp8 kernel on the same operands, and
+    the triad-only pod streams its passes."""
+    from k8s_gpu_scheduler_amd.models import workloads as W
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun
+    ex = DeviceExecutor(0)
+    ex.use_graphs = True
+    runs = [PodRun(0, "fp8_llm_2048", 0, 2, 2, masked=False), PodRun(1, "triad_only_2048", 2, 2, 2, masked=False)]
+    ex.warm(runs)
+    ex.launch_epoch(runs)
+    ex.wait_epoch(runs)
+    assert all(r.start.elapsed_time(r.end) > 0 for r in runs)
+    o, (a, bt, bias, c) = ex.buffers(W.get("fp8_llm_2048"), 0, 2).ops[0]
+    assert o.kind == "gemm8" and a.dtype == loadgen.FP8
+    ref = loadgen.gemm_fp8(a, bt, bias=bias, relu=True, cu_budget=64)
+    torch.cuda.synchronize()
+    assert torch.equal(c, ref)
+    x, y, z = ex.buffers(W.get("triad_only_2048"), 2, 2).ops[0][1]
+    assert torch.allclose(x, y + 1.0001 * z)
+    ex.close()
+
+
 def test_executor_serves_four_co_running_pod_streams_equally():
     """Four identical Burstable pods co-run on four streams and finish within a few percent of
     each other.  (A stream-wait pending on another hardware queue while they ran made the 4th

@@ -2,7 +2,7 @@
 
 For every catalog workload X: refit the co-run model on the MI355X groups WITHOUT X (every
 group containing X removed), cold-start X from its alone profile only (median alone ms per
-iteration of its 1-pod groups; its MFMA share), and measure the throughput error on X's
+iteration of its 1-pod groups; its MFMA share; its CU fill unless --no-fill), and measure the throughput error on X's
 measured co-run groups.  Compared with: the full fit's row for X (X seen in training) and the
 roofline prior row.  Writes a JSON report (profiles/r04_coldstart/).
 
@@ -35,8 +35,8 @@ def _err(model, groups, names, i):
 
 
 def one(args):
-    path, X, nfev = args
-    from k8s_gpu_scheduler_amd.models.coldstart import mfma_share, with_workload
+    path, X, nfev, use_fill = args
+    from k8s_gpu_scheduler_amd.models.coldstart import cu_fill, mfma_share, with_workload
     from k8s_gpu_scheduler_amd.models.corun import CorunModel, fit
     d = json.load(open(path))
     names = d["names"]
@@ -46,7 +46,7 @@ def one(args):
     test = [g for g in groups if X in g["w"] and len(g["w"]) >= 2]
     alone = [g["ms"][0] / g.get("iters", 20) for g in groups if g["w"] == [X]]
     m, rep = fit(train, names, max_nfev=nfev)
-    cold = with_workload(m, X, float(np.median(alone)), mfma_share(X))
+    cold = with_workload(m, X, float(np.median(alone)), mfma_share(X), fill=cu_fill(X) if use_fill else None)
     full = CorunModel.load()
     prior = CorunModel.prior(names)
     pr = CorunModel(names, m.alone_ms.copy(), m.u.copy(), m.v.copy())
@@ -64,10 +64,11 @@ def main() -> None:
     ap.add_argument("--jobs", type=int, default=6)
     ap.add_argument("--nfev", type=int, default=200)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04_coldstart", "loo.json"))
+    ap.add_argument("--no-fill", action="store_true", help="cold start without the CU-fill scaling (round 4)")
     a = ap.parse_args()
     names = json.load(open(a.groups))["names"]
     with ProcessPoolExecutor(a.jobs) as ex:
-        res = dict(ex.map(one, [(a.groups, X, a.nfev) for X in names]))
+        res = dict(ex.map(one, [(a.groups, X, a.nfev, not a.no_fill) for X in names]))
     cs = [r["cold_start"]["mae_pct"] for r in res.values()]
     fw = [r["fitted_with_x"]["mae_pct"] for r in res.values()]
     pr = [r["prior_row"]["mae_pct"] for r in res.values()]

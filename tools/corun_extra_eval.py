@@ -46,7 +46,7 @@ def main(argv=None) -> int:
     ap.add_argument("--loo", default=os.path.join(ROOT, "profiles", "r04_coldstart", "loo.json"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05_coldstart", "extra.json"))
     a = ap.parse_args(argv)
-    from k8s_gpu_scheduler_amd.models.coldstart import mfma_share, with_workload
+    from k8s_gpu_scheduler_amd.models.coldstart import cu_fill, fill_betas, mfma_share, with_workload
     from k8s_gpu_scheduler_amd.models.corun import CorunModel
     d = json.load(open(a.groups))
     groups, extra = d["groups"], d["extra"]
@@ -59,24 +59,26 @@ def main(argv=None) -> int:
 
     local = {n: alone_med(n) for n in base.names}
     variants = {}
-    for tag in ("fitted_alone", "box_alone"):
+    for tag in ("fitted_alone", "box_alone", "box_alone_no_fill"):
         m = base
-        if tag == "box_alone":
+        if tag.startswith("box_alone"):
             A = m.alone_ms.copy()
             for i, n in enumerate(m.names):
                 if local.get(n):
                     A[i] = local[n]
             m = CorunModel(list(m.names), A, m.u.copy(), m.v.copy(), dict(m.meta))
         for x in extra:
-            m = with_workload(m, x, alone_med(x), mfma_share(x))
+            m = with_workload(m, x, alone_med(x), mfma_share(x), fill=None if tag.endswith("no_fill") else cu_fill(x))
         variants[tag] = m
     report = {"groups": os.path.relpath(os.path.abspath(a.groups), ROOT), "n_groups": len(groups),
               "held_out_mae_pct": held_out, "bar_pct": round(2 * held_out, 3), "per_workload": {},
+              "fill_betas": fill_betas(base),
               "catalog_alone_box_over_fitted": {n: round(local[n] / float(base.alone_ms[base.index[n]]), 4)
                                                 for n in base.names if local.get(n)}}
     for x in extra:
         test = [g for g in groups if x in g["w"] and len(g["w"]) >= 2]
         r = {"alone_ms_per_iter": round(alone_med(x), 5), "mfma_share": round(mfma_share(x), 4),
+             "cu_fill": cu_fill(x),
              "test_groups": len(test), "neighbours": variants["fitted_alone"].meta["cold_start"][x]["neighbours"]}
         for tag, m in variants.items():
             xi = m.index[x]
@@ -87,6 +89,10 @@ def main(argv=None) -> int:
     xs = [r["box_alone"]["cold_start_x"]["mae_pct"] for r in report["per_workload"].values()]
     report["summary"] = {"cold_start_mae_pct": {x: r["box_alone"]["cold_start_x"]["mae_pct"]
                                                 for x, r in report["per_workload"].items()},
+                         "cold_start_mae_pct_without_fill": {x: r["box_alone_no_fill"]["cold_start_x"]["mae_pct"]
+                                                             for x, r in report["per_workload"].items()},
+                         "catalog_corunner_mae_pct": {x: r["box_alone"]["catalog_corunners"]["mae_pct"]
+                                                      for x, r in report["per_workload"].items()},
                          "max_ratio_to_held_out": round(max(xs) / held_out, 3), "within_2x": bool(max(xs) <= 2 * held_out)}
     print(json.dumps(report["summary"], indent=1))
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
