@@ -72,6 +72,100 @@ def test_plan_slots_puts_the_complementary_pod_next_to_the_inflight_one():
     assert len(set(sl2)) == 2
 
 
+def _random_slot_case(rng, W):
+    """plan_slots inputs shaped like an 8-GPU bench epoch's: measured pinned pods, per-slot chains
+    of unmeasured ones, 4 slots, 2-4 new pods (often repeating a workload), 2 phantoms per slot."""
+    S = 4
+    wid, it, st, prev, pin, slo = [], [], [], [], [], []
+    for _ in range(int(rng.integers(0, 8))):                    # measured, pinned
+        s0 = float(rng.uniform(-30, 0))
+        wid.append(int(rng.integers(0, W))), it.append(20.0), st.append(s0), prev.append(-1)
+        pin.append(s0 + float(rng.uniform(1, 40))), slo.append(float(rng.uniform(0, 900)))
+    tail = []
+    for q in range(S):
+        p = -1
+        for j in range(int(rng.integers(0, 4))):               # unmeasured chain on slot q
+            wid.append(int(rng.integers(0, W))), it.append(20.0), pin.append(0.0)
+            slo.append(float(rng.uniform(0, 900)))
+            st.append(float(rng.uniform(-5, 5)) if j == 0 else NEG), prev.append(p)
+            p = len(wid) - 1
+        tail.append(p)
+    free = rng.uniform(0, 10, S)
+    n = int(rng.integers(2, 5))
+    nw = rng.integers(0, W, n)
+    nw[1] = nw[0]                                               # a repeated workload
+    nslo = np.where(nw == nw[0], 400.0, rng.uniform(100, 900, n))
+    ph_off = np.arange(0, 2 * S + 1, 2, dtype=np.int64)
+    ph_w = rng.integers(0, W, 2 * S).astype(I32)
+    return ((np.array(wid, I32), np.array(it), np.array(st), np.array(prev, I32), np.array(pin), np.array(slo),
+             np.array(tail, I32), free, nw.astype(I32), np.full(n, 20.0), nslo, np.full(n, NEG)),
+            (ph_off, ph_w, np.full(2 * S, 20.0)))
+
+
+def _brute_slots(args, ph, alone, cmat, sigma, tol):
+    """Reference: every injective assignment simulated with chain_times, plan_slots' rule."""
+    import itertools
+    from math import erfc, log, sqrt
+    cw, ci, cs, cp, cpin, cslo, tail, free, nw, ni, nslo, nrel = args
+    ph_off, ph_w, ph_i = ph
+    m, n, S = len(cw), len(nw), len(tail)
+    res = []
+    for perm in itertools.permutations(range(S), n):
+        w, it, s0, pv, pe, sl = list(cw), list(ci), list(cs), list(cp), list(cpin), list(cslo)
+        last = list(tail)
+        for j, s in enumerate(perm):
+            w.append(nw[j]), it.append(ni[j]), sl.append(nslo[j]), pe.append(0.0)
+            pv.append(tail[s]), s0.append(nrel[j] if tail[s] >= 0 else max(free[s], nrel[j]))
+            last[s] = m + j
+        for q in range(S):
+            p = last[q]
+            for x in range(ph_off[q], ph_off[q + 1]):
+                w.append(ph_w[x]), it.append(ph_i[x]), sl.append(0.0), pe.append(0.0)
+                pv.append(p), s0.append(NEG if p >= 0 else free[q])
+                p = len(w) - 1
+        st, fin = core.chain_times(np.array(w, I32), np.array(it), np.array(s0), np.array(pv, I32), alone, cmat,
+                                   np.array(pe))[:2]
+        e = 0.0
+        for i in range(len(w)):
+            if (i < m and pv[i] < 0 and pe[i] > s0[i]) or sl[i] <= 0 or it[i] <= 0 or fin[i] >= 1e299:
+                continue
+            t = it[i] / max(fin[i] - st[i], 1e-12) * 1e3
+            e += 0.5 * erfc(-log(max(t, 1e-12) / sl[i]) / (sigma * sqrt(2.0)))
+        ends = []
+        for s in range(S):
+            x = free[s] if tail[s] < 0 else fin[tail[s]]
+            for j, sj in enumerate(perm):
+                if sj == s:
+                    x = fin[m + j]
+            ends.append(x)
+        res.append((perm, e, max(ends) - min(ends)))
+    min_sp = min(r[2] for r in res)
+    best, be, bs = None, -1.0, 1e300
+    for perm, e, sp in res:
+        if sp > min_sp + tol + 1e-9:
+            continue
+        if e > be + 1e-9 or (e > be - 1e-9 and sp < bs - 1e-9):
+            best, be, bs = perm, e, sp
+    return list(best), be, bs
+
+
+@pytest.mark.skipif(not has_chain, reason="_core not built")
+def test_plan_slots_fast_forward_and_twin_pruning_match_the_full_enumeration():
+    """plan_slots simulates the context prefix before the first new pod can start once
+    (fast_forward) and skips assignments that only permute identical new pods; both give the
+    assignment, expected SLOs met and spread of simulating every assignment in full."""
+    full = CR.CorunModel.load()
+    rng = np.random.default_rng(7)
+    for _ in range(60):
+        args, ph = _random_slot_case(rng, len(full.names))
+        ref = _brute_slots(args, ph, full.alone_ms, full.coupling(), 0.05, 2.0)
+        for ff in (True, False):
+            sl, st, fin, exp, spread, _ = core.plan_slots(*args, full.alone_ms, full.coupling(), 0.05, 2.0, 720,
+                                                          *ph, fast_forward=ff)
+            assert list(sl) == ref[0] and exp == pytest.approx(ref[1], abs=1e-9) and \
+                spread == pytest.approx(ref[2], abs=1e-9), (ff, list(sl), ref)
+
+
 def test_slot_timeline_chains_unmeasured_pods_and_pins_measured_ones():
     tl = SlotTimeline(depth=4, phantoms=2)
     g = ("n0", 0)
