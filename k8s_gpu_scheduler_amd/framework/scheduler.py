@@ -540,6 +540,8 @@ class Scheduler:
 
     def run(self) -> None:
         self.start_informers()
+        from ..utils.gctune import settle
+        settle()                            # the synced caches to the permanent GC generation
         last_cleanup = time.monotonic()
         while not self._stop.is_set():
             pi = self.queue.pop(0.2)

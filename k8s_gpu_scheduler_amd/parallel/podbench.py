@@ -108,8 +108,10 @@ class ControlPlane:
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
                  slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0,
-                 effort_down: Optional[float] = None, learn_corun: bool = True, kernel_policy: str = "off"):
+                 effort_down: Optional[float] = None, learn_corun: bool = True, kernel_policy: str = "off",
+                 gc_settle: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
+        self.gc_settle = gc_settle          # utils.gctune.settle() at the warmup -> timed transition
         self.cu_per_pod = cu_per_pod
         self.qos = qos
         self.rng = random.Random(seed)
@@ -377,6 +379,9 @@ class ControlPlane:
         planner = getattr(self.plugin, "planner", None)
         if planner is not None:
             planner.realign()
+        if self.gc_settle:
+            from ..utils.gctune import settle
+            settle()                        # start-up state to the permanent GC generation
 
     def _plan_feedback(self, pods: np.ndarray) -> None:
         """Report each GPU's measured busy time for the collected epoch next to what the planner
@@ -822,6 +827,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "guaranteed: request == limit -> hard CU mask per pod")
     ap.add_argument("--backend", default="", choices=["", "nccl", "gloo"],
                     help="torch.distributed backend (default: nccl = RCCL on GPU, gloo on CPU)")
+    ap.add_argument("--gc-settle", type=int, default=1,
+                    help="control plane: collect once and freeze the start-up objects out of the GC's "
+                         "scans at the warmup -> timed transition (utils.gctune; 0 = CPython default)")
     ap.add_argument("--control-plane", default="process", choices=["process", "inline"],
                     help="run apiserver+scheduler in a separate process (default) or inside rank 0")
     ap.add_argument("--graphs", type=int, default=1, choices=[0, 1],
@@ -921,7 +929,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
                      adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort,
                      effort_down=a.cp_effort_down, learn_corun=bool(a.corun_learn),
-                     kernel_policy=a.kernel_policy)
+                     kernel_policy=a.kernel_policy, gc_settle=bool(a.gc_settle))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
         from .controlplane_proc import ControlPlaneProc

@@ -205,9 +205,12 @@ class BurstPlanner:
         if self.timeline is not None:
             import os
             from concurrent.futures import ThreadPoolExecutor
-            # the GPUs' slot plans run side by side (native, without the interpreter lock):
-            # one thread per GPU of an 8-GPU node where the host has the cores
-            n = max(1, min(8, int(os.environ.get("GPUSCHED_SLOT_THREADS", str(min(8, os.cpu_count() or 1))))))
+            # the GPUs' slot plans can run side by side (native, without the interpreter lock;
+            # GPUSCHED_SLOT_THREADS=n).  Off by default since the slot planner's context
+            # fast-forward: at ~0.05 ms per GPU the threads' interpreter-lock hand-offs cost
+            # more than they overlap (box CPU, 8 GPUs, tools/cp_breakdown.py: 1.0-2.0 ms of
+            # slot planning per epoch on 8 threads vs ~0.4 ms of native work)
+            n = max(1, min(8, int(os.environ.get("GPUSCHED_SLOT_THREADS", "1"))))
             self._pool = ThreadPoolExecutor(n, thread_name_prefix="slot-plan") if n > 1 else None
         # measured backlog feedback from pod completions (plugins.gpu.feedback; deployed
         # clusters -- the bench corrects per collected epoch instead)
@@ -614,30 +617,31 @@ class BurstPlanner:
             dev_of[g] = d
         unit = getattr(self, "_burst_unit", 0)       # the burst's smallest slot size (_plan_corun)
         c_off, f_off = [0], [0]
-        cw, cs, ce, ft, pw, pi = [], [], [], [], [], []
+        parts = []                                   # per GPU: (w, start, end, free, ph wid, ph iters)
+        nc = nf = 0
         for g in range(n_groups):
             d = dev_of[g]
             if ndev[g] == 1 and unit > 0:
                 st = states[d]
                 slots = self._free_slots(st, unit, set())
-                w, s0, s1, fr, phw, phi = self.timeline.pipeline((owner[d],) + self.plugin.corun_group_key(st),
-                                                                 slots, model, core, with_phantoms=True)
-                cw += list(w)
-                cs += list(s0)
-                ce += list(s1)
-                ft += list(fr)
-                pw += list(phw)
-                pi += list(phi)
-            c_off.append(len(cw))
-            f_off.append(len(ft))
-        if not cw and not ft:
+                p = self.timeline.pipeline((owner[d],) + self.plugin.corun_group_key(st), slots, model, core,
+                                           with_phantoms=True)
+                parts.append(p)
+                nc += len(p[0])
+                nf += len(p[3])
+            c_off.append(nc)
+            f_off.append(nf)
+        if not nc and not nf:
             return None
-        out = (np.asarray(c_off, np.int64), np.asarray(cw, np.int32), np.asarray(cs, np.float64),
-               np.asarray(ce, np.float64), np.asarray(f_off, np.int64), np.asarray(ft, np.float64))
+
+        def cat(i, dt):
+            return np.concatenate([p[i] for p in parts]).astype(dt, copy=False)
+        out = (np.asarray(c_off, np.int64), cat(0, np.int32), cat(1, np.float64), cat(2, np.float64),
+               np.asarray(f_off, np.int64), cat(3, np.float64))
         if self.pipe_phantoms:
             # per free slot, the workload its stream runs next (-1: none), chained after the
             # slot's new pod (native plan_corun)
-            out += (np.asarray(pw, np.int32), np.asarray(pi, np.float64))
+            out += (cat(4, np.int32), cat(5, np.float64))
         return out
 
     def _plan_slots(self, assign, out, states, owner, dev_group, model, core, margin: float) -> Dict[str, int]:

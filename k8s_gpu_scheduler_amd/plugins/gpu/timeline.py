@@ -229,8 +229,10 @@ class SlotTimeline:
         # planner chains after the slot's new pod: a long pod co-runs with the NEXT epoch's
         # pods too, and without them its predicted co-runners thin out and it looks safe
         po = ctx["ph_off"]
-        ph_w = np.array([ctx["ph_wid"][po[i]] if po[i + 1] > po[i] else -1 for i in range(len(po) - 1)], np.int32)
-        ph_i = np.array([ctx["ph_iters"][po[i]] if po[i + 1] > po[i] else 0.0 for i in range(len(po) - 1)])
+        has = po[1:] > po[:-1]
+        first = np.minimum(po[:-1], max(len(ctx["ph_wid"]) - 1, 0))
+        ph_w = np.where(has, ctx["ph_wid"][first] if len(ctx["ph_wid"]) else -1, -1).astype(np.int32)
+        ph_i = np.where(has, ctx["ph_iters"][first] if len(ctx["ph_iters"]) else 0.0, 0.0)
         if k == 0:
             order = np.argsort(ctx["slot_free"], kind="stable")
             free = ctx["slot_free"][order]

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -78,6 +79,53 @@ class SpinPool {
   std::atomic<int> gen_{0}, left_{0};
   std::atomic<bool> quit_{false};
   const std::function<void(int)>* fn_ = nullptr;
+};
+
+// Open-addressing map from 64-bit keys (already well mixed) to values kept in a deque, so a
+// pointer to a value stays valid while other keys are inserted (the planner's memos: a few
+// thousand inserts and several times as many lookups per plan -- a node-based map allocated per
+// insert and chased a pointer per lookup).
+template <class V>
+class FlatMap {
+ public:
+  explicit FlatMap(size_t cap = 1024) { rehash(cap); }
+  V* find(uint64_t k) {
+    for (size_t i = k & mask_;; i = (i + 1) & mask_) {
+      const int32_t x = idx_[i];
+      if (x < 0) return nullptr;
+      if (keys_[i] == k) return &vals_[(size_t)x];
+    }
+  }
+  V* insert(uint64_t k, const V& v) {        // (k must not be present)
+    if ((vals_.size() + 1) * 2 > idx_.size()) rehash(idx_.size() * 2);
+    size_t i = k & mask_;
+    while (idx_[i] >= 0) i = (i + 1) & mask_;
+    keys_[i] = k;
+    idx_[i] = (int32_t)vals_.size();
+    vals_.push_back(v);
+    return &vals_.back();
+  }
+  size_t size() const { return vals_.size(); }
+
+ private:
+  void rehash(size_t cap) {
+    std::vector<uint64_t> ok = std::move(keys_);
+    std::vector<int32_t> oi = std::move(idx_);
+    keys_.assign(cap, 0);
+    idx_.assign(cap, -1);
+    mask_ = cap - 1;
+    for (size_t j = 0; j < oi.size(); ++j) {
+      if (oi[j] < 0) continue;
+      size_t i = ok[j] & mask_;
+      while (idx_[i] >= 0) i = (i + 1) & mask_;
+      keys_[i] = ok[j];
+      idx_[i] = oi[j];
+    }
+  }
+  std::vector<uint64_t> keys_;
+  std::vector<int32_t> idx_;
+  std::deque<V> vals_;
+  size_t mask_ = 0;
 };
 
 // fin[i] = wall ms at which pod i finishes (kBig for a service pod); tput_ms[i] = ms per
@@ -596,9 +644,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       double makespan;
       double tput[kMaxK];          // iterations/s per member, in the canonical (w, it) order
     };
-    std::unordered_map<uint64_t, PlainSim> plain_memo;
-    std::unordered_map<uint64_t, std::array<double, kMaxK>> pipe_memo;
-    std::unordered_map<uint64_t, GroupEval> verdict_memo;
+    FlatMap<PlainSim> plain_memo(2048);
+    FlatMap<std::array<double, kMaxK>> pipe_memo(2048);
     std::shared_mutex sim_mu;
     std::atomic<long> n_plain{0}, n_pipe{0};
     const bool threaded = std::getenv("GPUSCHED_PLAN_THREADS") && std::atoi(std::getenv("GPUSCHED_PLAN_THREADS")) > 1;
@@ -621,15 +668,15 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       std::sort(ord, ord + k, [&](int a, int b) { return w[a] != w[b] ? w[a] < w[b] : it[a] < it[b]; });
       uint64_t hk = mix(0x5bd1e995ull, (uint64_t)k);
       for (int q = 0; q < k; ++q) hk = mix(mix(hk, (uint64_t)(uint32_t)w[ord[q]]), dbits(it[ord[q]]));
-      PlainSim ps;
-      bool hit = false;
+      // memo hits are used in place (node-based map: references stay valid across inserts)
+      const PlainSim* psp = nullptr;
       {
         std::shared_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
         if (threaded) lk.lock();
-        auto f = plain_memo.find(hk);
-        if (f != plain_memo.end()) ps = f->second, hit = true;
+        psp = plain_memo.find(hk);
       }
-      if (!hit) {
+      if (!psp) {
+        PlainSim ps;
         int32_t cw[kMaxK];
         double cit[kMaxK], fin[kMaxK];
         for (int q = 0; q < k; ++q) cw[q] = w[ord[q]], cit[q] = it[ord[q]];
@@ -646,29 +693,14 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         n_plain.fetch_add(1, std::memory_order_relaxed);
         std::unique_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
         if (threaded) lk.lock();
-        plain_memo.emplace(hk, ps);
+        psp = plain_memo.find(hk);             // (another thread may have inserted it)
+        if (!psp) psp = plain_memo.insert(hk, ps);
       }
+      const PlainSim& ps = *psp;
       GroupEval e;
       e.makespan = ps.makespan * S[g];
       const double sg = phase_b ? sigma : 0.0;      // phase A needs makespans only
-      // SLO verdicts of a simulation's members: a function of the simulation (its key) and the
-      // members' SLOs in its canonical order -- memoised with the soft objective (an erfc per
-      // member), whose sets mostly repeat simulated multisets with the same SLOs
-      auto verdicts = [&](uint64_t sim_key, const double* tput, const int* perm) {
-        uint64_t vk = 0;
-        if (sg > 0) {
-          vk = mix(sim_key, 0x51ed27ull);
-          for (int q = 0; q < k; ++q) vk = mix(vk, dbits(sl[perm[q]]));
-          std::shared_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
-          if (threaded) lk.lock();
-          auto f = verdict_memo.find(vk);
-          if (f != verdict_memo.end()) {
-            const double mk = e.makespan;
-            e = f->second;
-            e.makespan = mk;
-            return;
-          }
-        }
+      auto verdicts = [&](const double* tput, const int* perm) {
         e.ok = e.bad = 0;
         e.deficit = e.expected = 0.0;
         for (int q = 0; q < k; ++q) {
@@ -677,14 +709,9 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
           if (sl[i] <= 0 || tput[q] >= sl[i]) ++e.ok;
           else ++e.bad, e.deficit += 1.0 - tput[q] / sl[i];
         }
-        if (sg > 0) {
-          std::unique_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
-          if (threaded) lk.lock();
-          verdict_memo.emplace(vk, e);
-        }
       };
       if (!use_pipe) {
-        verdicts(hk, ps.tput, ord);
+        verdicts(ps.tput, ord);
         return e;
       }
       // SLOs on the GPU's pipeline: in-flight pods pinned, new pods at the free slot times
@@ -700,7 +727,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         for (int64_t q = f0; q < f1; ++q) nh += p_hwid.data()[q] >= 0;
       if (nc + k + nh > kMaxK) nh = 0;
       if (nc + k > kMaxK) {
-        verdicts(hk, ps.tput, ord);
+        verdicts(ps.tput, ord);
         return e;
       }
       int po[kMaxK];
@@ -714,15 +741,14 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       uint64_t hp = mix(mix(0x27d4eb2fULL, (uint64_t)g), (uint64_t)k);
       for (int q = 0; q < k; ++q)
         hp = mix(mix(mix(hp, (uint64_t)res[po[q]]), (uint64_t)(uint32_t)w[po[q]]), dbits(it[po[q]]));
-      std::array<double, kMaxK> pt;
-      bool phit = false;
+      const std::array<double, kMaxK>* ptp = nullptr;
       {
         std::shared_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
         if (threaded) lk.lock();
-        auto f = pipe_memo.find(hp);
-        if (f != pipe_memo.end()) pt = f->second, phit = true;
+        ptp = pipe_memo.find(hp);
       }
-      if (!phit) {
+      if (!ptp) {
+        std::array<double, kMaxK> pt;
         int32_t pw[kMaxK], pv[kMaxK];
         double pit[kMaxK], pst[kMaxK], pen[kMaxK], pfin[kMaxK], pso[kMaxK];
         for (int c = 0; c < nc; ++c) {
@@ -791,9 +817,10 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
         n_pipe.fetch_add(1, std::memory_order_relaxed);
         std::unique_lock<std::shared_mutex> lk(sim_mu, std::defer_lock);
         if (threaded) lk.lock();
-        pipe_memo.emplace(hp, pt);
+        ptp = pipe_memo.find(hp);
+        if (!ptp) ptp = pipe_memo.insert(hp, pt);
       }
-      verdicts(hp, pt.data(), po);
+      verdicts(ptp->data(), po);
       return e;
     };
     // memo of group evaluations per phase and thread: a sweep re-evaluates mostly the same
@@ -802,7 +829,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     // the set.
     // key: a 64-bit mix of the sorted member codes and the GPU (no allocation per lookup; a
     // collision among the few thousand sets of one plan is ~1e-12 likely)
-    using Memo = std::unordered_map<uint64_t, GroupEval>;
+    using Memo = FlatMap<GroupEval>;
     auto key_of = [](const std::vector<int>& v) {
       uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)v.size();
       for (int x : v) {
@@ -824,7 +851,7 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     T = std::max(1, std::min({T, (int)std::max(1u, std::thread::hardware_concurrency()), 16}));
     // one memo per phase shared by the threads (a reader-writer lock: lookups far outnumber
     // inserts once the first sweep has run)
-    std::array<Memo, 2> memo;
+    std::array<Memo, 2> memo{Memo(4096), Memo(4096)};
     std::shared_mutex memo_mu;
     std::atomic<long> n_evals{0};
     auto eval_set = [&](int g, std::vector<int>& v, int tid) {
@@ -837,18 +864,16 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       n_evals.fetch_add(1, std::memory_order_relaxed);
       if (T > 1) {
         std::shared_lock<std::shared_mutex> lk(memo_mu);
-        auto hit = M.find(key);
-        if (hit != M.end()) return hit->second;
-      } else {
-        auto hit = M.find(key);
-        if (hit != M.end()) return hit->second;
+        if (const GroupEval* hit = M.find(key)) return *hit;
+      } else if (const GroupEval* hit = M.find(key)) {
+        return *hit;
       }
       const GroupEval r = eval_raw(g, v);
       if (T > 1) {
         std::unique_lock<std::shared_mutex> lk(memo_mu);
-        M.emplace(key, r);
+        if (!M.find(key)) M.insert(key, r);
       } else {
-        M.emplace(key, r);
+        M.insert(key, r);
       }
       return r;
     };
@@ -871,35 +896,36 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     };
     std::vector<Cand> cand;
     std::vector<Out> res;
-    std::vector<char> gpu_seen(NG, 0);
-    struct Sig {
-      int g;
-      int32_t w;
-      double it, slo, hbm;
-      bool operator==(const Sig& o) const { return g == o.g && w == o.w && it == o.it && slo == o.slo && hbm == o.hbm; }
-    };
-    std::vector<Sig> sig_seen;
+
     std::atomic<bool> failed{false};
     std::string err;
     std::mutex err_mu;
     auto evaluate = [&](bool swap) {
       res.resize(cand.size());
       const int n = (int)cand.size();
+      // a move batch is one pod leaving one GPU for each candidate: its source group (without
+      // the pod) is the same for every candidate -- evaluated once
+      GroupEval src{};
+      if (!swap && n > 0) {
+        std::vector<int> va(mem[cand[0].ga].begin(), mem[cand[0].ga].end());
+        va.erase(std::find(va.begin(), va.end(), cand[0].a));
+        src = eval_set(cand[0].ga, va, 0);
+      }
       auto job = [&](int tid) {
         std::vector<int> va, vb;
         for (int c = tid; c < n; c += T) {
           const Cand& x = cand[c];
           try {
-            va.assign(mem[x.ga].begin(), mem[x.ga].end());
             vb.assign(mem[x.gb].begin(), mem[x.gb].end());
             if (swap) {
+              va.assign(mem[x.ga].begin(), mem[x.ga].end());
               *std::find(va.begin(), va.end(), x.a) = x.b;
               *std::find(vb.begin(), vb.end(), x.b) = x.a;
+              res[c].ea = eval_set(x.ga, va, tid);
             } else {
-              va.erase(std::find(va.begin(), va.end(), x.a));
               vb.push_back(x.a);
+              res[c].ea = src;
             }
-            res[c].ea = eval_set(x.ga, va, tid);
             res[c].eb = eval_set(x.gb, vb, tid);
           } catch (const std::exception& ex) {
             std::lock_guard<std::mutex> lk(err_mu);
@@ -930,15 +956,10 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
           // box put a 4-pod burst on one GPU of two, GPUTEST_r04.json)
           if (P >= NG && nburst[g0] <= 1) continue;
           cand.clear();
-          // one candidate per GPU: a group's evaluation depends on its GPU, not on which of its
-          // devices takes the pod, so the first feasible device of a GPU is the one a
-          // device-by-device scan would accept (the others are identical candidates after it)
-          std::fill(gpu_seen.begin(), gpu_seen.end(), 0);
           for (py::ssize_t d = 0; d < D; ++d) {
             const int g1 = DG[d];
-            if (g1 == g0 || gpu_seen[g1] || free[d] < U[p] || hfree[d] + 1e-6 < H[p]) continue;
+            if (g1 == g0 || free[d] < U[p] || hfree[d] + 1e-6 < H[p]) continue;
             if (phase_b && saturated(ge[g0]) && saturated(ge[g1])) continue;
-            gpu_seen[g1] = 1;
             cand.push_back({(int)p, (int)d, g0, g1});
           }
           if (cand.empty()) continue;
@@ -967,7 +988,6 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
           py::ssize_t j0 = i + 1;
           while (j0 < P) {
             cand.clear();
-            sig_seen.clear();
             const int di = dev[i], gi = DG[di];
             for (py::ssize_t j = j0; j < P; ++j) {
               const int dj = dev[j], gj = DG[dj];
@@ -976,11 +996,6 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
               if (phase_b && saturated(ge[gi]) && saturated(ge[gj])) continue;
               // same workload and length: a no-op for the makespans (phase A)
               if (!phase_b && wid.data()[i] == wid.data()[j] && iters.data()[i] == iters.data()[j]) continue;
-              // a partner identical to an earlier one of this batch on the same GPU (workload,
-              // length, SLO, HBM) gives the same two groups: it cannot be the first accepted
-              const Sig sg{gj, wid.data()[j], iters.data()[j], slo.data()[j], H[j]};
-              if (std::find(sig_seen.begin(), sig_seen.end(), sg) != sig_seen.end()) continue;
-              sig_seen.push_back(sg);
               cand.push_back({(int)i, (int)j, gi, gj});
             }
             if (cand.empty()) break;

@@ -1,4 +1,5 @@
-"""Control-plane throughput at N GPUs (CPU only): ms to schedule one epoch of N x 4 pods.
+"""Control-plane throughput at N GPUs (CPU only): ms to schedule one epoch of N x 4 pods
+(median over the timed epochs; `mean` includes the occasional garbage-collector pause).
 
 Two configurations: the plain GPU plugin (no burst planner) and the bench defaults (co-run
 planner with backlog carry and measured feedback; each epoch's telemetry is fed back from the
@@ -24,9 +25,11 @@ def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
     import virtual_node_bench as V
     V.N_GPUS = n
     V.SIM.update(on=True, sigma=0.05, rng=np.random.default_rng(0), speed=[])
-    cp = ControlPlane(n, 4, 20, 0, **kwargs)
+    cp = ControlPlane(n, 4, 20, 0, gc_settle=os.environ.get("CP_GC_SETTLE", "1") == "1", **kwargs)
     ts = []
     for e in range(warm + epochs):
+        if e == warm:
+            cp.reset_stats()                 # the bench's warmup -> timed transition (GC settle)
         cp.finish_live()
         t = time.perf_counter()
         arr = cp.schedule_epoch()
@@ -34,7 +37,7 @@ def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
             ts.append(time.perf_counter() - t)
         if kwargs:
             V.epoch(cp, None, arr, "t")      # telemetry back into the control plane (not timed)
-    return float(np.median(ts))
+    return float(np.median(ts)), float(np.mean(ts))
 
 
 CONFIGS = [("plain", {}), ("bench-defaults", BENCH)]
@@ -51,6 +54,7 @@ for r in range(rounds):
         for n in ((int(only),) if only else (1, 2, 4, 8)):
             res.setdefault((name, n), []).append(run(n, kw))
 for (name, n), v in res.items():
-    dt = float(np.median(v))
-    print(f"{name} gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}"
-          + (f" rounds={[round(x * 1e3, 2) for x in v]}" if rounds > 1 else ""), flush=True)
+    dt = float(np.median([x[0] for x in v]))
+    mean = float(np.median([x[1] for x in v]))
+    print(f"{name} gpus={n} pods/epoch={4 * n} ms/epoch={dt * 1e3:.2f} mean={mean * 1e3:.2f} ms/pod={dt * 1e3 / (4 * n):.3f}"
+          + (f" rounds={[round(x[0] * 1e3, 2) for x in v]}" if rounds > 1 else ""), flush=True)
