@@ -428,6 +428,8 @@ class ControlPlane:
         planner = getattr(self.plugin, "planner", None)
         if planner is None:
             return None
+        if hasattr(planner, "flush"):
+            planner.flush()
         st = dict(planner.stats)
         n = st.get("model_slot_plans", 0)
         if n > 0:       # only when the co-run model's slot plans ran ("auto" at N=1 resolves to lpt)

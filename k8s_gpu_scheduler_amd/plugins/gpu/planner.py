@@ -224,6 +224,12 @@ class BurstPlanner:
                       "slot_pred_met": 0, "slot_spread_ms": 0.0, "slot_min_spread_ms": 0.0}
         self.budget_ms = 0.0
         self.budget: Optional[EffortController] = None
+        # slot plans still running on the native batch thread (_plan_slots): resolved when one of
+        # their pods is asked for (plan), before the next burst and before stats are read
+        import os as _os
+        self.slots_async = _os.environ.get("GPUSCHED_SLOTS_ASYNC", "1") != "0"
+        self._slot_pending: Optional[Dict[str, Any]] = None
+        self._slot_job_of: Dict[str, int] = {}
         import time
         self.clock = time.perf_counter          # plan timing (a test may script it)
 
@@ -302,6 +308,10 @@ class BurstPlanner:
         key = O.key(pod)
         hit = self.plans.get(key)
         if hit is not None:
+            j = self._slot_job_of.get(key)
+            if j is not None:
+                self._resolve_slots(j)
+                hit = self.plans.get(key)
             return hit
         from ... import _native
         core = _native.core()
@@ -441,6 +451,7 @@ class BurstPlanner:
     def _plan_corun(self, pod: Obj, nodes: List[str], model: Any, core: Any) -> Optional[Tuple[str, str]]:
         plugin = self.plugin
         key = O.key(pod)
+        self._resolve_slots()
         placed = [(nd, st) for nd in nodes for st in plugin.ledger.devices(nd) if st.device.healthy]
         if not placed:
             return None
@@ -546,6 +557,7 @@ class BurstPlanner:
         if self.timeline is not None:
             self.timeline.next_burst()
         if self.slot_policy == "model" or (self.slot_policy == "auto" and n_groups >= 2):
+            self._trigger_key = key
             slot_of = self._plan_slots(assign, out, states, owner, dev_group, model, core, margin)
         elif self.slot_policy in ("lpt", "auto"):
             slot_of = self._lpt_slots(assign, out, states, model)
@@ -566,6 +578,7 @@ class BurstPlanner:
 
     def _taken_slots(self) -> Dict[str, set]:
         """First units of the slots planned for still-pending pods, per device."""
+        self._resolve_slots()
         taken: Dict[str, set] = {}
         for k, pl in self.plans.items():
             if len(pl) > 2 and pl[2] is not None and k in self.plugin._pending_by_key:
@@ -652,6 +665,7 @@ class BurstPlanner:
         if not hasattr(core, "plan_slots"):
             return {}
         plugin = self.plugin
+        trigger = getattr(self, "_trigger_key", None)
         per_group_devs: Dict[int, int] = {}
         for g in dev_group:
             per_group_devs[g] = per_group_devs.get(g, 0) + 1
@@ -683,29 +697,80 @@ class BurstPlanner:
                     model.alone_ms, model.coupling(), float(self.slot_sigma), float(self.spread_ms), 720,
                     ctx["ph_off"], ctx["ph_wid"], ctx["ph_iters"])
             jobs.append((items, slots, ctx, args))
-        # the GPUs' slot plans are independent and the native call runs without the interpreter
-        # lock: several at once on the planner's worker threads
+        # the GPUs' slot plans are independent; only the first pod's is needed now.  Async (the
+        # default): one native batch thread runs them, the triggering pod's GPU first, while the
+        # burst's other pods go through their cycles; each is resolved when its pod is planned
+        # (plan), so the ~0.1 ms per GPU overlaps the Python scheduling work instead of adding to
+        # it.  Else: on the planner's worker threads (GPUSCHED_SLOT_THREADS) or in turn.
+        if self.slots_async and len(jobs) > 1 and hasattr(core, "plan_slots_async"):
+            first = next((i for i, jb in enumerate(jobs) if any(O.key(p) == trigger for p, _ in jb[0])), 0)
+            jobs.insert(0, jobs.pop(first))
+            batch = core.plan_slots_async([tuple(jb[3]) + (True,) for jb in jobs])
+            self._slot_pending = {"batch": batch, "jobs": jobs, "margin": margin, "left": set(range(len(jobs)))}
+            for j, jb in enumerate(jobs):
+                for p, _ in jb[0]:
+                    self._slot_job_of[O.key(p)] = j
+            res.update(self._slot_result(0, batch.result(0)))
+            return res
         if len(jobs) > 1 and self._pool is not None:
             outs = list(self._pool.map(lambda j: core.plan_slots(*j[3]), jobs))
         else:
             outs = [core.plan_slots(*j[3]) for j in jobs]
-        for (items, slots, ctx, _), (sl, st0, fin, exp, spread, min_spread) in zip(jobs, outs):
-            for (p, _), s in zip(items, sl):
-                res[O.key(p)] = slots[int(s)][0]
-            self.stats["slot_plans"] += 1
-            self.stats["slot_pods"] += len(items)
-            self.stats["model_slot_plans"] += 1
-            self.stats["model_slot_pods"] += len(items)
-            # the new pods predicted to meet their SLO on the chosen slots (hard counts; `exp`
-            # also covers the unmeasured context pods the choice re-predicts)
-            m0 = len(ctx["wid"])
-            for j, (_, r) in enumerate(items):
-                d_ms = float(fin[m0 + j] - st0[m0 + j])
-                if r.slo <= 0 or (d_ms > 0 and r.iters / d_ms * 1e3 >= r.slo * margin):
-                    self.stats["slot_pred_met"] += 1
-            self.stats["slot_spread_ms"] += float(spread)
-            self.stats["slot_min_spread_ms"] += float(min_spread)
+        for jb, out in zip(jobs, outs):
+            res.update(self._apply_slot_plan(jb, out, margin))
         return res
+
+    def _apply_slot_plan(self, job, out, margin: float) -> Dict[str, int]:
+        """One GPU's slot plan: the pods' slots, and the slot-plan stats."""
+        items, slots, ctx, _ = job
+        sl, st0, fin, exp, spread, min_spread = out
+        res = {}
+        for (p, _), s in zip(items, sl):
+            res[O.key(p)] = slots[int(s)][0]
+        self.stats["slot_plans"] += 1
+        self.stats["slot_pods"] += len(items)
+        self.stats["model_slot_plans"] += 1
+        self.stats["model_slot_pods"] += len(items)
+        # the new pods predicted to meet their SLO on the chosen slots (hard counts; `exp`
+        # also covers the unmeasured context pods the choice re-predicts)
+        m0 = len(ctx["wid"])
+        for j, (_, r) in enumerate(items):
+            d_ms = float(fin[m0 + j] - st0[m0 + j])
+            if r.slo <= 0 or (d_ms > 0 and r.iters / d_ms * 1e3 >= r.slo * margin):
+                self.stats["slot_pred_met"] += 1
+        self.stats["slot_spread_ms"] += float(spread)
+        self.stats["slot_min_spread_ms"] += float(min_spread)
+        return res
+
+    def _slot_result(self, j: int, out) -> Dict[str, int]:
+        pend = self._slot_pending
+        pend["left"].discard(j)
+        res = self._apply_slot_plan(pend["jobs"][j], out, pend["margin"])
+        for p, _ in pend["jobs"][j][0]:
+            self._slot_job_of.pop(O.key(p), None)
+        if not pend["left"]:
+            pend["batch"].join()
+            self._slot_pending = None
+        return res
+
+    def _resolve_slots(self, j: Optional[int] = None) -> None:
+        """Collect pending async slot plans (job j, or all) into the pods' plans."""
+        pend = self._slot_pending
+        if pend is None:
+            return
+        for i in ([j] if j is not None else sorted(pend["left"])):
+            if i not in pend["left"]:
+                continue
+            for k, u0 in self._slot_result(i, pend["batch"].result(i)).items():
+                pl = self.plans.get(k)
+                if pl is not None:
+                    self.plans[k] = (pl[0], pl[1], u0)
+            if self._slot_pending is None:
+                break
+
+    def flush(self) -> None:
+        """Finish every pending slot plan (stats readers; tests)."""
+        self._resolve_slots()
 
     def placed(self, pod: Obj, node: str, choice: Any, req: Any) -> None:
         """Reserve: the pod took `choice` -- append it to its GPU's slot timeline, and record

@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
 #include <deque>
 #include <array>
 #include <atomic>
@@ -1119,10 +1121,27 @@ py::tuple chain_times(I32 wid, F64 iters, F64 start, I32 prev, F64 alone, F64 cm
 // them the pipeline looks emptier than it will be and every prediction is optimistic (measured
 // on MI355X bench traces: -24 % mean log error, ~0 with three phantoms per slot repeating the
 // slot's recent workloads).  Phantoms press on the others; they are never counted.
-py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin, F64 c_slo, I32 slot_tail,
-                     F64 slot_free, I32 n_wid, F64 n_iters, F64 n_slo, F64 n_rel, F64 alone, F64 cmat, double sigma,
-                     double spread_tol, int max_enum, py::object ph_off_o, py::object ph_wid_o, py::object ph_it_o,
-                     bool fast_forward) {
+// plan_slots' inputs, validated and owned (so a batch can run on another thread without the
+// interpreter), and its result
+struct SlotJob {
+  int W = 0, m = 0, S = 0, n = 0;
+  std::vector<int32_t> c_wid, c_prev, slot_tail, n_wid, PW;
+  std::vector<double> c_iters, c_start, c_pin, c_slo, slot_free, n_iters, n_slo, n_rel, alone, cmat, PI;
+  std::vector<int64_t> PO;
+  double sigma = 0.05, spread_tol = 0.0;
+  int max_enum = 720;
+  bool fast_forward = true;
+};
+struct SlotOut {
+  std::vector<int32_t> best;
+  std::vector<double> st, fin;
+  double best_e = 0.0, best_sp = 0.0, min_sp = 0.0;
+};
+
+SlotJob make_slot_job(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin, F64 c_slo, I32 slot_tail,
+                      F64 slot_free, I32 n_wid, F64 n_iters, F64 n_slo, F64 n_rel, F64 alone, F64 cmat, double sigma,
+                      double spread_tol, int max_enum, py::object ph_off_o, py::object ph_wid_o, py::object ph_it_o,
+                      bool fast_forward) {
   int W;
   check_model(alone, cmat, W);
   const int m = (int)c_wid.shape(0), S = (int)slot_tail.shape(0), n = (int)n_wid.shape(0);
@@ -1140,9 +1159,9 @@ py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin,
     if (c_prev.data()[i] >= i) throw std::runtime_error("plan_slots: prev must point to an earlier member");
   for (int s = 0; s < S; ++s)
     if (slot_tail.data()[s] < -1 || slot_tail.data()[s] >= m) throw std::runtime_error("plan_slots: bad slot tail");
-  std::vector<int64_t> PO(S + 1, 0);
-  std::vector<int32_t> PW;
-  std::vector<double> PI;
+  SlotJob J;
+  J.W = W, J.m = m, J.S = S, J.n = n;
+  J.PO.assign(S + 1, 0);
   if (!ph_off_o.is_none()) {
     I64 po = ph_off_o.cast<I64>();
     I32 pw = ph_wid_o.cast<I32>();
@@ -1152,27 +1171,47 @@ py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin,
     for (int q = 0; q < S; ++q)
       if (po.data()[q + 1] < po.data()[q]) throw std::runtime_error("plan_slots: phantom offsets");
     check_wids(pw.data(), pw.shape(0), W, "plan_slots phantoms");
-    PO.assign(po.data(), po.data() + S + 1);
-    PW.assign(pw.data(), pw.data() + pw.shape(0));
-    PI.assign(pi.data(), pi.data() + pi.shape(0));
+    J.PO.assign(po.data(), po.data() + S + 1);
+    J.PW.assign(pw.data(), pw.data() + pw.shape(0));
+    J.PI.assign(pi.data(), pi.data() + pi.shape(0));
   }
+  if (m + n + (int)J.PW.size() > kMaxK) throw std::runtime_error("plan_slots: more than 64 members with phantoms");
+  auto cp32 = [](const I32& a) { return std::vector<int32_t>(a.data(), a.data() + a.size()); };
+  auto cp64 = [](const F64& a) { return std::vector<double>(a.data(), a.data() + a.size()); };
+  J.c_wid = cp32(c_wid), J.c_prev = cp32(c_prev), J.slot_tail = cp32(slot_tail), J.n_wid = cp32(n_wid);
+  J.c_iters = cp64(c_iters), J.c_start = cp64(c_start), J.c_pin = cp64(c_pin), J.c_slo = cp64(c_slo);
+  J.slot_free = cp64(slot_free), J.n_iters = cp64(n_iters), J.n_slo = cp64(n_slo), J.n_rel = cp64(n_rel);
+  J.alone = cp64(alone), J.cmat = cp64(cmat);
+  J.sigma = sigma, J.spread_tol = spread_tol, J.max_enum = max_enum, J.fast_forward = fast_forward;
+  return J;
+}
+
+// The slot plan itself (no Python objects: runs without the interpreter lock)
+SlotOut run_slot_job(const SlotJob& J) {
+  const int W = J.W, m = J.m, S = J.S, n = J.n;
+  const std::vector<int64_t>& PO = J.PO;
+  const std::vector<int32_t>& PW = J.PW;
+  const std::vector<double>& PI = J.PI;
+  const double sigma = J.sigma, spread_tol = J.spread_tol;
+  const int max_enum = J.max_enum;
+  const bool fast_forward = J.fast_forward;
   const int nph = (int)PW.size();
   if (m + n + nph > kMaxK) throw std::runtime_error("plan_slots: more than 64 members with phantoms");
   const int k = m + n + nph;
   int32_t w[kMaxK], pv[kMaxK];
   double it[kMaxK], s0[kMaxK], pe[kMaxK], sl[kMaxK];
   for (int i = 0; i < m; ++i) {
-    w[i] = c_wid.data()[i];
-    it[i] = c_iters.data()[i];
-    s0[i] = c_start.data()[i];
-    pv[i] = c_prev.data()[i];
-    pe[i] = c_pin.data()[i];
-    sl[i] = c_slo.data()[i];
+    w[i] = J.c_wid[i];
+    it[i] = J.c_iters[i];
+    s0[i] = J.c_start[i];
+    pv[i] = J.c_prev[i];
+    pe[i] = J.c_pin[i];
+    sl[i] = J.c_slo[i];
   }
   for (int j = 0; j < n; ++j) {
-    w[m + j] = n_wid.data()[j];
-    it[m + j] = n_iters.data()[j];
-    sl[m + j] = n_slo.data()[j];
+    w[m + j] = J.n_wid[j];
+    it[m + j] = J.n_iters[j];
+    sl[m + j] = J.n_slo[j];
     pe[m + j] = 0.0;
   }
   for (int q = 0; q < nph; ++q) {
@@ -1182,11 +1221,11 @@ py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin,
     pe[m + n + q] = 0.0;
     s0[m + n + q] = -kBig;
   }
-  const int32_t* T = slot_tail.data();
-  const double* F = slot_free.data();
-  const double* R = n_rel.data();
-  const double* A = alone.data();
-  const double* Cm = cmat.data();
+  const int32_t* T = J.slot_tail.data();
+  const double* F = J.slot_free.data();
+  const double* R = J.n_rel.data();
+  const double* A = J.alone.data();
+  const double* Cm = J.cmat.data();
   struct Res {
     double expected = -1.0, spread = kBig;
   };
@@ -1360,7 +1399,6 @@ py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin,
   std::vector<int> best(n), cur(n);
   double best_e = -1.0, best_sp = kBig, min_sp = kBig;
   {
-    py::gil_scoped_release nogil;
     // number of injective assignments S! / (S - n)!
     double count = 1.0;
     for (int j = 0; j < n; ++j) count *= (double)(S - j);
@@ -1469,14 +1507,107 @@ py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin,
       }
     }
   }
-  py::array_t<int32_t> out(n);
-  py::array_t<double> st_a(k), fin_a(k);
-  for (int j = 0; j < n; ++j) out.mutable_data()[j] = best[j];
+  SlotOut o;
+  o.best.assign(best.begin(), best.end());
+  o.st.assign(k, 0.0);
+  o.fin.assign(k, 0.0);
   {
-    const Res r = eval(best.data(), st_a.mutable_data(), fin_a.mutable_data());
+    const Res r = eval(best.data(), o.st.data(), o.fin.data());
     if (n == 0) best_sp = min_sp = r.spread;
   }
-  return py::make_tuple(out, st_a, fin_a, best_e, best_sp, min_sp);
+  o.best_e = best_e, o.best_sp = best_sp, o.min_sp = min_sp;
+  return o;
+}
+
+py::tuple slot_out_tuple(const SlotOut& o) {
+  py::array_t<int32_t> out((py::ssize_t)o.best.size());
+  py::array_t<double> st_a((py::ssize_t)o.st.size()), fin_a((py::ssize_t)o.fin.size());
+  std::copy(o.best.begin(), o.best.end(), out.mutable_data());
+  std::copy(o.st.begin(), o.st.end(), st_a.mutable_data());
+  std::copy(o.fin.begin(), o.fin.end(), fin_a.mutable_data());
+  return py::make_tuple(out, st_a, fin_a, o.best_e, o.best_sp, o.min_sp);
+}
+
+py::tuple plan_slots(I32 c_wid, F64 c_iters, F64 c_start, I32 c_prev, F64 c_pin, F64 c_slo, I32 slot_tail,
+                     F64 slot_free, I32 n_wid, F64 n_iters, F64 n_slo, F64 n_rel, F64 alone, F64 cmat, double sigma,
+                     double spread_tol, int max_enum, py::object ph_off_o, py::object ph_wid_o, py::object ph_it_o,
+                     bool fast_forward) {
+  const SlotJob J = make_slot_job(c_wid, c_iters, c_start, c_prev, c_pin, c_slo, slot_tail, slot_free, n_wid, n_iters,
+                                  n_slo, n_rel, alone, cmat, sigma, spread_tol, max_enum, ph_off_o, ph_wid_o, ph_it_o,
+                                  fast_forward);
+  SlotOut o;
+  {
+    py::gil_scoped_release nogil;
+    o = run_slot_job(J);
+  }
+  return slot_out_tuple(o);
+}
+
+// Several GPUs' slot plans on one background thread (plan_slots_async): the burst planner needs
+// the first pod's slot at once and the others only when their pods reach Reserve, so the native
+// work overlaps the scheduling cycles of the burst's other pods.  result(i) waits (without the
+// interpreter lock) for job i; jobs run in order.
+class SlotBatch {
+ public:
+  explicit SlotBatch(std::vector<SlotJob> jobs)
+      : jobs_(std::move(jobs)), outs_(jobs_.size()), errs_(jobs_.size()), done_(jobs_.size(), 0) {
+    th_ = std::thread([this] {
+      for (size_t i = 0; i < jobs_.size(); ++i) {
+        try {
+          outs_[i] = run_slot_job(jobs_[i]);
+        } catch (const std::exception& e) {
+          errs_[i] = e.what();
+          if (errs_[i].empty()) errs_[i] = "plan_slots failed";
+        }
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          done_[i] = 1;
+        }
+        cv_.notify_all();
+      }
+    });
+  }
+  ~SlotBatch() { join(); }
+  void join() {
+    if (th_.joinable()) th_.join();
+  }
+  size_t size() const { return jobs_.size(); }
+  py::tuple result(int i) {
+    if (i < 0 || (size_t)i >= jobs_.size()) throw std::out_of_range("SlotBatch: job index");
+    {
+      py::gil_scoped_release nogil;
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return done_[(size_t)i] != 0; });
+    }
+    if (!errs_[(size_t)i].empty()) throw std::runtime_error(errs_[(size_t)i]);
+    return slot_out_tuple(outs_[(size_t)i]);
+  }
+
+ private:
+  std::vector<SlotJob> jobs_;
+  std::vector<SlotOut> outs_;
+  std::vector<std::string> errs_;
+  std::vector<char> done_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread th_;
+};
+
+std::unique_ptr<SlotBatch> plan_slots_async(py::list jobs) {
+  std::vector<SlotJob> js;
+  js.reserve(jobs.size());
+  for (py::handle h : jobs) {
+    py::tuple a = h.cast<py::tuple>();
+    if (a.size() != 21) throw std::runtime_error("plan_slots_async: each job is plan_slots' 21 arguments");
+    js.push_back(make_slot_job(a[0].cast<I32>(), a[1].cast<F64>(), a[2].cast<F64>(), a[3].cast<I32>(),
+                               a[4].cast<F64>(), a[5].cast<F64>(), a[6].cast<I32>(), a[7].cast<F64>(),
+                               a[8].cast<I32>(), a[9].cast<F64>(), a[10].cast<F64>(), a[11].cast<F64>(),
+                               a[12].cast<F64>(), a[13].cast<F64>(), a[14].cast<double>(), a[15].cast<double>(),
+                               a[16].cast<int>(), py::reinterpret_borrow<py::object>(a[17]),
+                               py::reinterpret_borrow<py::object>(a[18]), py::reinterpret_borrow<py::object>(a[19]),
+                               a[20].cast<bool>()));
+  }
+  return std::make_unique<SlotBatch>(std::move(js));
 }
 
 }  // namespace
@@ -1490,6 +1621,12 @@ void register_corun(py::module_& m) {
         py::arg("sigma") = 0.05, py::arg("spread_tol") = 0.0, py::arg("max_enum") = 720,
         py::arg("ph_off") = py::none(), py::arg("ph_wid") = py::none(), py::arg("ph_iters") = py::none(),
         py::arg("fast_forward") = true);
+  py::class_<SlotBatch>(m, "SlotBatch")
+      .def("result", &SlotBatch::result, py::arg("i"))
+      .def("join", &SlotBatch::join, py::call_guard<py::gil_scoped_release>())
+      .def("__len__", &SlotBatch::size);
+  m.def("plan_slots_async", &plan_slots_async, py::arg("jobs"),
+        "Start several plan_slots jobs (tuples of its 21 positional arguments) on a background thread");
   m.def("corun_times", &corun_times, py::arg("wids"), py::arg("iters"), py::arg("mask"), py::arg("starts"),
         py::arg("alone_ms"), py::arg("cmat"), py::arg("pin_end") = py::none());
   m.def("corun_gpu_eval", &corun_gpu_eval, py::arg("off"), py::arg("r_wid"), py::arg("r_iters"), py::arg("r_slo"),

@@ -353,3 +353,35 @@ def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
     for _ in range(6):
         step(20, 5.6)                         # 28 %: level 1 (78 / 56 x 5.6 = 7.8 ms) fits 70 % of 20
     assert pl.effort == 1
+
+
+@pytest.mark.skipif(not (has_chain and hasattr(core, "plan_slots_async")), reason="_core not built")
+def test_async_slot_plans_give_the_synchronous_placements():
+    """The burst planner starts the GPUs' slot plans on the native batch thread and resolves each
+    when its pod is planned (planner.slots_async): an 8-GPU control plane at the bench defaults
+    makes exactly the placements -- GPU, slot, policy -- of the synchronous slot plans, epoch by
+    epoch, with the measured timelines fed back in between."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import virtual_node_bench as V
+    from k8s_gpu_scheduler_amd.parallel.podbench import ControlPlane
+    # (the online co-run learner off, as in the bench: its background refits land at wall-clock
+    # dependent epochs)
+    bench = dict(balance=1.0, plan_bursts=True, plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05,
+                 plan_carry=1.0, plan_feedback=True, plan_slots="auto", learn_corun=False)
+    runs = {}
+    for async_ in (True, False):
+        V.N_GPUS = 8
+        V.SIM.update(on=True, sigma=0.05, rng=np.random.default_rng(0), speed=[])
+        cp = ControlPlane(8, 4, 20, 0, **bench)
+        cp.plugin.planner.slots_async = async_
+        arrs = []
+        for _ in range(14):
+            cp.finish_live()
+            arr = cp.schedule_epoch()
+            arrs.append(np.array(arr, copy=True))
+            V.epoch(cp, None, arr, "t")
+        st = cp.planner_stats()
+        runs[async_] = (arrs, st["model_slot_plans"], st["slot_pods"])
+    assert runs[True][1] == runs[False][1] > 0 and runs[True][2] == runs[False][2]
+    for a, b in zip(runs[True][0], runs[False][0]):
+        assert np.array_equal(a, b)

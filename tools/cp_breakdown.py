@@ -19,7 +19,7 @@ from k8s_gpu_scheduler_amd.plugins.gpu import planner as P  # noqa: E402
 from k8s_gpu_scheduler_amd.plugins.gpu import timeline as TL  # noqa: E402
 
 BENCH = dict(balance=1.0, plan_bursts=True, plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05,
-             plan_carry=1.0, plan_feedback=True, plan_slots="auto")
+             plan_carry=1.0, plan_feedback=True, plan_slots="auto", learn_corun=False)
 acc = {}
 
 
@@ -50,7 +50,8 @@ def main() -> None:
     for lvl in levels:
         V.N_GPUS = 8
         V.SIM.update(on=True, sigma=0.05, rng=np.random.default_rng(0), speed=[])
-        cp = ControlPlane(8, 4, 20, 0, **(dict(BENCH, effort=lvl) if lvl else BENCH))
+        kw = {} if lvl < 0 else (dict(BENCH, effort=lvl) if lvl else BENCH)     # -1: plain plugin
+        cp = ControlPlane(8, 4, 20, 0, **kw)
         for _ in range(10):
             cp.finish_live()
             V.epoch(cp, None, cp.schedule_epoch(), "t")
@@ -65,18 +66,23 @@ def main() -> None:
             from k8s_gpu_scheduler_amd.utils.gctune import settle
             settle()
         acc.clear()
+        fw = cp.sched.frameworks[next(iter(cp.sched.frameworks))]
+        fw.metrics.ext_ns.clear()
+        fw.metrics.ext_calls.clear()
         ts = []
         for _ in range(60):
             cp.finish_live()
             t = time.perf_counter()
             arr = cp.schedule_epoch()
             ts.append(time.perf_counter() - t)
-            V.epoch(cp, None, arr, "t")
+            if kw:
+                V.epoch(cp, None, arr, "t")
         if mode == "off":
             gc.enable()
         parts = " ".join(f"{k}={v / 60 * 1e3:.3f}" for k, v in sorted(acc.items(), key=lambda x: -x[1]))
+        ext = " ".join(f"{k}={v / 60 / 1e6:.3f}" for k, v in sorted(fw.metrics.ext_ns.items(), key=lambda x: -x[1]))
         print(f"gc={mode or 'default'} level {lvl}: epoch {np.median(ts) * 1e3:.2f} ms (median) "
-              f"{np.mean(ts) * 1e3:.2f} (mean) | {parts}", flush=True)
+              f"{np.mean(ts) * 1e3:.2f} (mean) | {parts} || extension points ms/epoch: {ext}", flush=True)
 
 
 if __name__ == "__main__":

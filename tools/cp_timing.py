@@ -4,7 +4,8 @@
 Two configurations: the plain GPU plugin (no burst planner) and the bench defaults (co-run
 planner with backlog carry and measured feedback; each epoch's telemetry is fed back from the
 co-run model, as `tools/virtual_node_bench.py --simulate` does), so the planner's full
-per-epoch cost is in the figure.
+per-epoch cost is in the figure.  The online co-run learner is off, as in the bench since round 5
+(`--corun-learn 0`: its refits never landed inside a driver-length run).
 """
 import os
 import sys
@@ -18,7 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from k8s_gpu_scheduler_amd.parallel.podbench import ControlPlane  # noqa: E402
 
 BENCH = dict(balance=1.0, plan_bursts=True, plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05,
-             plan_carry=1.0, plan_feedback=True, plan_slots="auto")
+             plan_carry=1.0, plan_feedback=True, plan_slots="auto", learn_corun=False)
 
 
 def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
