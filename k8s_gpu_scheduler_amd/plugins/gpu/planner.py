@@ -78,8 +78,8 @@ class EffortController:
     CPU: profiles/r04_cp_rehearsal/jump_first/)."""
 
     # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py:
-    # 8.1 / 6.3 / 4.5 / 4.1 ms, profiles/r04_cp2/)
-    LEVEL_COST = (1.0, 0.78, 0.56, 0.5)
+    # 5.75 / 4.86 / 3.87 / 3.59 ms, profiles/r05_cp2/; round 4: 8.1 / 6.3 / 4.5 / 4.1)
+    LEVEL_COST = (1.0, 0.845, 0.673, 0.624)
 
     def __init__(self, planner: "BurstPlanner", down: float = 0.85, up: float = 0.5, target: float = 0.7,
                  settle: int = 3, window: int = 6):
