@@ -211,6 +211,7 @@ class ControlPlane:
         # cheaper effort level (planner.set_effort), and climbs back when there is room
         self.adaptive = adaptive
         self._last_start: Optional[float] = None
+        self._side_s = 0.0                  # finish_live + update_telemetry since the last schedule
         # the effort rule itself is the planner's (plugins.gpu.planner.EffortController): here
         # the time a plan may take is the pipeline period (the interval between schedule requests)
         self._effort = None
@@ -218,7 +219,7 @@ class ControlPlane:
         if planner is not None:
             from ..plugins.gpu.planner import EffortController
             self._effort = EffortController(planner, down=float(effort_down) if effort_down is not None else self.EFFORT_DOWN,
-                                            up=0.5, target=0.7, settle=3)
+                                            up=self.EFFORT_UP, target=0.7, settle=3)
             if os.environ.get("GPUSCHED_EFFORT_DEBUG"):
                 self._effort.debug = lambda msg: print(f"[effort] epoch {self.epoch} {msg}", file=sys.stderr, flush=True)
         self.effort_epochs: Dict[int, int] = {}
@@ -238,19 +239,25 @@ class ControlPlane:
         return out
 
     def finish_live(self) -> None:
+        t0 = time.perf_counter()
         for ns, name in self.live:
             try:
                 self.fc.delete("pods", name, ns)
             except Exception:
                 pass
         self.live = []
+        self._side_s += time.perf_counter() - t0
 
     EFFORT_DOWN = 0.85       # share of the pipeline period over which the planner steps down
+    # ... and under which it steps back up (when the next level is predicted to fit 70 %): 0.6
+    # since round 5's cheaper levels -- at 0.5 a level-2 control plane on the 8-rank rehearsal
+    # (3.9 of a ~7.6 ms period) never climbed back to level 1 (4.9 ms)
+    EFFORT_UP = 0.6
 
     def _adapt_effort(self, t0: float) -> None:
         """Adaptive planning effort (GPU runs): the control plane must schedule an epoch within
         the pipeline's period or it paces the GPUs (EffortController, the allowed time being the
-        interval between consecutive schedule requests; thresholds 85 % down / 50 % up, jump
+        interval between consecutive schedule requests; thresholds 85 % down / 60 % up, jump
         target 70 %, the control plane runs in its own process, overlapped with the GPUs)."""
         planner = getattr(self.plugin, "planner", None)
         if planner is None or self._effort is None:
@@ -306,7 +313,10 @@ class ControlPlane:
         dt = time.perf_counter() - t0
         self.sched_s += dt
         if self.epoch > 1 and self._effort is not None:   # the first epoch pays one-time costs
-            self._effort.add_cost(dt)
+            # the control plane's whole serial work per epoch: this schedule plus the pod
+            # deletions and telemetry it processed since the last one (its process does all three)
+            self._effort.add_cost(dt + self._side_s)
+        self._side_s = 0.0
         return arr
 
     # GEMM-heavy: at least this share of the pod's alone roofline time is MFMA work
@@ -507,6 +517,13 @@ class ControlPlane:
     def update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
         """per_gpu[g] = (busy_unit_ms, pods, slo_ok, hbm_used_gib[, per-workload
         (sum of observed GPU-seconds per iteration, pods) x len(W.NAMES)])."""
+        t0 = time.perf_counter()
+        try:
+            self._update_telemetry(per_gpu, wall_ms)
+        finally:
+            self._side_s += time.perf_counter() - t0
+
+    def _update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
         per_gpu = np.asarray(per_gpu, dtype=np.float64)
         smi = per_gpu.shape[1] >= TELE
         if smi:

@@ -39,6 +39,8 @@ for n in ("_plan_corun", "_plan_slots", "_pipe_context", "_burst", "_carry", "pl
     if hasattr(P.BurstPlanner, n):
         _wrap(P.BurstPlanner, n, n)
 _wrap(TL.SlotTimeline, "_context", "timeline._context")
+_wrap(ControlPlane, "update_telemetry", "cp.update_telemetry(outside the epoch)")
+_wrap(ControlPlane, "finish_live", "cp.finish_live(outside the epoch)")
 _wrap(TL.SlotTimeline, "pipeline", "timeline.pipeline")
 _wrap(_core, "plan_corun", "native.plan_corun")
 _wrap(_core, "plan_slots", "native.plan_slots(sum over threads)")
