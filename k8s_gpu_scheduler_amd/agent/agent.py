@@ -213,6 +213,8 @@ class NodeAgent:
         with evict_unhealthy, delete the pods assigned to newly failed devices."""
         if samples is None:
             samples = self.source.samples()
+        if not samples and not getattr(self.source, "has_telemetry", True):
+            return False                     # no telemetry source: no verdicts to reach
         before = self.health.unhealthy()
         devs = self.source.devices()
         changed = self.health.update(samples, devs)

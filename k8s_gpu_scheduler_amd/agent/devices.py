@@ -129,6 +129,9 @@ class StaticSource(DeviceSource):
         self.desc = list(descriptors)
         self.topo = topology
         self._samples = samples or []
+        # a source built without a sample list (synthetic nodes) has no telemetry at all: the
+        # health monitor then has nothing to judge -- its devices must not turn "unresponsive"
+        self.has_telemetry = samples is not None
         self.partition_calls: List[tuple] = []
         self.profiles = MI355X_PROFILES if profiles is None else profiles
         self.memory_partition = memory_partition

@@ -125,3 +125,17 @@ def test_ecc_failure_evicts_pods_when_enabled():
     assert ag.evicted == [O.key(victim)]
     names = {O.name(p) for p in fc.list("pods")[0]}
     assert O.name(victim) not in names and len(names) == 3
+
+
+def test_synthetic_node_without_telemetry_stays_healthy():
+    """A synthetic node (`agent --synthetic N`) has no telemetry source: its devices must not
+    turn "unresponsive" after miss_max empty polls (they did, and a system test binding a pod
+    a second after the agent started raced the flip under load)."""
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n1", gpus=0))
+    r = Redis(backend=FakeRedisBackend(FakeRedisEngine()))
+    ag = NodeAgent("n1", r, synthetic_node(4, node="n1"), client=fc)
+    for _ in range(6):
+        ag.step()
+    assert ag.health.unhealthy() == {}
+    assert all(d["healthy"] for d in schema.read_devices(r, "n1"))
