@@ -710,7 +710,7 @@ class BurstPlanner:
             for j, jb in enumerate(jobs):
                 for p, _ in jb[0]:
                     self._slot_job_of[O.key(p)] = j
-            res.update(self._slot_result(0, batch.result(0)))
+            res.update(self._slot_result(0, self._batch_result(batch, 0)))
             return res
         if len(jobs) > 1 and self._pool is not None:
             outs = list(self._pool.map(lambda j: core.plan_slots(*j[3]), jobs))
@@ -742,10 +742,21 @@ class BurstPlanner:
         self.stats["slot_min_spread_ms"] += float(min_spread)
         return res
 
+    @staticmethod
+    def _batch_result(batch, j: int):
+        """Job j of an async slot batch; None (the ledger's best-fit slots) if it failed -- the
+        slot plan only refines a placement, and its error would surface in a later pod's cycle."""
+        try:
+            return batch.result(j)
+        except Exception as e:
+            import logging
+            logging.getLogger(__name__).warning("slot plan %d failed: %s (best-fit slots)", j, e)
+            return None
+
     def _slot_result(self, j: int, out) -> Dict[str, int]:
         pend = self._slot_pending
         pend["left"].discard(j)
-        res = self._apply_slot_plan(pend["jobs"][j], out, pend["margin"])
+        res = self._apply_slot_plan(pend["jobs"][j], out, pend["margin"]) if out is not None else {}
         for p, _ in pend["jobs"][j][0]:
             self._slot_job_of.pop(O.key(p), None)
         if not pend["left"]:
@@ -761,7 +772,7 @@ class BurstPlanner:
         for i in ([j] if j is not None else sorted(pend["left"])):
             if i not in pend["left"]:
                 continue
-            for k, u0 in self._slot_result(i, pend["batch"].result(i)).items():
+            for k, u0 in self._slot_result(i, self._batch_result(pend["batch"], i)).items():
                 pl = self.plans.get(k)
                 if pl is not None:
                     self.plans[k] = (pl[0], pl[1], u0)
