@@ -111,7 +111,7 @@ class ControlPlane:
                  effort_down: Optional[float] = None, learn_corun: bool = True, kernel_policy: str = "off",
                  gc_settle: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
-        self.gc_settle = gc_settle          # utils.gctune.settle() at the warmup -> timed transition
+        self.gc_settle = gc_settle          # utils.gctune.settle() once the control plane is built
         self.cu_per_pod = cu_per_pod
         self.qos = qos
         self.rng = random.Random(seed)
@@ -228,6 +228,12 @@ class ControlPlane:
         self.unscheduled = 0
         # workload popularity (Zipf-like over the catalog, deterministic)
         self.weights = [1.0 / (1 + (i % 6)) for i in range(len(W.NAMES))]
+        if self.gc_settle:
+            # the built control plane (informer caches, ledger, model, compiled plugin state) to
+            # the permanent GC generation -- here, before any epoch: a full collection at the
+            # warmup -> timed transition would delay the first timed schedule
+            from ..utils.gctune import settle
+            settle()
 
     def arrivals(self) -> List[Dict[str, Any]]:
         n = self.n_gpus * self.pods_per_gpu
@@ -389,9 +395,6 @@ class ControlPlane:
         planner = getattr(self.plugin, "planner", None)
         if planner is not None:
             planner.realign()
-        if self.gc_settle:
-            from ..utils.gctune import settle
-            settle()                        # start-up state to the permanent GC generation
 
     def _plan_feedback(self, pods: np.ndarray) -> None:
         """Report each GPU's measured busy time for the collected epoch next to what the planner
@@ -848,7 +851,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="torch.distributed backend (default: nccl = RCCL on GPU, gloo on CPU)")
     ap.add_argument("--gc-settle", type=int, default=1,
                     help="control plane: collect once and freeze the start-up objects out of the GC's "
-                         "scans at the warmup -> timed transition (utils.gctune; 0 = CPython default)")
+                         "scans once it is built, before the warm-up (utils.gctune; 0 = CPython default)")
     ap.add_argument("--control-plane", default="process", choices=["process", "inline"],
                     help="run apiserver+scheduler in a separate process (default) or inside rank 0")
     ap.add_argument("--graphs", type=int, default=1, choices=[0, 1],

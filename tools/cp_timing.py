@@ -30,7 +30,7 @@ def run(n: int, kwargs: dict, epochs: int = 60, warm: int = 10) -> float:
     ts = []
     for e in range(warm + epochs):
         if e == warm:
-            cp.reset_stats()                 # the bench's warmup -> timed transition (GC settle)
+            cp.reset_stats()                 # the bench's warmup -> timed transition
         cp.finish_live()
         t = time.perf_counter()
         arr = cp.schedule_epoch()
