@@ -374,6 +374,10 @@ def test_async_slot_plans_give_the_synchronous_placements():
         V.SIM.update(on=True, sigma=0.05, rng=np.random.default_rng(0), speed=[])
         cp = ControlPlane(8, 4, 20, 0, **bench)
         cp.plugin.planner.slots_async = async_
+        # one LPT arrival window: the queue's wall-clock windows could split an epoch's
+        # arrivals differently in the two runs (a different scheduling order, not a different
+        # slot plan)
+        cp.plugin.args.lpt_window_s = 1e9
         arrs = []
         for _ in range(14):
             cp.finish_live()

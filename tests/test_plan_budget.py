@@ -87,8 +87,10 @@ def _place_bursts(plan_hints: bool, disable_defaults: bool):
     fc = FakeCluster()
     for n in ("n0", "n1", "n2"):
         fc.create("nodes", O.make_node(n, gpus=8))
+    # (one LPT arrival window: the queue's 1 s wall-clock windows could split a burst differently
+    # in the two runs -- a different scheduling order, not a different plan)
     args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.0, "w_balance": 1.0, "slo_objective": "corun",
-            "plan_bursts": True, "plan_tolerance": 0.3, "plan_carry": 1.0}
+            "plan_bursts": True, "plan_tolerance": 0.3, "plan_carry": 1.0, "lpt_window_s": 1e9}
     s = Scheduler(fc, default_gpu_config(args, disable_defaults=disable_defaults), full_registry(),
                   bind_async=False, seed=0,
                   extras={"ledger": DeviceLedger(), "telemetry": TelemetryCache(stale_s=0),
