@@ -32,7 +32,7 @@ def _serve(conn: Any, kwargs: dict) -> None:
         if kind == "schedule":
             cp.finish_live()
             arr = cp.schedule_epoch()
-            conn.send(("placements", arr, cp.sched_s, cp.unscheduled))
+            conn.send(("placements", arr, cp.sched_s, cp.unscheduled, cp.side_total_s))
         elif kind == "telemetry":
             cp.update_telemetry(msg[1], msg[2])
         elif kind == "reset_stats":
@@ -57,6 +57,7 @@ class ControlPlaneProc:
         child.close()
         self._outstanding = 0
         self.sched_s = 0.0
+        self.side_total_s = 0.0
         self.unscheduled = 0
 
     def request_schedule(self) -> None:
@@ -76,7 +77,7 @@ class ControlPlaneProc:
                 raise RuntimeError(f"control-plane process connection lost: {e}") from e
             if msg[0] == "placements":
                 self._outstanding -= 1
-                _, arr, self.sched_s, self.unscheduled = msg
+                _, arr, self.sched_s, self.unscheduled, self.side_total_s = msg
                 return arr
 
     def schedule_epoch(self) -> np.ndarray:

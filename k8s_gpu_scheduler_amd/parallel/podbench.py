@@ -212,6 +212,7 @@ class ControlPlane:
         self.adaptive = adaptive
         self._last_start: Optional[float] = None
         self._side_s = 0.0                  # finish_live + update_telemetry since the last schedule
+        self.side_total_s = 0.0             # ... summed since reset_stats (the timed region)
         # the effort rule itself is the planner's (plugins.gpu.planner.EffortController): here
         # the time a plan may take is the pipeline period (the interval between schedule requests)
         self._effort = None
@@ -252,7 +253,9 @@ class ControlPlane:
             except Exception:
                 pass
         self.live = []
-        self._side_s += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self._side_s += dt
+        self.side_total_s += dt
 
     EFFORT_DOWN = 0.85       # share of the pipeline period over which the planner steps down
     # ... and under which it steps back up (when the next level is predicted to fit 70 %): 0.6
@@ -391,6 +394,7 @@ class ControlPlane:
         """The warmup -> timed transition: zero the counters, and realign the planner's backlog,
         since the bench drained every GPU's pipeline (all idle at once) before timing."""
         self.sched_s = 0.0
+        self.side_total_s = 0.0
         self.unscheduled = 0
         planner = getattr(self.plugin, "planner", None)
         if planner is not None:
@@ -524,7 +528,9 @@ class ControlPlane:
         try:
             self._update_telemetry(per_gpu, wall_ms)
         finally:
-            self._side_s += time.perf_counter() - t0
+            dt = time.perf_counter() - t0
+            self._side_s += dt
+            self.side_total_s += dt
 
     def _update_telemetry(self, per_gpu: np.ndarray, wall_ms: float) -> None:
         per_gpu = np.asarray(per_gpu, dtype=np.float64)
@@ -1287,6 +1293,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             "host_ms_per_step_by_rank": [{k: round(float(v), 3) for k, v in zip(hkeys, t.cpu().tolist())}
                                          for t in host_all] if world > 1 else None,
             "control_plane_ms_per_epoch": round(cp.sched_s / max(a.steps, 1) * 1e3, 3),
+            # the control plane's other serial work per epoch: the pod deletions and telemetry
+            "control_plane_side_ms_per_epoch": round(getattr(cp, "side_total_s", 0.0) / max(a.steps, 1) * 1e3, 3),
             "simulated": not use_gpu,
         }
         print(json.dumps(result), flush=True)
