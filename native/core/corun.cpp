@@ -827,21 +827,22 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     };
     // memo of group evaluations per phase and thread: a sweep re-evaluates mostly the same
     // (GPU, member set) pairs as the previous one -- only the two groups of an accepted move /
-    // swap change.  The members are evaluated in sorted order, so a result is a function of
-    // the set.
-    // key: a 64-bit mix of the sorted member codes and the GPU (no allocation per lookup; a
-    // collision among the few thousand sets of one plan is ~1e-12 likely)
+    // swap change.  A result is a function of the set.
+    // key: an ORDER-FREE 64-bit hash of the set -- the sum of a mixed code per member, with the
+    // GPU and the size mixed in -- kept per GPU as members move (Ksum), so a candidate's key is
+    // one add / subtract and a memo hit needs no member list at all (a collision among the few
+    // thousand sets of one plan is ~1e-12 likely)
     using Memo = FlatMap<GroupEval>;
-    auto key_of = [](const std::vector<int>& v) {
-      uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)v.size();
-      for (int x : v) {
-        uint64_t z = h + 0x9e3779b97f4a7c15ull + (uint64_t)(uint32_t)x;
-        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-        h = z ^ (z >> 31);
-      }
-      return h;
+    auto hm = [](int member) {
+      uint64_t z = (uint64_t)(uint32_t)member + 0x9e3779b97f4a7c15ull;
+      z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+      z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+      return z ^ (z >> 31);
     };
+    auto set_key = [&](int g, uint64_t ksum, size_t k) { return mix(mix(ksum, (uint64_t)g + 0x51ull), (uint64_t)k); };
+    std::vector<uint64_t> Ksum(NG, 0);
+    for (int g = 0; g < NG; ++g)
+      for (int x : mem[g]) Ksum[g] += hm(x);
     // candidate evaluation runs on T threads (GPUSCHED_PLAN_THREADS, default 4): each batch
     // -- every move of one pod, or every swap partner of one pod -- is evaluated in parallel on
     // the current state, then the FIRST accepted candidate in the sequential order is applied,
@@ -856,12 +857,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     std::array<Memo, 2> memo{Memo(4096), Memo(4096)};
     std::shared_mutex memo_mu;
     std::atomic<long> n_evals{0};
-    auto eval_set = [&](int g, std::vector<int>& v, int tid) {
-      (void)tid;
-      std::sort(v.begin(), v.end());
-      v.push_back(g);
-      const uint64_t key = key_of(v);
-      v.pop_back();
+    // build(v): fills the member list -- only called on a memo miss
+    auto eval_key = [&](int g, uint64_t key, auto&& build) {
       auto& M = memo[phase_b ? 1 : 0];
       n_evals.fetch_add(1, std::memory_order_relaxed);
       if (T > 1) {
@@ -870,6 +867,9 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       } else if (const GroupEval* hit = M.find(key)) {
         return *hit;
       }
+      std::vector<int> v;
+      build(v);
+      std::sort(v.begin(), v.end());
       const GroupEval r = eval_raw(g, v);
       if (T > 1) {
         std::unique_lock<std::shared_mutex> lk(memo_mu);
@@ -881,10 +881,9 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
     };
     std::vector<GroupEval> ge(NG);
     auto eval_all = [&] {
-      for (int g = 0; g < NG; ++g) {
-        std::vector<int> v(mem[g].begin(), mem[g].end());
-        ge[g] = eval_set(g, v, 0);
-      }
+      for (int g = 0; g < NG; ++g)
+        ge[g] = eval_key(g, set_key(g, Ksum[g], mem[g].size()),
+                         [&](std::vector<int>& v) { v.assign(mem[g].begin(), mem[g].end()); });
     };
     eval_all();
     SpinPool pool(T);
@@ -909,26 +908,36 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
       // the pod) is the same for every candidate -- evaluated once
       GroupEval src{};
       if (!swap && n > 0) {
-        std::vector<int> va(mem[cand[0].ga].begin(), mem[cand[0].ga].end());
-        va.erase(std::find(va.begin(), va.end(), cand[0].a));
-        src = eval_set(cand[0].ga, va, 0);
+        const Cand& x = cand[0];
+        src = eval_key(x.ga, set_key(x.ga, Ksum[x.ga] - hm(x.a), mem[x.ga].size() - 1), [&](std::vector<int>& v) {
+          v.assign(mem[x.ga].begin(), mem[x.ga].end());
+          v.erase(std::find(v.begin(), v.end(), x.a));
+        });
       }
       auto job = [&](int tid) {
-        std::vector<int> va, vb;
+        (void)tid;
         for (int c = tid; c < n; c += T) {
           const Cand& x = cand[c];
           try {
-            vb.assign(mem[x.gb].begin(), mem[x.gb].end());
             if (swap) {
-              va.assign(mem[x.ga].begin(), mem[x.ga].end());
-              *std::find(va.begin(), va.end(), x.a) = x.b;
-              *std::find(vb.begin(), vb.end(), x.b) = x.a;
-              res[c].ea = eval_set(x.ga, va, tid);
+              res[c].ea = eval_key(x.ga, set_key(x.ga, Ksum[x.ga] - hm(x.a) + hm(x.b), mem[x.ga].size()),
+                                   [&](std::vector<int>& v) {
+                                     v.assign(mem[x.ga].begin(), mem[x.ga].end());
+                                     *std::find(v.begin(), v.end(), x.a) = x.b;
+                                   });
+              res[c].eb = eval_key(x.gb, set_key(x.gb, Ksum[x.gb] - hm(x.b) + hm(x.a), mem[x.gb].size()),
+                                   [&](std::vector<int>& v) {
+                                     v.assign(mem[x.gb].begin(), mem[x.gb].end());
+                                     *std::find(v.begin(), v.end(), x.b) = x.a;
+                                   });
             } else {
-              vb.push_back(x.a);
               res[c].ea = src;
+              res[c].eb = eval_key(x.gb, set_key(x.gb, Ksum[x.gb] + hm(x.a), mem[x.gb].size() + 1),
+                                   [&](std::vector<int>& v) {
+                                     v.assign(mem[x.gb].begin(), mem[x.gb].end());
+                                     v.push_back(x.a);
+                                   });
             }
-            res[c].eb = eval_set(x.gb, vb, tid);
           } catch (const std::exception& ex) {
             std::lock_guard<std::mutex> lk(err_mu);
             failed = true;
@@ -971,6 +980,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
             if (!accept(g0, g1, ge[g0], ge[g1], res[c].ea, res[c].eb)) continue;
             mem[g0].erase(std::find(mem[g0].begin(), mem[g0].end(), (int)p));
             mem[g1].push_back((int)p);
+            Ksum[g0] -= hm((int)p);
+            Ksum[g1] += hm((int)p);
             --nburst[g0];
             ++nburst[g1];
             free[d0] += U[p];
@@ -1008,6 +1019,8 @@ py::array_t<int32_t> plan_corun(I32 dev_in, I32 units, I32 wid, F64 iters, F64 s
               if (!accept(gi, gj, ge[gi], ge[gj], res[c].ea, res[c].eb)) continue;
               *std::find(mem[gi].begin(), mem[gi].end(), (int)i) = j;
               *std::find(mem[gj].begin(), mem[gj].end(), j) = (int)i;
+              Ksum[gi] += hm(j) - hm((int)i);
+              Ksum[gj] += hm((int)i) - hm(j);
               dev[i] = dj;
               dev[j] = di;
               hfree[di] += H[i] - H[j];
