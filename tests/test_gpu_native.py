@@ -349,9 +349,11 @@ def test_planner_feedback_moves_work_off_a_really_slower_gpu():
     print(state(12), "group errors", np.round(errs, 3), "backlog spreads", np.round(spreads, 2),
           "lazy captures", ex.lazy_captures)
     assert planner.speed(g1) > 1.2 * planner.speed(g0), state(12)      # GPU 1 measured slower
-    # (a burst is 4 pods of unequal length, so single bursts are lumpy; the CPU twin of this test,
-    # tests/test_backlog_control.py, holds the per-burst shares of these arrivals in [0.34, 0.49])
-    assert float(np.mean(share)) < 0.5 and min(share) >= 0.15 and max(share) <= 0.6, state(12)
+    # (a burst is 4 pods of unequal length, so a single burst's share is one of a handful of
+    # discrete splits around the 1 / 2.4 target -- 0.148 is GPU 1 taking only the burst's
+    # shortest pod after a 0.485 epoch.  The CPU twin with 8 % measurement noise, 16 noise
+    # seeds x 8 epochs: shares 0.148-0.592, per-run means 0.41-0.45; a starved GPU would be 0)
+    assert 0.3 < float(np.mean(share)) < 0.5 and min(share) >= 0.12 and max(share) <= 0.6, state(12)
     # bounded: never more than the planner's stored clip of a balanced burst's work
     assert max(spreads) <= planner.STORE_CLIP * planner._burst_ms + 1e-6, (spreads, state(12))
     assert np.mean(np.asarray(errs) <= 0.15) >= 0.8, errs
