@@ -98,6 +98,8 @@ def fill_betas(model: Any) -> Optional[Tuple[float, float]]:
     key = (model.version, tuple(model.names))
     if key in _BETAS:
         return _BETAS[key]
+    if len(_BETAS) >= 64:                # a long-running recommender refits many versions
+        _BETAS.clear()
     F = catalog_fills(model)
     Cm = model.u @ model.v.T
     n = len(model.names)
