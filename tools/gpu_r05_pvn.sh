@@ -4,7 +4,7 @@
 # speeds instead of the backlog integrator, no-empty-GPU rule, fast-forwarded slot plans).
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r05_pvn
+OUT=gpurun_out/${OUT_NAME:-r05_pvn}
 mkdir -p $OUT
 timeout -k 10 1100 python -u tools/pipelined_vn.py --gpus 8 --epochs 48 --warmup 5 --seeds 0 1 --passes 3 \
   --policies greedy planner planner-e1 planner-e2 --out $OUT/pipelined_vn.json > $OUT/pipelined_vn.log 2>&1
