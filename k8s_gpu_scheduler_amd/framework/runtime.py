@@ -79,6 +79,7 @@ class Framework:
                     self.weights[ref.name] = ref.weight
             self.points[point] = lst
         self._pool: Optional[ThreadPoolExecutor] = None
+        self._filter_forms: Optional[Tuple[List[Any], List[Any]]] = None   # (plugins, batch forms)
         self.score_in_parallel = any(getattr(p, "SCORE_DOES_IO", False) for p in self.points["score"])
         # plan hints: a score plugin that may already have decided a pod's node (the GPU plugin's
         # burst plan, `planned_node`) short-cuts the cycle -- Filter on that node only, no Score --
@@ -132,22 +133,25 @@ class Framework:
         return getattr(qs[0], "sort_key", None) if qs else None
 
     # ---------------------------------------------------------------- filter
+    # extension points are timed as a whole (kube-scheduler's framework_extension_point_duration);
+    # per-plugin clocks cost two clock reads and a metrics update per plugin per pod
     def run_pre_filter(self, state: CycleState, pod: Obj) -> Status:
-        clock, add = time.perf_counter_ns, self.metrics.add
-        for p in self.points["preFilter"]:
-            t0 = clock()
-            r = p.pre_filter(state, pod)
-            add("preFilter", clock() - t0)
-            if r is None:
-                continue
-            s = as_status(r)
-            if s.code == Code.SKIP:
-                state.skip_filter_plugins.add(p.name())
-                continue
-            if not s.ok:
-                s.plugin = s.plugin or p.name()
-                return s
-        return Status.success()
+        t0 = time.perf_counter_ns()
+        try:
+            for p in self.points["preFilter"]:
+                r = p.pre_filter(state, pod)
+                if r is None:
+                    continue
+                s = as_status(r)
+                if s.code == Code.SKIP:
+                    state.skip_filter_plugins.add(p.name())
+                    continue
+                if not s.ok:
+                    s.plugin = s.plugin or p.name()
+                    return s
+            return Status.success()
+        finally:
+            self.metrics.add("preFilter", time.perf_counter_ns() - t0)
 
     def run_filter(self, state: CycleState, pod: Obj, node_info: Any) -> Status:
         for p in self.points["filter"]:
@@ -173,8 +177,14 @@ class Framework:
         t0 = time.perf_counter_ns()
         feasible: List[Any] = []
         failed: Dict[str, Status] = {}
-        plugins = [p for p in self.points["filter"] if p.name() not in state.skip_filter_plugins]
-        batch = [getattr(p, "filter_nodes", None) for p in plugins]
+        if state.skip_filter_plugins:
+            plugins = [p for p in self.points["filter"] if p.name() not in state.skip_filter_plugins]
+            batch = [getattr(p, "filter_nodes", None) for p in plugins]
+        else:
+            if self._filter_forms is None:
+                ps = list(self.points["filter"])
+                self._filter_forms = (ps, [getattr(p, "filter_nodes", None) for p in ps])
+            plugins, batch = self._filter_forms
         chunk = max(16, min(256, limit * 2)) if limit else 256
         processed = 0
         i, n, done = 0, len(nodes), False
@@ -286,18 +296,19 @@ class Framework:
 
     # ---------------------------------------------------------------- reserve .. postBind
     def run_reserve(self, state: CycleState, pod: Obj, node: str) -> Status:
-        clock, add = time.perf_counter_ns, self.metrics.add
-        for p in self.points["reserve"]:
-            t0 = clock()
-            r = p.reserve(state, pod, node)
-            add("reserve", clock() - t0)
-            if r is None:
-                continue
-            s = as_status(r)
-            if not s.ok:
-                s.plugin = s.plugin or p.name()
-                return s
-        return Status.success()
+        t0 = time.perf_counter_ns()
+        try:
+            for p in self.points["reserve"]:
+                r = p.reserve(state, pod, node)
+                if r is None:
+                    continue
+                s = as_status(r)
+                if not s.ok:
+                    s.plugin = s.plugin or p.name()
+                    return s
+            return Status.success()
+        finally:
+            self.metrics.add("reserve", time.perf_counter_ns() - t0)
 
     def run_unreserve(self, state: CycleState, pod: Obj, node: str) -> None:
         for p in reversed(self.points["reserve"]):
@@ -326,18 +337,19 @@ class Framework:
         return (Status(Code.WAIT) if waiting else Status.success()), wait
 
     def run_pre_bind(self, state: CycleState, pod: Obj, node: str) -> Status:
-        clock, add = time.perf_counter_ns, self.metrics.add
-        for p in self.points["preBind"]:
-            t0 = clock()
-            r = p.pre_bind(state, pod, node)
-            add("preBind", clock() - t0)
-            if r is None:
-                continue
-            s = as_status(r)
-            if not s.ok:
-                s.plugin = s.plugin or p.name()
-                return s
-        return Status.success()
+        t0 = time.perf_counter_ns()
+        try:
+            for p in self.points["preBind"]:
+                r = p.pre_bind(state, pod, node)
+                if r is None:
+                    continue
+                s = as_status(r)
+                if not s.ok:
+                    s.plugin = s.plugin or p.name()
+                    return s
+            return Status.success()
+        finally:
+            self.metrics.add("preBind", time.perf_counter_ns() - t0)
 
     def run_bind(self, state: CycleState, pod: Obj, node: str) -> Status:
         for p in self.points["bind"]:
