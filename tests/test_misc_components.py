@@ -129,3 +129,18 @@ def test_host_modules_build_with_tsan():
     out = B.build(force=True, only=("_core",), san_kind="tsan")
     assert out and "_tsan" in out[0]
     os.remove(out[0])
+
+
+def test_gc_settle_freezes_the_startup_objects():
+    """utils.gctune.settle: one collection, then the surviving objects leave the collector's
+    scans (the control plane's start-up state) and the gen-0 threshold is raised."""
+    import gc
+    from k8s_gpu_scheduler_amd.utils import gctune
+    before = gc.get_threshold()
+    try:
+        gctune.settle(gen0=12345)
+        assert gc.get_freeze_count() > 0
+        assert gc.get_threshold()[0] >= 12345
+    finally:
+        gc.unfreeze()
+        gc.set_threshold(*before)
