@@ -108,7 +108,8 @@ class ControlPlane:
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
                  slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0,
-                 effort_down: Optional[float] = None, learn_corun: bool = True, kernel_policy: str = "off",
+                 effort_down: Optional[float] = None, effort_up: Optional[float] = None,
+                 effort_target: Optional[float] = None, learn_corun: bool = True, kernel_policy: str = "off",
                  gc_settle: bool = True):
         self.n_gpus, self.pods_per_gpu, self.iters = n_gpus, pods_per_gpu, iters
         self.gc_settle = gc_settle          # utils.gctune.settle() once the control plane is built
@@ -211,6 +212,7 @@ class ControlPlane:
         # cheaper effort level (planner.set_effort), and climbs back when there is room
         self.adaptive = adaptive
         self._last_start: Optional[float] = None
+        self.extra_s = float(os.environ.get("GPUSCHED_CP_EXTRA_MS", "0") or 0) / 1e3
         self._side_s = 0.0                  # finish_live + update_telemetry since the last schedule
         self.side_total_s = 0.0             # ... summed since reset_stats (the timed region)
         # the effort rule itself is the planner's (plugins.gpu.planner.EffortController): here
@@ -219,8 +221,10 @@ class ControlPlane:
         planner = getattr(self.plugin, "planner", None)
         if planner is not None:
             from ..plugins.gpu.planner import EffortController
-            self._effort = EffortController(planner, down=float(effort_down) if effort_down is not None else self.EFFORT_DOWN,
-                                            up=self.EFFORT_UP, target=0.7, settle=3)
+            self._effort = EffortController(
+                planner, down=float(effort_down) if effort_down is not None else self.EFFORT_DOWN,
+                up=float(effort_up) if effort_up is not None else self.EFFORT_UP,
+                target=float(effort_target) if effort_target is not None else self.EFFORT_TARGET, settle=3)
             if os.environ.get("GPUSCHED_EFFORT_DEBUG"):
                 self._effort.debug = lambda msg: print(f"[effort] epoch {self.epoch} {msg}", file=sys.stderr, flush=True)
         self.effort_epochs: Dict[int, int] = {}
@@ -258,16 +262,21 @@ class ControlPlane:
         self.side_total_s += dt
 
     EFFORT_DOWN = 0.85       # share of the pipeline period over which the planner steps down
-    # ... and under which it steps back up (when the next level is predicted to fit 70 %): 0.6
-    # since round 5's cheaper levels -- at 0.5 a level-2 control plane on the 8-rank rehearsal
-    # (3.9 of a ~7.6 ms period) never climbed back to level 1 (4.9 ms)
-    EFFORT_UP = 0.6
+    # ... under which it steps back up, when the next level is predicted to fit EFFORT_TARGET of
+    # the period.  Where the control plane starts pacing the GPUs was measured on the box CPU
+    # (tools/gpu_cp_knee.sh, profiles/r05_cp_knee/: the 8-rank rehearsal with a busy wait added
+    # to each epoch): ms / step stays flat up to ~5.85 ms of scheduling per 6.8 ms period (86 %,
+    # ~91 % with the deletions and telemetry) and rises beyond it.  Up 0.7 / target 0.8 keep a
+    # 10 % margin below that knee (round 5 first ran 0.6 / 0.7, which held an 8-GPU control
+    # plane at level 2 although level 1 was ~15 % below the knee)
+    EFFORT_UP = 0.7
+    EFFORT_TARGET = 0.8
 
     def _adapt_effort(self, t0: float) -> None:
         """Adaptive planning effort (GPU runs): the control plane must schedule an epoch within
         the pipeline's period or it paces the GPUs (EffortController, the allowed time being the
-        interval between consecutive schedule requests; thresholds 85 % down / 60 % up, jump
-        target 70 %, the control plane runs in its own process, overlapped with the GPUs)."""
+        interval between consecutive schedule requests; thresholds 85 % down / 70 % up, jump
+        target 80 %, the control plane runs in its own process, overlapped with the GPUs)."""
         planner = getattr(self.plugin, "planner", None)
         if planner is None or self._effort is None:
             return
@@ -318,6 +327,12 @@ class ControlPlane:
         self.queue_drop(dropped)
         if self.kernel_policy == "risk":
             self._kernel_policies(arr)
+        if self.extra_s > 0:
+            # pacing probe (GPUSCHED_CP_EXTRA_MS): a costlier control plane, emulated by a busy
+            # wait inside the epoch's schedule (tools/gpu_cp_knee.sh finds where it paces)
+            t_end = time.perf_counter() + self.extra_s
+            while time.perf_counter() < t_end:
+                pass
         self.epoch += 1
         dt = time.perf_counter() - t0
         self.sched_s += dt
@@ -718,7 +733,8 @@ def _effective_config(a: Any) -> Dict[str, Any]:
                 out.update(slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma)
             out.update(plan_effort=a.plan_effort, cp_adaptive=int(bool(a.cp_adaptive) and not a.sim))
             if a.cp_adaptive and not a.sim:
-                out["cp_effort_down"] = a.cp_effort_down
+                out.update(cp_effort_down=a.cp_effort_down, cp_effort_up=a.cp_effort_up,
+                           cp_effort_target=a.cp_effort_target)
         else:
             out["plan_objective"] = a.plan_objective
     elif corun:
@@ -838,14 +854,20 @@ def build_parser() -> argparse.ArgumentParser:
                     help="1: the executor re-slots each epoch's Burstable pods longest-first onto the least-loaded "
                          "CU slot (blind to SLOs); 0: pods run on the slot the scheduler chose")
     ap.add_argument("--cp-adaptive", type=int, default=1, choices=[0, 1],
-                    help="GPU runs: the control plane lowers the planner's effort (phantoms and sweeps, model slot "
-                         "plans, then sweeps) while scheduling an epoch takes > 85 %% of the pipeline period, "
-                         "and raises it again below 50 %% (planner.set_effort)")
+                    help="GPU runs: the control plane lowers the planner's effort (sweeps, then phantoms, model slot "
+                         "plans and pipeline evaluation, then sweeps) while scheduling an epoch takes > 85 %% of the pipeline period, "
+                         "and raises it again below 70 %% (planner.set_effort)")
     ap.add_argument("--cp-effort-down", type=float, default=ControlPlane.EFFORT_DOWN,
                     help="--cp-adaptive: the share of the pipeline period above which the planner's effort drops")
+    ap.add_argument("--cp-effort-up", type=float, default=ControlPlane.EFFORT_UP,
+                    help="--cp-adaptive: the share of the pipeline period under which the planner's effort rises "
+                         "(when the next level is predicted to fit --cp-effort-target)")
+    ap.add_argument("--cp-effort-target", type=float, default=ControlPlane.EFFORT_TARGET,
+                    help="--cp-adaptive: the share of the pipeline period a new effort level must be predicted to fit")
     ap.add_argument("--plan-effort", type=int, default=0, choices=[0, 1, 2, 3],
-                    help="the planner's starting effort level (0 = full; 1 = no phantoms, half the sweeps; 2 = "
-                         "also lpt slots and no pipeline evaluation; 3 = also one sweep per planning phase); with --cp-adaptive 0 or "
+                    help="the planner's starting effort level (0 = full; 1 = a quarter of the sweeps, phantoms kept; "
+                         "2 = half the sweeps, no phantoms, lpt slots and no pipeline evaluation; 3 = also one sweep "
+                         "per planning phase); with --cp-adaptive 0 or "
                          "--sim it stays fixed")
     ap.add_argument("--dump-placements", default="",
                     help="write every epoch's placements (JSON) for a hardware replay (tools/pipelined_vn.py)")
@@ -956,7 +978,8 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      plan_carry=a.plan_carry, plan_feedback=bool(a.plan_feedback), plan_slots=a.plan_slots,
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
                      adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort,
-                     effort_down=a.cp_effort_down, learn_corun=bool(a.corun_learn),
+                     effort_down=a.cp_effort_down, effort_up=a.cp_effort_up, effort_target=a.cp_effort_target,
+                     learn_corun=bool(a.corun_learn),
                      kernel_policy=a.kernel_policy, gc_settle=bool(a.gc_settle))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":

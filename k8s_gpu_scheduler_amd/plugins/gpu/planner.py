@@ -44,6 +44,7 @@ sets a per-GPU speed that scales the GPU's future increments, and the backlog is
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -77,9 +78,10 @@ class EffortController:
     from the start would carry that backlog into a timed region (rehearsed at 8 GPUs on the box
     CPU: profiles/r04_cp_rehearsal/jump_first/)."""
 
-    # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py:
-    # 5.75 / 4.86 / 3.87 / 3.59 ms, profiles/r05_cp2/; round 4: 8.1 / 6.3 / 4.5 / 4.1)
-    LEVEL_COST = (1.0, 0.845, 0.673, 0.624)
+    # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py
+    # and tools/gpu_cp_levels.sh: 5.78 / 4.68 / 4.09 ms, profiles/r05_cp_levels/; level 3 3.59 of
+    # 5.75, profiles/r05_cp2/; round 4: 8.1 / 6.3 / 4.5 / 4.1)
+    LEVEL_COST = (1.0, 0.81, 0.69, 0.63)
 
     def __init__(self, planner: "BurstPlanner", down: float = 0.85, up: float = 0.5, target: float = 0.7,
                  settle: int = 3, window: int = 6):
@@ -185,6 +187,16 @@ class BurstPlanner:
             # 2 phantom pods per slot: 65.6 % SLOs met vs 65.3 with 3 and 64.3 with 1 (8-GPU
             # pipelined simulation, 3 seeds), a smaller pipeline simulation per candidate
             self.timeline = SlotTimeline(depth=6, phantoms=2)
+            self.timeline.listener = self._lpt_measured
+        # measured slot levelling ("lpt" with a timeline): a levelled pod's predicted work is
+        # replaced by its measured time once it ran (in predicted-work units: measured ms over
+        # the GPU's recent measured / predicted ratio) -- a slot whose pods ran long gets the
+        # shorter pods next.  Open loop (GPUSCHED_LPT_FEEDBACK=0) the predicted sums stay level
+        # while the measured ones drift apart (MI355X N=1 trace: 108 vs 134.5 ms of 20 pods per
+        # slot stream, the long one pacing the pipeline, profiles/r05_lookahead/t20.json)
+        self.lpt_feedback = os.environ.get("GPUSCHED_LPT_FEEDBACK", "0") != "0"
+        self._lpt_pred: Dict[str, Tuple[Tuple[str, int, int], float]] = {}
+        self._lpt_ratio: Dict[str, List[float]] = {}        # device -> [decayed measured, decayed predicted]
         self.spread_ms = spread_ms
         # model error of a slot plan's predictions: a pod's co-runners are partly pods placed
         # AFTER it, unknown at planning time (MI355X bench traces: mean |log error| ~0.2 with
@@ -193,17 +205,16 @@ class BurstPlanner:
         self.pipe_eval = True        # plan_corun's SLO phase on the GPUs' pipelines (timeline)
         self.pipe_phantoms = True    # ... with each slot's next (phantom) pod chained after its new one
         self.sweeps_b: Optional[int] = None     # SLO-phase sweeps (None: `sweeps`)
-        # effort level (set_effort): 0 = as configured, 1 = no pipeline phantoms and half the
-        # sweeps, 2 = also slot levelling instead of the model's slot plans and no pipeline
-        # evaluation, 3 = also one sweep per phase -- a control plane that falls behind its GPUs
-        # trades plan quality for time.  (Dropping burst plans altogether is NOT cheaper at 8
+        # effort level (set_effort, EFFORT_LEVELS): 0 = as configured, 1 = a quarter of the
+        # sweeps (phantoms kept), 2 = half the sweeps, no phantoms, slot levelling instead of the
+        # model's slot plans and no pipeline evaluation, 3 = also one sweep per phase -- a control
+        # plane that falls behind its GPUs trades plan quality for time.  (Dropping burst plans altogether is NOT cheaper at 8
         # GPUs: Score then evaluates the co-run groups of every candidate GPU per pod, 22.6 vs
         # 17.0 ms per epoch for level 2 in tools/cp_timing.py, at greedy's SLOs.)
         self.effort = 0
         self._configured = (self.sweeps, self.slot_policy)
         self._pool = None
         if self.timeline is not None:
-            import os
             from concurrent.futures import ThreadPoolExecutor
             # the GPUs' slot plans can run side by side (native, without the interpreter lock;
             # GPUSCHED_SLOT_THREADS=n).  Off by default since the slot planner's context
@@ -260,15 +271,35 @@ class BurstPlanner:
             self.budget.decide()
         return out
 
+    # what each effort level plans with: (sweep divisor -- 0: one sweep --, pipeline phantoms,
+    # pipeline evaluation, model slot plans).  Level 1 keeps the phantoms and drops sweeps: on
+    # the 8-GPU pipelined virtual node (MI355X, profiles/r05_pvn_levels/) the phantoms carry the
+    # SLO quality (level 1 with phantoms and 1 sweep: 60.4 % SLOs, the full plan 60.2 %, round
+    # 5's first level 1 -- 2 sweeps, no phantoms -- 57.7 %, at the same pods/s) and the sweeps
+    # the cost (box CPU: 4.68 vs 5.02 ms per 8-GPU epoch, profiles/r05_cp_levels/)
+    EFFORT_LEVELS = ((1, True, True, True), (4, True, True, True), (2, False, False, False), (0, False, False, False))
+
+    @classmethod
+    def _effort_levels(cls) -> Tuple[Tuple[int, bool, bool, bool], ...]:
+        # experiments: GPUSCHED_EFFORT_LEVELS="1,1,1,1;2,0,1,1;2,0,0,0;0,0,0,0"
+        env = os.environ.get("GPUSCHED_EFFORT_LEVELS")
+        if not env:
+            return cls.EFFORT_LEVELS
+        rows = tuple(tuple(int(x) for x in r.split(",")) for r in env.split(";"))
+        if len(rows) != cls.MAX_EFFORT + 1 or any(len(r) != 4 for r in rows):
+            raise ValueError(f"GPUSCHED_EFFORT_LEVELS needs {cls.MAX_EFFORT + 1} rows of 4 fields: {env!r}")
+        return tuple((r[0], bool(r[1]), bool(r[2]), bool(r[3])) for r in rows)
+
     def set_effort(self, level: int) -> None:
         level = max(0, min(self.MAX_EFFORT, int(level)))
         sweeps, slots = self._configured
         self.effort = level
-        self.sweeps = sweeps if level == 0 else 1 if level >= 3 else max(1, sweeps // 2)
-        self.pipe_phantoms = level == 0
-        self.pipe_eval = level < 2
+        div, phantoms, pipe_eval, model_slots = self._effort_levels()[level]
+        self.sweeps = 1 if div == 0 else max(1, sweeps // div)
+        self.pipe_phantoms = phantoms
+        self.pipe_eval = pipe_eval
         if slots in ("model", "auto"):
-            self.slot_policy = slots if level < 2 else "lpt"
+            self.slot_policy = slots if model_slots else "lpt"
         self.stats["effort_changes"] = self.stats.get("effort_changes", 0) + 1
 
     # ---------------------------------------------------------------- inputs
@@ -613,9 +644,28 @@ class BurstPlanner:
                 slots.remove(u)
                 res[O.key(p)] = u
                 self._slot_work[(uuid, u, n)] = self._slot_work.get((uuid, u, n), 0.0) + work[O.key(p)]
+                if self.lpt_feedback and self.timeline is not None:
+                    self._lpt_pred[O.key(p)] = ((uuid, u, n), work[O.key(p)])
             self.stats["slot_plans"] += 1
             self.stats["slot_pods"] += len(items)
         return res
+
+    LPT_DECAY = 0.97        # the measured / predicted ratio's memory (~30 pods)
+
+    def _lpt_measured(self, key: str, ms: float) -> None:
+        """A levelled pod ran `ms`: its slot's cumulative work takes the measured time (scaled
+        to predicted-work units by the device's recent measured / predicted ratio) instead of
+        the prediction."""
+        hit = self._lpt_pred.pop(key, None)
+        if hit is None or ms <= 0:
+            return
+        slot, pred = hit
+        acc = self._lpt_ratio.setdefault(slot[0], [0.0, 0.0])
+        acc[0] = acc[0] * self.LPT_DECAY + ms
+        acc[1] = acc[1] * self.LPT_DECAY + pred
+        ratio = acc[0] / acc[1] if acc[1] > 0 else 1.0
+        if slot in self._slot_work and ratio > 0:
+            self._slot_work[slot] += ms / ratio - pred
 
     def _pipe_context(self, gkey: Dict[Tuple, int], states, owner, dev_group, model, core) -> Any:
         """plan_corun's `pipe`: per GPU group of one device, its timeline's in-flight pods
@@ -968,6 +1018,9 @@ class BurstPlanner:
             return
         if how == "unreserve" or (how == "delete" and self.drop_on_delete):
             tl.drop(key)
+            hit = self._lpt_pred.pop(key, None)
+            if how == "unreserve" and hit is not None and hit[0] in self._slot_work:
+                self._slot_work[hit[0]] -= hit[1]          # it never ran on that slot
         elif how == "terminal":
             from .feedback import container_span
             span = container_span(pod)

@@ -317,9 +317,10 @@ def test_control_plane_lowers_planning_effort_when_it_paces_the_gpus():
 @pytest.mark.skipif(core is None, reason="_core not built")
 def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
     """A control plane whose scheduling takes the whole period (it paces the GPUs) jumps from
-    level 0 straight to the first level whose predicted cost fits 70 % of the period (level 2:
-    0.56 of level 0's cost), after two consecutive over-threshold checks; the request intervals
-    right after the change are not sampled; with room again it climbs back one level."""
+    level 0 straight to the first level whose predicted cost fits 80 % of the period (level 2:
+    0.69 of level 0's cost; level 1's 0.81 does not fit), after two consecutive over-threshold
+    checks; the request intervals right after the change are not sampled; with room again it
+    climbs back one level."""
     from k8s_gpu_scheduler_amd.parallel import podbench as PB
     cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=4, iters=20, seed=1, balance=1.0, plan_bursts=True,
                          plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
@@ -345,13 +346,13 @@ def test_adaptive_effort_jumps_to_the_level_predicted_to_fit():
     assert levels[:2] == [0, 0] and levels[-1] == 2 and 1 not in levels
     assert not ctl._allowed and ctl._settle == ctl.settle_n == 3
     for _ in range(ctl.settle_n):
-        step(2, 5.6)                          # queued requests arrive back to back: not sampled
+        step(2, 7.5)                          # queued requests arrive back to back: not sampled
     assert not ctl._allowed and pl.effort == 2
     for _ in range(6):
-        step(10, 5.6)                         # 56 % of the period: stays
+        step(10, 7.5)                         # 75 % of the period (between up and down): stays
     assert pl.effort == 2
     for _ in range(6):
-        step(20, 5.6)                         # 28 %: level 1 (78 / 56 x 5.6 = 7.8 ms) fits 70 % of 20
+        step(20, 7.5)                         # 38 %: level 1 (81 / 69 x 7.5 = 8.8 ms) fits 80 % of 20
     assert pl.effort == 1
 
 

@@ -51,8 +51,8 @@ POLICIES = {
     # the bench default: burst planner on the co-run model, backlog carry, slot planning
     "planner": [],
     # the cheaper planning levels the adaptive control plane falls back to at 8 GPUs
-    # (planner.set_effort: 1 = no phantoms, half the sweeps; 2 = also lpt slots, no pipeline
-    # evaluation; 3 = also one sweep per phase)
+    # (planner.BurstPlanner.EFFORT_LEVELS: 1 = a quarter of the sweeps, phantoms kept; 2 = half the
+    # sweeps, no phantoms, lpt slots, no pipeline evaluation; 3 = also one sweep per phase)
     "planner-e1": ["--plan-effort", "1"],
     "planner-e2": ["--plan-effort", "2"],
     "planner-e3": ["--plan-effort", "3"],
@@ -64,13 +64,23 @@ POLICIES = {
     "planner-sig10": ["--corun-sigma", "0.1"],
     "planner-sig20": ["--corun-sigma", "0.2"],
     "random": ["--policy", "random"],
+    # alternative effort-level tables (planner.BurstPlanner.EFFORT_LEVELS) at level 1: phantoms
+    # kept with 2 sweeps (a) or 1 sweep (c); "-e1old": round 5's first level 1 (no phantoms, 2 sweeps)
+    "planner-e1a": ["--plan-effort", "1"],
+    "planner-e1c": ["--plan-effort", "1"],
+    "planner-e1old": ["--plan-effort", "1"],
+}
+POLICY_ENV = {
+    "planner-e1a": {"GPUSCHED_EFFORT_LEVELS": "1,1,1,1;2,1,1,1;2,0,0,0;0,0,0,0"},
+    "planner-e1c": {"GPUSCHED_EFFORT_LEVELS": "1,1,1,1;4,1,1,1;2,0,0,0;0,0,0,0"},
+    "planner-e1old": {"GPUSCHED_EFFORT_LEVELS": "1,1,1,1;2,0,1,1;2,0,0,0;0,0,0,0"},
 }
 
 
 def schedule(policy: str, flags, gpus: int, epochs: int, warmup: int, seed: int, path: str) -> dict:
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--sim", "--sim-model", "--gpus", str(gpus),
            "--steps", str(epochs), "--warmup", str(warmup), "--seed", str(seed), "--dump-placements", path, *flags]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=dict(os.environ, **POLICY_ENV.get(policy, {})))
     if p.returncode != 0:
         raise RuntimeError(f"scheduling {policy} failed: {p.stderr[-2000:]}")
     with open(path) as f:
