@@ -187,16 +187,6 @@ class BurstPlanner:
             # 2 phantom pods per slot: 65.6 % SLOs met vs 65.3 with 3 and 64.3 with 1 (8-GPU
             # pipelined simulation, 3 seeds), a smaller pipeline simulation per candidate
             self.timeline = SlotTimeline(depth=6, phantoms=2)
-            self.timeline.listener = self._lpt_measured
-        # measured slot levelling ("lpt" with a timeline): a levelled pod's predicted work is
-        # replaced by its measured time once it ran (in predicted-work units: measured ms over
-        # the GPU's recent measured / predicted ratio) -- a slot whose pods ran long gets the
-        # shorter pods next.  Open loop (GPUSCHED_LPT_FEEDBACK=0) the predicted sums stay level
-        # while the measured ones drift apart (MI355X N=1 trace: 108 vs 134.5 ms of 20 pods per
-        # slot stream, the long one pacing the pipeline, profiles/r05_lookahead/t20.json)
-        self.lpt_feedback = os.environ.get("GPUSCHED_LPT_FEEDBACK", "0") != "0"
-        self._lpt_pred: Dict[str, Tuple[Tuple[str, int, int], float]] = {}
-        self._lpt_ratio: Dict[str, List[float]] = {}        # device -> [decayed measured, decayed predicted]
         self.spread_ms = spread_ms
         # model error of a slot plan's predictions: a pod's co-runners are partly pods placed
         # AFTER it, unknown at planning time (MI355X bench traces: mean |log error| ~0.2 with
@@ -644,28 +634,9 @@ class BurstPlanner:
                 slots.remove(u)
                 res[O.key(p)] = u
                 self._slot_work[(uuid, u, n)] = self._slot_work.get((uuid, u, n), 0.0) + work[O.key(p)]
-                if self.lpt_feedback and self.timeline is not None:
-                    self._lpt_pred[O.key(p)] = ((uuid, u, n), work[O.key(p)])
             self.stats["slot_plans"] += 1
             self.stats["slot_pods"] += len(items)
         return res
-
-    LPT_DECAY = 0.97        # the measured / predicted ratio's memory (~30 pods)
-
-    def _lpt_measured(self, key: str, ms: float) -> None:
-        """A levelled pod ran `ms`: its slot's cumulative work takes the measured time (scaled
-        to predicted-work units by the device's recent measured / predicted ratio) instead of
-        the prediction."""
-        hit = self._lpt_pred.pop(key, None)
-        if hit is None or ms <= 0:
-            return
-        slot, pred = hit
-        acc = self._lpt_ratio.setdefault(slot[0], [0.0, 0.0])
-        acc[0] = acc[0] * self.LPT_DECAY + ms
-        acc[1] = acc[1] * self.LPT_DECAY + pred
-        ratio = acc[0] / acc[1] if acc[1] > 0 else 1.0
-        if slot in self._slot_work and ratio > 0:
-            self._slot_work[slot] += ms / ratio - pred
 
     def _pipe_context(self, gkey: Dict[Tuple, int], states, owner, dev_group, model, core) -> Any:
         """plan_corun's `pipe`: per GPU group of one device, its timeline's in-flight pods
@@ -1018,9 +989,6 @@ class BurstPlanner:
             return
         if how == "unreserve" or (how == "delete" and self.drop_on_delete):
             tl.drop(key)
-            hit = self._lpt_pred.pop(key, None)
-            if how == "unreserve" and hit is not None and hit[0] in self._slot_work:
-                self._slot_work[hit[0]] -= hit[1]          # it never ran on that slot
         elif how == "terminal":
             from .feedback import container_span
             span = container_span(pod)

@@ -19,7 +19,7 @@ uses to choose the slot of every new pod (plugins.gpu.planner).
 from __future__ import annotations
 
 import threading
-from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple
+from typing import Any, Dict, Hashable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -50,9 +50,6 @@ class SlotTimeline:
         self.unmatched = 0
         self._ver = 0                   # bumped by every change: context() results are memoised on it
         self._ctx_memo: Dict[Any, Dict[str, Any]] = {}
-        # called with (pod key, measured ms) after each measurement (the burst planner's
-        # measured slot levelling, BurstPlanner._lpt_measured)
-        self.listener: Optional[Callable[[str, float], None]] = None
 
     # ------------------------------------------------------------------ updates
     def next_burst(self) -> int:
@@ -73,27 +70,21 @@ class SlotTimeline:
         """The oldest unmeasured pod on the slot starting at `first_unit` ran [start, end)
         (times on the group's executor clock; a slot's pods run in placement order)."""
         self._ver += 1
-        hit = None
         with self._lock:
             slots = self._g.get(group)
-            if slots:
-                for slot, chain in slots.items():
-                    if slot[0] != first_unit:
-                        continue
-                    for e in chain:
-                        if e.end is None:
-                            e.start, e.end = float(start), float(end)
-                            self.measured += 1
-                            hit = e.key
-                            break
-                    if hit is not None:
-                        break
-            if hit is None:
+            if not slots:
                 self.unmatched += 1
                 return False
-        if self.listener is not None:
-            self.listener(hit, float(end) - float(start))
-        return True
+            for slot, chain in slots.items():
+                if slot[0] != first_unit:
+                    continue
+                for e in chain:
+                    if e.end is None:
+                        e.start, e.end = float(start), float(end)
+                        self.measured += 1
+                        return True
+            self.unmatched += 1
+            return False
 
     def drop(self, key: str) -> bool:
         """Remove a pod that will not run on its slot (unreserved, or deleted before it ran):
@@ -112,7 +103,6 @@ class SlotTimeline:
         """A pod identified by key ran [start, end) (a cluster's producer: the pod's container
         startedAt / finishedAt on the wall clock, instead of the executor's per-slot order)."""
         self._ver += 1
-        hit = False
         with self._lock:
             for slots in self._g.values():
                 for chain in slots.values():
@@ -120,15 +110,8 @@ class SlotTimeline:
                         if e.key == key:
                             e.start, e.end = float(start), float(end)
                             self.measured += 1
-                            hit = True
-                            break
-                    if hit:
-                        break
-                if hit:
-                    break
-        if hit and self.listener is not None:
-            self.listener(key, float(end) - float(start))
-        return hit
+                            return True
+        return False
 
     def realign(self) -> None:
         """Every group drained (e.g. a pipelined job synchronised its GPUs): only each group's
