@@ -390,3 +390,20 @@ def test_async_slot_plans_give_the_synchronous_placements():
     assert runs[True][1] == runs[False][1] > 0 and runs[True][2] == runs[False][2]
     for a, b in zip(runs[True][0], runs[False][0]):
         assert np.array_equal(a, b)
+
+
+def test_pacing_probe_adds_its_busy_wait_to_the_epoch_cost(monkeypatch):
+    """GPUSCHED_CP_EXTRA_MS (tools/gpu_cp_knee.sh): every epoch's schedule takes at least the
+    added busy wait, and the effort rule's cost samples include it."""
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    monkeypatch.setenv("GPUSCHED_CP_EXTRA_MS", "4")
+    cp = PB.ControlPlane(n_gpus=1, pods_per_gpu=4, iters=20, seed=1, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
+                         plan_slots="auto", adaptive=True, effort_up=0.65, effort_target=0.75)
+    assert cp.extra_s == 0.004
+    assert (cp._effort.up, cp._effort.target) == (0.65, 0.75)
+    for _ in range(3):
+        cp.finish_live()
+        cp.schedule_epoch()
+    assert cp.sched_s >= 3 * 0.004
+    assert min(cp._effort._costs) >= 0.004
