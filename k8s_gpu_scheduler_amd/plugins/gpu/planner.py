@@ -265,8 +265,9 @@ class BurstPlanner:
     # pipeline evaluation, model slot plans).  Level 1 keeps the phantoms and drops sweeps: on
     # the 8-GPU pipelined virtual node (MI355X, profiles/r05_pvn_levels/) the phantoms carry the
     # SLO quality (level 1 with phantoms and 1 sweep: 60.4 % SLOs, the full plan 60.2 %, round
-    # 5's first level 1 -- 2 sweeps, no phantoms -- 57.7 %, at the same pods/s) and the sweeps
-    # the cost (box CPU: 4.68 vs 5.02 ms per 8-GPU epoch, profiles/r05_cp_levels/)
+    # 5's first level 1 -- 2 sweeps, no phantoms -- 57.7 %, at the same pods/s; 59.5 vs 60.9 %
+    # in a 3-seed rerun, profiles/r05_pvn_final/) and the sweeps the cost (box CPU: 4.68 vs
+    # 5.02 ms per 8-GPU epoch, profiles/r05_cp_levels/)
     EFFORT_LEVELS = ((1, True, True, True), (4, True, True, True), (2, False, False, False), (0, False, False, False))
 
     @classmethod

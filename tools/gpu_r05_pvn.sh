@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${OUT_NAME:-r05_pvn}
 mkdir -p $OUT
-timeout -k 10 1100 python -u tools/pipelined_vn.py --gpus 8 --epochs 48 --warmup 5 --seeds 0 1 --passes 3 \
+timeout -k 10 1100 python -u tools/pipelined_vn.py --gpus 8 --epochs 48 --warmup 5 --seeds ${SEEDS:-0 1} --passes 3 \
   --policies ${POLICIES:-greedy planner planner-e1 planner-e2} --out $OUT/pipelined_vn.json > $OUT/pipelined_vn.log 2>&1
 rc=$?
 tail -1 $OUT/pipelined_vn.log | cut -c1-1500
