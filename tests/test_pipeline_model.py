@@ -407,3 +407,28 @@ def test_pacing_probe_adds_its_busy_wait_to_the_epoch_cost(monkeypatch):
         cp.schedule_epoch()
     assert cp.sched_s >= 3 * 0.004
     assert min(cp._effort._costs) >= 0.004
+
+
+def test_effort_level_table_and_its_override(monkeypatch):
+    """BurstPlanner.EFFORT_LEVELS: level 1 keeps the pipeline phantoms with a quarter of the
+    sweeps; GPUSCHED_EFFORT_LEVELS replaces the table (experiments) and is validated."""
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    from k8s_gpu_scheduler_amd.plugins.gpu.planner import BurstPlanner
+    cp = PB.ControlPlane(n_gpus=2, pods_per_gpu=4, iters=20, seed=1, balance=1.0, plan_bursts=True,
+                         plan_tolerance=0.3, slo_objective="corun", corun_sigma=0.05, plan_carry=1.0,
+                         plan_slots="auto", adaptive=False)
+    pl = cp.plugin.planner
+    sweeps = pl._configured[0]
+    pl.set_effort(1)
+    assert pl.pipe_phantoms and pl.pipe_eval and pl.slot_policy == "auto" and pl.sweeps == max(1, sweeps // 4)
+    pl.set_effort(2)
+    assert not pl.pipe_phantoms and not pl.pipe_eval and pl.slot_policy == "lpt" and pl.sweeps == max(1, sweeps // 2)
+    monkeypatch.setenv("GPUSCHED_EFFORT_LEVELS", "1,1,1,1;2,0,1,1;2,0,0,0;0,0,0,0")
+    pl.set_effort(1)                      # round 5's first level 1
+    assert not pl.pipe_phantoms and pl.pipe_eval and pl.sweeps == max(1, sweeps // 2)
+    monkeypatch.setenv("GPUSCHED_EFFORT_LEVELS", "1,1,1,1;2,0,1,1")
+    with pytest.raises(ValueError):
+        BurstPlanner._effort_levels()
+    monkeypatch.delenv("GPUSCHED_EFFORT_LEVELS")
+    pl.set_effort(0)
+    assert pl.pipe_phantoms and pl.sweeps == sweeps
