@@ -133,7 +133,9 @@ class DeviceExecutor:
         self._bufs: Dict[Tuple[str, int, int], _Buffers] = {}
         self._last_events: List[torch.cuda.Event] = []
         self._unit_last: Dict[int, Tuple[Tuple[int, int], torch.cuda.Event]] = {}
-        self.epoch_runs: List[List[PodRun]] = []
+        # (workload, units, iterations) of every pod launched, per epoch -- not the PodRuns: those
+        # hold two HIP events each, and a long run would keep every one of them alive
+        self.epoch_pods: List[List[Tuple[str, int, int]]] = []
         self._graphs: Dict[Tuple, "torch.cuda.CUDAGraph"] = {}
         self.lazy_captures = 0           # graphs captured by launch_epoch (not warm()): outside pod timing
         self.flops_done = 0.0
@@ -255,7 +257,7 @@ class DeviceExecutor:
             self.flops_done += w.flops * r.iters
             self.bytes_done += w.bytes * r.iters
         self._last_events = [ev for _, ev in {id(e): (k, e) for k, e in self._unit_last.values()}.values()]
-        self.epoch_runs.append(runs)
+        self.epoch_pods.append([(r.workload, r.n_units, r.iters) for r in runs])
 
     @staticmethod
     def pod_work(r: PodRun) -> float:

@@ -1200,7 +1200,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
             _nat.hip(required=True).xcd_probe(_mk_buf.data_ptr(), 8, torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
         marker()
-        n_runs0 = sum(len(r) for r in ex.epoch_runs)
+        n_runs0 = sum(len(r) for r in ex.epoch_pods)
     lazy0 = getattr(ex, "lazy_captures", 0)
     t_start = time.perf_counter()
     wall0 = time.time()
@@ -1222,7 +1222,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
     elapsed = time.perf_counter() - t_start
     if marker is not None:
         marker()
-        timed_pods = [(r.workload, r.n_units, r.iters) for ep in ex.epoch_runs for r in ep][n_runs0:]
+        timed_pods = [p for ep in ex.epoch_pods for p in ep][n_runs0:]
         with open(marker_path, "w") as f:
             json.dump({"pods": timed_pods, "gemm_share": bool(ex.gemm_share)}, f)
     wall1 = time.time()
