@@ -17,6 +17,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/longrun")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -25,13 +26,14 @@ def main() -> int:
     env = dict(os.environ, GPUSCHED_BENCH_TRACE=trace)
     with open(os.path.join(a.out, f"bench{a.steps}.log"), "w") as log:
         p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", str(a.steps),
-                            "--warmup", str(a.warmup), "--out", js], stdout=log, stderr=subprocess.STDOUT, env=env)
+                            "--warmup", str(a.warmup), "--seed", str(a.seed), "--out", js], stdout=log,
+                           stderr=subprocess.STDOUT, env=env)
     rss_mb = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss / 1024
     if p.returncode != 0:
         print(json.dumps({"rc": p.returncode, "max_rss_mb": rss_mb}))
         return p.returncode
     d = json.load(open(js))
-    out = {"steps": a.steps, "value": d["value"], "ms_per_step": d["ms_per_step"],
+    out = {"steps": a.steps, "seed": a.seed, "value": d["value"], "ms_per_step": d["ms_per_step"],
            "slo_attainment_pct": d["slo_attainment_pct"], "sol_pct": d["sol_pct"],
            "timed_graph_captures_rank0": d.get("timed_graph_captures_rank0"),
            "effort_epochs": (d.get("planner") or {}).get("effort_epochs"), "max_rss_mb_child": round(rss_mb, 1)}
