@@ -19,6 +19,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/longrun")
+    ap.add_argument("--extra", default="", help="more bench.py flags (one string)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     js = os.path.join(a.out, f"bench{a.steps}.json")
@@ -26,7 +27,7 @@ def main() -> int:
     env = dict(os.environ, GPUSCHED_BENCH_TRACE=trace)
     with open(os.path.join(a.out, f"bench{a.steps}.log"), "w") as log:
         p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", str(a.steps),
-                            "--warmup", str(a.warmup), "--seed", str(a.seed), "--out", js], stdout=log,
+                            "--warmup", str(a.warmup), "--seed", str(a.seed), "--out", js, *a.extra.split()], stdout=log,
                            stderr=subprocess.STDOUT, env=env)
     rss_mb = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss / 1024
     if p.returncode != 0:
@@ -36,7 +37,11 @@ def main() -> int:
     out = {"steps": a.steps, "seed": a.seed, "value": d["value"], "ms_per_step": d["ms_per_step"],
            "slo_attainment_pct": d["slo_attainment_pct"], "sol_pct": d["sol_pct"],
            "timed_graph_captures_rank0": d.get("timed_graph_captures_rank0"),
-           "effort_epochs": (d.get("planner") or {}).get("effort_epochs"), "max_rss_mb_child": round(rss_mb, 1)}
+           "effort_epochs": (d.get("planner") or {}).get("effort_epochs"), "max_rss_mb_child": round(rss_mb, 1),
+           "extra": a.extra}
+    for k in ("interference_mae", "corun_learner"):
+        if k in d:
+            out[k] = d[k]
     # pods completed per tenth of the run (GPU clock): does the rate drift over thousands of epochs?
     if os.path.exists(trace):
         ends = sorted(x[4] for x in json.load(open(trace))["pods"])
