@@ -420,6 +420,9 @@ class OnlineCorun:
         self._obs: List[Tuple[Tuple[int, ...], Tuple[float, ...], Tuple[float, ...], Tuple[float, ...],
                               Tuple[bool, ...]]] = []
         self._pending = 0
+        # every observed group, in order (GPUSCHED_CORUN_LOG=path: written by dump_log) -- a
+        # hardware run's observations replayed offline against refit variants
+        self.log: Optional[List[Any]] = [] if os.environ.get("GPUSCHED_CORUN_LOG") else None
         self.version = 0
         self.refits = 0
         self.err = {"prior": 0.0, "online": 0.0, "n": 0, "tput_sum": 0.0}
@@ -457,6 +460,9 @@ class OnlineCorun:
                 self.err["n"] += 1
                 self.err["tput_sum"] += tm
                 self._pending += 1
+            if self.log is not None:
+                self.log.append([[int(w) for w in wids], [float(x) for x in iters], list(st),
+                                 [float(x) for x in ms], list(tg)])
             self._obs.append((tuple(int(w) for w in wids), tuple(float(x) for x in iters), tuple(st),
                               tuple(float(x) for x in ms), tuple(tg)))
             if len(self._obs) > self.window:
@@ -520,6 +526,14 @@ class OnlineCorun:
             self.model = CorunModel(base.names, base.alone_ms * np.exp(x_new[:n_w]) * scale,
                                     base.u * np.exp(x_new[n_w]), base.v,
                                     dict(base.meta, version=f"{base.version}+online-{self.version}"))
+
+    def dump_log(self, path: Optional[str] = None) -> None:
+        """Write the observation log (GPUSCHED_CORUN_LOG) as JSON: names and groups."""
+        path = path or os.environ.get("GPUSCHED_CORUN_LOG")
+        if self.log is None or not path:
+            return
+        with open(path, "w") as f:
+            json.dump({"names": list(self.base.names), "groups": self.log}, f)
 
     def wait_idle(self, timeout_s: float = 10.0) -> None:
         t = time.time()

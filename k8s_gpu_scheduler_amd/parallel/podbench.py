@@ -526,6 +526,7 @@ class ControlPlane:
     def interference_mae(self) -> Optional[Dict[str, Any]]:
         out = self.online.mae() if self.online is not None else None
         if self.corun is not None:
+            self.corun.dump_log()           # GPUSCHED_CORUN_LOG: the learner's observations (end of run)
             m = self.corun.mae()
             q = float(np.mean(list(self.quarter_tput.values())))
             out = dict(out or {})
