@@ -572,9 +572,14 @@ def solve_refit(p: Dict[str, Any]) -> Dict[str, Any]:
         t = model.batch_times(wids, iters, mask, st, pin) - st
         return np.log(np.maximum(t, 1e-9) / np.maximum(ms, 1e-9))[sel]
 
+    # replay experiments (tools/corun_replay.py): "uncentred" = round 5's first refit, "noscale" =
+    # no global time scale
+    variant = p.get("variant") or os.environ.get("GPUSCHED_REFIT_VARIANT", "centred")
     x0 = np.asarray(p["x"], dtype=np.float64)
     r = resid(model_of(x0), tgt)
     scale = float(np.exp(-np.median(r))) if r.size else 1.0
+    if variant == "noscale":
+        scale = 1.0
     x_new, rejected = x0, 0
     if p["stage2"]:
         n_fit = max(1, (3 * G) // 4)
@@ -589,6 +594,17 @@ def solve_refit(p: Dict[str, Any]) -> Dict[str, Any]:
             x_new = sol.x
         else:
             rejected = 1
+    if variant != "uncentred":
+        # the global time scale and the per-workload log-scales are degenerate (scale x
+        # exp(x_w)): uncentred, they drifted apart refit after refit (MI355X bench log, 2,000
+        # steps: time scale 3.9 against x ~ -1.4) and the ridge then pulled toward a wrong origin
+        # -- online error 311 vs 240 for the offline model.  Centred, the per-workload scales
+        # stay deviations from the global one: 238 vs 240 (tools/corun_replay.py,
+        # profiles/r05_corun_replay/)
+        mu = float(np.mean(x_new[:n_w]))
+        x_new = np.array(x_new, dtype=np.float64)
+        x_new[:n_w] -= mu
+        scale *= float(np.exp(mu))
     return {"x": x_new, "scale": scale, "rejected": rejected}
 
 

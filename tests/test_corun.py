@@ -147,6 +147,25 @@ def test_online_corun_learns_a_slower_world():
     assert on.model.version != base.version
 
 
+def test_online_corun_keeps_per_workload_scales_centred():
+    """A world 30 % slower with per-workload deviations: refit after refit the global time scale
+    carries the 30 % and the per-workload log-scales stay centred on 0 (they are degenerate with
+    the scale; uncentred they drifted to a 3.9x scale on a hardware log and the ridge pulled
+    toward the wrong origin, tools/corun_replay.py); the online error beats the offline one."""
+    base = CR.CorunModel.load()
+    rng = np.random.default_rng(5)
+    dev = np.exp(rng.normal(0.0, 0.1, len(base.names)))
+    world = CR.CorunModel(base.names, base.alone_ms * 1.3 * dev, base.u, base.v)
+    on = CR.OnlineCorun(base, refit_every=32, window=256, background=False, min_obs=64, min_calib=64)
+    for _ in range(200):
+        ws = [int(x) for x in rng.integers(0, len(base.names), 4)]
+        on.observe_group(ws, [20] * 4, world.group_durations(ws, [20] * 4))
+    n_w = len(base.names)
+    assert on.refits > 0 and abs(float(np.mean(on._x[:n_w]))) < 1e-9
+    assert 1.15 < on.time_scale < 1.45
+    assert on.mae()["online"] < 0.7 * on.mae()["prior"]
+
+
 def test_online_corun_refits_in_a_worker_process():
     """The control plane's mode: refits run in a child process (no interpreter-lock
     contention with the scheduler) and the refitted model is installed on return."""
