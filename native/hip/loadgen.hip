@@ -1001,7 +1001,9 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // 3 / 4 (A/B arms): a co-running GEMM too small for one 256x256 tile per CU of its share
   // takes 256x128 (8 waves, 2 / 3 LDS stages) when that still gives every CU of the share a
   // block -- twice the arithmetic intensity per staged byte of 128x128 (85 vs 64 FLOP/B)
-  if (!alone && g_gemm_policy >= 3 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget)
+  // (exactly 3 / 4: arms 5-7 below are other tiles, and a `>= 3` test here used to shadow them)
+  if (!alone && (g_gemm_policy == 3 || g_gemm_policy == 4) && M % 256 == 0 && N % 128 == 0 &&
+      (M / 256) * (N / 128) >= budget)
     return g_gemm_policy == 3 ? 5 : 8;
   // 7: the co-running small GEMM on the 256x128 8-phase kernel when that gives every CU of the
   // share a block

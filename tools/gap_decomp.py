@@ -1,0 +1,264 @@
+"""Where the bench's step time goes against its floors.
+
+Replays the TIMED pods of one bench run (`bench.py --dump-placements F`, the driver's seed /
+steps / warmup) on one MI355X in several regimes, interleaved `--reps` times, and calibrates the
+amd-smi UMC activity that the bench samples against triads of known bandwidth:
+
+  replay            the pods through the bench's DeviceExecutor (4 Burstable slot streams,
+                    unit-ordered, HIP graphs): the bench's device work without its host / control
+                    plane; `replay_nograph` the same from eager launches (the filtered replays'
+                    reference)
+  replay_gemm       the same pods and slots with the stream kernels left out (GEMMs only)
+  replay_triad      ... with the GEMMs left out (stream kernels only)
+  serial_share      every kernel of every pod, in pod order, on ONE stream (no co-running),
+                    GEMM tiles for the pod's 64-CU share as in the bench
+  serial_full       the same with whole-chip GEMM tiles (the lone-kernel picker)
+  triad_serial      only the stream kernels, one stream (the HBM time at the lone rate)
+  gemm_serial_full  only the GEMMs, one stream, whole-chip tiles (the MFMA time at the lone rate)
+  gemm_serial_share only the GEMMs, one stream, share tiles
+  split_full        two streams side by side: every triad on one, every GEMM (whole-chip tiles)
+                    on the other -- the best overlap of the two kinds when pod order is free
+  split_share       the same with the share tiles, GEMMs spread over 4 streams by pod slot
+  mask_split_<u>    triads on a stream CU-masked to u of the 8 units, GEMMs on the other 8-u
+                    units (tiles for those CUs): disjoint CU partitions
+
+and `triad_units_<u>` (a 768 MB triad on u masked units: bandwidth vs CUs) and `umc_cal` (a
+triad at several grid sizes for ~0.4 s each: achieved TB/s vs amd-smi umc_activity).
+
+Writes --out (JSON) and prints one line per regime.  Read by tools/gap_report.py.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+# one hardware queue per stream (bench.py raises it the same way; HIP shares queues beyond it)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "32")
+from typing import Callable, Dict, List
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from k8s_gpu_scheduler_amd.models import workloads as W  # noqa: E402
+from k8s_gpu_scheduler_amd.ops import loadgen  # noqa: E402
+from k8s_gpu_scheduler_amd.ops.cumask import MaskedStream  # noqa: E402
+from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun  # noqa: E402
+from k8s_gpu_scheduler_amd.parallel.podbench import build_parser, gpu_executor  # noqa: E402
+from k8s_gpu_scheduler_amd.plugins.gpu.devices import CUS_PER_XCD as CUS_PER_UNIT, cu_slice_mask  # noqa: E402
+
+
+class KindExecutor(DeviceExecutor):
+    """DeviceExecutor whose pods run only one kind of op ('gemm' / 'triad'; '' = all)."""
+    kind = ""
+
+    def _enqueue_ops(self, r, bufs, st, budget):
+        for _ in range(r.iters):
+            for o, t in bufs.ops:
+                if self.kind == "gemm" and not o.is_gemm or self.kind == "triad" and o.is_gemm:
+                    continue
+                _one(o, t, st, budget, self.triad_blocks)
+
+
+def _one(o, t, st, budget: int, blocks: int = 0) -> None:
+    if o.kind == "gemm":
+        a, bt, bias, c = t
+        loadgen.gemm(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+    elif o.kind == "gemm8":
+        a, bt, bias, c = t
+        loadgen.gemm_fp8(a, bt, out=c, bias=bias, relu=o.relu, stream=st, cu_budget=budget)
+    else:
+        x, y, z = t
+        loadgen.triad(x, y, z, 1.0001, blocks=blocks, stream=st)
+
+
+def timed(fn: Callable[[], None]) -> float:
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--placements", required=True)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default="gpurun_out/gap/decomp.json")
+    ap.add_argument("--mask-units", default="2,3,4,5,6")
+    ap.add_argument("--skip-cal", action="store_true")
+    args = ap.parse_args()
+    dump = json.load(open(args.placements))
+    names = dump["workloads"]
+    epochs = [e["arr"] for e in dump["epochs"] if e["timed"]]
+    pods = [(names[int(r[3])], int(r[1]), int(r[2]), int(r[4])) for ep in epochs for r in ep if int(r[0]) == 0]
+    steps = len(epochs)
+    torch.cuda.set_device(0)
+    ba = build_parser().parse_args([])
+    ex = gpu_executor(ba, 0)
+    kx = KindExecutor(0)
+    kx.use_graphs = False
+    kx.triad_blocks = ex.triad_blocks
+    ex.warm([PodRun(0, wl, u, n, it, masked=False) for wl, u, n, it in pods])
+    kx._bufs, kx._streams = ex._bufs, ex._streams       # the same operands and slot streams
+    flops = sum(W.get(wl).flops * it for wl, _, _, it in pods)
+    mbytes = sum(W.get(wl).bytes * it for wl, _, _, it in pods)
+    tri_bytes = sum(sum(o.bytes for o in W.get(wl).ops if not o.is_gemm) * it for wl, _, _, it in pods)
+
+    def epochs_runs() -> List[List[PodRun]]:
+        out, i = [], 0
+        for ep in epochs:
+            rs = []
+            for r in ep:
+                if int(r[0]) != 0:
+                    continue
+                rs.append(PodRun(i, names[int(r[3])], int(r[1]), int(r[2]), int(r[4]), masked=False))
+                i += 1
+            out.append(rs)
+        return out
+
+    def replay(e: DeviceExecutor, kind: str = "") -> Callable[[], None]:
+        def f() -> None:
+            if isinstance(e, KindExecutor):
+                e.kind = kind
+            for rs in epochs_runs():
+                e.launch_epoch(rs)
+            e.wait_all()
+        return f
+
+    s_main = torch.cuda.Stream()
+    s_aux = [torch.cuda.Stream() for _ in range(4)]
+
+    def serial(kind: str, share: bool) -> Callable[[], None]:
+        def f() -> None:
+            for wl, u, n, it in pods:
+                bufs = ex.buffers(W.get(wl), u, n)
+                for _ in range(it):
+                    for o, t in bufs.ops:
+                        if kind == "gemm" and not o.is_gemm or kind == "triad" and o.is_gemm:
+                            continue
+                        _one(o, t, s_main, n * CUS_PER_UNIT if share else 0)
+        return f
+
+    def split(share: bool, tri_st=None, gemm_st=None, gemm_budget: int = 0) -> Callable[[], None]:
+        def f() -> None:
+            ts = tri_st or s_main
+            for wl, u, n, it in pods:
+                bufs = ex.buffers(W.get(wl), u, n)
+                gs = gemm_st or (s_aux[u // 2 % 4] if share else s_aux[0])
+                b = n * CUS_PER_UNIT if share else gemm_budget
+                for _ in range(it):
+                    for o, t in bufs.ops:
+                        _one(o, t, gs if o.is_gemm else ts, b)
+        return f
+
+    regimes: Dict[str, Callable[[], None]] = {
+        "replay": replay(ex),
+        "replay_nograph": replay(kx, ""),
+        "replay_gemm": replay(kx, "gemm"),
+        "replay_triad": replay(kx, "triad"),
+        "serial_share": serial("", True),
+        "serial_full": serial("", False),
+        "triad_serial": serial("triad", False),
+        "gemm_serial_full": serial("gemm", False),
+        "gemm_serial_share": serial("gemm", True),
+        "split_full": split(False),
+        "split_share": split(True),
+    }
+    masked: Dict[int, tuple] = {}
+    for u in [int(x) for x in args.mask_units.split(",") if x]:
+        ts = MaskedStream(cu_slice_mask(0, u))
+        gs = MaskedStream(cu_slice_mask(u, 8 - u))
+        masked[u] = (ts, gs)
+        regimes[f"mask_split_{u}"] = split(False, ts.stream, gs.stream, (8 - u) * CUS_PER_UNIT)
+
+    smi = None
+    try:
+        from k8s_gpu_scheduler_amd.telemetry.smi_sampler import ActivitySampler
+        smi = ActivitySampler([0], 0.005)
+        if not smi.start():
+            print("amd-smi sampler off:", smi.error, flush=True)
+            smi = None
+    except Exception as e:              # calibration is optional; timings are not
+        print("amd-smi sampler off:", e, flush=True)
+        smi = None
+
+    for f in regimes.values():          # one untimed pass each (graphs, queues, clocks)
+        f()
+    res: Dict[str, Dict[str, object]] = {k: {"ms": []} for k in regimes}
+    for rep in range(args.reps):
+        for k, f in regimes.items():
+            w0 = time.time()
+            ms = timed(f)
+            w1 = time.time()
+            res[k]["ms"].append(round(ms, 3))
+            if smi is not None:
+                smi.poll()
+                s = smi.summary(w0, w1)
+                res[k].setdefault("umc", []).append(s["umc_activity_pct_mean"])
+                res[k].setdefault("gfx", []).append(s["gfx_activity_pct_mean"])
+        print(f"rep {rep}: " + ", ".join(f"{k} {v['ms'][-1]:.1f}" for k, v in res.items()), flush=True)
+    for k, v in res.items():
+        v["ms_per_step"] = round(min(v["ms"]) / steps, 4)
+        v["ms_per_step_median"] = round(sorted(v["ms"])[len(v["ms"]) // 2] / steps, 4)
+
+    # triad bandwidth vs masked CU units (768 MB per pass)
+    n = 64 << 20
+    x, y, z = (torch.ones(n, device="cuda") for _ in range(3))
+    tb = {}
+    for u in (1, 2, 3, 4, 5, 6, 8):
+        ms_ = MaskedStream(cu_slice_mask(0, u))
+
+        def tri(st=ms_.stream) -> None:
+            for _ in range(20):
+                loadgen.triad(x, y, z, 1.0001, stream=st)
+        tri()
+        best = min(timed(tri) for _ in range(3))
+        tb[u] = round(12.0 * n * 20 / (best / 1e3) / 1e12, 3)
+        ms_.close()
+    print("triad TB/s by masked units:", tb, flush=True)
+
+    cal = []
+    if smi is not None and not args.skip_cal:
+        for blocks in (32, 64, 128, 256, 512, 8192):
+            def tri2(b=blocks) -> None:
+                loadgen.triad(x, y, z, 1.0001, blocks=b, stream=s_main)
+            tri2()
+            torch.cuda.synchronize()
+            w0 = time.time()
+            t0 = time.perf_counter()
+            k = 0
+            while time.perf_counter() - t0 < 0.45:
+                for _ in range(8):
+                    tri2()
+                k += 8
+                torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            w1 = time.time()
+            smi.poll()
+            s = smi.summary(w0 + 0.1, w1)         # skip the moving average's ramp
+            cal.append({"blocks": blocks, "tbps": round(12.0 * n * k / el / 1e12, 3),
+                        "umc_pct": s["umc_activity_pct_mean"], "gfx_pct": s["gfx_activity_pct_mean"],
+                        "samples": s["samples"]})
+            print("umc cal", cal[-1], flush=True)
+    if smi is not None:
+        smi.stop()
+    for ts, gs in masked.values():
+        ts.close()
+        gs.close()
+    out = {"steps": steps, "pods": len(pods), "model_flops_per_step": flops / steps,
+           "model_bytes_per_step": mbytes / steps, "triad_bytes_per_step": tri_bytes / steps,
+           "regimes": res, "triad_tbps_by_units": tb, "umc_calibration": cal,
+           "placements": args.placements, "reps": args.reps}
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    json.dump(out, open(args.out, "w"), indent=1)
+    for k, v in res.items():
+        print(f"{k:20s} {v['ms_per_step']:.3f} ms/step  umc {v.get('umc')}", flush=True)
+    ex.close()
+
+
+if __name__ == "__main__":
+    main()
