@@ -148,3 +148,66 @@ def test_direction_arrivals_stay_in_band_with_a_40pct_slower_gpu():
     assert share.min() >= 0.15 and share.max() <= 0.5, share
     assert abs(share.mean() - 1 / 2.4) < 0.05, share
     assert all(min(n) > 0 for n, *_ in res)
+
+
+# ---- the speed gate must see a 10-20 % slower GPU at realistic noise.
+# Round 5's gate (every one of 7 window observations on the slow side) left GPU 1's share at
+# 0.50 with +-8 % noise; the rank test (planner.rank_z, SPEED_Z) is the statistical decision.
+# A single run's 60-burst share moves by +-0.015 with the arrival / noise seed (4-pod bursts
+# split discretely and the SLO objective picks among near-balanced splits), so the bars are on
+# the mean over five seeds; seed 5 is the harness run VERDICT r5 quoted (round-5 gate: 0.504 /
+# 0.497 / 0.500 for the three cases below).
+SEEDS = (5, 6, 7, 8, 9)
+
+
+def _share(res, start=60):
+    return float(np.mean([s for _, s, _, _ in res][start:]))
+
+
+def _mean_share(slow, noise):
+    return float(np.mean([_share(_run(120, slow=slow, noise=noise, seed=sd)[0]) for sd in SEEDS]))
+
+
+def test_ten_percent_slower_gpu_is_seen_at_8pct_noise():
+    res, _ = _run(120, slow=(1.0, 1.1), noise=0.08)
+    assert _share(res) <= 0.485, _share(res)             # fair 0.5, target 1 / 2.1 = 0.476
+    assert all(min(n) > 0 for n, *_ in res)
+    assert _mean_share((1.0, 1.1), 0.08) <= 0.4875       # five seeds: 0.486 (round 5: ~0.50)
+
+
+def test_twenty_percent_slower_gpu_is_seen_at_15pct_noise():
+    assert _mean_share((1.0, 1.2), 0.15) <= 0.47         # target 1 / 2.2 = 0.455; five seeds 0.463
+
+
+def test_identical_gpus_at_8pct_noise_plan_as_if_noiseless():
+    assert abs(_mean_share((1.0, 1.0), 0.08) - 0.5) <= 0.01
+    same = []
+    for sd in SEEDS:
+        quiet, _ = _run(120, noise=0.0, seed=sd)
+        noisy, _ = _run(120, noise=0.08, seed=sd)
+        same.append(sum(a[0] == b[0] for a, b in zip(quiet, noisy)) / len(quiet))
+    assert np.mean(same) >= 0.9 and min(same) >= 0.85, same
+
+
+def test_rank_z_separates_shifted_windows_only():
+    from k8s_gpu_scheduler_amd.plugins.gpu.planner import rank_z
+    rng = np.random.default_rng(0)
+    same = [abs(rank_z(1 + 0.08 * rng.uniform(-1, 1, 16), 1 + 0.08 * rng.uniform(-1, 1, 48))) for _ in range(400)]
+    # identical distributions: |z| >= 2.33 in about 2 % of draws
+    assert np.mean(np.array(same) >= 2.33) < 0.05
+    slow = [rank_z(1.1 * (1 + 0.08 * rng.uniform(-1, 1, 16)), 1 + 0.08 * rng.uniform(-1, 1, 48)) for _ in range(100)]
+    assert min(slow) > 2.33
+    assert rank_z(np.array([1.0, 1.0]), np.array([1.0, 1.0])) == 0.0
+    assert rank_z(np.array([]), np.array([1.0])) == 0.0
+
+
+def test_direction_twin_over_seeds():
+    """The 40 %-slower direction case over five arrival seeds: GPU 1's mean share of epochs 6-11
+    within 0.06 of the 1 / 2.4 target for every seed and within 0.02 on average (round 6 gate:
+    0.37-0.46 per seed, 0.419 on average)."""
+    ms = []
+    for sd in SEEDS:
+        res, _ = _run(12, slow=(1.0, 1.4), seed=sd)
+        ms.append(float(np.mean([s for _, s, _, _ in res][6:])))
+    assert all(abs(m - 1 / 2.4) < 0.06 for m in ms), ms
+    assert abs(np.mean(ms) - 1 / 2.4) < 0.02, ms

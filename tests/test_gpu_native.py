@@ -285,15 +285,12 @@ def test_executor_epoch_and_bench_smoke():
     assert r["value"] > 0 and not r["simulated"] and r["unscheduled"] == 0
 
 
-def test_planner_feedback_moves_work_off_a_really_slower_gpu():
-    """The N-GPU bench's planner path on hardware, checked for DIRECTION: a 2-GPU control plane
-    (co-run planner + backlog carry + measured feedback) plans each epoch; each GPU's group runs
-    on the MI355X in turn (isolated, the bench's executor), and GPU 1's pods really run 40 % more
-    iterations than the model is told -- a GPU slower than its sibling.  After 12 epochs the
-    measured feedback must have raised GPU 1's measured speed ratio over GPU 0's and moved
-    planned work off it, without ever starving a GPU of a whole burst (the backlog is bounded,
-    planner.observe_time); and the co-run model's predicted group times must be within 15 % of
-    the measured ones for >= 80 % of GPU 0's (unslowed) groups."""
+def _direction_run(slow: float, epochs: int, first: int):
+    """The N-GPU bench's planner path on hardware: a 2-GPU control plane (co-run planner +
+    backlog carry + measured feedback) plans each epoch; each GPU's group runs on the MI355X in
+    turn (isolated, the bench's executor), and GPU 1's pods really run `slow` x the iterations
+    the model is told -- a GPU slower than its sibling.  Returns (planner, GPU 1 shares of epochs
+    >= first, backlog spreads, GPU 0 group errors, state printer)."""
     import numpy as np
     from k8s_gpu_scheduler_amd.models import workloads as W
     from k8s_gpu_scheduler_amd.parallel import podbench as PB
@@ -304,7 +301,7 @@ def test_planner_feedback_moves_work_off_a_really_slower_gpu():
     model = cp.corun.base if cp.corun is not None else planner.plugin.corun_model()
     ex = PB.gpu_executor(PB.build_parser().parse_args([]), 0)
     # every slot a pod of either GPU can land on, at both iteration counts (as the bench warms)
-    for it in (20, 28):
+    for it in sorted({20, int(round(20 * slow))}):
         ex.warm([PodRun(0, wl, u, 2, it, masked=False) for wl in W.NAMES for u in (0, 2, 4, 6)])
     share, errs, spreads = [], [], []
     fed = {}
@@ -316,9 +313,10 @@ def test_planner_feedback_moves_work_off_a_really_slower_gpu():
     planner.observe_time = spy
 
     def state(e):
-        return (f"epoch {e} backlog {planner.backlog} speeds "
-                f"{[planner.speed(k) for k in sorted(planner.backlog)]} fed {fed} shares {np.round(share, 3)}")
-    for e in range(12):
+        keys = sorted(planner.backlog)
+        return (f"epoch {e} backlog {planner.backlog} speeds {[planner.speed(k) for k in keys]} "
+                f"rel {planner.rel_speeds(keys) if keys else None} fed {fed} shares {np.round(share, 3)}")
+    for e in range(epochs):
         cp.finish_live()
         arr = cp.schedule_epoch()
         per_gpu = np.zeros((2, PB.TELE))
@@ -328,10 +326,10 @@ def test_planner_feedback_moves_work_off_a_really_slower_gpu():
         if planner.backlog:
             spreads.append(max(planner.backlog.values()) - min(planner.backlog.values()))
         work = {g: sum(model.alone_ms[model.wid(r.workload)] * r.iters for r in runs[g]) for g in (0, 1)}
-        if e >= 6:
+        if e >= first:
             share.append(work[1] / (work[0] + work[1]))
         for r in runs[1]:
-            r.iters = int(round(r.iters * 1.4))     # the slower GPU: work the model does not see
+            r.iters = int(round(r.iters * slow))    # the slower GPU: work the model does not see
         for g in (0, 1):                            # each GPU's group in isolation, in turn
             ex.launch_epoch(runs[g])
             ex.wait_all()
@@ -345,18 +343,48 @@ def test_planner_feedback_moves_work_off_a_really_slower_gpu():
                 errs.append(abs(pred - wall) / wall)
         cp.update_telemetry(per_gpu, 1.0)
     ex.close()
-    g0, g1 = (PB.NODE, 0), (PB.NODE, 1)
-    print(state(12), "group errors", np.round(errs, 3), "backlog spreads", np.round(spreads, 2),
+    print(state(epochs), "group errors", np.round(errs, 3), "backlog spreads", np.round(spreads, 2),
           "lazy captures", ex.lazy_captures)
+    return planner, share, spreads, errs, state
+
+
+def test_planner_feedback_moves_work_off_a_really_slower_gpu():
+    """DIRECTION on hardware, GPU 1 40 % slower: after 12 epochs the measured feedback must have
+    raised GPU 1's measured speed ratio over GPU 0's and moved planned work off it, without ever
+    starving a GPU of a whole burst (the backlog is bounded, planner.observe_time); and the co-run
+    model's predicted group times must be within 15 % of the measured ones for >= 80 % of GPU 0's
+    (unslowed) groups."""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    planner, share, spreads, errs, state = _direction_run(1.4, 12, 6)
+    g0, g1 = (PB.NODE, 0), (PB.NODE, 1)
     assert planner.speed(g1) > 1.2 * planner.speed(g0), state(12)      # GPU 1 measured slower
     # (a burst is 4 pods of unequal length, so a single burst's share is one of a handful of
-    # discrete splits around the 1 / 2.4 target -- 0.148 is GPU 1 taking only the burst's
-    # shortest pod after a 0.485 epoch.  The CPU twin with 8 % measurement noise, 16 noise
-    # seeds x 8 epochs: shares 0.148-0.592, per-run means 0.41-0.45; a starved GPU would be 0)
-    assert 0.3 < float(np.mean(share)) < 0.5 and min(share) >= 0.12 and max(share) <= 0.6, state(12)
+    # discrete splits around the 1 / 2.4 target.  Round 6's rank-test gate decides from the
+    # third observation on for a shift this large: the CPU twin (tests/test_backlog_control.py)
+    # keeps every burst of epochs 6-11 in [0.15, 0.5] on these arrivals)
+    assert 0.3 < float(np.mean(share)) < 0.5 and min(share) >= 0.15 and max(share) <= 0.55, state(12)
     # bounded: never more than the planner's stored clip of a balanced burst's work
     assert max(spreads) <= planner.STORE_CLIP * planner._burst_ms + 1e-6, (spreads, state(12))
     assert np.mean(np.asarray(errs) <= 0.15) >= 0.8, errs
+
+
+def test_planner_feedback_sees_a_15pct_slower_gpu():
+    """the same hardware path with GPU 1 only 15 % slower -- the size of a
+    power-capped or noisy-neighbour GPU, which round 5's all-observations gate could not see
+    through pipeline noise.  The rank-test gate must pass GPU 1's speed to the plans (rel speed
+    above GPU 0's).  (Which share that buys is a CPU-test property over many bursts and seeds,
+    tests/test_backlog_control.py: over 8 bursts of 4 pods the split is too discrete -- the CPU
+    twin of this case reads 0.48-0.51 -- so here it only must not starve either GPU.)"""
+    import numpy as np
+    from k8s_gpu_scheduler_amd.parallel import podbench as PB
+    planner, share, spreads, _, state = _direction_run(1.15, 16, 8)
+    g0, g1 = (PB.NODE, 0), (PB.NODE, 1)
+    rel = planner.rel_speeds([g0, g1])
+    assert planner.speed(g1) > 1.07 * planner.speed(g0), state(16)
+    assert rel[1] > rel[0], state(16)                                    # the gate passed it on
+    assert 0.3 < float(np.mean(share)) < 0.55 and min(share) > 0.0, state(16)
+    assert max(spreads) <= planner.STORE_CLIP * planner._burst_ms + 1e-6, (spreads, state(16))
 
 
 def test_rccl_probe_single_rank(tmp_path, monkeypatch):

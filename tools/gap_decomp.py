@@ -35,8 +35,11 @@ import os
 import sys
 import time
 
-# one hardware queue per stream (bench.py raises it the same way; HIP shares queues beyond it)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "32")
+# the bench's hardware-queue limit (bench.py).  Measured (profiles/r06_gap/): the same replay
+# runs 7.32 ms / step under a limit of 32 with ~20 streams alive in the process vs 6.75 / 6.69
+# under 16 / 8 with 5 -- every regime family below therefore runs in its own process with only
+# the streams it uses (the 4 slot streams, or 2 masked ones)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 from typing import Callable, Dict, List
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -88,8 +91,13 @@ def main() -> None:
     ap.add_argument("--placements", required=True)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default="gpurun_out/gap/decomp.json")
-    ap.add_argument("--mask-units", default="2,3,4,5,6")
-    ap.add_argument("--skip-cal", action="store_true")
+    ap.add_argument("--mask-units", default="", help="mask_split regimes for these unit counts (own process)")
+    ap.add_argument("--triad-units", action="store_true", help="triad TB/s vs masked units")
+    ap.add_argument("--umc-cal", action="store_true", help="triad TB/s vs amd-smi umc_activity")
+    ap.add_argument("--passes", type=int, default=1,
+                    help="back-to-back passes per timed regime run; amd-smi umc is averaged over the "
+                         "last half of the run (its firmware moving average lags a regime change)")
+    ap.add_argument("--only", default="", help="comma-separated regime names to run (default: all)")
     args = ap.parse_args()
     dump = json.load(open(args.placements))
     names = dump["workloads"]
@@ -102,7 +110,13 @@ def main() -> None:
     kx = KindExecutor(0)
     kx.use_graphs = False
     kx.triad_blocks = ex.triad_blocks
-    ex.warm([PodRun(0, wl, u, n, it, masked=False) for wl, u, n, it in pods])
+    mask_units = [int(x) for x in args.mask_units.split(",") if x]
+    core = not mask_units and not args.triad_units and not args.umc_cal
+    if core:
+        ex.warm([PodRun(0, wl, u, n, it, masked=False) for wl, u, n, it in pods])
+    else:                                               # operands only: no slot streams / queues
+        for wl, u, n, it in pods:
+            ex.buffers(W.get(wl), u, n)
     kx._bufs, kx._streams = ex._bufs, ex._streams       # the same operands and slot streams
     flops = sum(W.get(wl).flops * it for wl, _, _, it in pods)
     mbytes = sum(W.get(wl).bytes * it for wl, _, _, it in pods)
@@ -120,17 +134,25 @@ def main() -> None:
             out.append(rs)
         return out
 
-    def replay(e: DeviceExecutor, kind: str = "") -> Callable[[], None]:
+    def replay(e: DeviceExecutor, kind: str = "", ahead: int = 0) -> Callable[[], None]:
+        """ahead = 0: every epoch enqueued at once; L > 0: the bench's launch-ahead pipeline (epoch
+        e is launched once epoch e-L-1 has finished, host-polled as the bench's collect)."""
         def f() -> None:
             if isinstance(e, KindExecutor):
                 e.kind = kind
+            pending = []
             for rs in epochs_runs():
                 e.launch_epoch(rs)
+                pending.append(rs)
+                while ahead and len(pending) > ahead:
+                    e.wait_epoch(pending.pop(0))
             e.wait_all()
         return f
 
-    s_main = torch.cuda.Stream()
-    s_aux = [torch.cuda.Stream() for _ in range(4)]
+    # serial / split regimes reuse the 4 slot streams (no extra hardware queues)
+    s_aux = [ex.stream_for(u, 2, False).stream for u in (0, 2, 4, 6)] if core else []
+    s_main = s_aux[0] if core else None
+    s_tri = torch.cuda.Stream() if core else None       # split_share's triads (a 5th stream)
 
     def serial(kind: str, share: bool) -> Callable[[], None]:
         def f() -> None:
@@ -145,18 +167,19 @@ def main() -> None:
 
     def split(share: bool, tri_st=None, gemm_st=None, gemm_budget: int = 0) -> Callable[[], None]:
         def f() -> None:
-            ts = tri_st or s_main
+            ts = tri_st or (s_tri if share else s_aux[0])
             for wl, u, n, it in pods:
                 bufs = ex.buffers(W.get(wl), u, n)
-                gs = gemm_st or (s_aux[u // 2 % 4] if share else s_aux[0])
+                gs = gemm_st or (s_aux[u // 2 % 4] if share else s_aux[1])
                 b = n * CUS_PER_UNIT if share else gemm_budget
                 for _ in range(it):
                     for o, t in bufs.ops:
                         _one(o, t, gs if o.is_gemm else ts, b)
         return f
 
-    regimes: Dict[str, Callable[[], None]] = {
+    regimes: Dict[str, Callable[[], None]] = {} if not core else {
         "replay": replay(ex),
+        "replay_la2": replay(ex, "", 2),
         "replay_nograph": replay(kx, ""),
         "replay_gemm": replay(kx, "gemm"),
         "replay_triad": replay(kx, "triad"),
@@ -169,12 +192,15 @@ def main() -> None:
         "split_share": split(True),
     }
     masked: Dict[int, tuple] = {}
-    for u in [int(x) for x in args.mask_units.split(",") if x]:
+    for u in mask_units:
         ts = MaskedStream(cu_slice_mask(0, u))
         gs = MaskedStream(cu_slice_mask(u, 8 - u))
         masked[u] = (ts, gs)
         regimes[f"mask_split_{u}"] = split(False, ts.stream, gs.stream, (8 - u) * CUS_PER_UNIT)
 
+    if args.only:
+        keep = set(args.only.split(","))
+        regimes = {k: v for k, v in regimes.items() if k in keep}
     smi = None
     try:
         from k8s_gpu_scheduler_amd.telemetry.smi_sampler import ActivitySampler
@@ -192,12 +218,12 @@ def main() -> None:
     for rep in range(args.reps):
         for k, f in regimes.items():
             w0 = time.time()
-            ms = timed(f)
+            ms = timed(lambda: [f() for _ in range(args.passes)]) / args.passes
             w1 = time.time()
             res[k]["ms"].append(round(ms, 3))
             if smi is not None:
                 smi.poll()
-                s = smi.summary(w0, w1)
+                s = smi.summary(0.5 * (w0 + w1), w1)
                 res[k].setdefault("umc", []).append(s["umc_activity_pct_mean"])
                 res[k].setdefault("gfx", []).append(s["gfx_activity_pct_mean"])
         print(f"rep {rep}: " + ", ".join(f"{k} {v['ms'][-1]:.1f}" for k, v in res.items()), flush=True)
@@ -209,7 +235,7 @@ def main() -> None:
     n = 64 << 20
     x, y, z = (torch.ones(n, device="cuda") for _ in range(3))
     tb = {}
-    for u in (1, 2, 3, 4, 5, 6, 8):
+    for u in ((1, 2, 3, 4, 5, 6, 8) if args.triad_units else ()):
         ms_ = MaskedStream(cu_slice_mask(0, u))
 
         def tri(st=ms_.stream) -> None:
@@ -222,10 +248,10 @@ def main() -> None:
     print("triad TB/s by masked units:", tb, flush=True)
 
     cal = []
-    if smi is not None and not args.skip_cal:
+    if smi is not None and args.umc_cal:
         for blocks in (32, 64, 128, 256, 512, 8192):
             def tri2(b=blocks) -> None:
-                loadgen.triad(x, y, z, 1.0001, blocks=b, stream=s_main)
+                loadgen.triad(x, y, z, 1.0001, blocks=b)
             tri2()
             torch.cuda.synchronize()
             w0 = time.time()
