@@ -65,7 +65,8 @@ class NodeAgent:
                  hbm_tolerance_gib: float = 0.5, host_proc: str = "/host/proc", profile_dir: str = "",
                  partition_dry_run: bool = False, fabric: Any = None, set_checks: Any = None,
                  background_probes: bool = False,
-                 corun_send: Optional[Callable[[List[Dict[str, Any]]], Any]] = None):
+                 corun_send: Optional[Callable[[List[Dict[str, Any]]], Any]] = None,
+                 busy_poll_s: float = 0.1):
         self.node, self.redis, self.source, self.client = node, redis, source, client
         self.poll_s = poll_s
         self.exporter = exporter
@@ -121,6 +122,21 @@ class NodeAgent:
                                             pod_lookup=self._pod_lookup if client is not None else None)
         self.history_every = max(1, history_every)
         self._steps = 0
+        # per-pod GPU busy time from amd-smi's per-process engine counters (or a profiled
+        # pod's trace), written as the busy-ms annotation when the pod terminates
+        # (agent.busy; the completion feedback's millisecond measurement)
+        from .busy import BusyTracker
+        self.busy = BusyTracker()
+        # the busy sampler's own period (its thread, started with the agent): the occupancy
+        # integral's resolution; 0 = sample only in step()
+        self.busy_poll_s = busy_poll_s
+        self._busy_thread: Optional[threading.Thread] = None
+        if self.profiles is not None:
+            self.profiles.on_busy = self.busy.note_profiled
+        # this node's pods, listed once per step and shared by every user of the step (the
+        # usage attribution, the busy-ms pass, the co-run observer's lookups)
+        self._pod_cache: Optional[List[Dict[str, Any]]] = None
+        self._in_step = False
         self.health = health or HealthMonitor()
         # Evict the pods of a device that turned unhealthy (their controllers recreate them
         # and the scheduler places them elsewhere -- the elastic-recovery path); off by
@@ -252,16 +268,57 @@ class NodeAgent:
                 except Exception as e:
                     log.warning("evicting %s failed: %s", O.key(p), e)
 
+    def _node_pods(self) -> List[Dict[str, Any]]:
+        """Every pod bound to this node (any phase): one LIST per agent step, shared by the
+        step's users; outside a step a fresh LIST.  Raises on apiserver errors."""
+        if self._in_step and self._pod_cache is not None:
+            return self._pod_cache
+        pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        if self._in_step:
+            self._pod_cache = pods
+        if self.profiles is not None and hasattr(self.profiles, "note_pods"):
+            self.profiles.note_pods(pods)
+        return pods
+
     def _pods_on_node(self) -> Dict[str, Dict[str, Any]]:
         """uid -> pod object of the non-terminal pods bound to this node ({} without apiserver)."""
         if self.client is None:
             return {}
         try:
-            pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+            pods = self._node_pods()
         except Exception as e:
             log.debug("listing pods on %s failed: %s", self.node, e)
             return {}
         return {O.uid(p): p for p in pods if not O.is_terminal(p) and O.uid(p)}
+
+    def sample_busy(self) -> None:
+        """One busy-time sampling round over the attributed processes (agent.busy)."""
+        try:
+            gap = 2.0 * max(self.busy_poll_s, 0.05) if self._busy_thread is not None else 2.0 * self.poll_s
+            self.busy.sample(self.source, self.pod_resolver, len(self.source.devices()), max_gap_s=gap)
+        except Exception as e:
+            log.debug("process list for busy time failed: %s", e)
+
+    def _busy_loop(self) -> None:
+        while not self._stop.is_set():
+            self.sample_busy()
+            self._stop.wait(self.busy_poll_s)
+
+    def start_busy_sampler(self) -> None:
+        if self.busy_poll_s > 0 and self._busy_thread is None:
+            self._busy_thread = threading.Thread(target=self._busy_loop, daemon=True, name="busy-sampler")
+            self._busy_thread.start()
+
+    def track_busy(self) -> List[str]:
+        """Write busy-ms on this node's pods that have terminated since (agent.busy), after a
+        sampling round when no sampler thread runs.  Returns the pods annotated."""
+        if self._busy_thread is None:
+            self.sample_busy()
+        if self.client is None or not self.busy.tracked():
+            return []
+        done = self.busy.annotate_finished(self.client, self._node_pods())
+        self.busy.expire()
+        return done
 
     def pod_usage(self, uid_to_pod: Optional[Dict[str, str]] = None) -> Dict[str, Dict[str, Any]]:
         """Per-pod GPU usage from amd-smi's per-process list: processes are attributed to
@@ -555,6 +612,13 @@ class NodeAgent:
 
     # ------------------------------------------------------------------ loop
     def step(self) -> None:
+        self._in_step, self._pod_cache = True, None
+        try:
+            self._step()
+        finally:
+            self._in_step, self._pod_cache = False, None
+
+    def _step(self) -> None:
         try:
             self.reconcile_partitions()
         except Exception as e:
@@ -590,6 +654,8 @@ class NodeAgent:
                 log.warning("per-pod usage / HBM check failed: %s", e)
         if self.profiles is not None:
             try:
+                if self.client is not None:
+                    self._node_pods()           # this step's pods: the ingestor's known UIDs
                 self.profiles.step()
             except Exception as e:
                 log.warning("ingesting per-pod profiles failed: %s", e)
@@ -598,6 +664,10 @@ class NodeAgent:
                     self.corun.step()
                 except Exception as e:
                     log.warning("co-run observations failed: %s", e)
+        try:
+            self.track_busy()
+        except Exception as e:
+            log.warning("busy-ms pass failed: %s", e)
 
     def _pod_lookup(self, ns: str, name: str) -> Optional[Dict[str, Any]]:
         from ..kube.client import NotFound
@@ -608,7 +678,7 @@ class NodeAgent:
 
     def _running_on(self, uuid: str) -> set:
         """Keys of this node's non-terminal pods assigned to device `uuid`."""
-        pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        pods = self._node_pods()
         out = set()
         for p in pods:
             if O.is_terminal(p):
@@ -621,7 +691,7 @@ class NodeAgent:
         """Keys of this node's terminal pods on device `uuid` whose containers ran during
         `span` (epoch s: another pod's container startedAt .. finishedAt)."""
         from ..plugins.gpu.feedback import container_span
-        pods, _ = self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        pods = self._node_pods()
         out = set()
         for p in pods:
             if not O.is_terminal(p) or uuid not in (O.annotations(p).get(C.ANNOT_DEVICES) or "").split(","):
@@ -642,6 +712,7 @@ class NodeAgent:
             self._stop.wait(self.poll_s)
 
     def start(self) -> "NodeAgent":
+        self.start_busy_sampler()
         self._thread = threading.Thread(target=self.run, daemon=True, name="node-agent")
         self._thread.start()
         return self
@@ -652,6 +723,8 @@ class NodeAgent:
             self.probes.stop()
         if self._thread:
             self._thread.join(timeout=5)
+        if self._busy_thread is not None:
+            self._busy_thread.join(timeout=5)
 
 
 def publish_from_stdin(lines: List[str], redis: Redis) -> str:

@@ -21,6 +21,7 @@ import logging
 import os
 import subprocess
 import sys
+import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
@@ -56,6 +57,11 @@ class LaunchResult:
 
 
 _VAR = None
+
+
+def _rfc3339(t: float) -> str:
+    """The kubelet's container timestamp format: UTC, whole seconds."""
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))
 
 
 def _expand(s: str, env: Dict[str, str]) -> str:
@@ -101,6 +107,7 @@ class PodLauncher:
         self.launched: Dict[str, LaunchResult] = {}
         self.cwd: Optional[str] = None              # container working directory (None = ours)
         self.extra_env: Dict[str, str] = {}         # runtime-injected env (not the pod's)
+        self.running: Dict[int, str] = {}           # pid of a running container -> pod UID
 
     # ------------------------------------------------------------------ env
     def env_for(self, pod: Obj) -> Dict[str, str]:
@@ -155,18 +162,32 @@ class PodLauncher:
         full_env = dict(self.base_env)
         full_env.update(self.extra_env)
         full_env.update(env)
+        started = time.time()
         try:
-            p = subprocess.run(argv, env=full_env, capture_output=True, text=True, timeout=self.timeout_s,
-                               cwd=self.cwd)
-            res = LaunchResult(key, p.returncode, p.stdout, p.stderr, env)
-        except subprocess.TimeoutExpired as e:
-            res = LaunchResult(key, -9, e.stdout or "", (e.stderr or "") + "\ntimeout", env)
+            proc = subprocess.Popen(argv, env=full_env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                    cwd=self.cwd)
         except OSError as e:
             res = LaunchResult(key, 127, "", str(e), env)
+        else:
+            # the running container's pid -> pod UID (what a cgroup lookup gives a node agent)
+            self.running[proc.pid] = O.uid(pod)
+            try:
+                out, err = proc.communicate(timeout=self.timeout_s)
+                res = LaunchResult(key, proc.returncode, out, err, env)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+                out, err = proc.communicate()
+                res = LaunchResult(key, -9, out or "", (err or "") + "\ntimeout", env)
+            finally:
+                self.running.pop(proc.pid, None)
         self.launched[key] = res
         phase = "Succeeded" if res.rc == 0 else "Failed"
+        # as the kubelet reports it: RFC 3339 at whole seconds
+        term = {"exitCode": res.rc, "startedAt": _rfc3339(started), "finishedAt": _rfc3339(time.time())}
+        status = {"phase": phase, "containerStatuses": [{"name": (O.containers(pod) or [{}])[0].get("name", "main"),
+                                                         "state": {"terminated": term}}]}
         try:
-            self.client.patch("pods", O.name(pod), {"status": {"phase": phase}}, "merge", O.namespace(pod))
+            self.client.patch("pods", O.name(pod), {"status": status}, "merge", O.namespace(pod))
         except NotFound:
             pass
         return res

@@ -207,8 +207,11 @@ class ProfileIngestor:
     `pod_lookup(ns, name)` (the agent's API client): a directory is ingested for a pod that
     exists with that UID on this node -- defence in depth behind the webhook's per-container
     subPathExpr mount; the pod's own workload annotation names the history it goes to.  A pod
-    that no longer exists (deleted after it ran) keeps its run: its directory is ingested under
-    the name rule's workload while younger than `orphan_grace_s`.  Files over `max_file_bytes` are not read.  With a `corun` observer
+    that no longer exists (deleted after it ran) keeps its run only if the agent saw that
+    exact (namespace, name, UID) on this node (`note_pods`, fed by the agent's per-step pod
+    list): its directory is then ingested under the name rule's workload while younger than
+    `orphan_grace_s`; an unprovable orphan is dropped (a forged directory must not
+    feed another workload's history).  Files over `max_file_bytes` are not read.  With a `corun` observer
     (agent.corun_observer.CorunObserver) each traced pod's kernel interval on its device is
     also recorded, so pods that overlapped on one GPU become co-run observations."""
 
@@ -231,6 +234,22 @@ class ProfileIngestor:
         self.max_file_bytes = max_file_bytes
         self.ingested: List[Dict[str, Any]] = []
         self.rejected: List[str] = []
+        # uid -> (namespace, name, last seen) of pods the agent saw bound to this node
+        self.seen: Dict[str, Tuple[str, str, float]] = {}
+        # callback(uid, busy ms) for the agent's busy-ms annotation (agent.busy)
+        self.on_busy: Optional[Callable[[str, float], None]] = None
+
+    def note_pods(self, pods: List[Dict[str, Any]]) -> None:
+        """The pods bound to this node right now (any phase): the UIDs an orphaned profile
+        directory may belong to."""
+        now = time.time()
+        for p in pods:
+            u = O.uid(p)
+            if u:
+                self.seen[u] = (O.namespace(p), O.name(p), now)
+        if len(self.seen) > 65536:
+            for u in [u for u, v in self.seen.items() if now - v[2] > self.orphan_grace_s]:
+                self.seen.pop(u, None)
 
     def _finished(self) -> List[Tuple[str, List[str]]]:
         out = []
@@ -257,7 +276,9 @@ class ProfileIngestor:
                 age = time.time() - os.path.getmtime(d) if d else float("inf")
             except OSError:
                 age = float("inf")
-            return age <= self.orphan_grace_s, None
+            known = self.seen.get(uid)
+            provable = known is not None and known[:2] == (ns, name)
+            return provable and age <= self.orphan_grace_s, None
         if O.uid(pod) != uid:           # a different pod of that name: never this directory's
             return False, None
         if self.node and O.node_name_of(pod) not in ("", self.node):
@@ -321,6 +342,9 @@ class ProfileIngestor:
             pod = owner or {"metadata": {"name": name, "namespace": ns, "annotations": {}}}
             wl = workload_key(pod)
             first, last = sample.pop("first_ns", None), sample.pop("last_ns", None)
+            busy_ms = sample.get("busy_union_ms") or sample.get("gpu_busy_ms")
+            if self.on_busy is not None and busy_ms:
+                self.on_busy(uid, float(busy_ms))
             try:
                 self.history.append(wl, sample)
             except Exception as e:          # Redis blip: keep the directory for the next pass

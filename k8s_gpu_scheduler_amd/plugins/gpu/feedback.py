@@ -24,9 +24,13 @@ the median and shift the next plans off it.
 
 Predicted durations are recorded at Reserve (the pod's group on the co-run model, with the
 residents it was placed next to); completions arrive through the pod informer (the GPU
-plugin's `_on_pod`).  Optional `gpu-scheduler.amd.com/busy-ms` (the profiled GPU busy time
-the node agent's rocprof ingestor knows) is preferred over the container wall time when a pod
-carries it.
+plugin's `_on_pod`).  The measurement is `gpu-scheduler.amd.com/busy-ms` when the pod carries
+it: the node agent writes it on every pod that terminates on its GPUs, from amd-smi's
+per-process GPU engine time summed over the pod's processes, or from the rocprof trace of a
+profiled pod (agent.busy.BusyTracker).  Otherwise the containers' startedAt .. finishedAt --
+but the kubelet serialises those at WHOLE SECONDS (RFC 3339 without a fraction), so a span
+shorter than QUANTISED_MIN_SPAN_S is quantisation noise (a 2-s pod reads anything from 1 to 3
+s) and is not fed at all.
 
 Reference analog: the reference's Score reads resident state every cycle but never learns
 from completions (reference pkg/plugins/gpu_plugin/gpu_plugins.go:87-160, 558-757).
@@ -44,6 +48,9 @@ from ...api import objects as O
 
 Obj = Dict[str, Any]
 ANNOT_BUSY_MS = C.ANNOT_PREFIX + "busy-ms"
+# whole-second container timestamps: spans shorter than this are not measurements (+-1 s of
+# quantisation is > 5 % below 20 s)
+QUANTISED_MIN_SPAN_S = 20.0
 
 
 def _ts(s: str) -> Optional[float]:
@@ -69,21 +76,32 @@ def measured_ms(pod: Obj) -> Optional[float]:
                 return v
         except ValueError:
             pass
-    span = container_span(pod)
+    span = container_span(pod, QUANTISED_MIN_SPAN_S)
     return None if span is None else (span[1] - span[0]) * 1e3
 
 
-def container_span(pod: Obj) -> Optional[Tuple[float, float]]:
-    """(earliest startedAt, latest finishedAt) of the pod's terminated containers, epoch s."""
+def _whole_seconds(s: str) -> bool:
+    """An RFC 3339 time without a fractional second (the kubelet's serialisation)."""
+    return "." not in s.split("T")[-1]
+
+
+def container_span(pod: Obj, min_quantised_s: float = 0.0) -> Optional[Tuple[float, float]]:
+    """(earliest startedAt, latest finishedAt) of the pod's terminated containers, epoch s.
+    None when a span built from whole-second timestamps is shorter than `min_quantised_s`."""
     t0, t1 = None, None
+    coarse = True               # every timestamp whole-second (one with a fraction: fine-grained)
     for cs in (pod.get("status") or {}).get("containerStatuses") or []:
         term = (cs.get("state") or {}).get("terminated") or {}
-        a, b = _ts(term.get("startedAt", "")), _ts(term.get("finishedAt", ""))
+        sa, sb = term.get("startedAt", ""), term.get("finishedAt", "")
+        a, b = _ts(sa), _ts(sb)
         if a is None or b is None or b < a:
             continue
+        coarse = coarse and _whole_seconds(sa) and _whole_seconds(sb)
         t0 = a if t0 is None else min(t0, a)
         t1 = b if t1 is None else max(t1, b)
     if t0 is None or t1 is None or t1 <= t0:
+        return None
+    if coarse and t1 - t0 < min_quantised_s:
         return None
     return t0, t1
 
@@ -124,12 +142,18 @@ class CompletionFeedback:
     def completed(self, pod: Obj) -> bool:
         """A terminal pod: fold its measured-vs-predicted time into its group's backlog."""
         key = O.key(pod)
-        with self._lock:
-            hit = self._pred.pop(key, None)
-        if hit is None or (pod.get("status") or {}).get("phase") != "Succeeded":
+        if (pod.get("status") or {}).get("phase") != "Succeeded":
+            self.forget(key)                # failed: its time measures nothing
             return False
         ms = measured_ms(pod)
         if ms is None:
+            # no measurement YET: the node agent writes busy-ms after it sees the pod terminate
+            # (agent.busy), a later update of the same pod; the prediction stays pending until
+            # then or until the pod is deleted (forget)
+            return False
+        with self._lock:
+            hit = self._pred.pop(key, None)
+        if hit is None:
             return False
         group, pred = hit
         with self._lock:

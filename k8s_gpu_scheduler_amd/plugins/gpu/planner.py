@@ -1026,8 +1026,8 @@ class BurstPlanner:
         if how == "unreserve" or (how == "delete" and self.drop_on_delete):
             tl.drop(key)
         elif how == "terminal":
-            from .feedback import container_span
-            span = container_span(pod)
+            from .feedback import QUANTISED_MIN_SPAN_S, container_span
+            span = container_span(pod, QUANTISED_MIN_SPAN_S)
             if span is not None:
                 tl.measure_key(key, span[0] * 1e3, span[1] * 1e3)
             elif self.drop_on_delete:

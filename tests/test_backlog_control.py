@@ -122,13 +122,20 @@ def test_released_pods_leave_the_slot_timeline_and_the_feedback():
     p.released(pods["b"], "delete")
     fin = pods["c"]
     fin["status"] = {"phase": "Succeeded", "containerStatuses": [{"state": {"terminated": {
-        "startedAt": "2026-01-01T00:00:01Z", "finishedAt": "2026-01-01T00:00:03Z"}}}]}
+        "startedAt": "2026-01-01T00:00:01Z", "finishedAt": "2026-01-01T00:00:31Z"}}}]}
     p.released(fin, "terminal")
     ch = p.timeline.chains(g)
     keys = [k for c in ch.values() for k, _, _ in c]
     assert keys == [O.key(fin)]
     (_, s, e), = [x for c in ch.values() for x in c]
-    assert e - s == pytest.approx(2000.0)                  # measured from its container times (ms)
+    assert e - s == pytest.approx(30000.0)                 # measured from its container times (ms)
+    # a 2-s span of whole-second kubelet timestamps is quantisation noise: dropped, not measured
+    short = O.make_pod("s", gpu_cu=64)
+    p.timeline.place(g, (4, 2), O.key(short), 0, 20.0, 1.0)
+    short["status"] = {"phase": "Succeeded", "containerStatuses": [{"state": {"terminated": {
+        "startedAt": "2026-01-01T00:01:01Z", "finishedAt": "2026-01-01T00:01:03Z"}}}]}
+    p.released(short, "terminal")
+    assert O.key(short) not in [k for c in p.timeline.chains(g).values() for k, _, _ in c]
     assert p.feedback.forgot == [O.key(pods["a"]), O.key(pods["b"])]
     # the pipelined bench keeps deleted in-flight pods (its executor measures them)
     p.drop_on_delete = False

@@ -34,9 +34,22 @@ def test_measured_ms_from_container_statuses_and_annotation():
     pod["status"] = {"phase": "Succeeded", "containerStatuses": [
         {"state": {"terminated": {"startedAt": _iso(1.0), "finishedAt": _iso(3.5)}}},
         {"state": {"terminated": {"startedAt": _iso(0.5), "finishedAt": _iso(2.0)}}}]}
-    assert abs(measured_ms(pod) - 3000.0) < 1e-6
+    assert abs(measured_ms(pod) - 3000.0) < 1e-6          # sub-second timestamps: a measurement
     pod["metadata"].setdefault("annotations", {})["gpu-scheduler.amd.com/busy-ms"] = "12.5"
     assert measured_ms(pod) == 12.5
+
+
+def test_whole_second_container_spans_below_the_bound_are_not_measurements():
+    """the kubelet writes startedAt / finishedAt at whole seconds; a 2-s span
+    is anything from 1 to 3 s of run time, so it is not fed; 30 s is."""
+    from k8s_gpu_scheduler_amd.plugins.gpu.feedback import QUANTISED_MIN_SPAN_S, container_span
+    pod = O.make_pod("q", gpu_cu=64)
+    pod["status"] = {"phase": "Succeeded", "containerStatuses": [
+        {"state": {"terminated": {"startedAt": _iso(1.0), "finishedAt": _iso(3.0)}}}]}
+    assert _iso(1.0).endswith(":01Z")                      # whole seconds, as the kubelet writes them
+    assert measured_ms(pod) is None and container_span(pod) is not None
+    pod["status"]["containerStatuses"][0]["state"]["terminated"]["finishedAt"] = _iso(1.0 + QUANTISED_MIN_SPAN_S + 10)
+    assert measured_ms(pod) == pytest.approx((QUANTISED_MIN_SPAN_S + 10) * 1e3)
 
 
 def _run(slow: tuple, bursts: int = 24, seed: int = 0, overhead: float = 3.0):
@@ -101,5 +114,140 @@ def test_slow_gpu_sheds_planned_work_uniform_slowdown_changes_nothing():
     assert pl.speed(g1) > pl.speed(g0)
     # the share that levels the MEASURED work is 1 / 2.1 = 0.476 for a GPU 10 % slower: the
     # planner moves toward it and no further (round 4's unbounded integrator overshot to 0.44;
-    # each GPU is full every burst here, so only long / short swaps can move work)
-    assert 0.46 < slow_share < base_share - 0.005, (slow_share, base_share)
+    # each GPU is full every burst here, so only long / short swaps can move work).  One run's
+    # share moves by ~0.01 with the arrival seed, so the shed is judged over five seeds
+    # (round 6 rank-test gate: 0.019 on average, round 5's gate 0.015)
+    sheds = []
+    for sd in range(5):
+        b = base_share if sd == 0 else _run((1.0, 1.0), seed=sd)[0]
+        sl = slow_share if sd == 0 else _run((1.0, 1.1), seed=sd)[0]
+        assert 0.46 < sl < b, (sd, sl, b)
+        sheds.append(b - sl)
+    assert np.mean(sheds) >= 0.01, sheds
+
+
+def _run_agent(slow: tuple, with_agent: bool, bursts: int = 16, seed: int = 0):
+    """As _run, but the containers' times are whole seconds (2-s spans, as the kubelet writes
+    them for short pods) and -- with_agent -- the node agent measures each pod's GPU busy time
+    from its processes' engine counters (a scripted amd-smi process list: the pod's true co-run
+    time x slow[gpu]) and writes busy-ms once the pod is terminal (agent.busy)."""
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import StaticSource
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n0", gpus=2))
+    ledger = DeviceLedger()
+    model = CorunModel.load()
+    args = {"w_slo": 1.0, "w_pack": 0.25, "w_telemetry": 0.0, "w_balance": 1.0, "slo_objective": "corun",
+            "plan_bursts": True, "plan_tolerance": 0.3, "plan_carry": 1.0}
+    s = Scheduler(fc, default_gpu_config(args, disable_defaults=True), full_registry(), bind_async=False, seed=0,
+                  extras={"ledger": ledger, "telemetry": TelemetryCache(stale_s=0),
+                          "predictions": CachedPredictions(corun=model)})
+    s.start_informers()
+    plugin = s.frameworks[C.SCHEDULER_NAME].plugin(C.PLUGIN_NAME)
+    src = StaticSource([{"uuid": "GPU-a", "gpu": 0}, {"uuid": "GPU-b", "gpu": 1}], samples=[])
+    uid_of_pid = {}
+    ag = NodeAgent("n0", Redis(FakeRedisBackend(FakeRedisEngine())), src, client=fc, pod_resolver=uid_of_pid.get)
+    rng = np.random.default_rng(seed)
+    gpu_of = {d.device.uuid: d.device.gpu for d in ledger.devices("n0")}
+    t, pid = 0, 100
+    annotated = 0
+    for b in range(bursts):
+        names = []
+        for i in range(8):
+            wl = W.NAMES[int(rng.integers(len(W.NAMES)))]
+            nm = f"{wl.replace('_', '-')}-b{b}-{i}"
+            fc.create("pods", O.make_pod(nm, gpu_cu=64, env={C.ENV_ITERATIONS: "20000"}))
+            names.append((nm, wl))
+        assert all(r.node for r in s.schedule_pending())
+        groups = {0: [], 1: []}
+        for nm, wl in names:
+            pod = fc.get("pods", nm, "default")
+            groups[gpu_of[O.annotations(pod)[C.ANNOT_DEVICES]]].append((nm, wl))
+        src.procs = {0: [], 1: []}
+        for g, m in groups.items():
+            d = model.group_durations([model.wid(wl) for _, wl in m], [20000] * len(m))
+            for (nm, _), ms in zip(m, d):
+                pid += 1
+                uid_of_pid[pid] = O.uid(fc.get("pods", nm, "default"))
+                src.procs[g].append({"pid": pid, "gfx_ns": ms * slow[g] * 1e6, "vram_bytes": 0})
+        if with_agent:
+            ag.track_busy()                     # the pods' processes seen running
+        for nm, _ in names:
+            fc.patch("pods", nm, {"status": {"phase": "Succeeded", "containerStatuses": [
+                {"name": "main", "state": {"terminated": {"startedAt": _iso(t), "finishedAt": _iso(t + 2)}}}]}},
+                "merge", "default")
+        if with_agent:
+            annotated += len(ag.track_busy())   # terminal now: busy-ms written
+        for nm, _ in names:
+            fc.delete("pods", nm, "default")
+        t += 100
+    return plugin.planner, annotated
+
+
+@pytest.mark.skipif(not has_core, reason="_core not built")
+def test_agent_busy_ms_feeds_a_15pct_slower_gpu_and_2s_spans_do_not():
+    """whole-second container times, one GPU 15 % slow.  With the node agent
+    writing busy-ms the planner's measured speed of the slow GPU moves; without it the 2-s
+    container spans are quantisation noise and nothing is fed."""
+    pl, annotated = _run_agent((1.0, 1.15), with_agent=True)
+    g0, g1 = ("n0", 0), ("n0", 1)
+    assert annotated == 16 * 8
+    assert pl.feedback.applied > 0
+    assert pl.speed(g1) > 1.1 * pl.speed(g0), (pl.speed(g0), pl.speed(g1))
+    assert pl.rel_speeds([g0, g1])[1] > 1.03
+    bare, annotated = _run_agent((1.0, 1.15), with_agent=False)
+    assert annotated == 0
+    assert bare.feedback.applied == 0 and not bare._speed_obs
+    assert bare.speed(g1) == bare.speed(g0) == 1.0
+
+
+def test_busy_tracker_sums_processes_and_prefers_engine_time():
+    from k8s_gpu_scheduler_amd.agent.busy import BusyTracker
+    from k8s_gpu_scheduler_amd.plugins.gpu.feedback import ANNOT_BUSY_MS
+    bt = BusyTracker()
+    bt.observe("u1", 1, 2e6)
+    bt.observe("u1", 1, 5e6)                  # cumulative: the last (largest) value counts
+    bt.observe("u1", 2, 3e6)
+    assert bt.busy_ms("u1") == (8.0, "amd-smi")
+    bt.note_profiled("u2", 12.5)              # a profiled pod the driver reported no engine time for
+    bt.observe("u2", 3, 0)
+    assert bt.busy_ms("u2") == (12.5, "rocprof")
+    assert bt.busy_ms("nope") is None
+    fc = FakeCluster()
+    fc.create("pods", O.make_pod("p1", gpu_cu=64, node_name="n0", phase="Running"))
+    p1 = fc.get("pods", "p1", "default")
+    bt.observe(O.uid(p1), 9, 4e6)
+    assert bt.annotate_finished(fc, [p1]) == []            # still running: nothing written
+    fc.patch("pods", "p1", {"status": {"phase": "Succeeded"}}, "merge", "default")
+    assert bt.annotate_finished(fc, [fc.get("pods", "p1", "default")]) == ["default/p1"]
+    assert O.annotations(fc.get("pods", "p1", "default"))[ANNOT_BUSY_MS] == "4.000"
+    assert O.uid(p1) not in bt.tracked()
+
+
+def test_busy_tracker_integrates_cu_occupancy_when_no_engine_time():
+    """MI355X reports no per-process engine time for HIP compute (gfx_ns 0), but KFD's
+    cu_occupancy is non-zero while the process has waves on the GPU: the sampler's rounds with
+    occupancy integrate to the busy time (one sampling period of error per pod)."""
+    from k8s_gpu_scheduler_amd.agent.busy import BusyTracker
+
+    class Src:
+        occ = 0
+
+        def processes(self, i):
+            return [{"pid": 5, "gfx_ns": 0, "cu_occupancy": self.occ}]
+    bt, src = BusyTracker(), Src()
+    t = 100.0
+    for k in range(40):                      # 0.1-s rounds: idle 0.5 s, busy 2.5 s, idle 1 s
+        src.occ = 64 if 5 <= k < 30 else 0
+        bt.sample(src, {5: "u"}.get, 1, now=t, max_gap_s=0.2)
+        t += 0.1
+    ms, how = bt.busy_ms("u")
+    assert how == "amd-smi-occupancy" and ms == pytest.approx(2500.0, abs=101.0)
+    # a stalled sampler (a 5-s gap) counts at most max_gap_s of it
+    bt2 = BusyTracker()
+    src.occ = 64
+    bt2.sample(src, {5: "v"}.get, 1, now=0.0, max_gap_s=0.2)
+    bt2.sample(src, {5: "v"}.get, 1, now=5.0, max_gap_s=0.2)
+    assert bt2.busy_ms("v") == (pytest.approx(200.0), "amd-smi-occupancy")

@@ -152,3 +152,65 @@ def test_agent_flags_real_process_over_its_hbm_share():
     finally:
         child.kill()
         child.wait()
+
+
+def test_agent_writes_busy_ms_on_a_pod_run_by_the_launcher():
+    """VERDICT r5 item 3 on MI355X: a pod run by agent.launcher (the mini kubelet) does ~2 s of
+    GEMMs; the node agent's busy sampler attributes its process (amd-smi lists the HOST pid:
+    here the pid new to the list while the pod runs, a cgroup lookup in a cluster) and, once
+    the pod is terminal, writes gpu-scheduler.amd.com/busy-ms within 15 % of the process's own
+    HIP-event busy time -- where the kubelet-style container times are whole seconds."""
+    import sys
+    import threading
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import SmiSource
+    from k8s_gpu_scheduler_amd.agent.launcher import PodLauncher
+    from k8s_gpu_scheduler_amd.api import objects as O
+    from k8s_gpu_scheduler_amd.kube.client import FakeCluster
+    from k8s_gpu_scheduler_amd.plugins.gpu.feedback import ANNOT_BUSY_MS, measured_ms
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    try:
+        src = SmiSource()
+    except Exception as e:
+        pytest.skip(f"amd-smi unavailable: {e}")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, time, torch; sys.path.insert(0, %r)\n"
+            "from k8s_gpu_scheduler_amd.ops import loadgen\n"
+            "a = torch.rand(4096, 4096, device='cuda').to(torch.bfloat16); c = torch.empty_like(a)\n"
+            "loadgen.gemm(a, a, out=c); torch.cuda.synchronize()\n"
+            "e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)\n"
+            "e0.record(); t0 = time.time()\n"
+            "while time.time() - t0 < 2.0:\n"
+            "    [loadgen.gemm(a, a, out=c) for _ in range(32)]; torch.cuda.synchronize()\n"
+            "e1.record(); torch.cuda.synchronize(); print('{\"busy_ms\": %%f}' %% e0.elapsed_time(e1), flush=True)\n"
+            ) % root
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("box", gpus=1))
+    fc.create("pods", O.make_pod("busy-pod", gpu_cu=64, node_name="box"))
+    uid = O.uid(fc.get("pods", "busy-pod", "default"))
+    before = {int(p["pid"]) for i in range(len(src.devices())) for p in src.processes(i)}
+    launcher = PodLauncher(fc, "box", command=[sys.executable, "-c", code], timeout_s=90)
+
+    def resolver(pid):
+        return uid if launcher.running and pid not in before else None
+    ag = NodeAgent("box", Redis(FakeRedisBackend(FakeRedisEngine())), src, client=fc, pod_resolver=resolver,
+                   busy_poll_s=0.05)
+    ag.start_busy_sampler()
+    try:
+        res = launcher.run(fc.get("pods", "busy-pod", "default"))
+    finally:
+        ag._stop.set()
+        ag._busy_thread.join(timeout=5)
+    assert res.rc == 0, res.stderr[-2000:]
+    own = res.json()["busy_ms"]
+    done = ag.track_busy()
+    pod = fc.get("pods", "busy-pod", "default")
+    ann = O.annotations(pod)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, "busy_ms.json"), "w") as f:
+        json.dump({"own_hip_event_ms": own, "annotations": ann, "status": pod.get("status"), "annotated": done}, f,
+                  indent=1)
+    assert done == ["default/busy-pod"], (done, ann)
+    assert abs(float(ann[ANNOT_BUSY_MS]) - own) <= 0.15 * own, (ann, own)
+    assert measured_ms(pod) == pytest.approx(float(ann[ANNOT_BUSY_MS]))

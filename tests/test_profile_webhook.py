@@ -215,8 +215,14 @@ def test_ingestor_keeps_runs_of_deleted_pods_within_the_grace_and_rejects_foreig
     os.utime(old, (1.0, 1.0))                                             # an orphan from long ago
     live = {("default", "onnx-resnet50-2048-j"): {"metadata": {"name": "onnx-resnet50-2048-j",
                                                                "namespace": "default", "uid": "uid-NEW"}}}
+    forged = _write_profile(root, "default", "onnx-resnet50-4096-x", "uid-d", "main", "cu64-hbm8-it20", kern)
     ing = ProfileIngestor(root, RedisHistory(r), pod_lookup=lambda ns, n: live.get((ns, n)), orphan_grace_s=600.0)
+    # the agent saw the deleted pod (and the stale one) bound to its node before they went;
+    # uid-d was never seen here: a directory nobody can vouch for is dropped
+    ing.note_pods([{"metadata": {"name": "onnx-mobilenet-1024-job1", "namespace": "default", "uid": "uid-a"}},
+                   {"metadata": {"name": "onnx-ssd-mobilenet-1024-z", "namespace": "default", "uid": "uid-c"}}])
     assert ing.step() == 1
+    assert not RedisHistory(r).read("onnx_resnet50_4096") and not os.path.exists(forged)
     assert RedisHistory(r).read("onnx_mobilenet_1024")                    # the deleted pod's run kept
     assert not RedisHistory(r).read("onnx_resnet50_2048")                 # uid mismatch: rejected
     assert not RedisHistory(r).read("onnx_ssd_mobilenet_1024")            # stale orphan: dropped
