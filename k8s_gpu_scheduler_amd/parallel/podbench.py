@@ -264,7 +264,7 @@ class ControlPlane:
     EFFORT_DOWN = 0.85       # share of the pipeline period over which the planner steps down
     # ... under which it steps back up, when the next level is predicted to fit EFFORT_TARGET of
     # the period.  Where the control plane starts pacing the GPUs was measured on the box CPU
-    # (tools/gpu_cp_knee.sh, profiles/r05_cp_knee/: the 8-rank rehearsal with a busy wait added
+    # (tools/archive/gpu_cp_knee.sh, profiles/r05_cp_knee/: the 8-rank rehearsal with a busy wait added
     # to each epoch): ms / step stays flat up to ~5.85 ms of scheduling per 6.8 ms period (86 %,
     # ~91 % with the deletions and telemetry) and rises beyond it.  Up 0.7 / target 0.8 keep a
     # 10 % margin below that knee (round 5 first ran 0.6 / 0.7, which held an 8-GPU control
@@ -329,7 +329,7 @@ class ControlPlane:
             self._kernel_policies(arr)
         if self.extra_s > 0:
             # pacing probe (GPUSCHED_CP_EXTRA_MS): a costlier control plane, emulated by a busy
-            # wait inside the epoch's schedule (tools/gpu_cp_knee.sh finds where it paces)
+            # wait inside the epoch's schedule (tools/archive/gpu_cp_knee.sh finds where it paces)
             t_end = time.perf_counter() + self.extra_s
             while time.perf_counter() < t_end:
                 pass
@@ -909,7 +909,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
-    ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 6),
+    ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 5, 6, 7),
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
                     help="amd-smi activity sampling period across warmup + timed region (0 = off)")

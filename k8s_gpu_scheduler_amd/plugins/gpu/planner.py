@@ -93,7 +93,7 @@ class EffortController:
     CPU: profiles/r04_cp_rehearsal/jump_first/)."""
 
     # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py
-    # and tools/gpu_cp_levels.sh: 5.78 / 4.68 / 4.09 ms, profiles/r05_cp_levels/; level 3 3.59 of
+    # and tools/archive/gpu_cp_levels.sh: 5.78 / 4.68 / 4.09 ms, profiles/r05_cp_levels/; level 3 3.59 of
     # 5.75, profiles/r05_cp2/; round 4: 8.1 / 6.3 / 4.5 / 4.1)
     LEVEL_COST = (1.0, 0.81, 0.69, 0.63)
 

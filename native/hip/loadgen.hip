@@ -819,8 +819,11 @@ void xcd_probe(uintptr_t out, int blocks, uintptr_t stream) {
 // non-temporal 4x (6.5 TB/s vs 6.1 for torch.add) -- profiles/r01_kernel_bench.json.
 static int g_triad_variant = 6;
 
+// 5 = non-temporal 2x (22 VGPRs), 7 = non-temporal 3x (<= 32 VGPRs): a triad wave small enough
+// to fit beside an 8-phase GEMM block's 2 x 240 VGPRs per SIMD (the 4x variant's 38 VGPRs do
+// not, so a CU running a 256 x 256 GEMM block takes no triad wave at all; round 6 A/B)
 void set_triad_variant(int v) {
-  if (v < 0 || v > 6 || v == 5) throw std::runtime_error("triad variant must be 0..4 or 6 (auto)");
+  if (v < 0 || v > 7) throw std::runtime_error("triad variant must be 0..7 (6 = auto)");
   g_triad_variant = v;
 }
 
@@ -1194,6 +1197,7 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
     case 2: hipLaunchKernelGGL((stream_triad_u<4, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 3: hipLaunchKernelGGL((stream_triad_u<4, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 4: hipLaunchKernelGGL((stream_triad_u<8, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 7: hipLaunchKernelGGL((stream_triad_u<3, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     default: hipLaunchKernelGGL((stream_triad_u<2, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
   }
   HIP_CHECK(hipGetLastError());

@@ -393,7 +393,7 @@ def test_async_slot_plans_give_the_synchronous_placements():
 
 
 def test_pacing_probe_adds_its_busy_wait_to_the_epoch_cost(monkeypatch):
-    """GPUSCHED_CP_EXTRA_MS (tools/gpu_cp_knee.sh): every epoch's schedule takes at least the
+    """GPUSCHED_CP_EXTRA_MS (tools/archive/gpu_cp_knee.sh): every epoch's schedule takes at least the
     added busy wait, and the effort rule's cost samples include it."""
     from k8s_gpu_scheduler_amd.parallel import podbench as PB
     monkeypatch.setenv("GPUSCHED_CP_EXTRA_MS", "4")

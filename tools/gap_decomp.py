@@ -94,6 +94,8 @@ def main() -> None:
     ap.add_argument("--mask-units", default="", help="mask_split regimes for these unit counts (own process)")
     ap.add_argument("--triad-units", action="store_true", help="triad TB/s vs masked units")
     ap.add_argument("--umc-cal", action="store_true", help="triad TB/s vs amd-smi umc_activity")
+    ap.add_argument("--extra-streams", default="", help="K:before|after -- K idle streams that each "
+                    "dispatch one tiny kernel (so get a hardware queue) before / after the slot streams")
     ap.add_argument("--passes", type=int, default=1,
                     help="back-to-back passes per timed regime run; amd-smi umc is averaged over the "
                          "last half of the run (its firmware moving average lags a regime change)")
@@ -110,6 +112,18 @@ def main() -> None:
     kx = KindExecutor(0)
     kx.use_graphs = False
     kx.triad_blocks = ex.triad_blocks
+    extra = []
+
+    def make_extra() -> None:
+        k = int(args.extra_streams.split(":")[0])
+        for _ in range(k):
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                torch.zeros(1, device="cuda").add_(1)
+            extra.append(st)
+        torch.cuda.synchronize()
+    if args.extra_streams.endswith(":before"):
+        make_extra()
     mask_units = [int(x) for x in args.mask_units.split(",") if x]
     core = not mask_units and not args.triad_units and not args.umc_cal
     if core:
@@ -118,6 +132,8 @@ def main() -> None:
         for wl, u, n, it in pods:
             ex.buffers(W.get(wl), u, n)
     kx._bufs, kx._streams = ex._bufs, ex._streams       # the same operands and slot streams
+    if args.extra_streams.endswith(":after"):
+        make_extra()
     flops = sum(W.get(wl).flops * it for wl, _, _, it in pods)
     mbytes = sum(W.get(wl).bytes * it for wl, _, _, it in pods)
     tri_bytes = sum(sum(o.bytes for o in W.get(wl).ops if not o.is_gemm) * it for wl, _, _, it in pods)

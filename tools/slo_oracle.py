@@ -224,9 +224,17 @@ def main() -> None:
                                          "lpt": lpt_places(pods, places, model)}
     if a.greedy:
         gp, gpl, gt, _ = load(a.greedy)
-        if [[x[:2] for x in e] for e in gp] != [[x[:2] for x in e] for e in pods]:
-            raise SystemExit("--greedy dump has different arrivals")
-        pol["greedy"] = gpl
+        # the same arrivals, possibly listed in another order (the queue sorts each burst):
+        # match each of this dump's pods to an identical pod of the greedy dump's epoch
+        mapped = []
+        for ep, gep, gpe in zip(pods, gp, gpl):
+            if sorted(ep) != sorted(gep):
+                raise SystemExit("--greedy dump has different arrivals")
+            pool = collections.defaultdict(list)
+            for x, pl in zip(gep, gpe):
+                pool[x].append(pl)
+            mapped.append([pool[x].pop(0) for x in ep])
+        pol["greedy"] = mapped
     out: Dict[str, Any] = {"dump": a.dump, "n_gpus": d.get("n_gpus"), "seed": d.get("seed"), "lookahead": lookahead,
                            "bench_reported": d.get("sim"), "policies": {}}
     t = time.time()
