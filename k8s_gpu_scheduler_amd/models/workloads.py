@@ -160,22 +160,51 @@ CUS = 256                          # MI355X compute units
 POD_CU_BUDGET = 64                 # a bench pod's GEMM tile budget (2 CU-slice units x 32 CUs)
 
 
+# block tile (BM, BN) of the native GEMM kernels (native/hip/loadgen.hip kTileBM / kTileBN)
+_TILE = {1: (128, 128), 2: (64, 128), 3: (64, 64), 4: (256, 256), 10: (256, 256)}
+
+
+def default_gemm_workgroups(M: int, N: int, K: int, cu_budget: int = 0, fp8: bool = False) -> int:
+    """Workgroups the native GEMM launches for this shape under the DEFAULT kernel policy
+    (policy 1, no forced tile, split-K off) -- a pure-Python copy of pick_gemm_tile /
+    resolve_gemm_tile / fp8_tile_128 (native/hip/loadgen.hip), so the CU-fill feature needs no
+    HIP build and never reads the process-wide tile settings.  Pinned against the
+    native picker in tests/test_gemm_policy_picker.py."""
+    alone = cu_budget <= 0 or cu_budget >= CUS
+    budget = CUS if alone else cu_budget
+    if fp8:
+        need = 2 * CUS if alone else cu_budget
+        big = M % 128 == 0 and N % 128 == 0 and (M // 128) * (N // 128) >= need
+        return (M // 128) * (N // 128) if big else (M // 64) * (N // 64)
+    per_cu = 2 if alone else 1
+    if M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= budget:
+        t = 10
+    elif (M // 128) * (N // 128) >= per_cu * budget:
+        t = 1
+    elif (M // 64) * (N // 128) >= per_cu * budget and N % 128 == 0:
+        t = 2
+    else:
+        t = 3
+    if t == 10 and K < 128:
+        t = 4
+    bm, bn = _TILE[t]
+    if M % bm or N % bn:
+        bm, bn = _TILE[3]
+    return (M // bm) * (N // bn)
+
+
 def cu_fill(w: Workload, cu_budget: int = POD_CU_BUDGET) -> Optional[float]:
     """Fraction of the chip's CUs the workload's kernels occupy, weighted by their (roofline)
     time: min(1, workgroups / CUs) per kernel -- GEMM workgroups as the native tile picker
-    launches them for `cu_budget` (`_hip.gemm_workgroups`), the stream kernels' 8192 blocks
-    fill the chip.  A pod that leaves CUs idle alone leaves co-runners room; one that fills
-    the chip alone presses on and suffers from every co-runner (models.coldstart).  None when
-    the HIP extension is not built."""
-    from .. import _native
-    h = _native.hip(required=False)
-    if h is None:
-        return None
+    launches them for `cu_budget` under the default policy (default_gemm_workgroups), the
+    stream kernels' 8192 blocks fill the chip.  A pod that leaves CUs idle alone leaves
+    co-runners room; one that fills the chip alone presses on and suffers from every co-runner
+    (models.coldstart)."""
     t = f = 0.0
     for o in w.ops:
         dt = roofline_seconds(Workload(w.name, w.family, w.framework, w.batch, (o,), 0.0), 1.0)
         if o.is_gemm:
-            fo = min(1.0, h.gemm_workgroups(o.M, o.N, o.K, cu_budget, o.kind == "gemm8") / CUS)
+            fo = min(1.0, default_gemm_workgroups(o.M, o.N, o.K, cu_budget, o.kind == "gemm8") / CUS)
         else:
             fo = 1.0
         t += dt

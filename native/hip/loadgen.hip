@@ -977,7 +977,7 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 7) throw std::runtime_error("gemm policy must be 0..7");
+  if (p < 0 || p > 8) throw std::runtime_error("gemm policy must be 0..8");
   g_gemm_policy = p;
 }
 
@@ -1012,7 +1012,8 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // share a block
   if (!alone && g_gemm_policy == 7 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget) return 13;
   // 5 / 6 (A/B arms): the co-running small GEMM's 128x128 tile with 3 / 4 LDS stages
-  if (!alone && g_gemm_policy >= 5 && M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= budget)
+  if (!alone && (g_gemm_policy == 5 || g_gemm_policy == 6) && M % 128 == 0 && N % 128 == 0 &&
+      (M / 128) * (N / 128) >= budget)
     return g_gemm_policy == 5 ? 11 : 12;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
@@ -1023,8 +1024,22 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
 // S K-slices when its tiles leave CUs idle -- tiles x S <= CUs, every slice >= 1024 deep and a
 // multiple of 64 -- else 1.  Needs an fp32 workspace of S*M*N floats (splitk_workspace_floats).
 int pick_split_k(int M, int N, int K, int cu_budget) {
-  if (g_gemm_tile || g_split_k == 0) return 1;
-  if (!(cu_budget <= 0 || cu_budget >= kCus)) return 1;
+  if (g_gemm_tile) return 1;
+  const bool alone = cu_budget <= 0 || cu_budget >= kCus;
+  // policy 8 (A/B arm): a co-running pod's GEMM with fewer 256 x 256 tiles
+  // than CUs in its share runs the 8-phase kernel split S ways along K (S = tiles needed to
+  // cover the share, at most 4, every slice >= 512 deep), fp32 partials reduced by
+  // splitk_reduce, instead of the 128 x 128 tile
+  if (!alone && g_gemm_policy == 8) {
+    if (M % 256 || N % 256) return 1;
+    const int tiles = (M / 256) * (N / 256);
+    if (tiles >= cu_budget) return 1;
+    int S = std::min(4, (cu_budget + tiles - 1) / tiles);
+    while (S > 1 && (K % (64 * S) != 0 || K / S < 512)) --S;
+    return S;
+  }
+  if (g_split_k == 0) return 1;
+  if (!alone) return 1;
   if (M % 256 || N % 256) return 1;
   const int tiles = (M / 256) * (N / 256);
   if (tiles * 2 > kCus) return 1;

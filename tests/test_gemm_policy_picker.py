@@ -12,7 +12,7 @@ h = _native.hip(required=False)
 pytestmark = pytest.mark.skipif(h is None, reason="HIP extension not built")
 
 # policy -> tile for M=1024, N=2048 at a 64-CU budget
-SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13}
+SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1}
 
 
 @pytest.fixture(autouse=True)
@@ -28,7 +28,7 @@ def test_small_corun_gemm_tile_per_policy(policy):
     assert h.pick_gemm_tile(1024, 2048, 64) == SMALL[policy]
 
 
-@pytest.mark.parametrize("policy", range(8))
+@pytest.mark.parametrize("policy", range(9))
 def test_large_corun_and_lone_gemm_tiles(policy):
     h.set_gemm_policy(policy)
     # enough 256x256 tiles for the share: the 8-phase kernel for every policy but 0
@@ -41,3 +41,34 @@ def test_forced_tile_overrides_policy():
     h.set_gemm_policy(7)
     h.set_gemm_tile(3)
     assert h.pick_gemm_tile(1024, 2048, 64) == 3
+
+
+def test_policy8_splits_small_corun_gemms_along_k():
+    """Arm 8: a co-running GEMM with fewer 256 x 256 tiles than its share's
+    CUs runs the 8-phase kernel split along K; shapes the tile already fills are not split, and
+    lone GEMMs keep the lone rule (off by default)."""
+    h.set_gemm_policy(8)
+    assert h.pick_split_k(1024, 2560, 2560, 64) == 2           # 40 tiles -> 80 blocks
+    assert h.gemm_workgroups(1024, 2560, 2560, 64, False, True) == 80
+    assert h.splitk_workspace_floats(1024, 2560, 2560, 64) == 2 * 1024 * 2560
+    assert h.pick_split_k(1024, 1536, 1536, 64) == 3           # 24 tiles, slices of 512
+    assert h.pick_split_k(1024, 1024, 1024, 64) == 2           # 4 slices would be 256 deep
+    assert h.pick_split_k(2048, 2560, 2560, 64) == 1           # 80 tiles fill the share
+    assert h.pick_split_k(1024, 2560, 2560, 0) == 1            # lone: split-K stays off
+    h.set_gemm_policy(1)
+    assert h.pick_split_k(1024, 2560, 2560, 64) == 1
+
+
+def test_python_default_tile_rule_matches_the_native_picker():
+    """models.workloads.default_gemm_workgroups (the CU-fill feature's HIP-free copy of the default
+    policy) against the native picker on every catalog / extra GEMM at the bench's share, a lone
+    launch and a half share."""
+    from k8s_gpu_scheduler_amd.models import workloads as W
+    h.set_gemm_policy(1)
+    shapes = {(o.M, o.N, o.K, o.kind == "gemm8") for w in list(W.CATALOG.values()) + list(W.EXTRA.values())
+              for o in w.ops if o.is_gemm}
+    shapes |= {(256, 256, 64, False), (192, 320, 256, False), (8192, 8192, 8192, False), (640, 384, 128, False)}
+    for M, N, K, fp8 in sorted(shapes):
+        for budget in (0, 64, 128, 32):
+            assert W.default_gemm_workgroups(M, N, K, budget, fp8) == h.gemm_workgroups(M, N, K, budget, fp8), \
+                (M, N, K, budget, fp8)

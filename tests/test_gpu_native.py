@@ -128,6 +128,33 @@ def _split_k_case(hip, loadgen, M, N, K, relu, bias):
         assert (out.float() - ref).abs().max().item() <= tol
 
 
+@pytest.mark.parametrize("M,N,K,relu,bias", [(1024, 2560, 2560, True, True), (1024, 1536, 1536, True, False),
+                                             (1024, 1024, 2048, False, True)])
+def test_gemm_corun_split_k_policy8_matches_fp32_reference(hip, M, N, K, relu, bias):
+    """Arm 8: a co-running pod's GEMM at its 64-CU share, too small for one
+    256 x 256 tile per CU, runs split along K on the 8-phase kernel (2-4 slices) -> fp32 partials ->
+    reduce; checked against fp32 PyTorch with the race screen's repeated runs."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    hip.set_gemm_policy(8)
+    try:
+        assert hip.pick_split_k(M, N, K, 64) > 1
+        g = torch.Generator(device="cuda").manual_seed(M + 5 * N + K)
+        a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda", generator=g) if bias else None
+        ref = a.float() @ bt.float().T + (b if bias else 0)
+        if relu:
+            ref = torch.relu(ref)
+        tol = 0.01 * ref.abs().max().item() + 1e-2
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        for _ in range(4):
+            out.fill_(float("nan"))
+            loadgen.gemm(a, bt, out=out, bias=b, relu=relu, cu_budget=64)
+            assert (out.float() - ref).abs().max().item() <= tol
+    finally:
+        hip.set_gemm_policy(1)
+
+
 @pytest.mark.parametrize("slice_", [0, 1])
 def test_gemm_split_k_layout_identity(hip, slice_):
     """A = I placed in K slice 0 or 1 (zeros elsewhere) with an asymmetric B: pins the C layout

@@ -96,6 +96,8 @@ def main() -> None:
     ap.add_argument("--umc-cal", action="store_true", help="triad TB/s vs amd-smi umc_activity")
     ap.add_argument("--extra-streams", default="", help="K:before|after -- K idle streams that each "
                     "dispatch one tiny kernel (so get a hardware queue) before / after the slot streams")
+    ap.add_argument("--bench-args", default="", help="bench.py flags for the executor's kernel policy, "
+                    "e.g. '--gemm-policy 8'")
     ap.add_argument("--passes", type=int, default=1,
                     help="back-to-back passes per timed regime run; amd-smi umc is averaged over the "
                          "last half of the run (its firmware moving average lags a regime change)")
@@ -107,7 +109,7 @@ def main() -> None:
     pods = [(names[int(r[3])], int(r[1]), int(r[2]), int(r[4])) for ep in epochs for r in ep if int(r[0]) == 0]
     steps = len(epochs)
     torch.cuda.set_device(0)
-    ba = build_parser().parse_args([])
+    ba = build_parser().parse_args(args.bench_args.split())
     ex = gpu_executor(ba, 0)
     kx = KindExecutor(0)
     kx.use_graphs = False
