@@ -58,7 +58,7 @@ def load(path: str) -> Tuple[List[List[Pod]], List[List[Place]], List[bool], Dic
 
 
 def simulate(pods: List[List[Pod]], places: List[List[Place]], timed: Sequence[bool], lookahead: int = 2,
-             model: Any = None) -> Tuple[int, int, float]:
+             model: Any = None, outcomes: Any = None) -> Tuple[int, int, float]:
     """(SLOs met, pods, simulated ms) over the timed epochs: the bench's loop -- warm-up epochs,
     drained, then the timed ones, `lookahead` epochs in flight -- on the model pipeline."""
     ex = ModelPipelineExecutor(model=model, noise=0.0)
@@ -84,12 +84,16 @@ def simulate(pods: List[List[Pod]], places: List[List[Place]], timed: Sequence[b
                 if phase:
                     ok += sum(1 for r in rs if r.slo <= 0 or r.throughput >= r.slo)
                     n += len(rs)
+                    if outcomes is not None:
+                        outcomes.extend((r.workload, r.iters, r.slo, r.throughput) for r in rs)
         while pend:
             rs = pend.popleft()
             ex.wait_epoch(rs)
             if phase:
                 ok += sum(1 for r in rs if r.slo <= 0 or r.throughput >= r.slo)
                 n += len(rs)
+                if outcomes is not None:
+                    outcomes.extend((r.workload, r.iters, r.slo, r.throughput) for r in rs)
         if phase:
             t1 = ex.elapsed_ms
     return ok, n, t1 - t0
@@ -253,6 +257,29 @@ def main() -> None:
                                  "pods_per_s": round(n / ms * 1e3, 1), "search_s": round(time.time() - t, 1),
                                  "from_start": log}
     print("oracle", out["policies"]["oracle"], flush=True)
+    # which pods the oracle saves: per timed pod (workload, SLO / its alone rate) met by the
+    # planner / by the oracle -- the pods it rescues and the ones it gives up
+    o_pl, o_or = [], []
+    simulate(pods, places, timed, lookahead, model, o_pl)
+    simulate(pods, best_pl, timed, lookahead, model, o_or)
+    saved, lost = collections.Counter(), collections.Counter()
+    tight = {"saved": [], "lost": [], "both": [], "neither": []}
+    for (wl, it, slo, thr_p), (_, _, _, thr_o) in zip(o_pl, o_or):
+        alone = it / (model.alone_ms[model.wid(wl)] * it / 1e3)      # alone iterations / s
+        k = ("both" if thr_p >= slo and thr_o >= slo else "saved" if thr_o >= slo else
+             "lost" if thr_p >= slo else "neither")
+        tight[k].append(round(slo / alone, 3))
+        fam = wl.split("_", 1)[1].rsplit("_", 1)[0]
+        if k == "saved":
+            saved[fam] += 1
+        elif k == "lost":
+            lost[fam] += 1
+    out["oracle_pods"] = {k: {"n": len(v), "slo_over_alone_rate_mean": round(sum(v) / len(v), 3) if v else None}
+                          for k, v in tight.items()}
+    out["oracle_pods"]["saved_by_family"] = dict(saved)
+    out["oracle_pods"]["lost_by_family"] = dict(lost)
+    out["oracle_places"] = best_pl
+    print("oracle pods", out["oracle_pods"], flush=True)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         json.dump(out, open(a.out, "w"), indent=1)
