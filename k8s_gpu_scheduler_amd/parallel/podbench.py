@@ -757,20 +757,29 @@ def _runs_for(arr: np.ndarray, gpu: int):
     return out
 
 
-def _prewarm(dev: torch.device, ms: float) -> None:
-    """Back-to-back 4096^3 MFMA GEMMs for about `ms` (untimed setup), so the firmware's
-    moving-average activity counter that the amd-smi sampler reads starts the timed region
-    from a busy GPU rather than from the idle process start-up (see --prewarm-ms)."""
+def _prewarm(dev: torch.device, ms: float, kind: str = "mix") -> None:
+    """Back-to-back 4096^3 MFMA GEMMs interleaved with 768-MB HBM stream passes for about `ms`
+    (untimed setup), so the firmware's moving-average activity counters that the amd-smi sampler
+    reads (gfx AND umc) start the timed region from the bench's kind of load rather than from
+    the idle process start-up.  (GEMMs alone left umc_activity ramping up through the 135-ms
+    timed window: 31 % reported where the calibrated steady state of the same load is ~58 %,
+    profiles/r06_gap/README.md.)"""
     from ..ops import loadgen
     a = torch.rand(4096, 4096, device=dev).to(torch.bfloat16)
     bt = torch.rand(4096, 4096, device=dev).to(torch.bfloat16)
     c = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
+    n = 64 << 20
+    x, y, z = (torch.ones(n, device=dev) for _ in range(3))
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
-        for _ in range(16):
+        for _ in range(8):
             loadgen.gemm(a, bt, out=c)
+            if kind == "mix":
+                loadgen.triad(x, y, z, 1.0001)
+            else:
+                loadgen.gemm(a, bt, out=c)
         torch.cuda.synchronize(dev)
-    del a, bt, c
+    del a, bt, c, x, y, z
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -904,9 +913,12 @@ def build_parser() -> argparse.ArgumentParser:
                          "rest); 0: for the whole chip")
     ap.add_argument("--prewarm-ms", type=float, default=300.0,
                     help="untimed device warm-up before the warm-up epochs: this long of back-to-back MFMA "
-                         "GEMMs.  It does not change pods/s (interleaved A/B, profiles/r02_prewarm_ab.txt) but "
+                         "GEMMs and HBM stream passes.  It does not change pods/s (interleaved A/B, profiles/r02_prewarm_ab.txt) but "
                          "amd-smi's gfx_activity is a moving average: after the idle process start-up it reads "
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
+    ap.add_argument("--prewarm-kind", default="mix", choices=["mix", "gemm"],
+                    help="pre-warm load: GEMMs interleaved with HBM stream passes (mix: umc_activity starts the "
+                         "timed window near its steady state) or GEMMs only (the round-1..5 pre-warm)")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
     ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 5, 6, 7),
@@ -1076,7 +1088,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      for u in (0, 2, 4, 6)])
 
     if use_gpu and a.prewarm_ms > 0:
-        _prewarm(dev, a.prewarm_ms)
+        _prewarm(dev, a.prewarm_ms, a.prewarm_kind)
 
     totals = {"pods": 0.0, "busy_unit_ms": 0.0, "slo_ok": 0.0}
     state: Dict[str, Any] = {"next": cp.schedule_epoch() if rank == 0 else None}
