@@ -977,7 +977,7 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 8) throw std::runtime_error("gemm policy must be 0..8");
+  if (p < 0 || p > 9) throw std::runtime_error("gemm policy must be 0..9");
   g_gemm_policy = p;
 }
 
@@ -1135,8 +1135,25 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
     case 12: launch_gemm<128, 128, 2, 2, 1, 4, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;
     case 9:
     case 10: {
-      const dim3 grid((M / 256) * (N / 256)), block(512);
       const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
+      // policy 9 (A/B arm, round 6): a co-running pod's 8-phase GEMM with more 256 x 256 tiles than
+      // its CU share runs as back-to-back launches of whole tile rows of at most `cu_budget` tiles
+      // each, so it never holds more CUs than its share and the other pods' stream kernels keep
+      // the rest of the chip (profiles/r06_gap/: GEMM time not hidden under the streams is the
+      // largest term of the step)
+      const bool co = cu_budget > 0 && cu_budget < kCus;
+      if (t == 10 && co && g_gemm_policy == 9 && (M / 256) * (N / 256) > cu_budget) {
+        const int rows = std::max(1, cu_budget / (N / 256)) * 256;
+        const dim3 block(512);
+        for (int m0 = 0; m0 < M; m0 += rows) {
+          const int mm = std::min(rows, M - m0);
+          const dim3 g((mm / 256) * (N / 256));
+          launch_8ph<true>(A + (size_t)m0 * lda, B, Cp + (size_t)m0 * ldc, bp, mm, N, K, lda, ldb, ldc, relu, s, g,
+                           block, false);
+        }
+        break;
+      }
+      const dim3 grid((M / 256) * (N / 256)), block(512);
       if (t == 10)
         launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
       else

@@ -201,6 +201,11 @@ def test_launcher_builds_kubelet_env_from_assignment():
     assert b["HSA_CU_MASK"] is None and b["ROCR_VISIBLE_DEVICES"]       # Burstable: no hard mask
     assert w["HSA_CU_MASK"] is None and w["ROCR_VISIBLE_DEVICES"].startswith("GPU-")
     assert O.phase(fc.get("pods", "whole", "default")) == "Succeeded"
+    # kubelet-style container status: whole-second RFC 3339 times (what the completion feedback's
+    # quantisation bound is about), the exit code, and no container left in the pid map
+    term = fc.get("pods", "whole", "default")["status"]["containerStatuses"][0]["state"]["terminated"]
+    assert term["exitCode"] == 0 and term["startedAt"].endswith("Z") and "." not in term["finishedAt"]
+    assert la.running == {}
 
 
 def test_profiled_launcher_records_history(tmp_path, monkeypatch):

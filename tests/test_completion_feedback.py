@@ -251,3 +251,34 @@ def test_busy_tracker_integrates_cu_occupancy_when_no_engine_time():
     bt2.sample(src, {5: "v"}.get, 1, now=0.0, max_gap_s=0.2)
     bt2.sample(src, {5: "v"}.get, 1, now=5.0, max_gap_s=0.2)
     assert bt2.busy_ms("v") == (pytest.approx(200.0), "amd-smi-occupancy")
+
+
+def test_agent_busy_sampler_thread_annotates_a_finished_pod():
+    """The agent's own sampler thread (busy_poll_s) integrates a pod's occupancy while it runs;
+    the step's annotation pass writes busy-ms once the pod is terminal; stop() joins the thread."""
+    import time as _t
+    from k8s_gpu_scheduler_amd.agent.agent import NodeAgent
+    from k8s_gpu_scheduler_amd.agent.devices import StaticSource
+    from k8s_gpu_scheduler_amd.plugins.gpu.feedback import ANNOT_BUSY_MS
+    from k8s_gpu_scheduler_amd.store.fake_redis import FakeRedisBackend, FakeRedisEngine
+    from k8s_gpu_scheduler_amd.store.resp import Redis
+    fc = FakeCluster()
+    fc.create("nodes", O.make_node("n0", gpus=1))
+    fc.create("pods", O.make_pod("p", gpu_cu=64, node_name="n0", phase="Running"))
+    uid = O.uid(fc.get("pods", "p", "default"))
+    src = StaticSource([{"uuid": "GPU-a", "gpu": 0}], samples=[])
+    src.procs = {0: [{"pid": 42, "gfx_ns": 0, "cu_occupancy": 32}]}
+    ag = NodeAgent("n0", Redis(FakeRedisBackend(FakeRedisEngine())), src, client=fc, pod_resolver={42: uid}.get,
+                   busy_poll_s=0.02)
+    ag.start_busy_sampler()
+    try:
+        _t.sleep(0.4)
+        src.procs = {0: []}                                   # the process exited
+        fc.patch("pods", "p", {"status": {"phase": "Succeeded"}}, "merge", "default")
+        _t.sleep(0.05)
+        assert ag.track_busy() == ["default/p"]
+    finally:
+        ag.stop()
+    assert ag._busy_thread is not None and not ag._busy_thread.is_alive()
+    ms = float(O.annotations(fc.get("pods", "p", "default"))[ANNOT_BUSY_MS])
+    assert 250.0 <= ms <= 450.0, ms                           # ~0.4 s of occupancy, 20-ms rounds

@@ -12,7 +12,7 @@ h = _native.hip(required=False)
 pytestmark = pytest.mark.skipif(h is None, reason="HIP extension not built")
 
 # policy -> tile for M=1024, N=2048 at a 64-CU budget
-SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1}
+SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1, 9: 1}
 
 
 @pytest.fixture(autouse=True)
@@ -28,7 +28,7 @@ def test_small_corun_gemm_tile_per_policy(policy):
     assert h.pick_gemm_tile(1024, 2048, 64) == SMALL[policy]
 
 
-@pytest.mark.parametrize("policy", range(9))
+@pytest.mark.parametrize("policy", range(10))
 def test_large_corun_and_lone_gemm_tiles(policy):
     h.set_gemm_policy(policy)
     # enough 256x256 tiles for the share: the 8-phase kernel for every policy but 0

@@ -155,6 +155,30 @@ def test_gemm_corun_split_k_policy8_matches_fp32_reference(hip, M, N, K, relu, b
         hip.set_gemm_policy(1)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (2048, 2560, 1536), (4096, 2048, 1024)])
+def test_gemm_share_capped_policy9_matches_fp32_reference(hip, M, N, K):
+    """Arm 9: a co-running pod's 8-phase GEMM with more 256 x 256 tiles than its 64-CU share runs as
+    back-to-back launches of whole tile rows (<= 64 tiles each); every row slice lands in the
+    right place (fp32 PyTorch reference, repeated runs)."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    hip.set_gemm_policy(9)
+    try:
+        assert hip.pick_gemm_tile(M, N, 64) == 10
+        g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K)
+        a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda", generator=g)
+        ref = torch.relu(a.float() @ bt.float().T + b)
+        tol = 0.01 * ref.abs().max().item() + 1e-2
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        for _ in range(3):
+            out.fill_(float("nan"))
+            loadgen.gemm(a, bt, out=out, bias=b, relu=True, cu_budget=64)
+            assert (out.float() - ref).abs().max().item() <= tol
+    finally:
+        hip.set_gemm_policy(1)
+
+
 @pytest.mark.parametrize("slice_", [0, 1])
 def test_gemm_split_k_layout_identity(hip, slice_):
     """A = I placed in K slice 0 or 1 (zeros elsewhere) with an asymmetric B: pins the C layout
