@@ -771,7 +771,11 @@ __global__ void __launch_bounds__(256) stream_triad_kernel(float4* __restrict__ 
 // any store (U outstanding 16-B loads per stream per lane), block-contiguous so every
 // load instruction is one coalesced 1 KiB wave access; NT selects non-temporal
 // (streaming) loads/stores so the one-touch stream does not evict L2/MALL lines.
-template <int U, bool NT>
+// WT: the result goes out with `global_store_dwordx4 ... sc1` (write-through, the line is DROPPED
+// from the XCD's L2, MI355X_MICROARCH.md "stores of each flavour") instead of a non-temporal store
+// (which keeps the line in L2): a one-touch output stream then does not evict the co-running
+// GEMMs' operand panels from L2 (round-6 A/B, variant 8).  Vector stores only.
+template <int U, bool NT, bool WT = false>
 __global__ void __launch_bounds__(256) stream_triad_u(float4* __restrict__ a_, const float4* __restrict__ b_,
                                                       const float4* __restrict__ c_, float s, size_t n4) {
   auto a = reinterpret_cast<f32x4*>(a_);
@@ -799,7 +803,9 @@ __global__ void __launch_bounds__(256) stream_triad_u(float4* __restrict__ a_, c
       const size_t i = base + (size_t)k * blockDim.x;
       if (i < n4) {
         const f32x4 r = x[k] + s * y[k];
-        if (NT)
+        if (WT)
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(a + i), "v"(r) : "memory");
+        else if (NT)
           __builtin_nontemporal_store(r, a + i);
         else
           a[i] = r;
@@ -823,7 +829,7 @@ static int g_triad_variant = 6;
 // to fit beside an 8-phase GEMM block's 2 x 240 VGPRs per SIMD (the 4x variant's 38 VGPRs do
 // not, so a CU running a 256 x 256 GEMM block takes no triad wave at all; round 6 A/B)
 void set_triad_variant(int v) {
-  if (v < 0 || v > 7) throw std::runtime_error("triad variant must be 0..7 (6 = auto)");
+  if (v < 0 || v > 8) throw std::runtime_error("triad variant must be 0..8 (6 = auto)");
   g_triad_variant = v;
 }
 
@@ -1230,6 +1236,7 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
     case 3: hipLaunchKernelGGL((stream_triad_u<4, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 4: hipLaunchKernelGGL((stream_triad_u<8, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 7: hipLaunchKernelGGL((stream_triad_u<3, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
+    case 8: hipLaunchKernelGGL((stream_triad_u<4, true, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     default: hipLaunchKernelGGL((stream_triad_u<2, true>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
   }
   HIP_CHECK(hipGetLastError());

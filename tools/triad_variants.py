@@ -25,7 +25,7 @@ def main() -> None:
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     res = {}
     for rnd in range(3):
-        for v in (3, 5, 7):
+        for v in tuple(int(x) for x in os.environ.get("TRIAD_VARIANTS", "3,5,7").split(",")):
             h.set_triad_variant(v)
             for co in (False, True):
                 torch.cuda.synchronize()
