@@ -921,7 +921,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "timed window near its steady state) or GEMMs only (the round-1..5 pre-warm)")
     ap.add_argument("--triad-blocks", type=int, default=0,
                     help="workgroups per HBM-stream kernel launch (0 = the kernel's default)")
-    ap.add_argument("--triad-variant", type=int, default=6, choices=(0, 1, 2, 3, 4, 5, 6, 7, 8),
+    ap.add_argument("--triad-variant", type=int, default=6, choices=tuple(range(11)),
                     help="HBM-stream kernel variant (native set_triad_variant; 6 = auto by size)")
     ap.add_argument("--smi-period-ms", type=float, default=5.0,
                     help="amd-smi activity sampling period across warmup + timed region (0 = off)")

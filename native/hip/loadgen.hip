@@ -829,7 +829,7 @@ static int g_triad_variant = 6;
 // to fit beside an 8-phase GEMM block's 2 x 240 VGPRs per SIMD (the 4x variant's 38 VGPRs do
 // not, so a CU running a 256 x 256 GEMM block takes no triad wave at all; round 6 A/B)
 void set_triad_variant(int v) {
-  if (v < 0 || v > 8) throw std::runtime_error("triad variant must be 0..8 (6 = auto)");
+  if (v < 0 || v > 10) throw std::runtime_error("triad variant must be 0..10 (6 = auto)");
   g_triad_variant = v;
 }
 
@@ -1229,6 +1229,9 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
   const size_t n4 = n_floats / 4;
   int variant = g_triad_variant;
   if (variant == 6) variant = (n_floats * 12 <= (size_t)96 << 20) ? 1 : 3;
+  // 9 / 10 (A/B arms): write-through stores only for the largest streams (arrays >= 256 / 128 MiB,
+  // where a lone sc1 stream gains most), non-temporal below
+  if (variant == 9 || variant == 10) variant = n_floats * 4 >= ((size_t)(variant == 9 ? 256 : 128) << 20) ? 8 : 3;
   switch (variant) {
     case 0: hipLaunchKernelGGL(stream_triad_kernel, dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
     case 1: hipLaunchKernelGGL((stream_triad_u<2, false>), dim3(blocks), dim3(256), 0, st, A, B, Cc, s, n4); break;
