@@ -411,10 +411,11 @@ def test_planner_feedback_moves_work_off_a_really_slower_gpu():
     g0, g1 = (PB.NODE, 0), (PB.NODE, 1)
     assert planner.speed(g1) > 1.2 * planner.speed(g0), state(12)      # GPU 1 measured slower
     # (a burst is 4 pods of unequal length, so a single burst's share is one of a handful of
-    # discrete splits around the 1 / 2.4 target.  Round 6's rank-test gate decides from the
-    # third observation on for a shift this large: the CPU twin (tests/test_backlog_control.py)
-    # keeps every burst of epochs 6-11 in [0.15, 0.5] on these arrivals)
-    assert 0.3 < float(np.mean(share)) < 0.5 and min(share) >= 0.15 and max(share) <= 0.55, state(12)
+    # discrete splits around the 1 / 2.4 target: GPU 1 takes one pod or two.  Round 6's rank-test
+    # gate decides from the third observation on for a shift this large; on MI355X the bursts of
+    # epochs 6-11 read 0.34-0.49 in two runs and 0.148-0.485 in a third, where GPU 1 took only
+    # the burst's shortest pod once (round 5 saw the same 0.148) -- a starved GPU would be 0)
+    assert 0.3 < float(np.mean(share)) < 0.5 and min(share) >= 0.12 and max(share) <= 0.55, state(12)
     # bounded: never more than the planner's stored clip of a balanced burst's work
     assert max(spreads) <= planner.STORE_CLIP * planner._burst_ms + 1e-6, (spreads, state(12))
     assert np.mean(np.asarray(errs) <= 0.15) >= 0.8, errs
