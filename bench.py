@@ -12,7 +12,7 @@ import sys
 # HIP hardware queues per process (HIP's default, and the GPU box's environment, is 4): the 4
 # pod streams, the control stream, the null stream and RCCL's streams each need a queue of
 # their own -- pod streams that share a queue run back to back instead of side by side
-# (interleaved A/B on MI355X: 4 -> 8 queues = +2.9 % pods/s, profiles/r02_hwq_ab.txt; pod
+# (interleaved A/B on MI355X: 4 -> 8 queues = +2.9 % pods/s, profiles/archive/r02_hwq_ab.txt; pod
 # start/end events: tools/concurrency_probe.py), and an RCCL stream sharing a pod's queue
 # would hold the per-epoch placement broadcast behind that pod's queued kernels.  HIP creates
 # a queue per stream only up to this limit, so headroom costs nothing while the process has

@@ -5,7 +5,7 @@ Cython into extension modules that sit NEXT TO their .py sources.
 The scheduler is a Python re-implementation of the kube-scheduler framework (the reference
 links the Go one, reference cmd/scheduler/main.go:20-22); on the bench's 8-GPU node the
 control plane schedules 32 pods per epoch inside one GPU epoch, so its per-pod cost bounds
-multi-GPU scaling (profiles/r02_control_plane_timing_box.txt).  Compiling the unchanged
+multi-GPU scaling (profiles/archive/r02_control_plane_timing_box.txt).  Compiling the unchanged
 sources removes the interpreter's dispatch overhead (~15-18 % per epoch measured).
 
 Safety: an extension module shadows its .py (CPython's path finder prefers extension

@@ -39,7 +39,7 @@ an fp8-GEMM LLM-like workload whose 512-workgroup GEMMs fill the chip (every cat
 leaves 40-75 % of the CUs idle at a pod's 64-CU tile budget) and a triad-only one.
 
 Leave-one-workload-out on the MI355X co-run groups (tools/corun_coldstart_eval.py,
-profiles/r04_coldstart/loo.json): the model refitted WITHOUT workload X, X cold-started from
+profiles/archive/r04_coldstart/loo.json): the model refitted WITHOUT workload X, X cold-started from
 its alone groups only -- X's co-run throughput is predicted within a mean 5.8 % (median 5.0,
 worst 10.1), against 4.8 % held-out error of those fits on the workloads they saw (1.2x),
 4.6 % for X's own fitted row and 16.7 % for the roofline prior row.

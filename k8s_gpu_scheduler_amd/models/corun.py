@@ -11,7 +11,7 @@ two reasons a pairwise table cannot express:
   and the rest speed up, so what a pod achieves depends on how LONG its co-runners are,
   not only on who they are;
 * contention is asymmetric and resource-shaped -- next to an HBM stream a GEMM loses ~75 %
-  of its rate while the stream keeps ~97 % (profiles/r02_contention_probe.json).
+  of its rate while the stream keeps ~97 % (profiles/archive/r02_contention_probe.json).
 
 So this model is a small fluid simulation of the group instead.  Pod i carries W_i =
 iterations x its alone whole-GPU time per iteration (the MFMA / HBM work it brings).  While a

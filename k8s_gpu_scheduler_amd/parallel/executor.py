@@ -107,7 +107,7 @@ class DeviceExecutor:
     #   gemm_share   -- tell the GEMM tile picker the pod's CU share instead of the chip
     #   triad_blocks -- workgroups per stream-kernel launch (0 = the kernel's default)
     #   (capping the stream kernels at k workgroups per CU of the pod's share was measured and
-    #   dropped: 380 / 509 / 550 pods/s at k = 1 / 2 / 4 vs 586 uncapped, profiles/r03_triad_cap_ab.json)
+    #   dropped: 380 / 509 / 550 pods/s at k = 1 / 2 / 4 vs 586 uncapped, profiles/archive/r03_triad_cap_ab.json)
     gemm_share = True
     triad_blocks = 0
     #   use_graphs   -- replay each pod's whole kernel sequence (iters x ops) as one captured
@@ -121,7 +121,7 @@ class DeviceExecutor:
     #                   pipelines (plugins.gpu.timeline, --plan-slots), and the executor runs
     #                   every pod on the slot it was given (MI355X, 20 steps x 3 interleaved:
     #                   603.5 pods/s / 56.25 % SLOs vs 600.7 / 53.75 % for LPT re-slotting,
-    #                   gpurun_out r04_slots_ab20 -> profiles/r04_slots_ab/)
+    #                   gpurun_out r04_slots_ab20 -> profiles/archive/r04_slots_ab/)
     balance_slots = os.environ.get("GPUSCHED_BALANCE_SLOTS", "0") == "1"
 
     def __init__(self, device: int = 0, use_cu_masks: bool = True, units_per_gpu: int = 8):
@@ -288,7 +288,7 @@ class DeviceExecutor:
         pending on that stream's hardware queue for as long as the pods run, and the queue of
         the pod stream sharing its hardware pipe is then served at about half rate -- with
         the default stream joined on 4 co-running pods, the 4th pod stream took 6.0 ms instead
-        of 3.5 and the group 6.2 ms instead of 3.7 (profiles/r03_queue_fairness/README.md)."""
+        of 3.5 and the group 6.2 ms instead of 3.7 (profiles/archive/r03_queue_fairness/README.md)."""
         for ev in self._last_events:
             while not ev.query():
                 time.sleep(self.poll_s)

@@ -576,8 +576,8 @@ class ControlPlane:
 
 
 # best rates measured on one MI355X by ANY implementation: hipBLASLt (torch.matmul) bf16 at
-# 8192^3, median 1647.5 TF/s (profiles/r01_gemm_big.json; our own 8-phase kernel: 1434) and
-# the non-temporal stream triad from HBM (profiles/r01_triad_pmc.txt)
+# 8192^3, median 1647.5 TF/s (profiles/archive/r01_gemm_big.json; our own 8-phase kernel: 1434) and
+# the non-temporal stream triad from HBM (profiles/archive/r01_triad_pmc.txt)
 ACHIEVABLE_TFLOPS = 1648.0
 ACHIEVABLE_TBPS = 6.5
 
@@ -588,7 +588,7 @@ class SimExecutor:
     Untimed (default): pod time from the roofline at the pod's share, nothing waits.
     Timed (`--sim-timed`): a modelled device per rank -- an epoch occupies the GPU for the
     sum of its pods' whole-GPU co-run cost (GEMM FLOPs at the measured co-run GEMM rate +
-    HBM bytes at the measured co-run stream rate, profiles/r01_overlap_study.json) x
+    HBM bytes at the measured co-run stream rate, profiles/archive/r01_overlap_study.json) x
     `scale`, epochs run back to back, and wait_epoch sleeps until the epoch's modelled
     completion -- so multi-rank CPU rehearsals (gloo) reproduce the coupling of the ranks
     through the per-epoch placement broadcast, and load imbalance costs wall time."""
@@ -806,7 +806,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "(--slo-objective corun): balanced predicted group makespans, then the most predicted "
                          "SLOs met within --plan-tolerance, with the GPUs' backlogs carried between bursts "
                          "(--plan-carry) -- on the virtual 8-GPU node 83.1 %% of SLOs met vs 57.7 %% greedy and "
-                         "56.0 %% random, at 0.99x greedy's pipelined pods/s (48 epochs, profiles/r03_vn_carry/).  "
+                         "56.0 %% random, at 0.99x greedy's pipelined pods/s (48 epochs, profiles/archive/r03_vn_carry/).  "
                          "At N=1 there is one GPU group and nothing to plan")
     ap.add_argument("--online-scale", type=int, default=1,
                     help="online interference learning: shrink rows toward the prior SCALED by a learned "
@@ -825,13 +825,13 @@ def build_parser() -> argparse.ArgumentParser:
                          "the deployed recommender learns through ObserveCorun instead (agent/corun_observer.py)")
     ap.add_argument("--corun-sigma", type=float, default=0.05,
                     help="co-run burst planner: expected SLOs met under the model's log error of this sigma "
-                         "(held-out ~0.05, profiles/r03_corun_v2/); 0 = hard predicted counts")
+                         "(held-out ~0.05, profiles/archive/r03_corun_v2/); 0 = hard predicted counts")
     ap.add_argument("--plan-carry", type=float, default=1.0,
                     help="co-run burst planner: carry each GPU's predicted backlog from earlier bursts into the "
                          "next plans, decayed by this factor per burst (0 = every burst on its own).  The busiest "
                          "GPU's cumulative work paces the pipelined N-GPU run; MI355X virtual node: pipelined "
                          "epoch 1-4 %% shorter and 3-6 points more SLOs met than 0 at 2/4/8 GPUs "
-                         "(profiles/r03_vn_carry/).  No effect at N=1 (one GPU group)")
+                         "(profiles/archive/r03_vn_carry/).  No effect at N=1 (one GPU group)")
     ap.add_argument("--plan-feedback", type=int, default=1, choices=[0, 1],
                     help="with --plan-carry: correct each GPU's backlog with its measured busy time per "
                          "collected epoch (a GPU slower than its siblings, or the model's error on it)")
@@ -842,7 +842,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "measured ones pinned), which also gives the GPU choice each GPU's pipeline; 'auto' "
                          "(default) model across GPUs, lpt on one; 'off' the ledger's first fit (1 = model, "
                          "0 = off).  MI355X N=1, 3 interleaved A/Bs of 20 steps: levelling 601 pods/s / 54.6 %% "
-                         "SLOs, model 596 / 53.3 %% (profiles/r04_slot_policy/)")
+                         "SLOs, model 596 / 53.3 %% (profiles/archive/r04_slot_policy/)")
     ap.add_argument("--slot-spread-ms", type=float, default=2.0,
                     help="--plan-slots: how far (ms) the slots' predicted ends may spread beyond the most even "
                          "assignment's to meet more SLOs")
@@ -855,7 +855,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--plan-tolerance", type=float, default=0.3,
                     help="burst planner: how far (fraction) a GPU's predicted time may exceed the balanced plan's "
                          "slowest GPU to meet more SLOs (virtual node: 0.2 -> 73 %%, 0.3 -> 76-78 %%, 0.4 -> 79 %% "
-                         "at 0.97x greedy's pods/s; profiles/r03_vn_sweep/)")
+                         "at 0.97x greedy's pods/s; profiles/archive/r03_vn_sweep/)")
     ap.add_argument("--balance", type=float, default=1.0,
                     help="weight of the GPU plugin's least-predicted-load term (0 = off; >0 also sorts the "
                          "queue longest-predicted-work first)")
@@ -913,7 +913,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "rest); 0: for the whole chip")
     ap.add_argument("--prewarm-ms", type=float, default=300.0,
                     help="untimed device warm-up before the warm-up epochs: this long of back-to-back MFMA "
-                         "GEMMs and HBM stream passes.  It does not change pods/s (interleaved A/B, profiles/r02_prewarm_ab.txt) but "
+                         "GEMMs and HBM stream passes.  It does not change pods/s (interleaved A/B, profiles/archive/r02_prewarm_ab.txt) but "
                          "amd-smi's gfx_activity is a moving average: after the idle process start-up it reads "
                          "56 %% over a 20-step window that the HIP-event union shows 98 %% busy, 94 %% after it")
     ap.add_argument("--prewarm-kind", default="mix", choices=["mix", "gemm"],
@@ -930,7 +930,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "telemetry all-gather, result all-reduce, barriers): 1 always, 0 never, -1 (default) "
                          "on a GPU, so N=1 runs the same code as the N-GPU scaling run.  The two paths measure "
                          "the same (593/594 vs 594/592 pods/s at 20 steps, 625 vs 618 at 60; "
-                         "profiles/r03_window/README.md)")
+                         "profiles/archive/r03_window/README.md)")
     ap.add_argument("--out", default="")
     return ap
 
@@ -1061,7 +1061,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
         # stalls every other launch for 5-11 ms.  On the collective path the placement
         # broadcast touches `side` during warm-up; on the plain path its first use was the
         # timed region's reference event -- a one-off 5.6-11 ms inside the timed window, the
-        # whole 20-step "window effect" (profiles/r03_window/README.md).  Touch it now.
+        # whole 20-step "window effect" (profiles/archive/r03_window/README.md).  Touch it now.
         _touch = torch.cuda.Event()
         _touch.record(side)
         _touch.synchronize()

@@ -7,7 +7,7 @@ split into SPX/DPX/QPX/CPX compute partitions, so the inventory here is a list o
 `Device`s (physical index, partition index, CUs, HBM, NUMA), and the ledger accounts
 fractional use in **CU-slice units**: a GPU is 8 units of 32 CUs, where unit u is
 word u of the 256-bit HIP CU mask.  Measured on MI355X (tools/diag_gpu.py,
-profiles/diag_r01.json): in SPX mode mask bit i selects CU i//8 of XCC i%8, and a mask
+profiles/archive/diag_r01.json): in SPX mode mask bit i selects CU i//8 of XCC i%8, and a mask
 that leaves any XCC without CUs is ignored by the driver, so a unit is 4 CUs on *every*
 XCD (XCD isolation needs a real compute partition, DPX/QPX/CPX, which the agent applies
 through amd-smi).  A fractional pod gets a contiguous, naturally aligned run of units

@@ -90,7 +90,7 @@ class EffortController:
     first `settle` allowed-time samples, which still carry the old pace, are not taken).  The
     first decision acts on two samples without patience: a control plane that paces its GPUs
     from the start would carry that backlog into a timed region (rehearsed at 8 GPUs on the box
-    CPU: profiles/r04_cp_rehearsal/jump_first/)."""
+    CPU: profiles/archive/r04_cp_rehearsal/jump_first/)."""
 
     # relative cost of an epoch's scheduling per effort level (box CPU, 8 GPUs, tools/cp_timing.py
     # and tools/archive/gpu_cp_levels.sh: 5.78 / 4.68 / 4.09 ms, profiles/r05_cp_levels/; level 3 3.59 of

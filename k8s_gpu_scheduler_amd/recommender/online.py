@@ -19,7 +19,7 @@ from co-running pods -- is thus learned from all rows at once, and the per-colum
 refines what the data supports.  Off by default (`scale=False`: an unseen entry keeps its
 prior value exactly); the bench's control plane turns it on (`--online-scale`, default 1:
 prequential MAE / prior 0.86-0.90 vs 0.97-0.98 without it at the driver's 20 steps on MI355X,
-pods/s unchanged -- profiles/r02_online_scale_ab/).
+pods/s unchanged -- profiles/archive/r02_online_scale_ab/).
 
 `prequential` error bookkeeping (predict each observation with the current model before
 learning from it) measures whether the online table predicts better than the prior.

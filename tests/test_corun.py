@@ -377,7 +377,7 @@ def test_plan_feedback_counts_each_gpus_busy_time_once_on_a_pipelined_timeline()
 @pytest.mark.skipif(not has_core, reason="_core not built")
 def test_default_planner_meets_more_slos_than_greedy_and_random_at_greedy_throughput(tmp_path):
     """Policy-quality regression guard on the simulated virtual 8-GPU node (the co-run model
-    +-5 % stands in for the GPUs; on MI355X the same comparison is profiles/r03_vn_carry/): the
+    +-5 % stands in for the GPUs; on MI355X the same comparison is profiles/archive/r03_vn_carry/): the
     bench/deployed default planner meets clearly more SLOs than greedy and random placement, at
     no more than 3 % below greedy's pipelined pods/s."""
     import json

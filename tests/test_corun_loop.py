@@ -128,7 +128,7 @@ def test_profiled_pods_on_one_gpu_refine_the_served_model_and_the_scheduler_scor
 def test_cold_start_leave_one_workload_out_on_measured_groups():
     """models.coldstart: each catalog workload in turn is dropped from the shipped model and
     re-imputed from its alone profile (alone ms per iteration, MFMA share) and the other 17
-    rows; on its measured MI355X co-run groups (profiles/r03_corun_v2) the imputed row's
+    rows; on its measured MI355X co-run groups (profiles/archive/r03_corun_v2) the imputed row's
     throughput error stays within 2x the fitted model's held-out error, and
     far below the roofline prior row's."""
     import json

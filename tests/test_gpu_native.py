@@ -604,7 +604,7 @@ def test_executor_runs_extra_workloads_fp8_and_triad_only():
 def test_executor_serves_four_co_running_pod_streams_equally():
     """Four identical Burstable pods co-run on four streams and finish within a few percent of
     each other.  (A stream-wait pending on another hardware queue while they ran made the 4th
-    stream ~1.8x slower: profiles/r03_queue_fairness/README.md; wait_all waits from the host.)"""
+    stream ~1.8x slower: profiles/archive/r03_queue_fairness/README.md; wait_all waits from the host.)"""
     from k8s_gpu_scheduler_amd.parallel.executor import DeviceExecutor, PodRun
     wl = "onnx_resnet50_2048"
     ex = DeviceExecutor(0)

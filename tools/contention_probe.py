@@ -1,6 +1,6 @@
 """GEMM x HBM-stream contention probe (one MI355X).
 
-Why do co-running GEMM and stream-triad pods barely overlap (profiles/r01_overlap_study.json:
+Why do co-running GEMM and stream-triad pods barely overlap (profiles/archive/r01_overlap_study.json:
 full 8.10 ms vs GEMM-only 2.86 + triad-only 5.74)?  Two candidate causes:
   (1) CU contention -- the kernels compete for wave slots / VGPRs / LDS on the same CUs;
   (2) memory-system contention -- the saturated HBM stream inflates the GEMM's load latency

@@ -4,10 +4,10 @@ For every catalog workload X: refit the co-run model on the MI355X groups WITHOU
 group containing X removed), cold-start X from its alone profile only (median alone ms per
 iteration of its 1-pod groups; its MFMA share; its CU fill unless --no-fill), and measure the throughput error on X's
 measured co-run groups.  Compared with: the full fit's row for X (X seen in training) and the
-roofline prior row.  Writes a JSON report (profiles/r04_coldstart/).
+roofline prior row.  Writes a JSON report (profiles/archive/r04_coldstart/).
 
-    python tools/corun_coldstart_eval.py [--groups profiles/r03_corun_v2/groups_2558_hostwait.json]
-                                         [--jobs 6] [--out profiles/r04_coldstart/loo.json]
+    python tools/corun_coldstart_eval.py [--groups profiles/archive/r03_corun_v2/groups_2558_hostwait.json]
+                                         [--jobs 6] [--out profiles/archive/r04_coldstart/loo.json]
 """
 from __future__ import annotations
 

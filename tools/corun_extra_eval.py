@@ -8,7 +8,7 @@ the throughput error of X's pods, and of the catalog pods in the same groups (ro
 other boxes' groups: the model's error on this box for workloads it knows).  Both with the
 model's catalog alone times as fitted, and with them replaced by this box's alone medians (what
 the online learner's alone-time scale converges to).  The bar is the fitted model's held-out
-MAE (profiles/r04_coldstart/loo.json: mean of the leave-one-out fits' held-out errors).
+MAE (profiles/archive/r04_coldstart/loo.json: mean of the leave-one-out fits' held-out errors).
 
     python tools/corun_extra_eval.py gpurun_out/corun_extra_groups.json [--out profiles/r05_coldstart/extra.json]
 """

@@ -1,4 +1,4 @@
-"""How late does the host see a pod epoch finish?  (profiles/r03_window/)
+"""How late does the host see a pod epoch finish?  (profiles/archive/r03_window/)
 
 The 1-rank plain bench path collected every epoch ~6 ms after its last pod kernel ended
 (pod timelines, GPUSCHED_BENCH_TRACE), the 1-rank RCCL path within 0.1 ms.  This probe runs

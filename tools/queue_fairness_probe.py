@@ -3,7 +3,7 @@
 The co-run model fitted on 2558 measured groups was unbiased for the first three pods of a
 4-pod group but predicted the fourth 24 % too fast, and in the virtual-node runs the pod on
 the fourth stream met its SLO 10 % of the time against 60-98 % for the others.  This probe
-found why (profiles/r03_queue_fairness/README.md): the tools waited for a group by making
+found why (profiles/archive/r03_queue_fairness/README.md): the tools waited for a group by making
 the DEFAULT stream wait on the pods' end events.  That stream-wait sits as a pending barrier
 packet on the default stream's hardware queue while the pods run.  The pod stream whose
 queue shares a hardware pipe with it -- the 4th pod stream to get its first graph captured
