@@ -32,6 +32,7 @@ void gemm_fp8_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M, 
 void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_floats, int blocks, uintptr_t stream);
 void set_triad_variant(int v);
 void set_gemm_tile(int t);
+void set_w4_probe(int mask);
 void set_gemm_policy(int p);
 void set_wide_epilogue(int on);
 void set_xcd_blocks(int on);

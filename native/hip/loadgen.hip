@@ -27,6 +27,7 @@
 // fp32 PyTorch), the rest of the A/B record lives in profiles/.
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "api.h"
 #include "common.h"
@@ -737,6 +738,189 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     }
 }
 
+// Tile 14 (lone-GEMM study; forced with set_gemm_tile only): the 256 x 256
+// block tile on FOUR waves of 128 x 128 -- hipBLASLt's shape (profiles/r05_lone_gemm_pmc/:
+// 0.25 LDS reads per MFMA instead of the 8-phase kernel's 0.375).  Round 5's versions of this
+// structure stalled once per K-tile (1,016 TF) or spilled: the compiler kept a VGPR copy of the
+// 256 accumulators next to the AGPRs.  Here the MFMA is inline asm with the accumulator tied to
+// an AGPR ("+a"), so the accumulators cannot leave the AGPR file.
+__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// The compiler cannot see that the asm above is an MFMA, so it cannot insert the wait states
+// between an MFMA and a VALU access of its accumulator: these fences pin them.  An empty volatile
+// asm that "modifies" every accumulator keeps the compiler's own accumulator accesses on their
+// side of it (volatile asm statements keep their order).  agpr_after_init: after the zero-fill,
+// before the first MFMA; agpr_before_read: after the last MFMA, before the epilogue reads.
+__device__ __forceinline__ void agpr_fence(f32x4 (&acc)[8][8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+}
+__device__ __forceinline__ void agpr_after_init(f32x4 (&acc)[8][8]) {
+  agpr_fence(acc);
+  asm volatile("s_nop 7" ::: "memory");
+}
+__device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[8][8]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  agpr_fence(acc);
+}
+
+// The schedule: 64-deep operand tiles in a 5-slot LDS ring.  Timing probes of a first version
+// (32-deep sub-tiles in 4 slots, one barrier per 32 k; profiles/r06_lone_gemm/): its LDS-DMA cost
+// the single wave per SIMD ~0.22 ms of 0.79 at 8192^3, and fetching 8 rows x 128 B per
+// instruction (whole cache lines) instead of 16 rows x 64 B saved ~0.09 ms of that.  So the
+// operand tiles here are 256 rows x 64 k (128-B rows, stage_tile's KT = 64 image and swizzle):
+// A_t and B_t are 32 KiB each and take ring slots
+// (2t) % 5 and (2t+1) % 5 (160 KiB, the CU's whole LDS).  K-tile t runs two halves of 64 MFMAs:
+//   h0: MFMAs of k-step 0 (fragment set 0), reads of k-step 1 into set 1, glds of A_{t+2}
+//       (into B_{t-1}'s slot);
+//   lgkmcnt(0) + vmcnt (A_{t+1}, B_{t+1} landed; A_{t+2} may fly) + ONE barrier;
+//   h1: MFMAs of k-step 1 (set 1), reads of K-tile t+1's k-step 0 into set 0, glds of B_{t+2}
+//       (into A_t's slot).
+// The barrier certifies for every wave that A_{t+1} / B_{t+1} landed (RAW for h1's reads) and
+// that every read of A_t and B_{t-1} retired (WAR for the next two glds groups), so one barrier
+// per 128 MFMAs suffices.
+template <bool RELU, bool BIAS, int PROBE = 0>
+__global__ void __launch_bounds__(256, 1)
+gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
+                     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
+  constexpr int KT = 64, NSLOT = 5;
+  constexpr int SLOT = 256 * KT * 2;               // one operand tile: 32 KiB
+  constexpr int G = SLOT / 16 / 256;               // glds per thread per operand tile (8)
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, M / 256, N / 256, xmap, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int frow = lane & 15, fk = lane >> 4;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  agpr_after_init(acc);
+  bf16x8 fa[2][8], fb[2][8];
+  const int T = K / KT;                             // >= 2
+
+  // piece q of operand tile X_u (B if isb): rows (q * 256 + wave * 64 + lane) >> 3, 8 per
+  // instruction, by buffer_load ... lds through one descriptor per operand block: the per-thread
+  // part is one 32-bit voffset per operand ((r >> 1) & 7 does not depend on q), the piece and
+  // K-tile parts an SGPR soffset (the global_load_lds form with 64-bit per-lane addresses: within
+  // 1-2 %, profiles/r06_lone_gemm/)
+  const int rr = (wave * 64 + lane) >> 3, kq = ((wave * 64 + lane) & 7) ^ ((rr >> 1) & 7);
+  const int voA = rr * lda * 2 + kq * 16, voB = rr * ldb * 2 + kq * 16;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(Bt + (size_t)n0 * ldb), 0, 256 * ldb * 2, 0x00020000);
+  auto glds = [&](int u, bool isb, int q) {
+    char* dst = smem + ((2 * u + (isb ? 1 : 0)) % NSLOT) * SLOT + (q * 256 + wave * 64) * 16;
+    const int so = q * 32 * (isb ? ldb : lda) * 2 + u * KT * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isb ? rsB : rsA, (lptr_t)dst, 16, isb ? voB : voA, so, 0, 0);
+  };
+  auto slot = [&](int u, bool isb) -> const char* { return smem + ((2 * u + (isb ? 1 : 0)) % NSLOT) * SLOT; };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: A_0 B_0 A_1 B_1 in flight; wait for A_0 / B_0; k-step 0 of K-tile 0 into set 0
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int q = 0; q < G; ++q) glds(u, x == 1, q);
+  wait_vmcnt<2 * G>();
+  barrier();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    fa[0][q] = lds_frag<KT>(smem, wr * 128 + q * 16 + frow, fk);
+    fb[0][q] = lds_frag<KT>(smem + SLOT, wc * 128 + q * 16 + frow, fk);
+  }
+
+  // one half: 64 MFMAs on set S (k-step S of K-tile t); reads of (RU, k-step S^1) into set S^1
+  // when RD, one per 4 MFMAs; glds of operand tile (t+2, X = S) when ST, one per 8 MFMAs (other
+  // placements -- the glds in the odd groups, reads and glds in separate halves -- measured
+  // 1-2 % slower, profiles/r06_lone_gemm/)
+  auto half = [&](auto sc, auto rdc, auto stc, int t) {
+    constexpr int S = decltype(sc)::value;
+    constexpr bool RD = decltype(rdc)::value, ST = decltype(stc)::value;
+    const int ru = S == 0 ? t : t + 1;             // h0 reads k-step 1 of t, h1 k-step 0 of t+1
+    const char* ta = slot(ru, false);
+    const char* tb = slot(ru, true);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int i = (g * 4 + m) >> 3, j = (g * 4 + m) & 7;
+        mfma_agpr(acc[i][j], fb[S][j], fa[S][i]);
+      }
+      if constexpr (RD) {
+        if (g < 8) fa[S ^ 1][g] = lds_frag<KT>(ta, wr * 128 + g * 16 + frow, (S ^ 1) * 4 + fk);
+        else fb[S ^ 1][g - 8] = lds_frag<KT>(tb, wc * 128 + (g - 8) * 16 + frow, (S ^ 1) * 4 + fk);
+      }
+      if constexpr (ST) {
+        if ((g & 1) == 0) glds(t + 2, S == 1, g >> 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto sync = [&](auto wc_) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): this wave's reads retired
+    wait_vmcnt<decltype(wc_)::value>();
+    barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using IG = std::integral_constant<int, G>;
+  using Y = std::true_type;
+  using F = std::false_type;
+  // PROBE (timing study only): bit 0 drops the steady loop's glds, bit 1 its reads (wrong results)
+  using SR = std::integral_constant<bool, !(PROBE & 2)>;
+  using SS = std::integral_constant<bool, !(PROBE & 1)>;
+  int t = 0;
+  for (; t + 3 <= T; ++t) {                         // steady: stages A_{t+2}, B_{t+2}
+    half(I0{}, SR{}, SS{}, t);
+    sync(IG{});
+    half(I1{}, SR{}, SS{}, t);
+  }
+  if (t + 2 == T) {                                 // K-tile T-2: nothing left to stage
+    half(I0{}, Y{}, F{}, t);
+    sync(I0{});
+    half(I1{}, Y{}, F{}, t);
+    ++t;
+  }
+  half(I0{}, Y{}, F{}, t);                          // K-tile T-1
+  half(I1{}, F{}, F{}, t);
+  agpr_before_read(acc);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  barrier();
+
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = wc * 128 + j * 16 + fk * 4;
+    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 v = acc[i][j] + bv;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
+      wide_put<256>(smem, wr * 128 + i * 16 + frow, col, o);
+    }
+  }
+  __syncthreads();
+  wide_store<256, 256, 256>(smem, C, ldc, m0, n0);
+}
+
 // C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
 // bf16x4 out, grid-stride over M*N/4).
 template <bool RELU, bool BIAS>
@@ -961,8 +1145,13 @@ static int g_gemm_tile = 0;
 // co-running pod's small GEMM gets ~1 block per CU of its share, so its 4 waves (one per SIMD)
 // must hide the MALL / HBM latency of the next tiles by depth, not by a second resident block.
 // 13 = 256x128 8-phase (gemm_bf16_nt_256_8ph<..., BN = 128>, peeled + wide epilogue; K >= 128)
-static const int kTileBM[14] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256};
-static const int kTileBN[14] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128};
+// 14 = 256x256 on 4 waves of 128x128 with AGPR-tied inline-asm MFMAs, 64-deep operand tiles in a
+// 5-slot LDS ring (gemm_bf16_nt_256_w4l).  Forced only (K >= 128, C rows 16-B aligned): the
+// lone-GEMM study of profiles/r06_lone_gemm/, level with tile 10.  (Also measured there and
+// removed: 32-deep sub-tiles in 4 slots with one barrier per 32 or per 64 k, and register-staged
+// global loads -- 5-15 % behind.)
+static const int kTileBM[15] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256, 256};
+static const int kTileBN[15] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128, 256};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -987,8 +1176,14 @@ void set_gemm_policy(int p) {
   g_gemm_policy = p;
 }
 
+static int g_w4_probe = 0;
+void set_w4_probe(int mask) {
+  if (mask < 0 || mask > 3) throw std::runtime_error("w4 probe must be 0..3");
+  g_w4_probe = mask;
+}
+
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 13) throw std::runtime_error("gemm tile must be 0..13");
+  if (t < 0 || t > 14) throw std::runtime_error("gemm tile must be 0..14");
   g_gemm_tile = t;
 }
 
@@ -1080,6 +1275,7 @@ static int resolve_gemm_tile(int M, int N, int K, int cu_budget) {
   int t = pick_gemm_tile(M, N, cu_budget);
   if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
   if (t == 13 && K < 128) t = 5;
+  if (t == 14 && K < 128) t = 4;
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked by the caller)
   return t;
 }
@@ -1170,6 +1366,23 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
       const dim3 grid((M / 256) * (N / 128)), block(512);
       const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
       launch_8ph<true, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
+      break;
+    }
+    case 14: {
+      if (!wide_ok(Cp, ldc)) throw std::runtime_error("gemm tile 14: C rows must be 16-byte aligned");
+      if ((size_t)256 * std::max(lda, ldb) * 2 >= ((size_t)1 << 31))
+        throw std::runtime_error("gemm tile 14: a 256-row operand block must span < 2 GiB");
+      const dim3 grid((M / 256) * (N / 256)), block(256);
+      const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
+      const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / 256);
+      decltype(&gemm_bf16_nt_256_w4l<false, false>) k;
+      if (g_w4_probe)   // timing probes: steady-loop LDS-DMA (1), reads (2) or both (3) dropped
+        k = g_w4_probe == 1 ? gemm_bf16_nt_256_w4l<false, false, 1>
+            : g_w4_probe == 2 ? gemm_bf16_nt_256_w4l<false, false, 2> : gemm_bf16_nt_256_w4l<false, false, 3>;
+      else
+        k = relu ? (bp ? gemm_bf16_nt_256_w4l<true, true> : gemm_bf16_nt_256_w4l<true, false>)
+                 : (bp ? gemm_bf16_nt_256_w4l<false, true> : gemm_bf16_nt_256_w4l<false, false>);
+      hipLaunchKernelGGL(k, grid, block, 0, s, A, B, Cp, bp, M, N, K, lda, ldb, ldc, xmap);
       break;
     }
     default: launch_gemm<64, 64, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s); break;

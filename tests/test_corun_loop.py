@@ -135,7 +135,7 @@ def test_cold_start_leave_one_workload_out_on_measured_groups():
     from k8s_gpu_scheduler_amd.models.coldstart import impute_row, mfma_share
     from k8s_gpu_scheduler_amd.models.corun import pack_groups
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    d = json.load(open(os.path.join(root, "profiles", "r03_corun_v2", "groups_2558_hostwait.json")))
+    d = json.load(open(os.path.join(root, "profiles", "archive", "r03_corun_v2", "groups_2558_hostwait.json")))
     groups = [g for g in d["groups"] if len(g["w"]) >= 2]
     m = CorunModel.load()
     held_out = m.meta["report"]["test"]["mae_pct_of_mean"]

@@ -72,3 +72,25 @@ def test_python_default_tile_rule_matches_the_native_picker():
         for budget in (0, 64, 128, 32):
             assert W.default_gemm_workgroups(M, N, K, budget, fp8) == h.gemm_workgroups(M, N, K, budget, fp8), \
                 (M, N, K, budget, fp8)
+
+
+def test_four_wave_study_tile_is_forced_only():
+    """Tile 14 (the 4-wave 256 x 256 kernel of the round-6 lone-GEMM study) runs only when forced:
+    no policy picks it on any shape / budget, it launches one 256-thread block per 256 x 256 tile,
+    falls back to tile 4 below two K-tiles, and its timing probes are range-checked."""
+    for policy in range(10):
+        h.set_gemm_policy(policy)
+        for M, N in [(1024, 2048), (4096, 4096), (8192, 8192), (2048, 1024)]:
+            for budget in (0, 32, 64, 128):
+                assert h.pick_gemm_tile(M, N, budget) != 14
+    h.set_gemm_policy(1)
+    h.set_gemm_tile(14)
+    assert h.pick_gemm_tile(1024, 2048, 64) == 14
+    assert h.gemm_workgroups(8192, 8192, 8192, 0, False, False) == 32 * 32
+    assert h.gemm_workgroups(512, 512, 64, 0, False, False) == 4       # K < 128 -> tile 4, same grid
+    with pytest.raises(Exception):
+        h.set_gemm_tile(15)
+    for bad in (-1, 4):
+        with pytest.raises(Exception):
+            h.set_w4_probe(bad)
+    h.set_w4_probe(0)

@@ -60,11 +60,13 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13])
+@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13, 14])
 def test_gemm_256_8phase_numerics_and_race_screen(tile):
     """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled), and the
     128x128 multi-stage kernels (11, 12: 3 / 4 LDS stages, counted vmcnt), and the 8-phase
-    schedule on a 256x128 block (13: unequal half-tile glds counts in the waits): every
+    schedule on a 256x128 block (13: unequal half-tile glds counts in the waits), and the 4-wave
+    kernel with AGPR-tied inline-asm MFMAs (14: 5-slot LDS ring, one barrier per K-tile; the
+    accumulator fences are what keep its bias / ReLU epilogue right): every
     K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
@@ -873,7 +875,7 @@ def test_xcd_dispatch_and_tile_orders_bit_exact():
         torch.testing.assert_close(tref, y + 1.5 * z)
         for gone in ("set_xcd_mask", "set_c_nontemporal", "set_triad_aux"):
             assert not hasattr(h, gone), gone
-        for bad in (14, 15, -1):                  # (tiles 11-13 exist since round 5)
+        for bad in (15, 16, -1):                  # (tiles 11-13 exist since round 5, 14 since round 6)
             with pytest.raises(Exception):
                 h.set_gemm_tile(bad)
     finally:

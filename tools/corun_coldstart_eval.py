@@ -60,10 +60,10 @@ def one(args):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--groups", default=os.path.join(ROOT, "profiles", "r03_corun_v2", "groups_2558_hostwait.json"))
+    ap.add_argument("--groups", default=os.path.join(ROOT, "profiles", "archive", "r03_corun_v2", "groups_2558_hostwait.json"))
     ap.add_argument("--jobs", type=int, default=6)
     ap.add_argument("--nfev", type=int, default=200)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04_coldstart", "loo.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "archive", "r04_coldstart", "loo.json"))
     ap.add_argument("--no-fill", action="store_true", help="cold start without the CU-fill scaling (round 4)")
     a = ap.parse_args()
     names = json.load(open(a.groups))["names"]

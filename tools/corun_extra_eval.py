@@ -43,7 +43,7 @@ def errors(model, groups, sel_fn):
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("groups")
-    ap.add_argument("--loo", default=os.path.join(ROOT, "profiles", "r04_coldstart", "loo.json"))
+    ap.add_argument("--loo", default=os.path.join(ROOT, "profiles", "archive", "r04_coldstart", "loo.json"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05_coldstart", "extra.json"))
     a = ap.parse_args(argv)
     from k8s_gpu_scheduler_amd.models.coldstart import cu_fill, fill_betas, mfma_share, with_workload
