@@ -896,8 +896,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
-    ap.add_argument("--gemm-policy", type=int, default=1, choices=list(range(10)),
-                    help="GEMM tile policy: 1 (default) 8-phase 256x256 also for co-running pods it fills, 0 128x128 for co-running pods")
+    ap.add_argument("--gemm-policy", type=int, default=1, choices=list(range(11)),
+                    help="GEMM tile policy: 1 (default) 8-phase 256x256 also for co-running pods it fills, 0 128x128 for "
+                         "co-running pods, 10 the 4-wave 256x256 kernel (tile 14) where 1 takes the 8-phase one")
     ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],
                     help="GEMM epilogue (A/B knob): 1 LDS-staged 16-B row stores, 0 scattered 8-B stores")
     ap.add_argument("--launch", default="auto", choices=["auto", "spawn", "inline"],

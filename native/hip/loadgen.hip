@@ -1172,7 +1172,7 @@ static int g_gemm_policy = 1;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 9) throw std::runtime_error("gemm policy must be 0..9");
+  if (p < 0 || p > 10) throw std::runtime_error("gemm policy must be 0..10");
   g_gemm_policy = p;
 }
 
@@ -1201,6 +1201,11 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   const int per_cu = alone ? 2 : 1;
   const bool fits256 = (M % 256 == 0) && (N % 256 == 0) && (M / 256) * (N / 256) >= budget;
   if (alone && fits256) return g_gemm_policy == 2 ? 4 : 10;
+  // 10 (A/B arm, round 6): such co-running GEMMs on the 4-wave kernel (tile 14) -- one wave per
+  // SIMD at 416 registers and no LDS left over, so up to three 32-VGPR stream waves of the other
+  // pods fit on each of its SIMDs, where the 8-phase kernel's two 240-register waves leave room
+  // for one
+  if (!alone && fits256 && g_gemm_policy == 10) return 14;
   if (!alone && fits256 && g_gemm_policy >= 1) return 10;
   // 3 / 4 (A/B arms): a co-running GEMM too small for one 256x256 tile per CU of its share
   // takes 256x128 (8 waves, 2 / 3 LDS stages) when that still gives every CU of the share a
@@ -1369,7 +1374,11 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
       break;
     }
     case 14: {
-      if (!wide_ok(Cp, ldc)) throw std::runtime_error("gemm tile 14: C rows must be 16-byte aligned");
+      if (!wide_ok(Cp, ldc)) {
+        if (g_gemm_tile == 14) throw std::runtime_error("gemm tile 14: C rows must be 16-byte aligned");
+        launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, dim3((M / 256) * (N / 256)), dim3(512), false);
+        break;                                      // policy 10 on an unaligned C: the 8-phase kernel
+      }
       if ((size_t)256 * std::max(lda, ldb) * 2 >= ((size_t)1 << 31))
         throw std::runtime_error("gemm tile 14: a 256-row operand block must span < 2 GiB");
       const dim3 grid((M / 256) * (N / 256)), block(256);

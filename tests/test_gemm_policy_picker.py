@@ -12,7 +12,7 @@ h = _native.hip(required=False)
 pytestmark = pytest.mark.skipif(h is None, reason="HIP extension not built")
 
 # policy -> tile for M=1024, N=2048 at a 64-CU budget
-SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1, 9: 1}
+SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1, 9: 1, 10: 1}
 
 
 @pytest.fixture(autouse=True)
@@ -28,11 +28,12 @@ def test_small_corun_gemm_tile_per_policy(policy):
     assert h.pick_gemm_tile(1024, 2048, 64) == SMALL[policy]
 
 
-@pytest.mark.parametrize("policy", range(10))
+@pytest.mark.parametrize("policy", range(11))
 def test_large_corun_and_lone_gemm_tiles(policy):
     h.set_gemm_policy(policy)
-    # enough 256x256 tiles for the share: the 8-phase kernel for every policy but 0
-    assert h.pick_gemm_tile(4096, 4096, 64) == (1 if policy == 0 else 10)
+    # enough 256x256 tiles for the share: the 8-phase kernel for every policy but 0 (128x128) and
+    # 10 (the 4-wave kernel)
+    assert h.pick_gemm_tile(4096, 4096, 64) == {0: 1, 10: 14}.get(policy, 10)
     # a lone GEMM that fills the chip: tile 4 under policy 2, else the 8-phase kernel
     assert h.pick_gemm_tile(8192, 8192, 0) == (4 if policy == 2 else 10)
 
@@ -75,14 +76,18 @@ def test_python_default_tile_rule_matches_the_native_picker():
 
 
 def test_four_wave_study_tile_is_forced_only():
-    """Tile 14 (the 4-wave 256 x 256 kernel of the round-6 lone-GEMM study) runs only when forced:
-    no policy picks it on any shape / budget, it launches one 256-thread block per 256 x 256 tile,
-    falls back to tile 4 below two K-tiles, and its timing probes are range-checked."""
+    """Tile 14 (the 4-wave 256 x 256 kernel of the round-6 lone-GEMM study) runs only when forced or
+    under the co-run arm 10: no other policy picks it on any shape / budget, it launches one
+    256-thread block per 256 x 256 tile, falls back to tile 4 below two K-tiles, and its timing
+    probes are range-checked."""
     for policy in range(10):
         h.set_gemm_policy(policy)
         for M, N in [(1024, 2048), (4096, 4096), (8192, 8192), (2048, 1024)]:
             for budget in (0, 32, 64, 128):
                 assert h.pick_gemm_tile(M, N, budget) != 14
+    h.set_gemm_policy(10)
+    assert h.pick_gemm_tile(8192, 8192, 0) == 10               # arm 10 leaves lone GEMMs alone
+    assert h.gemm_workgroups(4096, 4096, 1024, 64, False, False) == 256
     h.set_gemm_policy(1)
     h.set_gemm_tile(14)
     assert h.pick_gemm_tile(1024, 2048, 64) == 14
