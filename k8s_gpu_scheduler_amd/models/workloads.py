@@ -166,7 +166,8 @@ _TILE = {1: (128, 128), 2: (64, 128), 3: (64, 64), 4: (256, 256), 10: (256, 256)
 
 def default_gemm_workgroups(M: int, N: int, K: int, cu_budget: int = 0, fp8: bool = False) -> int:
     """Workgroups the native GEMM launches for this shape under the DEFAULT kernel policy
-    (policy 1, no forced tile, split-K off) -- a pure-Python copy of pick_gemm_tile /
+    (policy 10, or 1: the same grids -- tile 14 launches tile 10's; no forced tile, split-K off)
+    -- a pure-Python copy of pick_gemm_tile /
     resolve_gemm_tile / fp8_tile_128 (native/hip/loadgen.hip), so the CU-fill feature needs no
     HIP build and never reads the process-wide tile settings.  Pinned against the
     native picker in tests/test_gemm_policy_picker.py."""

@@ -896,9 +896,12 @@ def build_parser() -> argparse.ArgumentParser:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
-    ap.add_argument("--gemm-policy", type=int, default=1, choices=list(range(11)),
-                    help="GEMM tile policy: 1 (default) 8-phase 256x256 also for co-running pods it fills, 0 128x128 for "
-                         "co-running pods, 10 the 4-wave 256x256 kernel (tile 14) where 1 takes the 8-phase one")
+    ap.add_argument("--gemm-policy", type=int, default=10, choices=list(range(11)),
+                    help="GEMM tile policy: 10 (default since round 6) the 4-wave 256x256 kernel (tile 14) for "
+                         "co-running GEMMs that fill their share with 256x256 tiles; 1 the 8-phase kernel there "
+                         "(the round 2-5 default); 0 128x128 for co-running pods")
+    ap.add_argument("--w4-prio", type=int, default=0, choices=[0, 1],
+                    help="the 4-wave GEMM (tile 14, --gemm-policy 10) at s_setprio 1 throughout (A/B knob)")
     ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],
                     help="GEMM epilogue (A/B knob): 1 LDS-staged 16-B row stores, 0 scattered 8-B stores")
     ap.add_argument("--launch", default="auto", choices=["auto", "spawn", "inline"],
@@ -944,6 +947,7 @@ def gpu_executor(a: Any, dev_idx: int = 0) -> Any:
     from .. import _native
     h = _native.hip(required=True)
     h.set_gemm_policy(a.gemm_policy)
+    h.set_w4_prio(a.w4_prio)
     h.set_wide_epilogue(a.wide_epilogue)
     h.set_xcd_blocks(a.xcd_blocks)
     h.set_xcd_group(a.xcd_group)

@@ -33,6 +33,7 @@ void stream_triad(uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n_float
 void set_triad_variant(int v);
 void set_gemm_tile(int t);
 void set_w4_probe(int mask);
+void set_w4_prio(int on);
 void set_gemm_policy(int p);
 void set_wide_epilogue(int on);
 void set_xcd_blocks(int on);

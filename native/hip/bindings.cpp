@@ -64,6 +64,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_triad_variant", &gs::set_triad_variant, py::arg("variant"));
   m.def("set_gemm_tile", &gs::set_gemm_tile, py::arg("tile"));
   m.def("set_w4_probe", &gs::set_w4_probe, py::arg("mask"));
+  m.def("set_w4_prio", &gs::set_w4_prio, py::arg("on"));
   m.def("set_gemm_policy", &gs::set_gemm_policy, py::arg("policy"));
   m.def("set_wide_epilogue", &gs::set_wide_epilogue, py::arg("on"));
   m.def("set_xcd_blocks", &gs::set_xcd_blocks, py::arg("on"));

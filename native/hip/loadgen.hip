@@ -783,7 +783,9 @@ __device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[8][8]) {
 // The barrier certifies for every wave that A_{t+1} / B_{t+1} landed (RAW for h1's reads) and
 // that every read of A_t and B_{t-1} retired (WAR for the next two glds groups), so one barrier
 // per 128 MFMAs suffices.
-template <bool RELU, bool BIAS, int PROBE = 0>
+// PRIO (A/B arm, set_w4_prio): the waves run at s_setprio 1 from start to end, ahead of co-resident
+// stream waves of other pods in the SIMD's issue arbitration.
+template <bool RELU, bool BIAS, int PROBE = 0, bool PRIO = false>
 __global__ void __launch_bounds__(256, 1)
 gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                      const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
@@ -806,6 +808,7 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   agpr_after_init(acc);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
   bf16x8 fa[2][8], fb[2][8];
   const int T = K / KT;                             // >= 2
 
@@ -1162,7 +1165,10 @@ static const int kTileBN[15] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 2
 // in round 1, with the older kernels, it had been even: profiles/r01_gemm_policy_ab.txt).
 // 0 = co-running pods always take the 128x128 / 2-per-CU picker.  2 = tile 4 instead of tile
 // 10 for lone GEMMs.
-static int g_gemm_policy = 1;
+// Default 10 since round 6: arm 1's tiles, except co-running GEMMs the 256x256 tile fills run the
+// 4-wave kernel (tile 14) -- 606.3 vs 596.4 pods/s, SLOs 61.8 vs 59.0 % over 5 interleaved bench
+// rounds on MI355X (600.6 vs 587.1 over 3 on another box; profiles/r06_w4corun/).
+static int g_gemm_policy = 10;
 // split-K for lone GEMMs whose 256x256 tiles leave CUs idle: -1 = auto (up to 8 slices), 0 = off,
 // 2..8 = at most that many slices.  Off by default: on the tall-K 2048x4096x8192 the split
 // kernel itself runs at ~1540 TF, but the fp32 partials + reduce pass (~144 MB of traffic) put
@@ -1177,6 +1183,8 @@ void set_gemm_policy(int p) {
 }
 
 static int g_w4_probe = 0;
+static int g_w4_prio = 0;
+void set_w4_prio(int on) { g_w4_prio = on ? 1 : 0; }
 void set_w4_probe(int mask) {
   if (mask < 0 || mask > 3) throw std::runtime_error("w4 probe must be 0..3");
   g_w4_probe = mask;
@@ -1388,6 +1396,9 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
       if (g_w4_probe)   // timing probes: steady-loop LDS-DMA (1), reads (2) or both (3) dropped
         k = g_w4_probe == 1 ? gemm_bf16_nt_256_w4l<false, false, 1>
             : g_w4_probe == 2 ? gemm_bf16_nt_256_w4l<false, false, 2> : gemm_bf16_nt_256_w4l<false, false, 3>;
+      else if (g_w4_prio)
+        k = relu ? (bp ? gemm_bf16_nt_256_w4l<true, true, 0, true> : gemm_bf16_nt_256_w4l<true, false, 0, true>)
+                 : (bp ? gemm_bf16_nt_256_w4l<false, true, 0, true> : gemm_bf16_nt_256_w4l<false, false, 0, true>);
       else
         k = relu ? (bp ? gemm_bf16_nt_256_w4l<true, true> : gemm_bf16_nt_256_w4l<true, false>)
                  : (bp ? gemm_bf16_nt_256_w4l<false, true> : gemm_bf16_nt_256_w4l<false, false>);

@@ -18,7 +18,7 @@ SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1, 9: 1, 10: 1}
 @pytest.fixture(autouse=True)
 def _restore():
     yield
-    h.set_gemm_policy(1)
+    h.set_gemm_policy(10)                                      # the default since round 6
     h.set_gemm_tile(0)
 
 
@@ -65,14 +65,15 @@ def test_python_default_tile_rule_matches_the_native_picker():
     policy) against the native picker on every catalog / extra GEMM at the bench's share, a lone
     launch and a half share."""
     from k8s_gpu_scheduler_amd.models import workloads as W
-    h.set_gemm_policy(1)
     shapes = {(o.M, o.N, o.K, o.kind == "gemm8") for w in list(W.CATALOG.values()) + list(W.EXTRA.values())
               for o in w.ops if o.is_gemm}
     shapes |= {(256, 256, 64, False), (192, 320, 256, False), (8192, 8192, 8192, False), (640, 384, 128, False)}
-    for M, N, K, fp8 in sorted(shapes):
-        for budget in (0, 64, 128, 32):
-            assert W.default_gemm_workgroups(M, N, K, budget, fp8) == h.gemm_workgroups(M, N, K, budget, fp8), \
-                (M, N, K, budget, fp8)
+    for policy in (10, 1):                                     # tile 14 launches tile 10's grid
+        h.set_gemm_policy(policy)
+        for M, N, K, fp8 in sorted(shapes):
+            for budget in (0, 64, 128, 32):
+                assert W.default_gemm_workgroups(M, N, K, budget, fp8) == h.gemm_workgroups(M, N, K, budget, fp8), \
+                    (policy, M, N, K, budget, fp8)
 
 
 def test_four_wave_study_tile_is_forced_only():
@@ -99,3 +100,9 @@ def test_four_wave_study_tile_is_forced_only():
         with pytest.raises(Exception):
             h.set_w4_probe(bad)
     h.set_w4_probe(0)
+
+
+def test_default_policy_is_the_four_wave_corun_arm():
+    h.set_gemm_tile(0)
+    h.set_gemm_policy(10)
+    assert h.pick_gemm_tile(4096, 4096, 64) == 14 and h.pick_gemm_tile(8192, 8192, 0) == 10

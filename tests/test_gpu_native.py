@@ -154,7 +154,7 @@ def test_gemm_corun_split_k_policy8_matches_fp32_reference(hip, M, N, K, relu, b
             loadgen.gemm(a, bt, out=out, bias=b, relu=relu, cu_budget=64)
             assert (out.float() - ref).abs().max().item() <= tol
     finally:
-        hip.set_gemm_policy(1)
+        hip.set_gemm_policy(10)
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (2048, 2560, 1536), (4096, 2048, 1024)])
@@ -178,7 +178,42 @@ def test_gemm_share_capped_policy9_matches_fp32_reference(hip, M, N, K):
             loadgen.gemm(a, bt, out=out, bias=b, relu=True, cu_budget=64)
             assert (out.float() - ref).abs().max().item() <= tol
     finally:
-        hip.set_gemm_policy(1)
+        hip.set_gemm_policy(10)
+
+
+@pytest.mark.parametrize("prio", [0, 1])
+def test_gemm_corun_policy10_four_wave_matches_fp32_reference(hip, prio):
+    """Arm 10: a co-running pod's GEMM that fills its share with 256 x 256 tiles runs the 4-wave
+    kernel (tile 14), in the XCD-block tile order, with and without whole-kernel priority; the
+    unaligned-C fallback takes the 8-phase kernel (fp32 PyTorch reference, repeated runs)."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    hip.set_gemm_policy(10)
+    hip.set_w4_prio(prio)
+    try:
+        for M, N, K in [(4096, 4096, 1024), (2048, 2560, 2560), (8192, 2048, 192)]:
+            assert hip.pick_gemm_tile(M, N, 64) == 14
+            g = torch.Generator(device="cuda").manual_seed(M + 5 * N + K + prio)
+            a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+            bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+            b = torch.randn(N, device="cuda", generator=g)
+            ref = torch.relu(a.float() @ bt.float().T + b)
+            tol = 0.01 * ref.abs().max().item() + 1e-2
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            for _ in range(3):
+                out.fill_(float("nan"))
+                loadgen.gemm(a, bt, out=out, bias=b, relu=True, cu_budget=64)
+                assert (out.float() - ref).abs().max().item() <= tol, (M, N, K)
+        # C rows 8-B but not 16-B aligned: the 8-phase kernel instead (a forced tile 14 would raise)
+        M, N, K = 1024, 1024, 512
+        a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+        wide = torch.empty(M, N + 4, device="cuda", dtype=torch.bfloat16)
+        out = wide[:, 4:]
+        loadgen.gemm(a, bt, out=out, cu_budget=64)
+        torch.testing.assert_close(out.float(), a.float() @ bt.float().T, atol=0.1, rtol=0.02)
+    finally:
+        hip.set_w4_prio(0)
+        hip.set_gemm_policy(10)
 
 
 @pytest.mark.parametrize("slice_", [0, 1])
