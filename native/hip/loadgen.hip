@@ -753,17 +753,20 @@ __device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& b, const bf1
 // asm that "modifies" every accumulator keeps the compiler's own accumulator accesses on their
 // side of it (volatile asm statements keep their order).  agpr_after_init: after the zero-fill,
 // before the first MFMA; agpr_before_read: after the last MFMA, before the epilogue reads.
-__device__ __forceinline__ void agpr_fence(f32x4 (&acc)[8][8]) {
+template <int NI, int NJ>
+__device__ __forceinline__ void agpr_fence(f32x4 (&acc)[NI][NJ]) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
 }
-__device__ __forceinline__ void agpr_after_init(f32x4 (&acc)[8][8]) {
+template <int NI, int NJ>
+__device__ __forceinline__ void agpr_after_init(f32x4 (&acc)[NI][NJ]) {
   agpr_fence(acc);
   asm volatile("s_nop 7" ::: "memory");
 }
-__device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[8][8]) {
+template <int NI, int NJ>
+__device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[NI][NJ]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   agpr_fence(acc);
 }
@@ -785,31 +788,35 @@ __device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[8][8]) {
 // per 128 MFMAs suffices.
 // PRIO (A/B arm, set_w4_prio): the waves run at s_setprio 1 from start to end, ahead of co-resident
 // stream waves of other pods in the SIMD's issue arbitration.
-template <bool RELU, bool BIAS, int PROBE = 0, bool PRIO = false>
+template <bool RELU, bool BIAS, int PROBE = 0, bool PRIO = false, int BN = 256>
 __global__ void __launch_bounds__(256, 1)
 gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                      const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
+  static_assert(BN == 256 || BN == 128, "4-wave block tile is 256 x 256 or 256 x 128");
   constexpr int KT = 64, NSLOT = 5;
-  constexpr int SLOT = 256 * KT * 2;               // one operand tile: 32 KiB
-  constexpr int G = SLOT / 16 / 256;               // glds per thread per operand tile (8)
+  constexpr int SLOT = 256 * KT * 2;               // one ring slot: a 256-row operand tile, 32 KiB
+  constexpr int GA = SLOT / 16 / 256;              // glds per thread for an A tile (8)
+  constexpr int GB = BN * KT * 2 / 16 / 256;       // ... for a B tile (8 or 4)
+  constexpr int NJ = BN / 32;                      // 16-column fragments per wave (wave tile 128 x BN/2)
+  constexpr int NG = 2 * NJ;                       // groups of 4 MFMAs per half
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
 
   int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, M / 256, N / 256, xmap, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
+  tile_coords(blockIdx.x, gridDim.x, M / 256, N / BN, xmap, tm, tn);
+  const int m0 = tm * 256, n0 = tn * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x & (kWave - 1);
   const int wr = wave >> 1, wc = wave & 1;
   const int frow = lane & 15, fk = lane >> 4;
 
-  f32x4 acc[8][8];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   agpr_after_init(acc);
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-  bf16x8 fa[2][8], fb[2][8];
+  bf16x8 fa[2][8], fb[2][NJ];
   const int T = K / KT;                             // >= 2
 
   // piece q of operand tile X_u (B if isb): rows (q * 256 + wave * 64 + lane) >> 3, 8 per
@@ -820,7 +827,7 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   const int rr = (wave * 64 + lane) >> 3, kq = ((wave * 64 + lane) & 7) ^ ((rr >> 1) & 7);
   const int voA = rr * lda * 2 + kq * 16, voB = rr * ldb * 2 + kq * 16;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
-  const auto rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(Bt + (size_t)n0 * ldb), 0, 256 * ldb * 2, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(Bt + (size_t)n0 * ldb), 0, BN * ldb * 2, 0x00020000);
   auto glds = [&](int u, bool isb, int q) {
     char* dst = smem + ((2 * u + (isb ? 1 : 0)) % NSLOT) * SLOT + (q * 256 + wave * 64) * 16;
     const int so = q * 32 * (isb ? ldb : lda) * 2 + u * KT * 2;
@@ -836,20 +843,22 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   // prologue: A_0 B_0 A_1 B_1 in flight; wait for A_0 / B_0; k-step 0 of K-tile 0 into set 0
 #pragma unroll
   for (int u = 0; u < 2; ++u)
+  {
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int q = 0; q < GA; ++q) glds(u, false, q);
 #pragma unroll
-      for (int q = 0; q < G; ++q) glds(u, x == 1, q);
-  wait_vmcnt<2 * G>();
+    for (int q = 0; q < GB; ++q) glds(u, true, q);
+  }
+  wait_vmcnt<GA + GB>();
   barrier();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    fa[0][q] = lds_frag<KT>(smem, wr * 128 + q * 16 + frow, fk);
-    fb[0][q] = lds_frag<KT>(smem + SLOT, wc * 128 + q * 16 + frow, fk);
-  }
+  for (int q = 0; q < 8; ++q) fa[0][q] = lds_frag<KT>(smem, wr * 128 + q * 16 + frow, fk);
+#pragma unroll
+  for (int q = 0; q < NJ; ++q) fb[0][q] = lds_frag<KT>(smem + SLOT, wc * (BN / 2) + q * 16 + frow, fk);
 
-  // one half: 64 MFMAs on set S (k-step S of K-tile t); reads of (RU, k-step S^1) into set S^1
-  // when RD, one per 4 MFMAs; glds of operand tile (t+2, X = S) when ST, one per 8 MFMAs (other
+  // one half: 8 x NJ MFMAs on set S (k-step S of K-tile t) in NG groups of 4; the 8 + NJ reads of
+  // (RU, k-step S^1) into set S^1 when RD, spread evenly (BN = 256: one per group); the glds of
+  // operand tile (t+2, X = S) when ST, spread evenly (BN = 256: every second group; other
   // placements -- the glds in the odd groups, reads and glds in separate halves -- measured
   // 1-2 % slower, profiles/r06_lone_gemm/)
   auto half = [&](auto sc, auto rdc, auto stc, int t) {
@@ -858,19 +867,26 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     const int ru = S == 0 ? t : t + 1;             // h0 reads k-step 1 of t, h1 k-step 0 of t+1
     const char* ta = slot(ru, false);
     const char* tb = slot(ru, true);
+    constexpr int NR = 8 + NJ, NS = S == 0 ? GA : GB;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const int i = (g * 4 + m) >> 3, j = (g * 4 + m) & 7;
+        const int i = (g * 4 + m) / NJ, j = (g * 4 + m) % NJ;
         mfma_agpr(acc[i][j], fb[S][j], fa[S][i]);
       }
       if constexpr (RD) {
-        if (g < 8) fa[S ^ 1][g] = lds_frag<KT>(ta, wr * 128 + g * 16 + frow, (S ^ 1) * 4 + fk);
-        else fb[S ^ 1][g - 8] = lds_frag<KT>(tb, wc * 128 + (g - 8) * 16 + frow, (S ^ 1) * 4 + fk);
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          if (q * NG / NR != g) continue;
+          if (q < 8) fa[S ^ 1][q] = lds_frag<KT>(ta, wr * 128 + q * 16 + frow, (S ^ 1) * 4 + fk);
+          else fb[S ^ 1][q - 8] = lds_frag<KT>(tb, wc * (BN / 2) + (q - 8) * 16 + frow, (S ^ 1) * 4 + fk);
+        }
       }
       if constexpr (ST) {
-        if ((g & 1) == 0) glds(t + 2, S == 1, g >> 1);
+#pragma unroll
+        for (int p = 0; p < NS; ++p)
+          if (p * NG / NS == g) glds(t + 2, S == 1, p);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -882,7 +898,7 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using IG = std::integral_constant<int, G>;
+  using IG = std::integral_constant<int, GA>;      // A_{t+2} (staged in h0) may fly at the sync
   using Y = std::true_type;
   using F = std::false_type;
   // PROBE (timing study only): bit 0 drops the steady loop's glds, bit 1 its reads (wrong results)
@@ -907,8 +923,8 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   barrier();
 
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = wc * 128 + j * 16 + fk * 4;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = wc * (BN / 2) + j * 16 + fk * 4;
     f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
     if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
 #pragma unroll
@@ -917,11 +933,11 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
-      wide_put<256>(smem, wr * 128 + i * 16 + frow, col, o);
+      wide_put<BN>(smem, wr * 128 + i * 16 + frow, col, o);
     }
   }
   __syncthreads();
-  wide_store<256, 256, 256>(smem, C, ldc, m0, n0);
+  wide_store<256, BN, 256>(smem, C, ldc, m0, n0);
 }
 
 // C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
@@ -1150,11 +1166,12 @@ static int g_gemm_tile = 0;
 // 13 = 256x128 8-phase (gemm_bf16_nt_256_8ph<..., BN = 128>, peeled + wide epilogue; K >= 128)
 // 14 = 256x256 on 4 waves of 128x128 with AGPR-tied inline-asm MFMAs, 64-deep operand tiles in a
 // 5-slot LDS ring (gemm_bf16_nt_256_w4l).  Forced only (K >= 128, C rows 16-B aligned): the
-// lone-GEMM study of profiles/r06_lone_gemm/, level with tile 10.  (Also measured there and
+// lone-GEMM study of profiles/r06_lone_gemm/, level with tile 10; the co-run default since
+// round 6, policy 10).  15 = the same kernel on a 256x128 block (wave tile 128 x 64; policy 11).  (Also measured there and
 // removed: 32-deep sub-tiles in 4 slots with one barrier per 32 or per 64 k, and register-staged
 // global loads -- 5-15 % behind.)
-static const int kTileBM[15] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256, 256};
-static const int kTileBN[15] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128, 256};
+static const int kTileBM[16] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256, 256, 256};
+static const int kTileBN[16] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128, 256, 128};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -1178,7 +1195,7 @@ static int g_gemm_policy = 10;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 10) throw std::runtime_error("gemm policy must be 0..10");
+  if (p < 0 || p > 11) throw std::runtime_error("gemm policy must be 0..11");
   g_gemm_policy = p;
 }
 
@@ -1191,7 +1208,7 @@ void set_w4_probe(int mask) {
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 14) throw std::runtime_error("gemm tile must be 0..14");
+  if (t < 0 || t > 15) throw std::runtime_error("gemm tile must be 0..15");
   g_gemm_tile = t;
 }
 
@@ -1213,7 +1230,10 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // SIMD at 416 registers and no LDS left over, so up to three 32-VGPR stream waves of the other
   // pods fit on each of its SIMDs, where the 8-phase kernel's two 240-register waves leave room
   // for one
-  if (!alone && fits256 && g_gemm_policy == 10) return 14;
+  if (!alone && fits256 && (g_gemm_policy == 10 || g_gemm_policy == 11)) return 14;
+  // 11 (A/B arm): arm 10, and a co-running GEMM too small for that but filling its share with
+  // 256 x 128 blocks on the same 4-wave kernel (tile 15) instead of the 128 x 128 tile
+  if (!alone && g_gemm_policy == 11 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget) return 15;
   if (!alone && fits256 && g_gemm_policy >= 1) return 10;
   // 3 / 4 (A/B arms): a co-running GEMM too small for one 256x256 tile per CU of its share
   // takes 256x128 (8 waves, 2 / 3 LDS stages) when that still gives every CU of the share a
@@ -1289,6 +1309,7 @@ static int resolve_gemm_tile(int M, int N, int K, int cu_budget) {
   if ((t == 9 || t == 10) && K < 128) t = 4;     // the 8-phase prologue stages two K-tiles
   if (t == 13 && K < 128) t = 5;
   if (t == 14 && K < 128) t = 4;
+  if (t == 15 && K < 128) t = 5;
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked by the caller)
   return t;
 }
@@ -1381,19 +1402,27 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
       launch_8ph<true, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, grid, block, lone);
       break;
     }
-    case 14: {
+    case 14:
+    case 15: {
       if (!wide_ok(Cp, ldc)) {
-        if (g_gemm_tile == 14) throw std::runtime_error("gemm tile 14: C rows must be 16-byte aligned");
-        launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, dim3((M / 256) * (N / 256)), dim3(512), false);
-        break;                                      // policy 10 on an unaligned C: the 8-phase kernel
+        if (g_gemm_tile == t) throw std::runtime_error("gemm tiles 14 / 15: C rows must be 16-byte aligned");
+        if (t == 14)                                // a policy on an unaligned C: the 8-phase kernels
+          launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, dim3((M / 256) * (N / 256)), dim3(512), false);
+        else
+          launch_8ph<true, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, dim3((M / 256) * (N / 128)), dim3(512), false);
+        break;
       }
       if ((size_t)256 * std::max(lda, ldb) * 2 >= ((size_t)1 << 31))
-        throw std::runtime_error("gemm tile 14: a 256-row operand block must span < 2 GiB");
-      const dim3 grid((M / 256) * (N / 256)), block(256);
+        throw std::runtime_error("gemm tiles 14 / 15: a 256-row operand block must span < 2 GiB");
+      const int bn = t == 14 ? 256 : 128;
+      const dim3 grid((M / 256) * (N / bn)), block(256);
       const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
-      const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / 256);
+      const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / bn);
       decltype(&gemm_bf16_nt_256_w4l<false, false>) k;
-      if (g_w4_probe)   // timing probes: steady-loop LDS-DMA (1), reads (2) or both (3) dropped
+      if (t == 15)
+        k = relu ? (bp ? gemm_bf16_nt_256_w4l<true, true, 0, false, 128> : gemm_bf16_nt_256_w4l<true, false, 0, false, 128>)
+                 : (bp ? gemm_bf16_nt_256_w4l<false, true, 0, false, 128> : gemm_bf16_nt_256_w4l<false, false, 0, false, 128>);
+      else if (g_w4_probe)   // timing probes: steady-loop LDS-DMA (1), reads (2) or both (3) dropped
         k = g_w4_probe == 1 ? gemm_bf16_nt_256_w4l<false, false, 1>
             : g_w4_probe == 2 ? gemm_bf16_nt_256_w4l<false, false, 2> : gemm_bf16_nt_256_w4l<false, false, 3>;
       else if (g_w4_prio)

@@ -60,13 +60,14 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13, 14, 15])
 def test_gemm_256_8phase_numerics_and_race_screen(tile):
     """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled), and the
     128x128 multi-stage kernels (11, 12: 3 / 4 LDS stages, counted vmcnt), and the 8-phase
     schedule on a 256x128 block (13: unequal half-tile glds counts in the waits), and the 4-wave
     kernel with AGPR-tied inline-asm MFMAs (14: 5-slot LDS ring, one barrier per K-tile; the
-    accumulator fences are what keep its bias / ReLU epilogue right): every
+    accumulator fences are what keep its bias / ReLU epilogue right; 15: the same on a 256 x 128
+    block, unequal A / B glds counts): every
     K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
@@ -177,6 +178,29 @@ def test_gemm_share_capped_policy9_matches_fp32_reference(hip, M, N, K):
             out.fill_(float("nan"))
             loadgen.gemm(a, bt, out=out, bias=b, relu=True, cu_budget=64)
             assert (out.float() - ref).abs().max().item() <= tol
+    finally:
+        hip.set_gemm_policy(10)
+
+
+def test_gemm_corun_policy11_256x128_four_wave_matches_fp32_reference(hip):
+    """Arm 11: arm 10, plus co-running GEMMs that fill their share only with 256 x 128 blocks on
+    the 4-wave kernel (tile 15) -- fp32 PyTorch reference, repeated runs."""
+    from k8s_gpu_scheduler_amd.ops import loadgen
+    hip.set_gemm_policy(11)
+    try:
+        for M, N, K, tile in [(1024, 2048, 1024, 15), (1024, 2560, 2560, 15), (4096, 4096, 512, 14)]:
+            assert hip.pick_gemm_tile(M, N, 64) == tile
+            g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+            a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+            bt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+            b = torch.randn(N, device="cuda", generator=g)
+            ref = torch.relu(a.float() @ bt.float().T + b)
+            tol = 0.01 * ref.abs().max().item() + 1e-2
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            for _ in range(3):
+                out.fill_(float("nan"))
+                loadgen.gemm(a, bt, out=out, bias=b, relu=True, cu_budget=64)
+                assert (out.float() - ref).abs().max().item() <= tol, (M, N, K)
     finally:
         hip.set_gemm_policy(10)
 
