@@ -809,14 +809,24 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   const int wr = wave >> 1, wc = wave & 1;
   const int frow = lane & 15, fk = lane >> 4;
 
+  // the accumulators start at the bias (D = C^T layout: 4 consecutive columns per lane), so the
+  // epilogue holds no bias registers (at BN = 256 that kept the kernel at 148 VGPRs instead of 129)
   f32x4 acc[8][NJ];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int j = 0; j < NJ; ++j) {
+    f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BIAS) b0 = *reinterpret_cast<const f32x4*>(bias + n0 + wc * (BN / 2) + j * 16 + fk * 4);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 8; ++i) acc[i][j] = b0;
+  }
   agpr_after_init(acc);
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-  bf16x8 fa[2][8], fb[2][NJ];
+  // BN = 256: one A fragment set.  The MFMAs run row by row, so A fragment i is dead after row i
+  // and the next k-step's fragment i is read into the same registers right behind it; B keeps two
+  // sets.  96 fragment VGPRs instead of 128 put the kernel at 384 registers, so three 38-VGPR
+  // stream waves of other pods fit beside each of its waves instead of two.
+  constexpr bool SINGLE_A = NJ == 8;
+  bf16x8 fa[SINGLE_A ? 1 : 2][8], fb[2][NJ];
   const int T = K / KT;                             // >= 2
 
   // piece q of operand tile X_u (B if isb): rows (q * 256 + wave * 64 + lane) >> 3, 8 per
@@ -868,14 +878,18 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     const char* ta = slot(ru, false);
     const char* tb = slot(ru, true);
     constexpr int NR = 8 + NJ, NS = S == 0 ? GA : GB;
+    constexpr int SA = SINGLE_A ? 0 : S;           // A set in use
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int i = (g * 4 + m) / NJ, j = (g * 4 + m) % NJ;
-        mfma_agpr(acc[i][j], fb[S][j], fa[S][i]);
+        mfma_agpr(acc[i][j], fb[S][j], fa[SA][i]);
       }
-      if constexpr (RD) {
+      if constexpr (RD && SINGLE_A) {              // row g/2 done: its next A fragment; B at even groups
+        if (g & 1) fa[0][g >> 1] = lds_frag<KT>(ta, wr * 128 + (g >> 1) * 16 + frow, (S ^ 1) * 4 + fk);
+        else fb[S ^ 1][g >> 1] = lds_frag<KT>(tb, wc * (BN / 2) + (g >> 1) * 16 + frow, (S ^ 1) * 4 + fk);
+      } else if constexpr (RD) {
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
           if (q * NG / NR != g) continue;
@@ -925,11 +939,9 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = wc * (BN / 2) + j * 16 + fk * 4;
-    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (BIAS) bv = *reinterpret_cast<const f32x4*>(bias + n0 + col);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      f32x4 v = acc[i][j] + bv;
+      const f32x4 v = acc[i][j];
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);

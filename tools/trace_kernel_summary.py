@@ -24,6 +24,8 @@ MARKER = "xcd_probe_kernel"
 def family(name: str) -> str:
     if "256_8ph" in name:
         return "gemm_256x256_8phase"
+    if "256_w4l" in name:
+        return "gemm_256x128_4wave" if name.split("(")[0].rstrip(">").endswith("128") else "gemm_256x256_4wave"
     if "gemm_bf16_nt_kernel" in name:
         return "gemm_tile_" + name.split("<", 1)[1].split(",")[0].strip() + "x" + name.split(",")[1].strip()
     if "gemm_fp8" in name:
