@@ -1179,7 +1179,9 @@ static int g_gemm_tile = 0;
 // 14 = 256x256 on 4 waves of 128x128 with AGPR-tied inline-asm MFMAs, 64-deep operand tiles in a
 // 5-slot LDS ring (gemm_bf16_nt_256_w4l).  Forced only (K >= 128, C rows 16-B aligned): the
 // lone-GEMM study of profiles/r06_lone_gemm/, level with tile 10; the co-run default since
-// round 6, policy 10).  15 = the same kernel on a 256x128 block (wave tile 128 x 64; policy 11).  (Also measured there and
+// round 6, policy 10).  15 = the same kernel on a 256x128 block (wave tile 128 x 64; policy 11).
+// (Also measured and removed: tile 14's schedule on v_mfma_f32_32x32x16_bf16 -- half the MFMA
+// instructions, exact, but 1,434 vs 1,483 TF/s at 8192^3, profiles/r06_lone_gemm/mfma32/.)  (Also measured there and
 // removed: 32-deep sub-tiles in 4 slots with one barrier per 32 or per 64 k, and register-staged
 // global loads -- 5-15 % behind.)
 static const int kTileBM[16] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256, 256, 256};
