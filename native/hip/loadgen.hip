@@ -1209,7 +1209,7 @@ static int g_gemm_policy = 10;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 11) throw std::runtime_error("gemm policy must be 0..11");
+  if (p < 0 || p > 12) throw std::runtime_error("gemm policy must be 0..12");
   g_gemm_policy = p;
 }
 
@@ -1245,6 +1245,9 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // pods fit on each of its SIMDs, where the 8-phase kernel's two 240-register waves leave room
   // for one
   if (!alone && fits256 && (g_gemm_policy == 10 || g_gemm_policy == 11)) return 14;
+  // 12 (A/B arm): every co-running GEMM the 256 x 256 tile divides on the 4-wave kernel, even with
+  // fewer tiles than its share's CUs (the other pods' stream waves take the rest)
+  if (!alone && g_gemm_policy == 12 && M % 256 == 0 && N % 256 == 0) return 14;
   // 11 (A/B arm): arm 10, and a co-running GEMM too small for that but filling its share with
   // 256 x 128 blocks on the same 4-wave kernel (tile 15) instead of the 128 x 128 tile
   if (!alone && g_gemm_policy == 11 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= budget) return 15;
