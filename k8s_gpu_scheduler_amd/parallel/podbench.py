@@ -105,6 +105,7 @@ class ControlPlane:
                  balance: float = 1.0, learn_interference: bool = True, plan_bursts: bool = False,
                  plan_tolerance: float = 0.05, plan_objective: str = "slo", complement: float = 0.0,
                  online_scale: bool = False, slo_objective: str = "terms", corun_model: Any = None,
+                 corun_model_path: str = "",
                  corun_margin: float = 0.0, corun_sigma: float = 0.0, plan_carry: float = 0.0,
                  plan_feedback: bool = True, plan_slots: Any = False, slot_spread_ms: float = 2.0,
                  slot_sigma: float = 0.2, adaptive: bool = False, effort: int = 0,
@@ -128,7 +129,7 @@ class ControlPlane:
         self.corun = None
         if slo_objective != "terms":
             from ..models.corun import CorunModel, OnlineCorun
-            base = corun_model or CorunModel.load()
+            base = corun_model or (CorunModel.load(corun_model_path) if corun_model_path else CorunModel.load())
             if base is not None:
                 self.predictions.install_corun(base)
             if base is not None and learn_corun:
@@ -823,6 +824,8 @@ def build_parser() -> argparse.ArgumentParser:
                          "Off by default: its first refit needs 256 observed pods (a refit on fewer made the model "
                          "worse on replayed bench timelines), which a 20-step N=1 run (80 pods) never reaches -- "
                          "the deployed recommender learns through ObserveCorun instead (agent/corun_observer.py)")
+    ap.add_argument("--corun-model", default="",
+                    help="co-run model file for the scheduler (default: the shipped data/corun_mi355x.json)")
     ap.add_argument("--corun-sigma", type=float, default=0.05,
                     help="co-run burst planner: expected SLOs met under the model's log error of this sigma "
                          "(held-out ~0.05, profiles/archive/r03_corun_v2/); 0 = hard predicted counts")
@@ -999,7 +1002,7 @@ def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
                      slot_spread_ms=a.slot_spread_ms, slot_sigma=a.slot_sigma,
                      adaptive=bool(a.cp_adaptive) and not a.sim, effort=a.plan_effort,
                      effort_down=a.cp_effort_down, effort_up=a.cp_effort_up, effort_target=a.cp_effort_target,
-                     learn_corun=bool(a.corun_learn),
+                     learn_corun=bool(a.corun_learn), corun_model_path=a.corun_model,
                      kernel_policy=a.kernel_policy, gc_settle=bool(a.gc_settle))
     cp: Any = None
     if rank == 0 and a.control_plane == "process":
