@@ -939,7 +939,7 @@ def test_xcd_dispatch_and_tile_orders_bit_exact():
         torch.testing.assert_close(tref, y + 1.5 * z)
         for gone in ("set_xcd_mask", "set_c_nontemporal", "set_triad_aux"):
             assert not hasattr(h, gone), gone
-        for bad in (15, 16, -1):                  # (tiles 11-13 exist since round 5, 14 since round 6)
+        for bad in (16, 17, -1):                  # (tiles 11-13 exist since round 5, 14-15 since round 6)
             with pytest.raises(Exception):
                 h.set_gemm_tile(bad)
     finally:
