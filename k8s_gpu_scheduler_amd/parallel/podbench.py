@@ -899,12 +899,13 @@ def build_parser() -> argparse.ArgumentParser:
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="epochs kept in flight per GPU before collecting (>= 1)")
-    ap.add_argument("--gemm-policy", type=int, default=10, choices=list(range(13)),
+    ap.add_argument("--gemm-policy", type=int, default=10, choices=list(range(14)),
                     help="GEMM tile policy: 10 (default since round 6) the 4-wave 256x256 kernel (tile 14) for "
                          "co-running GEMMs that fill their share with 256x256 tiles; 1 the 8-phase kernel there "
                          "(the round 2-5 default); 0 128x128 for co-running pods; 11 = 10 plus the 4-wave "
                          "kernel on 256x128 blocks for co-running GEMMs too small for 256x256; 12 the 4-wave "
-                         "kernel for every co-running GEMM 256x256 divides")
+                         "kernel for every co-running GEMM 256x256 divides; 13 = 10 plus the 4-wave kernel on "
+                         "128x128 blocks where 10 takes the 128x128 tile")
     ap.add_argument("--w4-prio", type=int, default=0, choices=[0, 1],
                     help="the 4-wave GEMM (tile 14, --gemm-policy 10) at s_setprio 1 throughout (A/B knob)")
     ap.add_argument("--wide-epilogue", type=int, default=1, choices=[0, 1],

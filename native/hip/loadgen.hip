@@ -788,22 +788,24 @@ __device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[NI][NJ]) {
 // per 128 MFMAs suffices.
 // PRIO (A/B arm, set_w4_prio): the waves run at s_setprio 1 from start to end, ahead of co-resident
 // stream waves of other pods in the SIMD's issue arbitration.
-template <bool RELU, bool BIAS, int PROBE = 0, bool PRIO = false, int BN = 256>
-__global__ void __launch_bounds__(256, 1)
+template <bool RELU, bool BIAS, int PROBE = 0, bool PRIO = false, int BN = 256, int BM = 256>
+__global__ void __launch_bounds__(256, BM == 128 ? 2 : 1)
 gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                      const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int xmap) {
-  static_assert(BN == 256 || BN == 128, "4-wave block tile is 256 x 256 or 256 x 128");
+  static_assert((BM == 256 && (BN == 256 || BN == 128)) || (BM == 128 && BN == 128),
+                "4-wave block tile is 256 x 256, 256 x 128 or 128 x 128");
   constexpr int KT = 64, NSLOT = 5;
-  constexpr int SLOT = 256 * KT * 2;               // one ring slot: a 256-row operand tile, 32 KiB
-  constexpr int GA = SLOT / 16 / 256;              // glds per thread for an A tile (8)
+  constexpr int SLOT = (BM > BN ? BM : BN) * KT * 2;  // one ring slot: the larger operand tile
+  constexpr int GA = BM * KT * 2 / 16 / 256;       // glds per thread for an A tile (8 or 4)
   constexpr int GB = BN * KT * 2 / 16 / 256;       // ... for a B tile (8 or 4)
-  constexpr int NJ = BN / 32;                      // 16-column fragments per wave (wave tile 128 x BN/2)
-  constexpr int NG = 2 * NJ;                       // groups of 4 MFMAs per half
+  constexpr int WM = BM / 2, WN = BN / 2;          // wave tile (2 x 2 waves)
+  constexpr int NI = WM / 16, NJ = WN / 16;        // 16-row / 16-column fragments per wave
+  constexpr int NG = NI * NJ / 4;                  // groups of 4 MFMAs per half
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
 
   int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, M / 256, N / BN, xmap, tm, tn);
-  const int m0 = tm * 256, n0 = tn * BN;
+  tile_coords(blockIdx.x, gridDim.x, M / BM, N / BN, xmap, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x & (kWave - 1);
   const int wr = wave >> 1, wc = wave & 1;
@@ -811,13 +813,13 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 
   // the accumulators start at the bias (D = C^T layout: 4 consecutive columns per lane), so the
   // epilogue holds no bias registers (at BN = 256 that kept the kernel at 148 VGPRs instead of 129)
-  f32x4 acc[8][NJ];
+  f32x4 acc[NI][NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (BIAS) b0 = *reinterpret_cast<const f32x4*>(bias + n0 + wc * (BN / 2) + j * 16 + fk * 4);
+    if constexpr (BIAS) b0 = *reinterpret_cast<const f32x4*>(bias + n0 + wc * WN + j * 16 + fk * 4);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i][j] = b0;
+    for (int i = 0; i < NI; ++i) acc[i][j] = b0;
   }
   agpr_after_init(acc);
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
@@ -825,8 +827,8 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   // and the next k-step's fragment i is read into the same registers right behind it; B keeps two
   // sets.  96 fragment VGPRs instead of 128 put the kernel at 384 registers, so three 38-VGPR
   // stream waves of other pods fit beside each of its waves instead of two.
-  constexpr bool SINGLE_A = NJ == 8;
-  bf16x8 fa[SINGLE_A ? 1 : 2][8], fb[2][NJ];
+  constexpr bool SINGLE_A = NI == 8 && NJ == 8;
+  bf16x8 fa[SINGLE_A ? 1 : 2][NI], fb[2][NJ];
   const int T = K / KT;                             // >= 2
 
   // piece q of operand tile X_u (B if isb): rows (q * 256 + wave * 64 + lane) >> 3, 8 per
@@ -836,7 +838,7 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   // 1-2 %, profiles/r06_lone_gemm/)
   const int rr = (wave * 64 + lane) >> 3, kq = ((wave * 64 + lane) & 7) ^ ((rr >> 1) & 7);
   const int voA = rr * lda * 2 + kq * 16, voB = rr * ldb * 2 + kq * 16;
-  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A + (size_t)m0 * lda), 0, 256 * lda * 2, 0x00020000);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A + (size_t)m0 * lda), 0, BM * lda * 2, 0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(Bt + (size_t)n0 * ldb), 0, BN * ldb * 2, 0x00020000);
   auto glds = [&](int u, bool isb, int q) {
     char* dst = smem + ((2 * u + (isb ? 1 : 0)) % NSLOT) * SLOT + (q * 256 + wave * 64) * 16;
@@ -862,9 +864,9 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   wait_vmcnt<GA + GB>();
   barrier();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) fa[0][q] = lds_frag<KT>(smem, wr * 128 + q * 16 + frow, fk);
+  for (int q = 0; q < NI; ++q) fa[0][q] = lds_frag<KT>(smem, wr * WM + q * 16 + frow, fk);
 #pragma unroll
-  for (int q = 0; q < NJ; ++q) fb[0][q] = lds_frag<KT>(smem + SLOT, wc * (BN / 2) + q * 16 + frow, fk);
+  for (int q = 0; q < NJ; ++q) fb[0][q] = lds_frag<KT>(smem + SLOT, wc * WN + q * 16 + frow, fk);
 
   // (Measured and removed: the four waves issuing their LDS-DMA pieces in pairs at staggered
   // groups, wave w at groups w, w + 4, ... -- 1,277 vs 1,483 TF/s lone, -2.7 % pods/s;
@@ -880,7 +882,7 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     const int ru = S == 0 ? t : t + 1;             // h0 reads k-step 1 of t, h1 k-step 0 of t+1
     const char* ta = slot(ru, false);
     const char* tb = slot(ru, true);
-    constexpr int NR = 8 + NJ, NS = S == 0 ? GA : GB;
+    constexpr int NR = NI + NJ, NS = S == 0 ? GA : GB;
     constexpr int SA = SINGLE_A ? 0 : S;           // A set in use
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -890,14 +892,14 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
         mfma_agpr(acc[i][j], fb[S][j], fa[SA][i]);
       }
       if constexpr (RD && SINGLE_A) {              // row g/2 done: its next A fragment; B at even groups
-        if (g & 1) fa[0][g >> 1] = lds_frag<KT>(ta, wr * 128 + (g >> 1) * 16 + frow, (S ^ 1) * 4 + fk);
-        else fb[S ^ 1][g >> 1] = lds_frag<KT>(tb, wc * (BN / 2) + (g >> 1) * 16 + frow, (S ^ 1) * 4 + fk);
+        if (g & 1) fa[0][g >> 1] = lds_frag<KT>(ta, wr * WM + (g >> 1) * 16 + frow, (S ^ 1) * 4 + fk);
+        else fb[S ^ 1][g >> 1] = lds_frag<KT>(tb, wc * WN + (g >> 1) * 16 + frow, (S ^ 1) * 4 + fk);
       } else if constexpr (RD) {
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
           if (q * NG / NR != g) continue;
-          if (q < 8) fa[S ^ 1][q] = lds_frag<KT>(ta, wr * 128 + q * 16 + frow, (S ^ 1) * 4 + fk);
-          else fb[S ^ 1][q - 8] = lds_frag<KT>(tb, wc * (BN / 2) + (q - 8) * 16 + frow, (S ^ 1) * 4 + fk);
+          if (q < NI) fa[S ^ 1][q] = lds_frag<KT>(ta, wr * WM + q * 16 + frow, (S ^ 1) * 4 + fk);
+          else fb[S ^ 1][q - NI] = lds_frag<KT>(tb, wc * WN + (q - NI) * 16 + frow, (S ^ 1) * 4 + fk);
         }
       }
       if constexpr (ST) {
@@ -941,18 +943,18 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int col = wc * (BN / 2) + j * 16 + fk * 4;
+    const int col = wc * WN + j * 16 + fk * 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const f32x4 v = acc[i][j];
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (__bf16)(RELU ? (v[r] > 0.f ? v[r] : 0.f) : v[r]);
-      wide_put<BN>(smem, wr * 128 + i * 16 + frow, col, o);
+      wide_put<BN>(smem, wr * WM + i * 16 + frow, col, o);
     }
   }
   __syncthreads();
-  wide_store<256, BN, 256>(smem, C, ldc, m0, n0);
+  wide_store<BM, BN, 256>(smem, C, ldc, m0, n0);
 }
 
 // C[m, n..n+3] = act(sum_s ws[s][m, n..n+3] + bias) as bf16 -- the split-K epilogue (float4 in,
@@ -1182,13 +1184,14 @@ static int g_gemm_tile = 0;
 // 14 = 256x256 on 4 waves of 128x128 with AGPR-tied inline-asm MFMAs, 64-deep operand tiles in a
 // 5-slot LDS ring (gemm_bf16_nt_256_w4l).  Forced only (K >= 128, C rows 16-B aligned): the
 // lone-GEMM study of profiles/r06_lone_gemm/, level with tile 10; the co-run default since
-// round 6, policy 10).  15 = the same kernel on a 256x128 block (wave tile 128 x 64; policy 11).
+// round 6, policy 10).  15 = the same kernel on a 256x128 block (wave tile 128 x 64; policy 11);
+// 16 = on a 128x128 block (wave tile 64 x 64, 80 KiB ring, 2 blocks per CU; policy 13).
 // (Also measured and removed: tile 14's schedule on v_mfma_f32_32x32x16_bf16 -- half the MFMA
 // instructions, exact, but 1,434 vs 1,483 TF/s at 8192^3, profiles/r06_lone_gemm/mfma32/.)  (Also measured there and
 // removed: 32-deep sub-tiles in 4 slots with one barrier per 32 or per 64 k, and register-staged
 // global loads -- 5-15 % behind.)
-static const int kTileBM[16] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256, 256, 256};
-static const int kTileBN[16] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128, 256, 128};
+static const int kTileBM[17] = {0, 128, 64, 64, 256, 256, 128, 64, 256, 256, 256, 128, 128, 256, 256, 256, 128};
+static const int kTileBN[17] = {0, 128, 128, 64, 256, 128, 128, 128, 128, 256, 256, 128, 128, 128, 256, 128, 128};
 
 // Tile policy.  Lone GEMMs that still get one block per CU use the 8-phase 256x256 with the
 // peeled steady-state loop (tile 10; tile 9 4096^3 1306 vs 1109 TF for tile 4, 8192^3 1434 vs
@@ -1212,7 +1215,7 @@ static int g_gemm_policy = 10;
 static int g_split_k = 0;
 
 void set_gemm_policy(int p) {
-  if (p < 0 || p > 12) throw std::runtime_error("gemm policy must be 0..12");
+  if (p < 0 || p > 13) throw std::runtime_error("gemm policy must be 0..13");
   g_gemm_policy = p;
 }
 
@@ -1226,7 +1229,7 @@ void set_w4_probe(int mask) {
 }
 
 void set_gemm_tile(int t) {
-  if (t < 0 || t > 15) throw std::runtime_error("gemm tile must be 0..15");
+  if (t < 0 || t > 16) throw std::runtime_error("gemm tile must be 0..16");
   g_gemm_tile = t;
 }
 
@@ -1248,7 +1251,7 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   // SIMD at 416 registers and no LDS left over, so up to three 32-VGPR stream waves of the other
   // pods fit on each of its SIMDs, where the 8-phase kernel's two 240-register waves leave room
   // for one
-  if (!alone && fits256 && (g_gemm_policy == 10 || g_gemm_policy == 11)) return 14;
+  if (!alone && fits256 && (g_gemm_policy == 10 || g_gemm_policy == 11 || g_gemm_policy == 13)) return 14;
   // 12 (A/B arm): every co-running GEMM the 256 x 256 tile divides on the 4-wave kernel, even with
   // fewer tiles than its share's CUs (the other pods' stream waves take the rest)
   if (!alone && g_gemm_policy == 12 && M % 256 == 0 && N % 256 == 0) return 14;
@@ -1270,6 +1273,9 @@ int pick_gemm_tile(int M, int N, int cu_budget) {
   if (!alone && (g_gemm_policy == 5 || g_gemm_policy == 6) && M % 128 == 0 && N % 128 == 0 &&
       (M / 128) * (N / 128) >= budget)
     return g_gemm_policy == 5 ? 11 : 12;
+  // 13 (A/B arm): arm 10, and the co-running GEMMs the 128 x 128 tile fills on the 4-wave kernel
+  // at 128 x 128 (tile 16) instead of the compiler-scheduled tile 1
+  if (!alone && g_gemm_policy == 13 && (M / 128) * (N / 128) >= budget) return 16;
   if ((M / 128) * (N / 128) >= per_cu * budget) return 1;
   if ((M / 64) * (N / 128) >= per_cu * budget && N % 128 == 0) return 2;
   return 3;
@@ -1331,6 +1337,7 @@ static int resolve_gemm_tile(int M, int N, int K, int cu_budget) {
   if (t == 13 && K < 128) t = 5;
   if (t == 14 && K < 128) t = 4;
   if (t == 15 && K < 128) t = 5;
+  if (t == 16 && K < 128) t = 1;
   if (M % kTileBM[t] || N % kTileBN[t]) t = 3;   // 64x64 always divides (checked by the caller)
   return t;
 }
@@ -1424,23 +1431,29 @@ void gemm_bf16_nt(uintptr_t a, uintptr_t bt, uintptr_t c, uintptr_t bias, int M,
       break;
     }
     case 14:
-    case 15: {
+    case 15:
+    case 16: {
       if (!wide_ok(Cp, ldc)) {
-        if (g_gemm_tile == t) throw std::runtime_error("gemm tiles 14 / 15: C rows must be 16-byte aligned");
+        if (g_gemm_tile == t) throw std::runtime_error("gemm tiles 14-16: C rows must be 16-byte aligned");
         if (t == 14)                                // a policy on an unaligned C: the 8-phase kernels
           launch_8ph<true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, dim3((M / 256) * (N / 256)), dim3(512), false);
-        else
+        else if (t == 15)
           launch_8ph<true, 128>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s, dim3((M / 256) * (N / 128)), dim3(512), false);
+        else
+          launch_gemm<128, 128, 2, 2, 2, 2, 64, true>(A, B, Cp, bp, M, N, K, lda, ldb, ldc, relu, s);
         break;
       }
       if ((size_t)256 * std::max(lda, ldb) * 2 >= ((size_t)1 << 31))
-        throw std::runtime_error("gemm tiles 14 / 15: a 256-row operand block must span < 2 GiB");
-      const int bn = t == 14 ? 256 : 128;
-      const dim3 grid((M / 256) * (N / bn)), block(256);
+        throw std::runtime_error("gemm tiles 14-16: a 256-row operand block must span < 2 GiB");
+      const int bm = t == 16 ? 128 : 256, bn = t == 14 ? 256 : 128;
+      const dim3 grid((M / bm) * (N / bn)), block(256);
       const bool lone = g_lone_plain_order && (cu_budget <= 0 || cu_budget >= kCus);
-      const int xmap = lone ? 0 : pick_xcd_map(M / 256, N / bn);
+      const int xmap = lone ? 0 : pick_xcd_map(M / bm, N / bn);
       decltype(&gemm_bf16_nt_256_w4l<false, false>) k;
-      if (t == 15)
+      if (t == 16)
+        k = relu ? (bp ? gemm_bf16_nt_256_w4l<true, true, 0, false, 128, 128> : gemm_bf16_nt_256_w4l<true, false, 0, false, 128, 128>)
+                 : (bp ? gemm_bf16_nt_256_w4l<false, true, 0, false, 128, 128> : gemm_bf16_nt_256_w4l<false, false, 0, false, 128, 128>);
+      else if (t == 15)
         k = relu ? (bp ? gemm_bf16_nt_256_w4l<true, true, 0, false, 128> : gemm_bf16_nt_256_w4l<true, false, 0, false, 128>)
                  : (bp ? gemm_bf16_nt_256_w4l<false, true, 0, false, 128> : gemm_bf16_nt_256_w4l<false, false, 0, false, 128>);
       else if (g_w4_probe)   // timing probes: steady-loop LDS-DMA (1), reads (2) or both (3) dropped

@@ -12,7 +12,7 @@ h = _native.hip(required=False)
 pytestmark = pytest.mark.skipif(h is None, reason="HIP extension not built")
 
 # policy -> tile for M=1024, N=2048 at a 64-CU budget
-SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1, 9: 1, 10: 1, 11: 15, 12: 14}
+SMALL = {0: 1, 1: 1, 2: 1, 3: 5, 4: 8, 5: 11, 6: 12, 7: 13, 8: 1, 9: 1, 10: 1, 11: 15, 12: 14, 13: 16}
 
 
 @pytest.fixture(autouse=True)
@@ -28,12 +28,12 @@ def test_small_corun_gemm_tile_per_policy(policy):
     assert h.pick_gemm_tile(1024, 2048, 64) == SMALL[policy]
 
 
-@pytest.mark.parametrize("policy", range(13))
+@pytest.mark.parametrize("policy", range(14))
 def test_large_corun_and_lone_gemm_tiles(policy):
     h.set_gemm_policy(policy)
     # enough 256x256 tiles for the share: the 8-phase kernel for every policy but 0 (128x128) and
     # 10 (the 4-wave kernel)
-    assert h.pick_gemm_tile(4096, 4096, 64) == {0: 1, 10: 14, 11: 14, 12: 14}.get(policy, 10)
+    assert h.pick_gemm_tile(4096, 4096, 64) == {0: 1, 10: 14, 11: 14, 12: 14, 13: 14}.get(policy, 10)
     # a lone GEMM that fills the chip: tile 4 under policy 2, else the 8-phase kernel
     assert h.pick_gemm_tile(8192, 8192, 0) == (4 if policy == 2 else 10)
 
@@ -95,7 +95,7 @@ def test_four_wave_study_tile_is_forced_only():
     assert h.gemm_workgroups(8192, 8192, 8192, 0, False, False) == 32 * 32
     assert h.gemm_workgroups(512, 512, 64, 0, False, False) == 4       # K < 128 -> tile 4, same grid
     with pytest.raises(Exception):
-        h.set_gemm_tile(16)
+        h.set_gemm_tile(17)
     h.set_gemm_tile(15)                                        # its 256 x 128 sibling (policy 11)
     assert h.gemm_workgroups(1024, 2048, 1024, 64, False, False) == 4 * 16
     h.set_gemm_tile(0)

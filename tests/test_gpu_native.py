@@ -60,14 +60,14 @@ def test_gemm_every_tile_variant(tile):
         h.set_gemm_tile(0)
 
 
-@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [9, 10, 11, 12, 13, 14, 15, 16])
 def test_gemm_256_8phase_numerics_and_race_screen(tile):
     """The 8-phase 256x256 kernel (tile 9; tile 10 = its steady-state loop peeled), and the
     128x128 multi-stage kernels (11, 12: 3 / 4 LDS stages, counted vmcnt), and the 8-phase
     schedule on a 256x128 block (13: unequal half-tile glds counts in the waits), and the 4-wave
     kernel with AGPR-tied inline-asm MFMAs (14: 5-slot LDS ring, one barrier per K-tile; the
     accumulator fences are what keep its bias / ReLU epilogue right; 15: the same on a 256 x 128
-    block, unequal A / B glds counts): every
+    block, unequal A / B glds counts; 16: on a 128 x 128 block, two blocks per CU): every
     K-tile count from the minimum (2) through odd
     counts (the buffer parity flips) to long loops, several grid sizes, each shape run
     repeatedly -- a mis-counted vmcnt or a restage too early shows up as rare wrong tiles
@@ -182,13 +182,14 @@ def test_gemm_share_capped_policy9_matches_fp32_reference(hip, M, N, K):
         hip.set_gemm_policy(10)
 
 
-def test_gemm_corun_policy11_256x128_four_wave_matches_fp32_reference(hip):
-    """Arm 11: arm 10, plus co-running GEMMs that fill their share only with 256 x 128 blocks on
-    the 4-wave kernel (tile 15) -- fp32 PyTorch reference, repeated runs."""
+@pytest.mark.parametrize("policy,small_tile", [(11, 15), (13, 16)])
+def test_gemm_corun_policy11_13_four_wave_matches_fp32_reference(hip, policy, small_tile):
+    """Arms 11 / 13: arm 10, plus co-running GEMMs too small for 256 x 256 tiles on the 4-wave
+    kernel at 256 x 128 (tile 15) / 128 x 128 (tile 16) -- fp32 PyTorch reference, repeated runs."""
     from k8s_gpu_scheduler_amd.ops import loadgen
-    hip.set_gemm_policy(11)
+    hip.set_gemm_policy(policy)
     try:
-        for M, N, K, tile in [(1024, 2048, 1024, 15), (1024, 2560, 2560, 15), (4096, 4096, 512, 14)]:
+        for M, N, K, tile in [(1024, 2048, 1024, small_tile), (1024, 2560, 2560, small_tile), (4096, 4096, 512, 14)]:
             assert hip.pick_gemm_tile(M, N, 64) == tile
             g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
             a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
@@ -939,7 +940,7 @@ def test_xcd_dispatch_and_tile_orders_bit_exact():
         torch.testing.assert_close(tref, y + 1.5 * z)
         for gone in ("set_xcd_mask", "set_c_nontemporal", "set_triad_aux"):
             assert not hasattr(h, gone), gone
-        for bad in (16, 17, -1):                  # (tiles 11-13 exist since round 5, 14-15 since round 6)
+        for bad in (17, 18, -1):                  # (tiles 11-13 exist since round 5, 14-16 since round 6)
             with pytest.raises(Exception):
                 h.set_gemm_tile(bad)
     finally:

@@ -75,7 +75,7 @@ def main() -> None:
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     h = _native.hip(required=True)
     try:
-        if not all([check(h, t) for t in (14, 15)]):
+        if not all([check(h, t) for t in (14, 15, 16)]):
             print("NUMERICS FAILED", flush=True)
             sys.exit(1)
         perf(h, iters)
