@@ -10,7 +10,7 @@ O=$R/gpurun_out/${PMC_OUT:-pmc_bench}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 export GPUSCHED_PROFILE_MARKERS=$O/timed_pods.json
-B="python3 $R/bench.py --steps ${PMC_STEPS:-6} --warmup 1 --control-plane inline --graphs 0 --prewarm-ms 0"
+B="python3 $R/bench.py --steps ${PMC_STEPS:-6} --warmup 1 --control-plane inline --graphs 0 --prewarm-ms 0 ${PMC_ARGS:-}"
 i=0
 for c in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))

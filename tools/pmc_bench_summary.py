@@ -23,14 +23,17 @@ MARKER = "xcd_probe_kernel"
 TILE_FAMILY = {1: "gemm_tile_128x128", 2: "gemm_tile_64x128", 3: "gemm_tile_64x64", 4: "gemm_tile_256x256",
                5: "gemm_tile_256x128", 6: "gemm_tile_128x128", 7: "gemm_tile_64x128", 8: "gemm_tile_256x128",
                9: "gemm_256x256_8phase", 10: "gemm_256x256_8phase", 13: "gemm_256x128_8phase",
-               14: "gemm_256x256_4wave", 15: "gemm_256x128_4wave"}
+               14: "gemm_256x256_4wave", 15: "gemm_256x128_4wave", 16: "gemm_128x128_4wave"}
 
 
 def family(name: str) -> str:
     if "256_8ph" in name:
         return "gemm_256x256_8phase"
     if "256_w4l" in name:
-        return "gemm_256x128_4wave" if name.rstrip(")").split("(")[0].rstrip(">").endswith("128") else "gemm_256x256_4wave"
+        tparams = name.split("(")[0].rstrip(">").split(",")
+        bn = tparams[4].strip() if len(tparams) > 4 else "256"
+        bm = tparams[5].strip() if len(tparams) > 5 else "256"
+        return f"gemm_{bm}x{bn}_4wave"
     if "gemm_bf16_nt_kernel" in name:
         return "gemm_tile_" + name.split("<", 1)[1].split(",")[0] + "x" + name.split(",")[1].strip()
     if "stream_triad" in name:

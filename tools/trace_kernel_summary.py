@@ -25,7 +25,10 @@ def family(name: str) -> str:
     if "256_8ph" in name:
         return "gemm_256x256_8phase"
     if "256_w4l" in name:
-        return "gemm_256x128_4wave" if name.split("(")[0].rstrip(">").endswith("128") else "gemm_256x256_4wave"
+        tparams = name.split("(")[0].rstrip(">").split(",")
+        bn = tparams[4].strip() if len(tparams) > 4 else "256"
+        bm = tparams[5].strip() if len(tparams) > 5 else "256"
+        return f"gemm_{bm}x{bn}_4wave"
     if "gemm_bf16_nt_kernel" in name:
         return "gemm_tile_" + name.split("<", 1)[1].split(",")[0].strip() + "x" + name.split(",")[1].strip()
     if "gemm_fp8" in name:
