@@ -738,9 +738,10 @@ gemm_bf16_nt_256_8ph(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     }
 }
 
-// Tile 14 (lone-GEMM study; forced with set_gemm_tile only): the 256 x 256
-// block tile on FOUR waves of 128 x 128 -- hipBLASLt's shape (profiles/r05_lone_gemm_pmc/:
-// 0.25 LDS reads per MFMA instead of the 8-phase kernel's 0.375).  Round 5's versions of this
+// Tile 14 (built for the lone-GEMM study; the co-run default since round 6,
+// policy 10): the 256 x 256 block tile on FOUR waves of 128 x 128 -- hipBLASLt's shape
+// (profiles/r05_lone_gemm_pmc/: 0.25 LDS reads per MFMA instead of the 8-phase kernel's 0.375).
+// Tiles 15 / 16 are the same kernel on 256 x 128 / 128 x 128 blocks (A/B knobs).  Round 5's versions of this
 // structure stalled once per K-tile (1,016 TF) or spilled: the compiler kept a VGPR copy of the
 // 256 accumulators next to the AGPRs.  Here the MFMA is inline asm with the accumulator tied to
 // an AGPR ("+a"), so the accumulators cannot leave the AGPR file.
@@ -751,8 +752,9 @@ __device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& b, const bf1
 // The compiler cannot see that the asm above is an MFMA, so it cannot insert the wait states
 // between an MFMA and a VALU access of its accumulator: these fences pin them.  An empty volatile
 // asm that "modifies" every accumulator keeps the compiler's own accumulator accesses on their
-// side of it (volatile asm statements keep their order).  agpr_after_init: after the zero-fill,
-// before the first MFMA; agpr_before_read: after the last MFMA, before the epilogue reads.
+// side of it (volatile asm statements keep their order).  agpr_after_init: after the accumulators'
+// bias / zero fill, before the first MFMA; agpr_before_read: after the last MFMA, before the
+// epilogue reads.
 template <int NI, int NJ>
 __device__ __forceinline__ void agpr_fence(f32x4 (&acc)[NI][NJ]) {
 #pragma unroll
@@ -775,9 +777,10 @@ __device__ __forceinline__ void agpr_before_read(f32x4 (&acc)[NI][NJ]) {
 // (32-deep sub-tiles in 4 slots, one barrier per 32 k; profiles/r06_lone_gemm/): its LDS-DMA cost
 // the single wave per SIMD ~0.22 ms of 0.79 at 8192^3, and fetching 8 rows x 128 B per
 // instruction (whole cache lines) instead of 16 rows x 64 B saved ~0.09 ms of that.  So the
-// operand tiles here are 256 rows x 64 k (128-B rows, stage_tile's KT = 64 image and swizzle):
-// A_t and B_t are 32 KiB each and take ring slots
-// (2t) % 5 and (2t+1) % 5 (160 KiB, the CU's whole LDS).  K-tile t runs two halves of 64 MFMAs:
+// operand tiles here are BM / BN rows x 64 k (128-B rows, stage_tile's KT = 64 image and swizzle):
+// A_t and B_t take ring slots (2t) % 5 and (2t+1) % 5 of the larger tile's size (256 x 256: 32 KiB
+// each, 160 KiB = the CU's whole LDS; 128 x 128: 80 KiB, two blocks per CU).  K-tile t runs two
+// halves of (BM / 32) x (BN / 32) MFMAs (64 at 256 x 256):
 //   h0: MFMAs of k-step 0 (fragment set 0), reads of k-step 1 into set 1, glds of A_{t+2}
 //       (into B_{t-1}'s slot);
 //   lgkmcnt(0) + vmcnt (A_{t+1}, B_{t+1} landed; A_{t+2} may fly) + ONE barrier;
