@@ -871,9 +871,10 @@ gemm_bf16_nt_256_w4l(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 #pragma unroll
   for (int q = 0; q < NJ; ++q) fb[0][q] = lds_frag<KT>(smem + SLOT, wc * WN + q * 16 + frow, fk);
 
-  // (Measured and removed: the four waves issuing their LDS-DMA pieces in pairs at staggered
-  // groups, wave w at groups w, w + 4, ... -- 1,277 vs 1,483 TF/s lone, -2.7 % pods/s;
-  // profiles/r06_lone_gemm/stagger/.)
+  // (Measured and removed: the four waves issuing their LDS-DMA pieces at different points -- in
+  // pairs at groups w, w + 4, ... for wave w (1,277 vs 1,483 TF/s lone, -2.7 % pods/s) or the odd
+  // waves in the odd groups (1,282 vs 1,493, -2.2 %); the waves' lockstep issue is the faster one,
+  // profiles/r06_lone_gemm/stagger/, parity/.)
   // one half: 8 x NJ MFMAs on set S (k-step S of K-tile t) in NG groups of 4; the 8 + NJ reads of
   // (RU, k-step S^1) into set S^1 when RD, spread evenly (BN = 256: one per group); the glds of
   // operand tile (t+2, X = S) when ST, spread evenly (BN = 256: every second group; other
@@ -1224,6 +1225,7 @@ void set_gemm_policy(int p) {
 
 static int g_w4_probe = 0;
 static int g_w4_prio = 0;
+
 
 void set_w4_prio(int on) { g_w4_prio = on ? 1 : 0; }
 void set_w4_probe(int mask) {
