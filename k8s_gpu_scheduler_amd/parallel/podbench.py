@@ -897,8 +897,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="run apiserver+scheduler in a separate process (default) or inside rank 0")
     ap.add_argument("--graphs", type=int, default=1, choices=[0, 1],
                     help="1: replay each pod's kernel sequence as one captured HIP graph")
-    ap.add_argument("--lookahead", type=int, default=2,
-                    help="epochs kept in flight per GPU before collecting (>= 1)")
+    ap.add_argument("--lookahead", type=int, default=3,
+                    help="epochs kept in flight per GPU before collecting (>= 1).  3 since round 6: with the 4-wave "
+                         "co-run GEMM, 612.7 / 607.9 vs 602.8 / 600.6 pods/s for 2 on two boxes (4 interleaved "
+                         "rounds each; 4 and 5 add <= 0.4 %% more at 1-2.5 fewer SLO points), profiles/r06_lookahead/")
     ap.add_argument("--gemm-policy", type=int, default=10, choices=list(range(14)),
                     help="GEMM tile policy: 10 (default since round 6) the 4-wave 256x256 kernel (tile 14) for "
                          "co-running GEMMs that fill their share with 256x256 tiles; 1 the 8-phase kernel there "
