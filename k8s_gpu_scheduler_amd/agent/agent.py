@@ -130,6 +130,7 @@ class NodeAgent:
         # the busy sampler's own period (its thread, started with the agent): the occupancy
         # integral's resolution; 0 = sample only in step()
         self.busy_poll_s = busy_poll_s
+        self._busy_query_s = 0.0          # EMA of one process-list round's own duration
         self._busy_thread: Optional[threading.Thread] = None
         if self.profiles is not None:
             self.profiles.on_busy = self.busy.note_profiled
@@ -292,10 +293,19 @@ class NodeAgent:
         return {O.uid(p): p for p in pods if not O.is_terminal(p) and O.uid(p)}
 
     def sample_busy(self) -> None:
-        """One busy-time sampling round over the attributed processes (agent.busy)."""
+        """One busy-time sampling round over the attributed processes (agent.busy).  An interval
+        counts at most 2.5 sampling periods, where the period is the poll wait plus the process
+        query's own (averaged) duration: amd-smi's process list can take longer than the poll
+        wait on a loaded node, and capping at twice the wait alone dropped a quarter of a pod's
+        busy time on MI355X (1,480 vs 2,002 ms); a sampler stalled well past its period still
+        does not count its stall."""
         try:
-            gap = 2.0 * max(self.busy_poll_s, 0.05) if self._busy_thread is not None else 2.0 * self.poll_s
+            wait = max(self.busy_poll_s, 0.05) if self._busy_thread is not None else self.poll_s
+            gap = 2.5 * (wait + self._busy_query_s)
+            t0 = time.monotonic()
             self.busy.sample(self.source, self.pod_resolver, len(self.source.devices()), max_gap_s=gap)
+            dt = time.monotonic() - t0
+            self._busy_query_s = dt if self._busy_query_s == 0.0 else 0.8 * self._busy_query_s + 0.2 * dt
         except Exception as e:
             log.debug("process list for busy time failed: %s", e)
 
